@@ -1,0 +1,196 @@
+"""Op API of the framework.
+
+Every op takes torch tensors and dispatches on the tensor's device:
+  * ``cuda`` (ROCm/HIP) tensors -> the hand-written gfx950 HIP kernels in ``_C``
+    (``csrc/kernels/*.hip``). If the extension is missing this raises.
+  * CPU tensors -> ``ops.reference`` (pure PyTorch; the test/oracle path).
+
+There is exactly one GPU implementation per op (no backend selection, no Triton).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+from ._ext import available as ext_available  # noqa: F401
+from ._ext import ext
+
+BF16 = torch.bfloat16
+
+# Linear epilogue modes (must match csrc/kernels/common.h)
+MODE_STORE = 0
+MODE_RESIDUAL = 1
+MODE_SWIGLU = 2
+
+
+def _is_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+class _Workspace:
+    """Grow-only scratch buffers (per device, per name). Sized during warm-up so that
+    nothing is allocated while a decode step is being captured into a hipGraph."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def get(self, name: str, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
+        key = (name, device, dtype)
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < numel:
+            buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            self._bufs[key] = buf
+        return buf[:numel]
+
+    def clear(self):
+        self._bufs.clear()
+
+
+workspace = _Workspace()
+
+
+# ----------------------------------------------------------------------------------
+def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """ids int32 [M] -> fp32 [M, D] rows of the bf16 table (residual stream is fp32)."""
+    if not _is_gpu(table):
+        return ref.embedding(ids, table)
+    out = torch.empty(ids.numel(), table.shape[1], dtype=torch.float32, device=table.device)
+    ext().embedding(ids.reshape(-1).to(torch.int32), table, out)
+    return out
+
+
+def rms_scale(x: torch.Tensor, eps: float) -> torch.Tensor:
+    if not _is_gpu(x):
+        return ref.rms_scale(x, eps)
+    out = torch.empty(x.shape, dtype=BF16, device=x.device)
+    ext().rms_scale(x, out, float(eps))
+    return out
+
+
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
+    """Stand-alone RMSNorm (fp32 out); the model folds norm weights into GEMMs instead."""
+    if not _is_gpu(x):
+        return ref.rmsnorm(x, weight, eps)
+    out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    ext().rmsnorm(x.float().contiguous(), weight.float().contiguous(), out, float(eps))
+    return out
+
+
+# ----------------------------------------------------------------------------------
+def linear(x: torch.Tensor, w, rms_eps: Optional[float] = None, out_dtype=BF16,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``y = [inv_rms(x) *] x @ W^T``; ``w`` is a ``models.weights.PackedLinear``."""
+    if not _is_gpu(x):
+        r = ref.linear(x, w.dense(), rms_eps, out_dtype)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    m = x.shape[0]
+    if out is None:
+        out = torch.empty(m, w.n, dtype=out_dtype, device=x.device)
+    _gpu_linear(x, w, out, MODE_STORE, rms_eps, True)
+    return out
+
+
+def linear_residual(x: torch.Tensor, w, residual: torch.Tensor, rms_eps: Optional[float] = None,
+                    accumulate: bool = True) -> torch.Tensor:
+    """``residual (fp32) += y`` (or ``= y`` when ``accumulate`` is False)."""
+    if not _is_gpu(x):
+        return ref.linear_residual(x, w.dense(), residual, rms_eps, accumulate)
+    _gpu_linear(x, w, residual, MODE_RESIDUAL, rms_eps, accumulate)
+    return residual
+
+
+def linear_swiglu(x: torch.Tensor, w, rms_eps: Optional[float] = None) -> torch.Tensor:
+    """``silu(x W1^T) * (x W3^T)`` with W1/W3 packed as alternating 16-row tiles."""
+    if not _is_gpu(x):
+        return ref.linear_swiglu(x, w.dense(), rms_eps)
+    out = torch.empty(x.shape[0], w.n // 2, dtype=BF16, device=x.device)
+    _gpu_linear(x, w, out, MODE_SWIGLU, rms_eps, True)
+    return out
+
+
+def _gpu_linear(x, w, out, mode, rms_eps, accumulate):
+    assert x.is_contiguous() and out.is_contiguous()
+    assert x.shape[1] == w.k, (x.shape, w.k)
+    m = x.shape[0]
+    e = ext()
+    if m > e.SKINNY_MAX_M:
+        # Large-M (prefill) path: bf16 normalised activations, then the MFMA tiled GEMM.
+        if rms_eps is not None:
+            x = rms_scale(x, rms_eps)
+        elif x.dtype != BF16:
+            x = x.to(BF16)
+        e.gemm(x, w.weight, w.n, w.k, out, mode, bool(accumulate))
+    else:
+        e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
+                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate))
+
+
+# ----------------------------------------------------------------------------------
+def rope_kv_write(qkv: torch.Tensor, table: torch.Tensor, positions: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, seq_len: int,
+                  n_heads: int, n_kv_heads: int, head_dim: int) -> torch.Tensor:
+    """Rotate q/k (interleaved RoPE) and write k/v into the cache. ``slot0`` is an int or a
+    device int32 tensor of shape [1] (graph-capturable). Returns q ``[B*S, H, Dh]`` bf16."""
+    if not _is_gpu(qkv):
+        s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
+        return ref.rope_kv_write(qkv, table, positions, k_cache, v_cache, s0, seq_len,
+                                 n_heads, n_kv_heads, head_dim)
+    m = qkv.shape[0]
+    q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=qkv.device)
+    slot_t = _slot_tensor(slot0, qkv.device)
+    ext().rope_kv_write(qkv, table, positions.reshape(-1).to(torch.int32), k_cache, v_cache,
+                        slot_t, int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q)
+    return q
+
+
+def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor,
+              key_mask: Optional[torch.Tensor] = None, max_kv: Optional[int] = None) -> torch.Tensor:
+    """Causal/padded attention of ``q [B, S, H, Dh]`` (queries at cache slots slot0+s)
+    against ``[B, Hkv, T, Dh]`` caches. Returns ``[B*S, H*Dh]`` bf16.
+
+    ``max_kv`` bounds the number of key slots the launch must cover (defaults to the cache
+    length T so the launch shape is static and graph-capturable)."""
+    bsz, s, h, dh = q.shape
+    if not _is_gpu(q):
+        s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
+        return ref.attention(q, k_cache, v_cache, s0, kv_start, key_mask).reshape(bsz * s, h * dh)
+    out = torch.empty(bsz * s, h * dh, dtype=BF16, device=q.device)
+    slot_t = _slot_tensor(slot0, q.device)
+    t_cap = int(max_kv) if max_kv is not None else k_cache.shape[2]
+    e = ext()
+    if s == 1:
+        nsplit = e.attn_decode_splits(bsz, k_cache.shape[1], t_cap)
+        ws = workspace.get("attn_decode", bsz * h * nsplit * (dh + 2), torch.float32, q.device)
+        e.attn_decode(q, k_cache, v_cache, slot_t, kv_start, key_mask, out, ws, t_cap, nsplit)
+    else:
+        e.attn_prefill(q, k_cache, v_cache, slot_t, kv_start, key_mask, out)
+    return out
+
+
+_SLOT_CACHE = {}
+
+
+def _slot_tensor(slot0, device):
+    if torch.is_tensor(slot0):
+        return slot0
+    # Host int -> small device tensor (not graph-capturable; the engine passes tensors).
+    t = torch.tensor([int(slot0)], dtype=torch.int32, device=device)
+    return t
+
+
+# ----------------------------------------------------------------------------------
+def argmax(logits: torch.Tensor):
+    """Row argmax (first max index, like ``jnp.argmax``). Returns (idx int32[B], val fp32[B])."""
+    if not _is_gpu(logits):
+        v, i = logits.float().max(-1)
+        return ref.argmax(logits), v
+    b = logits.shape[0]
+    idx = torch.empty(b, dtype=torch.int32, device=logits.device)
+    val = torch.empty(b, dtype=torch.float32, device=logits.device)
+    ext().argmax(logits, idx, val)
+    return idx, val

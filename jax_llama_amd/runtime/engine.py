@@ -1,0 +1,278 @@
+"""Generation engine: prefill + hipGraph-replayed decode steps.
+
+Semantics follow HF ``FlaxGenerationMixin.generate`` (transformers<5), which the reference
+inherits (``generation.py:28-41`` builds the ``GenerationConfig``):
+
+  * ``sequences = full((B, max_length), pad)``; the prompt occupies ``[:, :S]``;
+  * the prefill is the first loop-body call, then the decode loop runs while
+    ``cur_len < max_length`` and not every row has produced ``eos``;
+  * a finished row emits ``pad``; ``is_sent_finished |= next == eos``;
+  * greedy = ``argmax`` (first max); sampling = temperature -> top-k (default 50) -> top-p ->
+    categorical;
+  * positions: ``cumsum(mask) - 1`` for the prompt, then ``last + 1`` per step
+    (``model.py:758, 771``).
+
+MI355X execution model (replaces XLA's compiled ``lax.while_loop``):
+  * the whole decode step (embedding, all layers, lm_head, sampler, state update) reads its
+    inputs — token ids, positions, the cache slot, ``cur_len`` and the finished flags — from
+    device buffers and writes the next state back, so it is captured ONCE into a hipGraph
+    (``torch.cuda.CUDAGraph`` is hipGraph on ROCm) and replayed per token with no host
+    work besides the launch;
+  * the host polls the finished flags only every ``check_every`` steps (rows that finished
+    earlier keep emitting ``pad``, so polling late never changes the output).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+
+_NEG_INF = float("-inf")
+
+
+@dataclass
+class GenerationConfig:
+    """Subset of HF ``GenerationConfig`` used by the reference (``generation.py:32-40``)."""
+
+    max_length: Optional[int] = None
+    max_new_tokens: Optional[int] = None
+    do_sample: bool = False
+    temperature: float = 1.0
+    top_k: int = 50  # HF default; the reference never overrides it
+    top_p: float = 1.0
+    num_beams: int = 1
+    pad_token_id: Optional[int] = None
+    eos_token_id: Optional[int] = None
+    seed: int = 0
+
+
+@dataclass
+class GenerateOutput:
+    sequences: torch.Tensor
+
+
+# --------------------------------------------------------------------------------------
+# Sampling
+# --------------------------------------------------------------------------------------
+def _greedy(model, logits_local: torch.Tensor) -> torch.Tensor:
+    idx, val = ops.argmax(logits_local)
+    comm = model.comm
+    if comm.size == 1:
+        return idx
+    idx = idx + comm.rank * logits_local.shape[1]
+    vals = comm.all_gather(val)  # [tp, B]
+    idxs = comm.all_gather(idx)
+    best = vals.argmax(0)  # first max in rank order == smallest global index among ties
+    return idxs.gather(0, best[None]).squeeze(0).to(torch.int32)
+
+
+def _sample(model, logits_local: torch.Tensor, gc: GenerationConfig, gen: Optional[torch.Generator]):
+    """temperature -> top-k -> top-p -> categorical (Gumbel-max), exact under vocab sharding."""
+    comm = model.comm
+    x = logits_local.float()
+    if gc.temperature is not None and gc.temperature != 1.0:
+        x = x / gc.temperature
+    if gc.top_k:
+        k = min(gc.top_k, x.shape[1])
+        vals, idx = torch.topk(x, k, dim=-1)
+        idx = idx + comm.rank * x.shape[1]
+        if comm.size > 1:
+            gv = comm.all_gather(vals).permute(1, 0, 2).reshape(x.shape[0], -1)
+            gi = comm.all_gather(idx).permute(1, 0, 2).reshape(x.shape[0], -1)
+            vals, sel = torch.topk(gv, k, dim=-1)
+            idx = gi.gather(1, sel)
+    else:
+        full = model.gather_logits(x)
+        vals, idx = torch.sort(full, dim=-1, descending=True)
+    if gc.top_p is not None and gc.top_p < 1.0:
+        # vals are sorted descending (topk returns sorted)
+        probs = torch.softmax(vals, -1)
+        cum = probs.cumsum(-1)
+        keep = torch.roll(cum < gc.top_p, 1, dims=-1)
+        keep[:, 0] = True
+        vals = torch.where(keep, vals, torch.full_like(vals, _NEG_INF))
+    u = torch.rand(vals.shape, device=vals.device, generator=gen, dtype=torch.float32)
+    gumbel = -torch.log(-torch.log(u.clamp_min(1e-20)).clamp_min(1e-20))
+    choice = (vals + gumbel).argmax(-1)
+    return idx.gather(1, choice[:, None]).squeeze(1).to(torch.int32)
+
+
+# --------------------------------------------------------------------------------------
+class DecodeEngine:
+    """Owns the KV cache and the device-resident decode state for one (B, max_length)."""
+
+    def __init__(self, model, batch_size: int, max_length: int, use_graph: Optional[bool] = None,
+                 check_every: int = 16):
+        self.model = model
+        self.b = batch_size
+        self.max_length = max_length
+        dev = model.device
+        self.device = dev
+        if use_graph is None:
+            use_graph = dev.type == "cuda" and os.environ.get("JLA_NO_GRAPH", "0") != "1"
+        self.use_graph = use_graph
+        self.check_every = check_every
+        self.cache = model.init_cache(batch_size, max_length)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.tokens = torch.zeros(batch_size, 1, **i32)
+        self.positions = torch.zeros(batch_size, 1, **i32)
+        self.kv_start = torch.zeros(batch_size, **i32)
+        self.finished = torch.zeros(batch_size, **i32)
+        self.cur_len = torch.zeros(1, **i32)
+        self.sequences = torch.zeros(batch_size, max_length, **i32)
+        self.key_mask: Optional[torch.Tensor] = None
+        self._graph = None
+        self._graph_key = None
+        self._gen: Optional[torch.Generator] = None
+        self.gc: Optional[GenerationConfig] = None
+
+    # ---------------------------------------------------------------------------------
+    def _next_token(self, logits_local):
+        if self.gc.do_sample:
+            return _sample(self.model, logits_local, self.gc, self._gen)
+        return _greedy(self.model, logits_local)
+
+    def _update(self, nxt: torch.Tensor):
+        """Device-side HF loop-body bookkeeping (pad for finished rows, eos tracking,
+        sequences write, position/slot/cur_len advance)."""
+        if self.device.type == "cuda":
+            ops.ext().decode_update(nxt, self.finished, self.sequences, self.cur_len, self.tokens,
+                                    self.positions, self.cache.index_t, int(self.gc.pad_token_id),
+                                    int(self.gc.eos_token_id))
+            return
+        fin = self.finished.bool()
+        nxt = torch.where(fin, torch.full_like(nxt, self.gc.pad_token_id), nxt)
+        self.finished.copy_((fin | (nxt == self.gc.eos_token_id)).to(torch.int32))
+        cl = int(self.cur_len.item())
+        if cl < self.max_length:
+            self.sequences[:, cl] = nxt
+        self.tokens[:, 0] = nxt
+        self.positions.add_(1)
+        self.cache.index_t.add_(1)
+        self.cur_len.add_(1)
+
+    def _decode_step(self):
+        logits, *_ = self.model.forward_tokens(self.tokens, self.positions, self.cache, self.cache.index_t,
+                                               self.kv_start, self.key_mask, logits_mode="last")
+        self._update(self._next_token(logits))
+
+    # ---------------------------------------------------------------------------------
+    def prefill(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor]):
+        model, dev = self.model, self.device
+        ids = input_ids.to(dev, torch.int32)
+        b, s = ids.shape
+        assert b == self.b and s < self.max_length
+        if attention_mask is None:
+            mask = torch.ones(b, s, dtype=torch.int32)
+        else:
+            mask = attention_mask.to("cpu", torch.int32)
+        positions = (mask.cumsum(-1) - 1).to(torch.int32)
+        ext_mask = torch.ones(b, self.max_length, dtype=torch.int32)
+        ext_mask[:, :s] = mask
+        from ..models.llama import mask_to_kv_start
+        kv_start, key_mask = mask_to_kv_start(ext_mask, dev)
+        self.kv_start.copy_(kv_start)
+        self.key_mask = key_mask
+        self.cache.reset()
+        self.sequences.fill_(self.gc.pad_token_id)
+        self.sequences[:, :s] = ids
+        self.finished.zero_()
+        pos_dev = positions.to(dev)
+        logits, *_ = model.forward_tokens(ids, pos_dev, self.cache, 0, self.kv_start, self.key_mask,
+                                          logits_mode="last")
+        self.cache.advance(s)
+        nxt = self._next_token(logits)
+        # state for the loop body: cur_len = S, token/pos of the last prompt position
+        self.cur_len.fill_(s)
+        self.positions.copy_(pos_dev[:, -1:])
+        # _update writes sequences[:, S], advances pos (+1), slot (+1 -> S+1 ... ) and cur_len.
+        # The prefill already advanced the slot by S; undo the update's +1 on the slot.
+        self.cache.index_t.sub_(1)
+        self._update(nxt)
+        self.cache.index = s  # host mirror (decode steps track the slot on the device)
+        return s + 1
+
+    def _ensure_graph(self):
+        key = (self.gc.do_sample, self.key_mask is not None)
+        if self._graph is not None and self._graph_key == key:
+            return
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        # Capture records kernels without executing them; state buffers are static.
+        with torch.cuda.graph(g):
+            self._decode_step()
+        self._graph, self._graph_key = g, key
+
+    def run(self, input_ids, attention_mask, gc: GenerationConfig) -> torch.Tensor:
+        self.gc = gc
+        if gc.do_sample:
+            self._gen = torch.Generator(device=self.device)
+            self._gen.manual_seed(int(gc.seed))
+            if self.use_graph:
+                # graph-safe RNG: default generator (philox offsets advance per replay)
+                self._gen = None
+                torch.manual_seed(int(gc.seed))
+        cur = self.prefill(input_ids, attention_mask)
+        steps_left = self.max_length - cur
+        done = steps_left <= 0
+        first = True
+        step = 0
+        while not done:
+            if self.use_graph and not first:
+                self._ensure_graph()
+                self._graph.replay()
+            else:
+                self._decode_step()  # first step eager: warms up workspaces before capture
+                first = False
+            step += 1
+            steps_left -= 1
+            if steps_left <= 0:
+                break
+            if step % self.check_every == 0 and bool(self.finished.all().item()):
+                break
+        return self.sequences
+
+
+_ENGINES = {}
+
+
+def get_engine(model, batch_size: int, max_length: int) -> DecodeEngine:
+    key = (id(model), batch_size, max_length)
+    eng = _ENGINES.get(key)
+    if eng is None:
+        if len(_ENGINES) > 4:
+            _ENGINES.clear()
+        eng = DecodeEngine(model, batch_size, max_length)
+        _ENGINES[key] = eng
+    return eng
+
+
+def generate(model, input_ids, attention_mask=None, generation_config: Optional[GenerationConfig] = None,
+             prng_key=None, **kwargs) -> GenerateOutput:
+    gc = generation_config or GenerationConfig()
+    for k, v in kwargs.items():
+        if hasattr(gc, k):
+            setattr(gc, k, v)
+    if gc.num_beams != 1:
+        raise NotImplementedError("beam search is not used by the reference (num_beams=1)")
+    ids = input_ids if torch.is_tensor(input_ids) else torch.as_tensor(input_ids)
+    b, s = ids.shape
+    if gc.max_length is None:
+        gc.max_length = s + (gc.max_new_tokens if gc.max_new_tokens is not None else 20)
+    if gc.pad_token_id is None:
+        gc.pad_token_id = model.config.pad_token_id if model.config.pad_token_id >= 0 else 0
+    if gc.eos_token_id is None:
+        gc.eos_token_id = model.config.eos_token_id
+    if prng_key is not None:
+        gc.seed = int(prng_key) if not torch.is_tensor(prng_key) else int(prng_key.reshape(-1)[0])
+    if s >= gc.max_length:
+        return GenerateOutput(sequences=ids.to(model.device, torch.int32)[:, : gc.max_length])
+    eng = get_engine(model, b, gc.max_length)
+    seq = eng.run(ids, attention_mask if attention_mask is None or torch.is_tensor(attention_mask)
+                  else torch.as_tensor(attention_mask), gc)
+    return GenerateOutput(sequences=seq.clone())

@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Build the native extensions of jax_llama_amd IN-TREE (gfx950 only).
+
+  * ``jax_llama_amd/_C*.so``   — the HIP kernels (``csrc/kernels/*.hip``, hipcc
+    ``--offload-arch=gfx950``) + torch bindings (``csrc/bindings.cpp``);
+  * ``jax_llama_amd/_bpe*.so`` — the C++ byte-pair-merge core of the Llama-3 tokenizer;
+  * ``jax_llama_amd/_comm*.so`` — the xGMI custom all-reduce (``csrc/comm/*.hip``), if present.
+
+No hipify, no CUDA, no JIT cache: objects go to ``build/`` (incremental, mtime based) and the
+final ``.so`` files land next to the Python package so they travel with the repo snapshot.
+
+Usage: ``python build.py [-j N] [--force] [--only C|bpe|comm]``
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "jax_llama_amd"
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build"
+ARCH = "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX")
+
+
+def _torch_paths():
+    import torch
+    tdir = Path(torch.__file__).resolve().parent
+    inc = [tdir / "include", tdir / "include" / "torch" / "csrc" / "api" / "include"]
+    return tdir, inc, tdir / "lib"
+
+
+def _py_include():
+    return sysconfig.get_paths()["include"]
+
+
+def _pybind_include():
+    import pybind11
+    return pybind11.get_include()
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(map(str, cmd)) + "\n" + r.stdout)
+        raise SystemExit(f"build failed: {cmd[-1]}")
+    return r.stdout
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__"]
+
+
+def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):
+    if force or _stale(obj, [src, *headers]):
+        obj.parent.mkdir(parents=True, exist_ok=True)
+        _run([HIPCC, *HIP_FLAGS, *extra, "-c", str(src), "-o", str(obj)])
+        return True
+    return False
+
+
+def build_C(jobs: int, force: bool) -> Path:
+    tdir, tinc, tlib = _torch_paths()
+    kdir = CSRC / "kernels"
+    headers = sorted(kdir.glob("*.h"))
+    srcs = sorted(kdir.glob("*.hip"))
+    objs = [BUILD / "C" / (s.stem + ".o") for s in srcs]
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force), zip(srcs, objs)))
+    bsrc = CSRC / "bindings.cpp"
+    bobj = BUILD / "C" / "bindings.o"
+    if force or _stale(bobj, [bsrc, *headers]):
+        inc = [f"-I{p}" for p in tinc] + [f"-I{_py_include()}", f"-I{CSRC}"]
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+              "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1",
+              "-Wno-deprecated-declarations", "-Wno-unused-result", *inc, "-c", str(bsrc), "-o", str(bobj)])
+    out = PKG / f"_C{EXT_SUFFIX}"
+    if force or _stale(out, [*objs, bobj]):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), str(bobj), "-o", str(out),
+              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+              "-lamdhip64", f"-Wl,-rpath,{tlib}"])
+    return out
+
+
+def build_bpe(force: bool) -> Path:
+    src = CSRC / "bpe" / "bpe.cpp"
+    out = PKG / f"_bpe{EXT_SUFFIX}"
+    if force or _stale(out, [src]):
+        _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{_pybind_include()}", f"-I{_py_include()}",
+              str(src), "-o", str(out)])
+    return out
+
+
+def build_comm(jobs: int, force: bool):
+    cdir = CSRC / "comm"
+    srcs = sorted(cdir.glob("*.hip")) if cdir.exists() else []
+    if not srcs:
+        return None
+    headers = sorted(cdir.glob("*.h")) + sorted((CSRC / "kernels").glob("*.h"))
+    objs = [BUILD / "comm" / (s.stem + ".o") for s in srcs]
+    for s, o in zip(srcs, objs):
+        _compile_hip(s, o, headers, force)
+    bsrc = cdir / "bindings.cpp"
+    tdir, tinc, tlib = _torch_paths()
+    bobj = BUILD / "comm" / "bindings.o"
+    if force or _stale(bobj, [bsrc, *headers]):
+        inc = [f"-I{p}" for p in tinc] + [f"-I{_py_include()}", f"-I{CSRC}"]
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+              "-DTORCH_EXTENSION_NAME=_comm", "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1",
+              "-Wno-deprecated-declarations", *inc, "-c", str(bsrc), "-o", str(bobj)])
+    out = PKG / f"_comm{EXT_SUFFIX}"
+    if force or _stale(out, [*objs, bobj]):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), str(bobj), "-o", str(out),
+              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+              "-lamdhip64", f"-Wl,-rpath,{tlib}"])
+    return out
+
+
+def build_all(jobs: int = 8, force: bool = False, only=None):
+    outs = []
+    if only in (None, "bpe"):
+        outs.append(build_bpe(force))
+    if only in (None, "C"):
+        outs.append(build_C(jobs, force))
+    if only in (None, "comm"):
+        o = build_comm(jobs, force)
+        if o is not None:
+            outs.append(o)
+    return outs
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", choices=["C", "bpe", "comm"])
+    a = ap.parse_args()
+    for o in build_all(a.j, a.force, a.only):
+        print("built", o.relative_to(ROOT))

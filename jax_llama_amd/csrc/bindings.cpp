@@ -1,0 +1,225 @@
+// Python bindings of the gfx950 kernels (module jax_llama_amd._C).
+//
+// Thin: validate dtypes/shapes/contiguity on the host (a wrong shape must never reach a kernel),
+// take raw pointers and launch on torch's current HIP stream (so hipGraph capture through
+// torch.cuda.graph records these launches). Kernel code lives in csrc/kernels/*.hip.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include "kernels/launchers.h"
+
+namespace {
+
+using torch::Tensor;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(bool cond, const char* msg) { TORCH_CHECK(cond, "jax_llama_amd._C: ", msg); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "jax_llama_amd._C: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "jax_llama_amd._C: ", name, " must be contiguous");
+}
+
+void rc(int r, const char* what) {
+  TORCH_CHECK(r == 0, "jax_llama_amd._C: ", what, " failed (code ", r, ")");
+}
+
+template <typename T>
+T* ptr(const Tensor& t) {
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+const jla::bf16_t* cbf(const Tensor& t) { return reinterpret_cast<const jla::bf16_t*>(t.data_ptr()); }
+jla::bf16_t* bf(const Tensor& t) { return reinterpret_cast<jla::bf16_t*>(t.data_ptr()); }
+
+void embedding(Tensor ids, Tensor table, Tensor out) {
+  check_gpu(ids, "ids");
+  check_gpu(table, "table");
+  check_gpu(out, "out");
+  check(ids.scalar_type() == torch::kInt32 && table.scalar_type() == torch::kBFloat16 &&
+            out.scalar_type() == torch::kFloat32,
+        "embedding dtypes");
+  const int M = ids.numel(), D = table.size(1), V = table.size(0);
+  check(out.numel() == (int64_t)M * D, "embedding out shape");
+  rc(jla::embedding(ptr<int32_t>(ids), cbf(table), ptr<float>(out), M, D, V, stream()), "embedding");
+}
+
+void rms_scale(Tensor x, Tensor out, double eps) {
+  check_gpu(x, "x");
+  check_gpu(out, "out");
+  check(x.scalar_type() == torch::kFloat32 && out.scalar_type() == torch::kBFloat16, "rms_scale dtypes");
+  const int D = x.size(-1), M = x.numel() / D;
+  check(out.numel() == x.numel(), "rms_scale out shape");
+  rc(jla::rms_scale(ptr<float>(x), bf(out), M, D, (float)eps, stream()), "rms_scale");
+}
+
+void rmsnorm(Tensor x, Tensor w, Tensor out, double eps) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(out, "out");
+  check(x.scalar_type() == torch::kFloat32 && w.scalar_type() == torch::kFloat32 &&
+            out.scalar_type() == torch::kFloat32,
+        "rmsnorm dtypes");
+  const int D = x.size(-1), M = x.numel() / D;
+  check(w.numel() == D && out.numel() == x.numel(), "rmsnorm shapes");
+  rc(jla::rmsnorm(ptr<float>(x), ptr<float>(w), ptr<float>(out), M, D, (float)eps, stream()), "rmsnorm");
+}
+
+void check_packed(const Tensor& w, int64_t n, int64_t k) {
+  check_gpu(w, "weight");
+  check(w.scalar_type() == torch::kBFloat16, "weight must be bf16");
+  check(w.dim() == 4 && w.size(0) == n / 16 && w.size(1) == k / 32 && w.size(2) == 64 && w.size(3) == 8,
+        "weight must be fragment-packed [N/16, K/32, 64, 8]");
+}
+
+void check_linear_out(const Tensor& out, int64_t m, int64_t n, int64_t mode) {
+  check_gpu(out, "out");
+  const int64_t ncols = (mode == 2) ? n / 2 : n;
+  check(out.numel() == m * ncols, "linear out shape");
+  if (mode == 1) check(out.scalar_type() == torch::kFloat32, "residual must be fp32");
+  if (mode == 2) check(out.scalar_type() == torch::kBFloat16, "swiglu out must be bf16");
+  if (mode == 0)
+    check(out.scalar_type() == torch::kBFloat16 || out.scalar_type() == torch::kFloat32, "out must be bf16/fp32");
+}
+
+void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, double rms_eps,
+                   bool accumulate) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
+  check(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16, "x must be fp32/bf16");
+  const int64_t m = x.size(0);
+  check(m <= SKINNY_MAX_M, "linear_skinny: M too large");
+  check_linear_out(out, m, n, mode);
+  rc(jla::linear_skinny(x.data_ptr(), x.scalar_type() == torch::kFloat32, w.data_ptr(), out.data_ptr(), m, n, k,
+                        mode, (float)rms_eps, accumulate, out.scalar_type() == torch::kFloat32, stream()),
+     "linear_skinny");
+}
+
+void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
+  const int64_t m = x.size(0);
+  check_linear_out(out, m, n, mode);
+  rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
+               out.scalar_type() == torch::kFloat32, stream()),
+     "gemm");
+}
+
+void rope_kv_write(Tensor qkv, Tensor table, Tensor positions, Tensor kc, Tensor vc, Tensor slot, int64_t seq_len,
+                   int64_t h, int64_t hkv, int64_t dh, Tensor q) {
+  for (auto* t : {&qkv, &table, &positions, &kc, &vc, &slot, &q}) check_gpu(*t, "rope_kv_write arg");
+  check(qkv.scalar_type() == torch::kBFloat16 && kc.scalar_type() == torch::kBFloat16 &&
+            vc.scalar_type() == torch::kBFloat16 && q.scalar_type() == torch::kBFloat16,
+        "rope_kv_write bf16 tensors");
+  check(table.scalar_type() == torch::kFloat32 && table.dim() == 3 && table.size(1) == dh / 2 && table.size(2) == 2,
+        "rope table must be fp32 [L, Dh/2, 2]");
+  check(positions.scalar_type() == torch::kInt32 && slot.scalar_type() == torch::kInt32, "int32 positions/slot");
+  const int64_t m = qkv.size(0);
+  check(qkv.dim() == 2 && qkv.size(1) == (h + 2 * hkv) * dh, "qkv shape");
+  check(positions.numel() == m && m % seq_len == 0, "positions shape");
+  const int64_t b = m / seq_len;
+  check(kc.dim() == 4 && kc.size(0) == b && kc.size(1) == hkv && kc.size(3) == dh && vc.sizes() == kc.sizes(),
+        "cache shape [B, Hkv, T, Dh]");
+  check(q.numel() == m * h * dh, "q out shape");
+  rc(jla::rope_kv_write(cbf(qkv), ptr<float>(table), table.size(0), ptr<int32_t>(positions), bf(kc), bf(vc),
+                        ptr<int32_t>(slot), m, seq_len, h, hkv, dh, kc.size(2), bf(q), stream()),
+     "rope_kv_write");
+}
+
+void check_attn(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tensor& slot, const Tensor& kv_start,
+                const c10::optional<Tensor>& key_mask, const Tensor& out) {
+  for (auto* t : {&q, &kc, &vc, &slot, &kv_start, &out}) check_gpu(*t, "attention arg");
+  check(q.scalar_type() == torch::kBFloat16 && kc.scalar_type() == torch::kBFloat16 &&
+            vc.scalar_type() == torch::kBFloat16 && out.scalar_type() == torch::kBFloat16,
+        "attention bf16 tensors");
+  check(q.dim() == 4 && kc.dim() == 4 && kc.sizes() == vc.sizes(), "attention shapes");
+  check(kc.size(0) == q.size(0) && kc.size(3) == q.size(3), "cache/q shape mismatch");
+  check(q.size(2) % kc.size(1) == 0, "H must be a multiple of Hkv");
+  check(slot.scalar_type() == torch::kInt32 && kv_start.scalar_type() == torch::kInt32 &&
+            kv_start.numel() == q.size(0),
+        "slot/kv_start");
+  check(out.numel() == q.numel(), "attention out shape");
+  if (key_mask.has_value()) {
+    check_gpu(*key_mask, "key_mask");
+    check(key_mask->scalar_type() == torch::kUInt8 && key_mask->dim() == 2 && key_mask->size(0) == q.size(0),
+          "key_mask must be uint8 [B, L]");
+  }
+}
+
+void attn_decode(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c10::optional<Tensor> key_mask,
+                 Tensor out, Tensor ws, int64_t t_cap, int64_t nsplit) {
+  check_attn(q, kc, vc, slot, kv_start, key_mask, out);
+  check(q.size(1) == 1, "attn_decode: one query per row");
+  const int64_t b = q.size(0), h = q.size(2), dh = q.size(3), hkv = kc.size(1), T = kc.size(2);
+  check(t_cap <= T, "t_cap exceeds the cache length");
+  check_gpu(ws, "ws");
+  check(ws.scalar_type() == torch::kFloat32 && ws.numel() >= b * h * nsplit * (dh + 2), "workspace too small");
+  const uint8_t* km = key_mask.has_value() ? ptr<uint8_t>(*key_mask) : nullptr;
+  const int ml = key_mask.has_value() ? key_mask->size(1) : 0;
+  rc(jla::attn_decode(cbf(q), cbf(kc), cbf(vc), ptr<int32_t>(slot), ptr<int32_t>(kv_start), km, ml, bf(out),
+                      ptr<float>(ws), b, h, hkv, dh, T, t_cap, nsplit, stream()),
+     "attn_decode");
+}
+
+void attn_prefill(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c10::optional<Tensor> key_mask,
+                  Tensor out) {
+  check_attn(q, kc, vc, slot, kv_start, key_mask, out);
+  const uint8_t* km = key_mask.has_value() ? ptr<uint8_t>(*key_mask) : nullptr;
+  const int ml = key_mask.has_value() ? key_mask->size(1) : 0;
+  rc(jla::attn_prefill(cbf(q), cbf(kc), cbf(vc), ptr<int32_t>(slot), ptr<int32_t>(kv_start), km, ml, bf(out),
+                       q.size(0), q.size(1), q.size(2), kc.size(1), q.size(3), kc.size(2), stream()),
+     "attn_prefill");
+}
+
+void argmax(Tensor logits, Tensor idx, Tensor val) {
+  check_gpu(logits, "logits");
+  check_gpu(idx, "idx");
+  check_gpu(val, "val");
+  check(logits.scalar_type() == torch::kFloat32 && logits.dim() == 2, "logits must be fp32 [B, V]");
+  check(idx.scalar_type() == torch::kInt32 && val.scalar_type() == torch::kFloat32 &&
+            idx.numel() == logits.size(0) && val.numel() == logits.size(0),
+        "argmax outputs");
+  rc(jla::argmax(ptr<float>(logits), logits.size(0), logits.size(1), ptr<int32_t>(idx), ptr<float>(val), stream()),
+     "argmax");
+}
+
+void decode_update(Tensor nxt, Tensor finished, Tensor sequences, Tensor cur_len, Tensor tokens, Tensor positions,
+                   Tensor slot, int64_t pad, int64_t eos) {
+  for (auto* t : {&nxt, &finished, &sequences, &cur_len, &tokens, &positions, &slot}) {
+    check_gpu(*t, "decode_update arg");
+    check(t->scalar_type() == torch::kInt32, "decode_update: int32 tensors");
+  }
+  const int64_t b = nxt.numel();
+  check(finished.numel() == b && tokens.numel() == b && positions.numel() == b && sequences.dim() == 2 &&
+            sequences.size(0) == b,
+        "decode_update shapes");
+  rc(jla::decode_update(ptr<int32_t>(nxt), ptr<int32_t>(finished), ptr<int32_t>(sequences), ptr<int32_t>(cur_len),
+                        ptr<int32_t>(tokens), ptr<int32_t>(positions), ptr<int32_t>(slot), b, sequences.size(1), pad,
+                        eos, stream()),
+     "decode_update");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "jax_llama_amd gfx950 (MI355X) HIP kernels";
+  m.attr("SKINNY_MAX_M") = SKINNY_MAX_M;
+  m.attr("ARCH") = "gfx950";
+  m.def("embedding", &embedding);
+  m.def("rms_scale", &rms_scale);
+  m.def("rmsnorm", &rmsnorm);
+  m.def("linear_skinny", &linear_skinny);
+  m.def("gemm", &gemm);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("attn_decode_splits", [](int64_t b, int64_t hkv, int64_t t) { return jla::attn_decode_splits(b, hkv, t); });
+  m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
+        py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("t_cap"),
+        py::arg("nsplit"));
+  m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
+        py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));
+  m.def("argmax", &argmax);
+  m.def("decode_update", &decode_update);
+}

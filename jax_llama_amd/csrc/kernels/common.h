@@ -1,0 +1,96 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels of jax_llama_amd.
+//
+// Conventions
+//  * bf16 is carried as raw uint16_t (``bf16_t``) and converted with explicit round-to-nearest-even,
+//    matching torch's float->bfloat16 cast bit for bit (the CPU reference path relies on this).
+//  * Linear weights use the MFMA fragment-packed layout (see ops/reference.py: pack_frag16x32):
+//        P[nt][ks][lane][e] = W[16*nt + (lane & 15)][32*ks + 8*(lane >> 4) + e]
+//    so one 16(n) x 32(k) block is the B operand of one v_mfma_f32_16x16x32_bf16 and one 1 KiB
+//    contiguous run that a wave fetches with a single global_load_dwordx4 per lane.
+//  * Waves are 64 lanes. Block sizes are multiples of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Linear epilogue modes (mirrors ops/__init__.py)
+#define MODE_STORE 0
+#define MODE_RESIDUAL 1
+#define MODE_SWIGLU 2
+
+#define JLA_DEV __device__ __forceinline__
+
+JLA_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+JLA_DEV bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+JLA_DEV uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// unpack the 8 bf16 of a 16-byte vector into floats
+JLA_DEV void unpack8(const u32x4 v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+
+JLA_DEV u32x4 pack8(const float* f) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack2bf(f[2 * i], f[2 * i + 1]);
+  return r;
+}
+
+JLA_DEV f32x4 mfma16x16x32(const u32x4 a, const u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+// Non-temporal 16-byte load for once-read streams (decode weights).
+JLA_DEV u32x4 load_nt(const u32x4* p) { return __builtin_nontemporal_load(p); }
+
+JLA_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+JLA_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `red` must hold >= 16 floats. All threads get the result.
+JLA_DEV float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+JLA_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
+
+// Host-side error check used by every launcher.
+#define JLA_CHECK_LAUNCH()                                                        \
+  do {                                                                            \
+    hipError_t e__ = hipGetLastError();                                           \
+    if (e__ != hipSuccess) return (int)e__;                                       \
+  } while (0)

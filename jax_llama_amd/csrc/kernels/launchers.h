@@ -1,0 +1,37 @@
+// Host launchers of the gfx950 kernels (pure HIP translation units; no torch headers).
+// Every launcher returns 0 on success, <0 on a shape/argument error, >0 for a hipError_t.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SKINNY_MAX_M 64
+
+namespace jla {
+typedef uint16_t bf16_t;
+
+int embedding(const int32_t* ids, const bf16_t* table, float* out, int M, int D, int V, hipStream_t s);
+int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
+int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
+
+int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
+                  float rms_eps, int accumulate, int out_f32, hipStream_t s);
+int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
+         hipStream_t s);
+
+int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
+                  bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,
+                  hipStream_t s);
+
+int attn_decode_chunk(int B, int Hkv, int T);
+int attn_decode_splits(int B, int Hkv, int T);
+int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
+                const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int B, int H, int Hkv, int Dh, int T,
+                int t_cap, int nsplit, hipStream_t s);
+int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
+                 const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,
+                 hipStream_t s);
+
+int argmax(const float* logits, int B, int V, int32_t* idx, float* val, hipStream_t s);
+int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,
+                  int32_t* positions, int32_t* slot, int B, int L, int pad, int eos, hipStream_t s);
+}  // namespace jla

@@ -1,0 +1,83 @@
+// Embedding gather and RMSNorm kernels (reference: model.py:28-48 RMSNorm, :611-617 wte).
+//
+// The residual stream is fp32 [M, D]. RMSNorm weights are folded into the next projection at load
+// time, so the decode path never runs these norm kernels: the skinny GEMM computes inv_rms in its
+// own K loop. These kernels serve the prefill path (rms_scale -> bf16 GEMM operand), the final
+// norm of hidden-state outputs, and the embedding lookup.
+#include "common.h"
+#include "launchers.h"
+
+namespace jla {
+
+// one block per row; 16-byte vectorised bf16 loads, fp32 stores
+__global__ void __launch_bounds__(256) embedding_kernel(const int32_t* __restrict__ ids,
+                                                        const bf16_t* __restrict__ table,
+                                                        float* __restrict__ out, int D, int V) {
+  const int row = blockIdx.x;
+  int id = ids[row];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * D);
+  float4* dst = reinterpret_cast<float4*>(out + (size_t)row * D);
+  for (int i = threadIdx.x; i < D / 8; i += blockDim.x) {
+    float f[8];
+    unpack8(src[i], f);
+    dst[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    dst[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+}
+
+int embedding(const int32_t* ids, const bf16_t* table, float* out, int M, int D, int V, hipStream_t s) {
+  if (D % 8) return -1;
+  if (M == 0) return 0;
+  embedding_kernel<<<M, 256, 0, s>>>(ids, table, out, D, V);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
+// out_bf16[m, :] = bf16(x[m, :] * rsqrt(mean(x^2) + eps)); optional weight (fp32) -> fp32 out.
+template <bool WEIGHTED>
+__global__ void __launch_bounds__(256) rms_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                  void* __restrict__ out, int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const float4* xr = reinterpret_cast<const float4*>(x + (size_t)row * D);
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < D / 4; i += blockDim.x) {
+    float4 v = xr[i];
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  if (WEIGHTED) {
+    float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + (size_t)row * D);
+    const float4* wr = reinterpret_cast<const float4*>(w);
+    for (int i = threadIdx.x; i < D / 4; i += blockDim.x) {
+      float4 v = xr[i], g = wr[i];
+      o[i] = make_float4(v.x * inv * g.x, v.y * inv * g.y, v.z * inv * g.z, v.w * inv * g.w);
+    }
+  } else {
+    uint2* o = reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + (size_t)row * D);
+    for (int i = threadIdx.x; i < D / 4; i += blockDim.x) {
+      float4 v = xr[i];
+      o[i] = make_uint2(pack2bf(v.x * inv, v.y * inv), pack2bf(v.z * inv, v.w * inv));
+    }
+  }
+}
+
+int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s) {
+  if (D % 4) return -1;
+  if (M == 0) return 0;
+  rms_kernel<false><<<M, 256, 0, s>>>(x, nullptr, out, D, eps);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
+int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s) {
+  if (D % 4) return -1;
+  if (M == 0) return 0;
+  rms_kernel<true><<<M, 256, 0, s>>>(x, w, out, D, eps);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace jla

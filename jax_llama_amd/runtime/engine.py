@@ -197,6 +197,11 @@ class DecodeEngine:
         self.cache.index = s  # host mirror (decode steps track the slot on the device)
         return s + 1
 
+    def prefill_only(self, input_ids, attention_mask, gc: GenerationConfig) -> int:
+        """Prefill + first token only (time-to-first-token measurement)."""
+        self.gc = gc
+        return self.prefill(input_ids, attention_mask)
+
     def _ensure_graph(self):
         key = (self.gc.do_sample, self.key_mask is not None)
         if self._graph is not None and self._graph_key == key:

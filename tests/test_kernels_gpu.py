@@ -1,0 +1,186 @@
+"""Numerics of every gfx950 HIP kernel against the pure-PyTorch fp32 reference of the same op
+(``jax_llama_amd/ops/reference.py``). GPU-only (``-m gpu``); the HIP path must be the one that runs:
+``ops._ext.ext()`` raises if the extension is missing, it never falls back."""
+from __future__ import annotations
+
+import math
+
+import pytest
+import torch
+
+from jax_llama_amd import ops
+from jax_llama_amd.models.weights import PackedLinear
+from jax_llama_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF16 = torch.bfloat16
+
+
+def _close(a, b, rtol, atol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item()
+    assert err <= atol + rtol * scale, f"max err {err:.3e} (ref max {scale:.3e})"
+
+
+def test_extension_loaded():
+    e = ops.ext()
+    assert e.ARCH == "gfx950"
+    assert e.__file__.startswith(__import__("os").path.dirname(__import__("jax_llama_amd").__file__))
+
+
+def test_embedding():
+    table = torch.randn(1000, 256, dtype=BF16)
+    ids = torch.randint(0, 1000, (37,), dtype=torch.int32)
+    out = ops.embedding(ids.to(DEV), table.to(DEV))
+    torch.testing.assert_close(out.cpu(), ref.embedding(ids, table), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("m,d", [(1, 4096), (7, 256), (130, 8192)])
+def test_rms(m, d):
+    x = torch.randn(m, d) * 3
+    w = torch.randn(d)
+    out = ops.rms_scale(x.to(DEV), 1e-5)
+    _close(out, ref.rms_scale(x, 1e-5), 1e-2, 1e-2)
+    out2 = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-5)
+    _close(out2, ref.rmsnorm(x, w, 1e-5), 1e-5, 1e-4)
+
+
+def _mk_linear(n, k, fold=None):
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    return w, PackedLinear.from_dense(w, DEV, fold=fold), PackedLinear.from_dense(w, "cpu", fold=fold)
+
+
+def test_pack_roundtrip():
+    w = torch.randn(64, 96).to(BF16)
+    p = ref.pack_frag16x32(w)
+    torch.testing.assert_close(ref.unpack_frag16x32(p, 64, 96), w, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("m", [1, 5, 16, 17, 33, 64])
+@pytest.mark.parametrize("n,k", [(256, 512), (48, 4096), (4096, 224)])
+@pytest.mark.parametrize("rms", [False, True])
+def test_linear_store(m, n, k, rms):
+    x = torch.randn(m, k) * 2
+    w, pg, pc = _mk_linear(n, k)
+    eps = 1e-5 if rms else None
+    y = ops.linear(x.to(DEV), pg, rms_eps=eps)
+    _close(y, ops.linear(x, pc, rms_eps=eps), 2e-2, 2e-2)
+    y32 = ops.linear(x.to(DEV), pg, rms_eps=eps, out_dtype=torch.float32)
+    _close(y32, ref.linear(x, w, eps, torch.float32), 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("m", [1, 16, 64, 65, 200])
+def test_linear_residual_and_bf16_input(m):
+    k, n = 1024, 512
+    x = (torch.randn(m, k)).to(BF16)
+    w, pg, pc = _mk_linear(n, k)
+    h = torch.randn(m, n)
+    hg = h.to(DEV)
+    ops.linear_residual(x.to(DEV), pg, hg)
+    _close(hg, ref.linear_residual(x, w, h.clone()), 1e-2, 1e-3)
+    hg2 = h.to(DEV)
+    ops.linear_residual(x.to(DEV), pg, hg2, accumulate=False)
+    _close(hg2, ref.linear_residual(x, w, h.clone(), accumulate=False), 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("m", [1, 3, 16, 40, 64, 100, 257])
+@pytest.mark.parametrize("k", [512, 1376])
+def test_linear_swiglu(m, k):
+    f = 352
+    w1 = (torch.randn(f, k) * 0.05).to(BF16)
+    w3 = (torch.randn(f, k) * 0.05).to(BF16)
+    gu = ref.interleave_gate_up(w1, w3)
+    x = torch.randn(m, k)
+    pg = PackedLinear.from_dense(gu, DEV)
+    y = ops.linear_swiglu(x.to(DEV), pg, rms_eps=1e-5)
+    g = ref.linear(x, w1, 1e-5, torch.float32)
+    u = ref.linear(x, w3, 1e-5, torch.float32)
+    expect = torch.nn.functional.silu(g) * u
+    _close(y, expect, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (300, 6144 // 8, 4096 // 8), (129, 1040, 96)])
+def test_gemm_large_m(m, n, k):
+    x = torch.randn(m, k)
+    w, pg, pc = _mk_linear(n, k)
+    y = ops.linear(x.to(DEV), pg, rms_eps=1e-6, out_dtype=torch.float32)
+    xs = ref.rms_scale(x, 1e-6)
+    expect = xs.float() @ w.float().t()
+    _close(y, expect, 1e-2, 1e-3)
+
+
+def test_rope_kv_write():
+    b, s, h, hkv, dh, t = 3, 5, 8, 2, 128, 16
+    qkv = torch.randn(b * s, (h + 2 * hkv) * dh).to(BF16)
+    table = ref.rope_table(dh, 64, 10000.0)
+    pos = torch.randint(-1, 40, (b * s,), dtype=torch.int32)
+    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+    vc = torch.zeros_like(kc)
+    q = ref.rope_kv_write(qkv, table, pos, kc, vc, 3, s, h, hkv, dh)
+    kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+    slot = torch.tensor([3], dtype=torch.int32, device=DEV)
+    qg = ops.rope_kv_write(qkv.to(DEV), table.to(DEV), pos.to(DEV), kg, vg, slot, s, h, hkv, dh)
+    _close(qg, q, 1e-2, 1e-2)
+    _close(kg, kc, 1e-2, 1e-2)
+    torch.testing.assert_close(vg.cpu(), vc, rtol=0, atol=0)
+
+
+def _cache(b, hkv, t, dh):
+    return (torch.randn(b, hkv, t, dh) * 0.5).to(BF16), torch.randn(b, hkv, t, dh).to(BF16)
+
+
+@pytest.mark.parametrize("rep", [1, 2, 4, 8])
+@pytest.mark.parametrize("t,slot", [(40, 17), (300, 299), (1030, 700)])
+def test_attention_decode(rep, t, slot):
+    b, hkv, dh = 3, 2, 128
+    h = hkv * rep
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, 1, h, dh).to(BF16)
+    kv_start = torch.tensor([0, 5, slot + 1], dtype=torch.int32)  # last row: no valid key -> zeros
+    expect = ref.attention(q, kc, vc, slot, kv_start).reshape(b, h * dh)
+    got = ops.attention(q.to(DEV), kc.to(DEV), vc.to(DEV), torch.tensor([slot], dtype=torch.int32, device=DEV),
+                        kv_start.to(DEV))
+    _close(got, expect, 2e-2, 2e-2)
+    assert torch.isfinite(got.float()).all()
+    assert got[2].float().abs().max().item() == 0.0
+
+
+def test_attention_decode_key_mask():
+    b, hkv, rep, t, dh, slot = 2, 2, 4, 96, 128, 80
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, 1, hkv * rep, dh).to(BF16)
+    mask = (torch.rand(b, t) > 0.3).to(torch.uint8)
+    mask[:, slot] = 1
+    kv_start = torch.zeros(b, dtype=torch.int32)
+    expect = ref.attention(q, kc, vc, slot, kv_start, mask).reshape(b, -1)
+    got = ops.attention(q.to(DEV), kc.to(DEV), vc.to(DEV), torch.tensor([slot], dtype=torch.int32, device=DEV),
+                        kv_start.to(DEV), mask.to(DEV))
+    _close(got, expect, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("rep", [1, 4])
+@pytest.mark.parametrize("s,slot0", [(7, 0), (64, 0), (130, 10)])
+def test_attention_prefill(rep, s, slot0):
+    b, hkv, dh = 2, 2, 128
+    h = hkv * rep
+    t = slot0 + s + 3
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, s, h, dh).to(BF16)
+    kv_start = torch.tensor([0, min(slot0 + 4, slot0 + s - 1)], dtype=torch.int32)
+    expect = ref.attention(q, kc, vc, slot0, kv_start).reshape(b * s, h * dh)
+    got = ops.attention(q.to(DEV), kc.to(DEV), vc.to(DEV), torch.tensor([slot0], dtype=torch.int32, device=DEV),
+                        kv_start.to(DEV))
+    _close(got, expect, 2e-2, 2e-2)
+    assert torch.isfinite(got.float()).all()
+
+
+def test_argmax_first_index():
+    x = torch.randn(4, 128256)
+    x[1, 77] = 100.0
+    x[1, 9000] = 100.0  # tie: first index wins
+    idx, val = ops.argmax(x.to(DEV))
+    assert idx.cpu().tolist() == x.argmax(-1).tolist()
+    assert idx[1].item() == 77
+    torch.testing.assert_close(val.cpu(), x.max(-1).values)

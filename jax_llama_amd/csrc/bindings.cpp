@@ -8,6 +8,8 @@
 
 #include "kernels/launchers.h"
 
+#define MODE_QKV_ID 3
+
 namespace {
 
 using torch::Tensor;
@@ -84,17 +86,59 @@ void check_linear_out(const Tensor& out, int64_t m, int64_t n, int64_t mode) {
 }
 
 void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, double rms_eps,
-                   bool accumulate) {
+                   bool accumulate, int64_t variant) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
   check(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16, "x must be fp32/bf16");
+  check(mode >= 0 && mode <= 2, "linear_skinny mode");
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_skinny: M too large");
   check_linear_out(out, m, n, mode);
   rc(jla::linear_skinny(x.data_ptr(), x.scalar_type() == torch::kFloat32, w.data_ptr(), out.data_ptr(), m, n, k,
-                        mode, (float)rms_eps, accumulate, out.scalar_type() == torch::kFloat32, stream()),
+                        mode, (float)rms_eps, accumulate, out.scalar_type() == torch::kFloat32, nullptr, variant,
+                        stream()),
      "linear_skinny");
+}
+
+// fused qkv projection + RoPE + KV-cache write (decode / small M)
+void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions, Tensor kc,
+                Tensor vc, Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q,
+                int64_t variant) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  for (auto* t : {&table, &positions, &kc, &vc, &slot, &q}) check_gpu(*t, "linear_qkv arg");
+  check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
+  check(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16, "x must be fp32/bf16");
+  const int64_t m = x.size(0);
+  check(m <= SKINNY_MAX_M, "linear_qkv: M too large");
+  check(n == (h + 2 * hkv) * dh && dh % 16 == 0, "qkv width");
+  check(table.scalar_type() == torch::kFloat32 && table.dim() == 3 && table.size(1) == dh / 2 && table.size(2) == 2,
+        "rope table must be fp32 [L, Dh/2, 2]");
+  check(positions.scalar_type() == torch::kInt32 && positions.numel() == m && slot.scalar_type() == torch::kInt32,
+        "positions/slot");
+  check(m % seq_len == 0, "M must be B * seq_len");
+  const int64_t b = m / seq_len;
+  check(kc.scalar_type() == torch::kBFloat16 && kc.dim() == 4 && kc.size(0) == b && kc.size(1) == hkv &&
+            kc.size(3) == dh && vc.sizes() == kc.sizes() && vc.scalar_type() == torch::kBFloat16,
+        "cache shape [B, Hkv, T, Dh]");
+  check(q.scalar_type() == torch::kBFloat16 && q.numel() == m * h * dh, "q out");
+  jla::QKVArgs qa;
+  qa.table = reinterpret_cast<const float2*>(table.data_ptr());
+  qa.table_len = table.size(0);
+  qa.positions = ptr<int32_t>(positions);
+  qa.kc = bf(kc);
+  qa.vc = bf(vc);
+  qa.slot = ptr<int32_t>(slot);
+  qa.S = seq_len;
+  qa.H = h;
+  qa.Hkv = hkv;
+  qa.Dh = dh;
+  qa.T = kc.size(2);
+  qa.q = bf(q);
+  rc(jla::linear_skinny(x.data_ptr(), x.scalar_type() == torch::kFloat32, w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID,
+                        (float)rms_eps, 0, 0, &qa, variant, stream()),
+     "linear_qkv");
 }
 
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate) {
@@ -150,17 +194,19 @@ void check_attn(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tenso
 }
 
 void attn_decode(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c10::optional<Tensor> key_mask,
-                 Tensor out, Tensor ws, int64_t t_cap, int64_t nsplit) {
+                 Tensor out, Tensor ws, Tensor tickets, int64_t t_cap, int64_t nsplit) {
   check_attn(q, kc, vc, slot, kv_start, key_mask, out);
   check(q.size(1) == 1, "attn_decode: one query per row");
   const int64_t b = q.size(0), h = q.size(2), dh = q.size(3), hkv = kc.size(1), T = kc.size(2);
   check(t_cap <= T, "t_cap exceeds the cache length");
   check_gpu(ws, "ws");
+  check_gpu(tickets, "tickets");
   check(ws.scalar_type() == torch::kFloat32 && ws.numel() >= b * h * nsplit * (dh + 2), "workspace too small");
+  check(tickets.scalar_type() == torch::kInt32 && tickets.numel() >= b * hkv, "tickets too small");
   const uint8_t* km = key_mask.has_value() ? ptr<uint8_t>(*key_mask) : nullptr;
   const int ml = key_mask.has_value() ? key_mask->size(1) : 0;
   rc(jla::attn_decode(cbf(q), cbf(kc), cbf(vc), ptr<int32_t>(slot), ptr<int32_t>(kv_start), km, ml, bf(out),
-                      ptr<float>(ws), b, h, hkv, dh, T, t_cap, nsplit, stream()),
+                      ptr<float>(ws), ptr<int32_t>(tickets), b, h, hkv, dh, T, t_cap, nsplit, stream()),
      "attn_decode");
 }
 
@@ -214,9 +260,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_skinny", &linear_skinny);
   m.def("gemm", &gemm);
   m.def("rope_kv_write", &rope_kv_write);
-  m.def("attn_decode_splits", [](int64_t b, int64_t hkv, int64_t t) { return jla::attn_decode_splits(b, hkv, t); });
+  m.def("attn_decode_splits",
+        [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });
+  m.def("linear_qkv", &linear_qkv);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
-        py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("t_cap"),
+        py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
         py::arg("nsplit"));
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));

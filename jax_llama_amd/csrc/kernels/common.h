@@ -22,6 +22,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define MODE_STORE 0
 #define MODE_RESIDUAL 1
 #define MODE_SWIGLU 2
+#define MODE_QKV 3
 
 #define JLA_DEV __device__ __forceinline__
 

@@ -1,93 +1,136 @@
 // Skinny (decode) linear layer: y[M, N] = epilogue( [inv_rms(x) *] x[M, K] @ W[N, K]^T ), M <= 64.
 //
 // Reference ops: every nn.Dense of model.py (wq/wk/wv :210, wo :294, w1/w3/w2 :338, lm_head :736)
-// plus the RMSNorm that precedes qkv / w1|w3 / lm_head (model.py:384, :395, :662) and the residual
-// adds (:392, :398).
+// plus the RMSNorm that precedes qkv / w1|w3 / lm_head (model.py:384, :395, :662), the residual
+// adds (:392, :398), and -- for the fused qkv projection -- RoPE + the KV-cache write
+// (apply_rotary_emb :58-92, _concatenate_to_cache :169-199).
 //
 // Decode is HBM-bound on the weight stream (batch 1..64 rows), so the kernel is organised around
 // streaming the packed weights exactly once at full bandwidth:
-//   * one workgroup = NT consecutive 16-column n-tiles x the WHOLE K, split across NW = 8 waves
-//     (intra-workgroup split-K: wave w takes k-steps w, w+8, w+16, ... so the 8 waves of a
-//     workgroup fetch 8 consecutive KiB of the n-tile's contiguous packed block at a time);
-//   * each k-step is one 1 KiB non-temporal global_load_dwordx4 per n-tile (the B operand of
-//     v_mfma_f32_16x16x32_bf16 as-is) plus the 16(m) x 32(k) activation fragment, read straight
-//     from the L2-resident x (fp32 residual stream converted to bf16 in registers);
+//   * one workgroup = NT consecutive 16-column n-tiles x the WHOLE K, split across NW waves
+//     (intra-workgroup split-K: wave w takes k-steps w, w+NW, ... so the waves of a workgroup
+//     fetch consecutive KiB of the n-tile's contiguous packed block);
+//   * each k-step is one 1 KiB non-temporal global_load_dwordx4 per n-tile (already the B operand
+//     of v_mfma_f32_16x16x32_bf16) plus the 16(m) x 32(k) activation fragment (L2-resident x);
+//   * the main loop is a rolling register pipeline: U slots, each slot refilled with the k-step
+//     U ahead right after its MFMA, so every wave keeps U KiB (x NT) in flight at all times with
+//     no branches and no vmcnt(0) (past-the-end refills read a zero fragment: MFMA adds 0);
 //   * MT = ceil(M/16) m-tiles reuse each weight fragment (M <= 16 costs the same as M = 1);
-//   * the sum of squares for RMSNorm is accumulated from the same activation loads (every x element
-//     is loaded exactly once per workgroup), so the norm costs no extra pass and no extra launch;
-//   * the 8 partial accumulators are reduced through LDS and a fused epilogue applies the norm scale
-//     and stores bf16/fp32, accumulates into the fp32 residual stream, or applies SiLU(gate)*up for
-//     the interleaved [w1;w3] weight (gate/up alternate in 16-row tiles so one workgroup owns both).
+//   * RMSNorm's sum of squares comes from the same activation loads (each x element is loaded
+//     exactly once per workgroup): no extra pass, no extra launch;
+//   * partial accumulators are reduced through LDS; the fused epilogue applies the norm scale and
+//     stores bf16/fp32, accumulates into the fp32 residual stream, applies SiLU(gate)*up over the
+//     interleaved [w1;w3] weight, or (QKV mode) rotates q/k pairs with RoPE and writes q plus the
+//     k/v cache rows at the device-side cache slot.
 // No atomics: results are deterministic and the residual add happens exactly once.
 #include "common.h"
 #include "launchers.h"
 
 namespace jla {
 
-constexpr int GEMV_NW = 8;  // waves per workgroup
+__device__ u32x4 g_zero_frag[64];  // 1 KiB of zeros (static storage is zero-initialised)
+
+// Loads of the main loop are issued as inline asm so the ring's waits are counted by hand:
+// hipcc's own waitcnt insertion drains the whole ring (vmcnt(0)) at the loop back-edge, which turns
+// the pipeline back into batches (checked in the .s). Each slot is waited with one counted
+// s_waitcnt vmcnt(L*(U-1)) and its registers are pinned behind that wait ("+v"), so no consumer
+// can read them early (cdna_hip_programming.md section 5.7, form (ii)).
+JLA_DEV u32x4 asm_load_nt(const void* p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+JLA_DEV u32x4 asm_load(const void* p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+JLA_DEV u32x4 asm_load16(const void* p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <int N>
+JLA_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+JLA_DEV void pin(u32x4& r) { asm volatile("" : "+v"(r)); }
 
 template <typename XT>
-struct XFrag;
+struct XRaw;
 
 template <>
-struct XFrag<float> {
-  // lane's 8 consecutive fp32 activations -> bf16 fragment; accumulate squares for RMSNorm
-  static JLA_DEV u32x4 load(const float* x, size_t off, float& ss) {
-    const float4* p = reinterpret_cast<const float4*>(x + off);
-    float4 a = p[0], b = p[1];
-    ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
+struct XRaw<float> {  // 8 fp32 activations per lane (two 16-byte loads)
+  static constexpr int LOADS = 2;
+  u32x4 a, b;
+  JLA_DEV void load(const float* p) {
+    a = asm_load(p);
+    b = asm_load16(p);
+  }
+  JLA_DEV void pin_regs() {
+    pin(a);
+    pin(b);
+  }
+  JLA_DEV u32x4 frag(float& ss) const {
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[i] = __uint_as_float(a[i]);
+      f[4 + i] = __uint_as_float(b[i]);
+    }
     u32x4 r;
-    r[0] = pack2bf(a.x, a.y);
-    r[1] = pack2bf(a.z, a.w);
-    r[2] = pack2bf(b.x, b.y);
-    r[3] = pack2bf(b.z, b.w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ss += f[2 * i] * f[2 * i] + f[2 * i + 1] * f[2 * i + 1];
+      r[i] = pack2bf(f[2 * i], f[2 * i + 1]);
+    }
     return r;
   }
 };
 
 template <>
-struct XFrag<bf16_t> {
-  static JLA_DEV u32x4 load(const bf16_t* x, size_t off, float& ss) {
-    u32x4 r = *reinterpret_cast<const u32x4*>(x + off);
+struct XRaw<bf16_t> {  // 8 bf16 activations per lane (one 16-byte load)
+  static constexpr int LOADS = 1;
+  u32x4 v;
+  JLA_DEV void load(const bf16_t* p) { v = asm_load(p); }
+  JLA_DEV void pin_regs() { pin(v); }
+  JLA_DEV u32x4 frag(float& ss) const {
     float f[8];
-    unpack8(r, f);
+    unpack8(v, f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) ss += f[i] * f[i];
-    return r;
+    return v;
   }
 };
 
-template <typename XT, int MT, int NT, int MODE>
-__global__ void __launch_bounds__(GEMV_NW * 64)
+template <typename XT, int MT, int NT, int MODE, int NW, int U>
+__global__ void __launch_bounds__(NW * 64)
     linear_skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out,
-                         int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32) {
-  // k-steps in flight per wave (8 KiB of weights at M <= 16); fp32 activations cost 2x the
-  // registers of bf16 ones, so fewer steps are kept in flight for MT > 1 to stay spill-free.
-  constexpr int U0 = (NT == 1) ? 8 : 4;
-  constexpr int UD = (sizeof(XT) == 4 && MT > 1) ? MT : 1;
-  constexpr int U = (U0 / UD) < 2 ? 2 : (U0 / UD);
+                         int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa) {
   extern __shared__ float smem[];
-  float* red = smem;                                    // [NW][MT][NT][64][4]
-  float* red_ss = red + GEMV_NW * MT * NT * 256;        // [NW][MT][16]
-  float* inv_rms = red_ss + GEMV_NW * MT * 16;          // [MT*16]
+  float* red = smem;                              // [NW][MT][NT][64][4]
+  float* red_ss = red + NW * MT * NT * 256;       // [NW][MT][16]
+  float* inv_rms = red_ss + NW * MT * 16;         // [MT*16]
 
   const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
   const int KS = K >> 5;
   const int NTT = N >> 4;
   const int nt0 = blockIdx.x * NT;
 
-  // clamp tiles of a ragged last workgroup (computed but not stored)
-  int ntile[NT];
+  const u32x4* wt[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) ntile[t] = min(nt0 + t, NTT - 1);
-
-  size_t xoff[MT];
+  for (int t = 0; t < NT; ++t) wt[t] = W + (size_t)min(nt0 + t, NTT - 1) * KS * 64 + lane;
+  const XT* xp[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    int row = min(mt * 16 + (lane & 15), M - 1);  // padding rows re-read the last row (not stored)
-    xoff[mt] = (size_t)row * K + 8 * (lane >> 4);
+    const int row = min(mt * 16 + (lane & 15), M - 1);  // padding rows re-read the last row (not stored)
+    xp[mt] = x + (size_t)row * K + 8 * (lane >> 4);
   }
+  const u32x4* zfrag = g_zero_frag + lane;
+  const XT* zx = reinterpret_cast<const XT*>(g_zero_frag);
+
+  const int n = (KS - w + NW - 1) / NW;  // k-steps of this wave: ks = w + i*NW, i < n
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -98,42 +141,38 @@ __global__ void __launch_bounds__(GEMV_NW * 64)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
 
-  const u32x4* wt[NT];
+  u32x4 bq[U][NT];
+  XRaw<XT> aq[U][MT];
+  constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
+  auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
+    const bool valid = i < n;
+    const size_t ks = (size_t)(w + i * NW);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) wt[t] = W + (size_t)ntile[t] * KS * 64 + lane;
-
-  int ks = w;
-  // main loop: U k-steps per iteration, all loads issued before the MFMAs
-  for (; ks + (U - 1) * GEMV_NW < KS; ks += U * GEMV_NW) {
-    u32x4 b[U][NT];
-    u32x4 a[U][MT];
+    for (int t = 0; t < NT; ++t) b[t] = asm_load_nt(valid ? (const void*)(wt[t] + ks * 64) : (const void*)zfrag);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int mt = 0; mt < MT; ++mt) a[mt].load(valid ? xp[mt] + ks * 32 : zx);
+  };
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b[u][t] = load_nt(wt[t] + (size_t)(ks + u * GEMV_NW) * 64);
+  for (int u = 0; u < U; ++u) issue(u, bq[u], aq[u]);
+  for (int i0 = 0; i0 < n; i0 += U) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      wait_vmcnt<L * (U - 1)>();  // slot u (the oldest L loads) has landed
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) a[u][mt] = XFrag<XT>::load(x, xoff[mt] + (size_t)(ks + u * GEMV_NW) * 32, ss[mt]);
+      for (int t = 0; t < NT; ++t) pin(bq[u][t]);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+      u32x4 af[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) af[mt] = aq[u][mt].frag(ss[mt]);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(a[u][mt], b[u][t], acc[mt][t]);
+        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(af[mt], bq[u][t], acc[mt][t]);
+      issue(i0 + U + u, bq[u], aq[u]);  // refill: k-step U ahead (zero fragment past the end)
+    }
   }
-  // remainder k-steps
-  for (; ks < KS; ks += GEMV_NW) {
-    u32x4 b[NT], a[MT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) b[t] = load_nt(wt[t] + (size_t)ks * 64);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt] = XFrag<XT>::load(x, xoff[mt] + (size_t)ks * 32, ss[mt]);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(a[mt], b[t], acc[mt][t]);
-  }
+  wait_vmcnt<0>();  // retire the past-the-end refills before the registers are reused
 
   // ---- cross-wave reduction through LDS
 #pragma unroll
@@ -155,112 +194,172 @@ __global__ void __launch_bounds__(GEMV_NW * 64)
     float r = 1.f;
     if (use_rms) {
       float s = 0.f;
-      for (int ww = 0; ww < GEMV_NW; ++ww) s += red_ss[ww * MT * 16 + threadIdx.x];
+      for (int ww = 0; ww < NW; ++ww) s += red_ss[ww * MT * 16 + threadIdx.x];
       r = rsqrtf(s / (float)K + eps);
     }
     inv_rms[threadIdx.x] = r;
   }
   __syncthreads();
 
+  auto reduced = [&](int mt, int t, int ln, int i) {
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) v += red[(((ww * MT + mt) * NT + t) * 64 + ln) * 4 + i];
+    return v;
+  };
+
   // ---- fused epilogue; c (column within the tile) is the fastest index -> 64 B row segments
-  if (MODE == MODE_SWIGLU) {
+  if constexpr (MODE == MODE_SWIGLU) {
     constexpr int NP = NT / 2;
     const int F = N >> 1;
     bf16_t* o = static_cast<bf16_t*>(out);
-    for (int e = threadIdx.x; e < MT * NP * 256; e += GEMV_NW * 64) {
+    for (int e = threadIdx.x; e < MT * NP * 256; e += NW * 64) {
       const int c = e & 15, ml = (e >> 4) & 15, p = (e >> 8) % NP, mt = e / (256 * NP);
       const int m = mt * 16 + ml;
       const int ln = (ml >> 2) * 16 + c, i = ml & 3;
-      float g = 0.f, u = 0.f;
-      for (int ww = 0; ww < GEMV_NW; ++ww) {
-        g += red[(((ww * MT + mt) * NT + 2 * p) * 64 + ln) * 4 + i];
-        u += red[(((ww * MT + mt) * NT + 2 * p + 1) * 64 + ln) * 4 + i];
-      }
       const int gtile = nt0 + 2 * p;
-      if (m < M && gtile + 1 < NTT + 1 && gtile < NTT) {
+      if (m < M && gtile < NTT) {
         const float sc = inv_rms[m];
-        g *= sc;
-        u *= sc;
+        const float g = reduced(mt, 2 * p, ln, i) * sc, u = reduced(mt, 2 * p + 1, ln, i) * sc;
         o[(size_t)m * F + (gtile >> 1) * 16 + c] = f2bf(silu(g) * u);
       }
     }
   } else {
-    for (int e = threadIdx.x; e < MT * NT * 256; e += GEMV_NW * 64) {
+    for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
       const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
       const int m = mt * 16 + ml;
       const int ln = (ml >> 2) * 16 + c, i = ml & 3;
-      float v = 0.f;
-      for (int ww = 0; ww < GEMV_NW; ++ww) v += red[(((ww * MT + mt) * NT + t) * 64 + ln) * 4 + i];
       const int tile = nt0 + t;
-      if (m < M && tile < NTT) {
-        v *= inv_rms[m];
-        const size_t idx = (size_t)m * N + tile * 16 + c;
-        if (MODE == MODE_RESIDUAL) {
+      if (m >= M || tile >= NTT) continue;
+      const float v = reduced(mt, t, ln, i) * inv_rms[m];
+      const int col = tile * 16 + c;
+      if constexpr (MODE == MODE_QKV) {
+        // column -> (head, d); RoPE pairs (d, d^1) are both in this 16-column tile
+        const int head = col / qa.Dh, d = col - head * qa.Dh;
+        const int b = m / qa.S, s = m - b * qa.S;
+        float r = v;
+        if (head < qa.H + qa.Hkv) {
+          const float pv = reduced(mt, t, ln ^ 1, i) * inv_rms[m];
+          int pos = qa.positions[m];
+          pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
+          const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d >> 1)];
+          r = (d & 1) ? (pv * cs.y + v * cs.x) : (v * cs.x - pv * cs.y);
+        }
+        if (head < qa.H) {
+          qa.q[((size_t)m * qa.H + head) * qa.Dh + d] = f2bf(r);
+        } else {
+          const int slot = qa.slot[0] + s;
+          if (slot < qa.T) {
+            const bool is_k = head < qa.H + qa.Hkv;
+            const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
+            bf16_t* cache = is_k ? qa.kc : qa.vc;
+            cache[(((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d] = f2bf(r);
+          }
+        }
+      } else {
+        const size_t idx = (size_t)m * N + col;
+        if constexpr (MODE == MODE_RESIDUAL) {
           float* o = static_cast<float*>(out);
           o[idx] = accumulate ? o[idx] + v : v;
-        } else if (out_f32) {
-          static_cast<float*>(out)[idx] = v;
         } else {
-          static_cast<bf16_t*>(out)[idx] = f2bf(v);
+          if (out_f32)
+            static_cast<float*>(out)[idx] = v;
+          else
+            static_cast<bf16_t*>(out)[idx] = f2bf(v);
         }
       }
     }
   }
 }
 
-template <typename XT, int MT, int NT, int MODE>
+template <typename XT, int MT, int NT, int MODE, int NW>
 static int launch_skinny(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
-                         int accumulate, int out_f32, hipStream_t s) {
+                         int accumulate, int out_f32, const QKVArgs& qa, hipStream_t s) {
+  // k-steps in flight per wave: 8 KiB of weights per wave at MT = 1; fp32 activations double the
+  // activation registers, so MT > 1 keeps fewer steps in flight to stay spill-free.
+  constexpr int U0 = (NT == 1) ? 8 : 4;
+  constexpr int UD = (sizeof(XT) == 4 && MT > 1) ? MT : (MT > 2 ? 2 : 1);
+  constexpr int U = (U0 / UD) < 2 ? 2 : (U0 / UD);
   const int NTT = N >> 4;
   const int grid = (NTT + NT - 1) / NT;
-  const size_t lds = sizeof(float) * (GEMV_NW * MT * NT * 256 + GEMV_NW * MT * 16 + MT * 16);
+  const size_t lds = sizeof(float) * (NW * MT * NT * 256 + NW * MT * 16 + MT * 16);
+  auto kern = &linear_skinny_kernel<XT, MT, NT, MODE, NW, U>;
   if (lds > 65536) {  // opt in to > 64 KiB of dynamic LDS once (not a stream op: capture-safe)
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&linear_skinny_kernel<XT, MT, NT, MODE>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
   }
-  linear_skinny_kernel<XT, MT, NT, MODE><<<grid, GEMV_NW * 64, lds, s>>>(
-      static_cast<const XT*>(x), static_cast<const u32x4*>(W), out, M, N, K, eps, use_rms, accumulate, out_f32);
+  kern<<<grid, NW * 64, lds, s>>>(static_cast<const XT*>(x), static_cast<const u32x4*>(W), out, M, N, K, eps,
+                                  use_rms, accumulate, out_f32, qa);
   JLA_CHECK_LAUNCH();
   return 0;
 }
 
+// waves per workgroup: more waves when there are few workgroups (small N) so every CU keeps
+// enough weight bytes in flight; variant (1: 4, 2: 8, 3: 16 waves) overrides for tuning.
+static int pick_nw(int ngroups, int variant) {
+  if (variant == 1) return 4;
+  if (variant == 2) return 8;
+  if (variant == 3) return 16;
+  return ngroups <= 512 ? 16 : 8;
+}
+
+template <typename XT, int MT, int NT, int MODE>
+static int dispatch_nw(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
+                       int accumulate, int out_f32, const QKVArgs& qa, int variant, hipStream_t s) {
+  const int ngroups = ((N >> 4) + NT - 1) / NT;
+  if constexpr (MT == 1) {
+    switch (pick_nw(ngroups, variant)) {
+      case 4: return launch_skinny<XT, MT, NT, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      case 16: return launch_skinny<XT, MT, NT, MODE, 16>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      default: break;
+    }
+  }
+  return launch_skinny<XT, MT, NT, MODE, 8>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+}
+
 template <typename XT, int MT, int MODE>
 static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
-                       int accumulate, int out_f32, hipStream_t s) {
-  const int NTT = N >> 4;
-  // one n-tile per workgroup unless that leaves > 2 workgroups per CU anyway; SwiGLU needs the
-  // gate/up tile pair in one workgroup.
-  if (MODE == MODE_SWIGLU || NTT >= 1024)
-    return launch_skinny<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, s);
-  return launch_skinny<XT, MT, (MODE == MODE_SWIGLU ? 2 : 1), MODE>(x, W, out, M, N, K, eps, use_rms, accumulate,
-                                                                     out_f32, s);
+                       int accumulate, int out_f32, const QKVArgs& qa, int variant, hipStream_t s) {
+  // SwiGLU needs the gate/up tile pair in one workgroup; very wide outputs (lm_head, w1|w3) use
+  // 2 tiles per workgroup to halve the activation re-reads.
+  if constexpr (MODE == MODE_SWIGLU) {
+    return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+  } else {
+    if (MODE != MODE_QKV && (N >> 4) >= 2048)
+      return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+    return dispatch_nw<XT, MT, 1, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+  }
 }
 
 template <typename XT, int MODE>
 static int dispatch_mt(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
-                       int accumulate, int out_f32, hipStream_t s) {
-  if (M <= 16) return dispatch_nt<XT, 1, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, s);
-  if (M <= 32) return dispatch_nt<XT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, s);
-  return dispatch_nt<XT, 4, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, s);
+                       int accumulate, int out_f32, const QKVArgs& qa, int variant, hipStream_t s) {
+  if (M <= 16) return dispatch_nt<XT, 1, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+  if (M <= 32) return dispatch_nt<XT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+  return dispatch_nt<XT, 4, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
 }
 
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
-                  float rms_eps, int accumulate, int out_f32, hipStream_t s) {
+                  float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s) {
   if (M <= 0) return 0;
   if (M > SKINNY_MAX_M || (N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
+  if (mode == MODE_QKV && (!qkv || qkv->Dh % 16 || M % qkv->S)) return -1;
   const int use_rms = rms_eps >= 0.f;
   const float eps = use_rms ? rms_eps : 0.f;
-#define JLA_MODE(XT)                                                                                          \
-  switch (mode) {                                                                                             \
-    case MODE_STORE: return dispatch_mt<XT, MODE_STORE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, s); \
-    case MODE_RESIDUAL: return dispatch_mt<XT, MODE_RESIDUAL>(x, W, out, M, N, K, eps, use_rms, accumulate, 1, s);   \
-    case MODE_SWIGLU: return dispatch_mt<XT, MODE_SWIGLU>(x, W, out, M, N, K, eps, use_rms, accumulate, 0, s);       \
-    default: return -1;                                                                                       \
+  QKVArgs qa{};
+  if (qkv) qa = *qkv;
+#define JLA_ARGS x, W, out, M, N, K, eps, use_rms, accumulate
+#define JLA_MODE(XT)                                                                                 \
+  switch (mode) {                                                                                    \
+    case MODE_STORE: return dispatch_mt<XT, MODE_STORE>(JLA_ARGS, out_f32, qa, variant, s);          \
+    case MODE_RESIDUAL: return dispatch_mt<XT, MODE_RESIDUAL>(JLA_ARGS, 1, qa, variant, s);          \
+    case MODE_SWIGLU: return dispatch_mt<XT, MODE_SWIGLU>(JLA_ARGS, 0, qa, variant, s);              \
+    case MODE_QKV: return dispatch_mt<XT, MODE_QKV>(JLA_ARGS, 0, qa, variant, s);                    \
+    default: return -1;                                                                              \
   }
   if (x_is_f32) {
     JLA_MODE(float)
@@ -268,6 +367,7 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
     JLA_MODE(bf16_t)
   }
 #undef JLA_MODE
+#undef JLA_ARGS
 }
 
 }  // namespace jla

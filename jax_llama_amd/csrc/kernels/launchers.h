@@ -13,8 +13,20 @@ int embedding(const int32_t* ids, const bf16_t* table, float* out, int M, int D,
 int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
 
+// Epilogue arguments of the fused qkv projection (MODE_QKV): RoPE + KV-cache write.
+struct QKVArgs {
+  const float2* table;        // [table_len, Dh/2] (cos, sin)
+  int table_len;
+  const int32_t* positions;   // [M]
+  bf16_t* kc;                 // [B, Hkv, T, Dh] (this layer)
+  bf16_t* vc;
+  const int32_t* slot;        // device int32[1]: cache slot of sequence position 0
+  int S, H, Hkv, Dh, T;       // tokens per sequence in this call, heads, kv heads, head dim, cache len
+  bf16_t* q;                  // [M, H, Dh] rotated queries
+};
+
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
-                  float rms_eps, int accumulate, int out_f32, hipStream_t s);
+                  float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          hipStream_t s);
 
@@ -22,11 +34,12 @@ int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const in
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,
                   hipStream_t s);
 
-int attn_decode_chunk(int B, int Hkv, int T);
-int attn_decode_splits(int B, int Hkv, int T);
+int attn_decode_chunk(int B, int Hkv, int T, int rep);
+int attn_decode_splits(int B, int Hkv, int T, int rep);
+// ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
-                const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int B, int H, int Hkv, int Dh, int T,
-                int t_cap, int nsplit, hipStream_t s);
+                const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int32_t* tickets, int B, int H,
+                int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s);
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,
                  hipStream_t s);

@@ -257,10 +257,9 @@ class LLaMAForCausalLM:
         for i, lw in enumerate(self.layers):
             if collect_hidden:
                 hidden.append(h.reshape(b, s, d).clone())
-            qkv = ops.linear(h, lw.qkv, rms_eps=self.eps)
             kc, vc = cache.layer(i)
-            q = ops.rope_kv_write(qkv, self.rope, positions, kc, vc, slot0, s,
-                                  self.n_heads, self.n_kv_heads, self.head_dim)
+            q = ops.linear_qkv_rope(h, lw.qkv, self.eps, self.rope, positions, kc, vc, slot0, s,
+                                    self.n_heads, self.n_kv_heads, self.head_dim)
             q4 = q.reshape(b, s, self.n_heads, self.head_dim)
             if collect_attn:
                 s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())

@@ -9,6 +9,7 @@ There is exactly one GPU implementation per op (no backend selection, no Triton)
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -23,6 +24,10 @@ BF16 = torch.bfloat16
 MODE_STORE = 0
 MODE_RESIDUAL = 1
 MODE_SWIGLU = 2
+MODE_QKV = 3
+
+# GEMV tuning override (0 = built-in heuristic; 1/2/3 = 4/8/16 waves per workgroup)
+GEMV_VARIANT = int(os.environ.get("JLA_GEMV_VARIANT", "0"))
 
 
 def _is_gpu(t: torch.Tensor) -> bool:
@@ -41,6 +46,15 @@ class _Workspace:
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < numel:
             buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
+            self._bufs[key] = buf
+        return buf[:numel]
+
+    def get_zeroed(self, name: str, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
+        """Zero-initialised on (re)allocation only: for self-resetting device counters."""
+        key = ("zeroed:" + name, device, dtype)
+        buf = self._bufs.get(key)
+        if buf is None or buf.numel() < numel:
+            buf = torch.zeros(max(numel, 1), dtype=dtype, device=device)
             self._bufs[key] = buf
         return buf[:numel]
 
@@ -127,7 +141,7 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate):
         e.gemm(x, w.weight, w.n, w.k, out, mode, bool(accumulate))
     else:
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
-                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate))
+                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate), GEMV_VARIANT)
 
 
 # ----------------------------------------------------------------------------------
@@ -148,6 +162,29 @@ def rope_kv_write(qkv: torch.Tensor, table: torch.Tensor, positions: torch.Tenso
     return q
 
 
+def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.Tensor, positions: torch.Tensor,
+                    k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, seq_len: int, n_heads: int,
+                    n_kv_heads: int, head_dim: int) -> torch.Tensor:
+    """Fused ``qkv = [inv_rms(x) *] x @ Wqkv^T`` + interleaved RoPE on q/k + KV-cache write at slots
+    ``slot0 + s``. Returns rotated q ``[M, H, Dh]`` bf16. Decode (M <= 64) is one kernel (the
+    RoPE/cache write is the GEMV epilogue, rotating the fp32 accumulators); prefill runs the MFMA
+    GEMM then the RoPE/KV-write kernel."""
+    if not _is_gpu(x):
+        s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
+        return ref.linear_qkv_rope(x, w.dense(), rms_eps, table, positions, k_cache, v_cache, s0, seq_len,
+                                   n_heads, n_kv_heads, head_dim)
+    m = x.shape[0]
+    e = ext()
+    if m > e.SKINNY_MAX_M:
+        qkv = linear(x, w, rms_eps=rms_eps)
+        return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads, head_dim)
+    q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
+    e.linear_qkv(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
+                 positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, x.device),
+                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, GEMV_VARIANT)
+    return q
+
+
 def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor,
               key_mask: Optional[torch.Tensor] = None, max_kv: Optional[int] = None) -> torch.Tensor:
     """Causal/padded attention of ``q [B, S, H, Dh]`` (queries at cache slots slot0+s)
@@ -164,9 +201,11 @@ def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slo
     t_cap = int(max_kv) if max_kv is not None else k_cache.shape[2]
     e = ext()
     if s == 1:
-        nsplit = e.attn_decode_splits(bsz, k_cache.shape[1], t_cap)
+        hkv = k_cache.shape[1]
+        nsplit = e.attn_decode_splits(bsz, hkv, t_cap, h // hkv)
         ws = workspace.get("attn_decode", bsz * h * nsplit * (dh + 2), torch.float32, q.device)
-        e.attn_decode(q, k_cache, v_cache, slot_t, kv_start, key_mask, out, ws, t_cap, nsplit)
+        tickets = workspace.get_zeroed("attn_tickets", bsz * hkv, torch.int32, q.device)
+        e.attn_decode(q, k_cache, v_cache, slot_t, kv_start, key_mask, out, ws, tickets, t_cap, nsplit)
     else:
         e.attn_prefill(q, k_cache, v_cache, slot_t, kv_start, key_mask, out)
     return out

@@ -157,6 +157,23 @@ def rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0: int, seq_len: 
     return qr
 
 
+def linear_qkv_rope(x, w_dense, rms_eps, table, positions, k_cache, v_cache, slot0: int, seq_len: int,
+                    n_heads: int, n_kv_heads: int, head_dim: int) -> torch.Tensor:
+    """Fused-kernel rounding points: fp32 projection -> fp32 RoPE -> one bf16 rounding."""
+    y = _mm(x, w_dense, rms_eps)  # fp32 [M, (H+2Hkv)*Dh]
+    m = y.shape[0]
+    b = m // seq_len
+    hq, hk = n_heads * head_dim, n_kv_heads * head_dim
+    q = apply_rope(y[:, :hq].reshape(m, n_heads, head_dim), table, positions).to(BF16)
+    k = apply_rope(y[:, hq:hq + hk].reshape(m, n_kv_heads, head_dim), table, positions)
+    v = y[:, hq + hk:].reshape(m, n_kv_heads, head_dim)
+    k_cache[:, :, slot0:slot0 + seq_len] = k.reshape(b, seq_len, n_kv_heads, head_dim).permute(0, 2, 1, 3).to(
+        k_cache.dtype)
+    v_cache[:, :, slot0:slot0 + seq_len] = v.reshape(b, seq_len, n_kv_heads, head_dim).permute(0, 2, 1, 3).to(
+        v_cache.dtype)
+    return q
+
+
 # ----------------------------------------------------------------------------------
 # Attention over the cache
 # ----------------------------------------------------------------------------------

@@ -184,3 +184,36 @@ def test_argmax_first_index():
     assert idx.cpu().tolist() == x.argmax(-1).tolist()
     assert idx[1].item() == 77
     torch.testing.assert_close(val.cpu(), x.max(-1).values)
+
+
+@pytest.mark.parametrize("m,s", [(1, 1), (16, 1), (48, 1), (6, 3), (130, 65)])
+def test_linear_qkv_rope_fused(m, s):
+    h, hkv, dh, k, t = 4, 2, 128, 512, 80
+    b = m // s
+    n = (h + 2 * hkv) * dh
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    x = torch.randn(m, k)
+    table = ref.rope_table(dh, 256, 500000.0)
+    pos = torch.randint(0, 200, (m,), dtype=torch.int32)
+    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+    vc = torch.zeros_like(kc)
+    q = ref.linear_qkv_rope(x, w, 1e-5, table, pos, kc, vc, 7, s, h, hkv, dh)
+    kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+    pg = PackedLinear.from_dense(w, DEV)
+    qg = ops.linear_qkv_rope(x.to(DEV), pg, 1e-5, table.to(DEV), pos.to(DEV), kg, vg,
+                             torch.tensor([7], dtype=torch.int32, device=DEV), s, h, hkv, dh)
+    _close(qg, q, 2e-2, 2e-2)
+    _close(kg, kc, 2e-2, 2e-2)
+    _close(vg, vc, 2e-2, 2e-2)
+
+
+def test_gemv_variants_agree():
+    x = torch.randn(16, 2048, device=DEV)
+    w = PackedLinear.from_dense((torch.randn(512, 2048) * 0.05).to(BF16), DEV)
+    outs = []
+    for v in (1, 2, 3):
+        ops.GEMV_VARIANT = v
+        outs.append(ops.linear(x, w, rms_eps=1e-5, out_dtype=torch.float32))
+    ops.GEMV_VARIANT = 0
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)

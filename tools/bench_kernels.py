@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the decode hot kernels at real model shapes (one MI355X).
+
+Weights rotate over enough copies (> 2x the 256 MiB Infinity Cache) that every timed call streams
+from HBM, as in a real decode step. Prints one JSON line per (op, shape, variant) with
+microseconds and effective TB/s. Usage: python tools/bench_kernels.py [--model llama3-8b] [--m 1 16]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from jax_llama_amd import ops  # noqa: E402
+from jax_llama_amd.config import get_preset  # noqa: E402
+from jax_llama_amd.models.weights import PackedLinear  # noqa: E402
+
+DEV = "cuda"
+
+
+def timeit(fn, iters=30):
+    for _ in range(3):
+        fn(0)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for i in range(iters):
+        fn(i)
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) * 1000.0 / iters
+
+
+def copies_for(nbytes):
+    return max(2, int((600 << 20) // max(nbytes, 1)) + 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--m", type=int, nargs="+", default=[1, 16])
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
+    ap.add_argument("--tp", type=int, default=1)
+    args = ap.parse_args()
+    cfg = get_preset(args.model)
+    d, f, hd = cfg.hidden_size, cfg.intermediate_size // args.tp, cfg.head_dim
+    h, hkv = cfg.num_attention_heads // args.tp, cfg.num_key_value_heads // args.tp
+    shapes = {
+        "qkv": ((h + 2 * hkv) * hd, d, torch.float32, ops.MODE_QKV),
+        "o": (d, h * hd, torch.bfloat16, ops.MODE_RESIDUAL),
+        "gate_up": (2 * f, d, torch.float32, ops.MODE_SWIGLU),
+        "down": (d, f, torch.bfloat16, ops.MODE_RESIDUAL),
+        "lm_head": (cfg.vocab_size // args.tp, d, torch.float32, ops.MODE_STORE),
+    }
+    e = ops.ext()
+    for name, (n, k, xdt, mode) in shapes.items():
+        nbytes = n * k * 2
+        ws = [PackedLinear.random(n, k, DEV) for _ in range(copies_for(nbytes))]
+        for m in args.m:
+            x = torch.randn(m, k, device=DEV).to(xdt)
+            for var in args.variants:
+                ops.GEMV_VARIANT = var
+                if mode == ops.MODE_QKV:
+                    table = torch.randn(4096, hd // 2, 2, device=DEV)
+                    pos = torch.zeros(m, dtype=torch.int32, device=DEV)
+                    kc = torch.zeros(m, hkv, 512, hd, dtype=torch.bfloat16, device=DEV)
+                    vc = torch.zeros_like(kc)
+                    slot = torch.zeros(1, dtype=torch.int32, device=DEV)
+
+                    def fn(i, x=x, table=table, pos=pos, kc=kc, vc=vc, slot=slot):
+                        ops.linear_qkv_rope(x, ws[i % len(ws)], 1e-5, table, pos, kc, vc, slot, 1, h, hkv, hd)
+                elif mode == ops.MODE_RESIDUAL:
+                    out = torch.zeros(m, n, device=DEV)
+
+                    def fn(i, x=x, out=out):
+                        ops.linear_residual(x, ws[i % len(ws)], out)
+                elif mode == ops.MODE_SWIGLU:
+                    def fn(i, x=x):
+                        ops.linear_swiglu(x, ws[i % len(ws)], rms_eps=1e-5)
+                else:
+                    def fn(i, x=x):
+                        ops.linear(x, ws[i % len(ws)], rms_eps=1e-5, out_dtype=torch.float32)
+                us = timeit(fn)
+                print(json.dumps({"op": name, "n": n, "k": k, "m": m, "variant": var, "us": round(us, 2),
+                                  "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+    ops.GEMV_VARIANT = 0
+    # decode attention at the bench shape
+    for b, t in ((16, 384), (1, 4096), (64, 1024)):
+        kc = torch.randn(b, hkv, t, hd, device=DEV).to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        q = torch.randn(b, 1, h, hd, device=DEV).to(torch.bfloat16)
+        slot = torch.tensor([t - 1], dtype=torch.int32, device=DEV)
+        ks = torch.zeros(b, dtype=torch.int32, device=DEV)
+        us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
+        nbytes = 2 * kc.numel() * 2
+        print(json.dumps({"op": "attn_decode", "b": b, "t": t, "us": round(us, 2),
+                          "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -80,7 +80,13 @@ def build_C(jobs: int, force: bool) -> Path:
     srcs = sorted(kdir.glob("*.hip"))
     objs = [BUILD / "C" / (s.stem + ".o") for s in srcs]
     with ThreadPoolExecutor(max_workers=jobs) as ex:
-        list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force), zip(srcs, objs)))
+        rebuilt = list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force), zip(srcs, objs)))
+    # the GEMV's hand-counted load ring must never be read before its wait: check the assembly
+    for src, did in zip(srcs, rebuilt):
+        if did and src.stem == "gemv":
+            asm = BUILD / "C" / "gemv.s"
+            _run([HIPCC, *HIP_FLAGS, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
+            _run([sys.executable, str(ROOT / "tools" / "check_asm_ring.py"), str(asm)])
     bsrc = CSRC / "bindings.cpp"
     bobj = BUILD / "C" / "bindings.o"
     if force or _stale(bobj, [bsrc, *headers]):

@@ -28,15 +28,16 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 JLA_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-JLA_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// fp32 -> bf16 round-to-nearest-even: gfx950's v_cvt_pk_bf16_f32 (one instruction for two values,
+// no branches); bit-identical to torch's float->bfloat16 cast for finite values.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+JLA_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 JLA_DEV uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // unpack the 8 bf16 of a 16-byte vector into floats

@@ -35,20 +35,32 @@ __device__ u32x4 g_zero_frag[64];  // 1 KiB of zeros (static storage is zero-ini
 // the pipeline back into batches (checked in the .s). Each slot is waited with one counted
 // s_waitcnt vmcnt(L*(U-1)) and its registers are pinned behind that wait ("+v"), so no consumer
 // can read them early (cdna_hip_programming.md section 5.7, form (ii)).
-JLA_DEV u32x4 asm_load_nt(const void* p) {
-  u32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
-  return r;
+// The destination is a "+v" (tied) operand: the ring slot is one variable whose register the
+// allocator keeps across the loop back-edge (no phi copies of in-flight registers; verified by
+// tools/check_asm_ring.py on the generated assembly).
+// With ASM = false (used where register pressure makes the allocator shuffle ring registers,
+// i.e. MT > 1) the same ring uses ordinary compiler-counted loads: always correct, sometimes
+// drained at the back-edge. build.py runs tools/check_asm_ring.py on every build.
+template <bool ASM>
+JLA_DEV void asm_load_nt(u32x4& r, const void* p) {
+  if constexpr (ASM)
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "+v"(r) : "v"(p) : "memory");
+  else
+    r = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
-JLA_DEV u32x4 asm_load(const void* p) {
-  u32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
-  return r;
+template <bool ASM>
+JLA_DEV void asm_load(u32x4& r, const void* p) {
+  if constexpr (ASM)
+    asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(r) : "v"(p) : "memory");
+  else
+    r = *reinterpret_cast<const u32x4*>(p);
 }
-JLA_DEV u32x4 asm_load16(const void* p) {
-  u32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(r) : "v"(p) : "memory");
-  return r;
+template <bool ASM>
+JLA_DEV void asm_load16(u32x4& r, const void* p) {
+  if constexpr (ASM)
+    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "+v"(r) : "v"(p) : "memory");
+  else
+    r = reinterpret_cast<const u32x4*>(p)[1];
 }
 template <int N>
 JLA_DEV void wait_vmcnt() {
@@ -63,9 +75,10 @@ template <>
 struct XRaw<float> {  // 8 fp32 activations per lane (two 16-byte loads)
   static constexpr int LOADS = 2;
   u32x4 a, b;
+  template <bool ASM>
   JLA_DEV void load(const float* p) {
-    a = asm_load(p);
-    b = asm_load16(p);
+    asm_load<ASM>(a, p);
+    asm_load16<ASM>(b, p);
   }
   JLA_DEV void pin_regs() {
     pin(a);
@@ -92,7 +105,10 @@ template <>
 struct XRaw<bf16_t> {  // 8 bf16 activations per lane (one 16-byte load)
   static constexpr int LOADS = 1;
   u32x4 v;
-  JLA_DEV void load(const bf16_t* p) { v = asm_load(p); }
+  template <bool ASM>
+  JLA_DEV void load(const bf16_t* p) {
+    asm_load<ASM>(v, p);
+  }
   JLA_DEV void pin_regs() { pin(v); }
   JLA_DEV u32x4 frag(float& ss) const {
     float f[8];
@@ -141,27 +157,32 @@ __global__ void __launch_bounds__(NW * 64)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
 
-  u32x4 bq[U][NT];
-  XRaw<XT> aq[U][MT];
+  u32x4 bq[U][NT] = {};
+  XRaw<XT> aq[U][MT] = {};
   constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
+  constexpr bool ASM = MT == 1;                  // hand-counted ring (see asm_load_nt)
   auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
     const bool valid = i < n;
     const size_t ks = (size_t)(w + i * NW);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) b[t] = asm_load_nt(valid ? (const void*)(wt[t] + ks * 64) : (const void*)zfrag);
+    for (int t = 0; t < NT; ++t)
+      asm_load_nt<ASM>(b[t], valid ? (const void*)(wt[t] + ks * 64) : (const void*)zfrag);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt].load(valid ? xp[mt] + ks * 32 : zx);
+    for (int mt = 0; mt < MT; ++mt) a[mt].template load<ASM>(valid ? xp[mt] + ks * 32 : zx);
   };
-#pragma unroll
-  for (int u = 0; u < U; ++u) issue(u, bq[u], aq[u]);
-  for (int i0 = 0; i0 < n; i0 += U) {
+  // No separate prologue: the first trip computes on the zero-initialised slots (MFMA adds 0) while
+  // issuing k-steps 0..U-1, so every ring register has exactly one definition site (the tied
+  // refill) and the compiler never needs to copy an in-flight register across the loop entry.
+  for (int i0 = -U; i0 < n; i0 += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      wait_vmcnt<L * (U - 1)>();  // slot u (the oldest L loads) has landed
+      if constexpr (ASM) {
+        wait_vmcnt<L * (U - 1)>();  // slot u (the oldest L loads) has landed
 #pragma unroll
-      for (int t = 0; t < NT; ++t) pin(bq[u][t]);
+        for (int t = 0; t < NT; ++t) pin(bq[u][t]);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+        for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+      }
       u32x4 af[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) af[mt] = aq[u][mt].frag(ss[mt]);
@@ -172,7 +193,7 @@ __global__ void __launch_bounds__(NW * 64)
       issue(i0 + U + u, bq[u], aq[u]);  // refill: k-step U ahead (zero fragment past the end)
     }
   }
-  wait_vmcnt<0>();  // retire the past-the-end refills before the registers are reused
+  if constexpr (ASM) wait_vmcnt<0>();  // retire the past-the-end refills before the registers are reused
 
   // ---- cross-wave reduction through LDS
 #pragma unroll
@@ -303,7 +324,7 @@ static int pick_nw(int ngroups, int variant) {
   if (variant == 1) return 4;
   if (variant == 2) return 8;
   if (variant == 3) return 16;
-  return ngroups <= 512 ? 16 : 8;
+  return 4;  // measured best on MI355X for every Llama-3-8B projection at M = 1 and 16
 }
 
 template <typename XT, int MT, int NT, int MODE>

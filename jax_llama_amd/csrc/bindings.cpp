@@ -85,8 +85,30 @@ void check_linear_out(const Tensor& out, int64_t m, int64_t n, int64_t mode) {
     check(out.scalar_type() == torch::kBFloat16 || out.scalar_type() == torch::kFloat32, "out must be bf16/fp32");
 }
 
+// Decode linear dispatch. variant: 0 = auto (M == 1 -> K-split GEMV, else split-K skinny GEMM),
+// 1/2/3 = K-split GEMV (gemv.hip) with 4/8/16 waves, 4 = split-K skinny GEMM (skinny.hip).
+void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* out, int64_t mode, double rms_eps,
+                bool accumulate, bool out_f32, const jla::QKVArgs* qa, int64_t variant, const Tensor& ws,
+                const Tensor& tickets) {
+  const int64_t m = x.size(0);
+  const bool f32 = x.scalar_type() == torch::kFloat32;
+  if (variant == 0) variant = (m == 1) ? 1 : 4;
+  if (variant == 4) {
+    check_gpu(ws, "ws");
+    check_gpu(tickets, "tickets");
+    check(ws.scalar_type() == torch::kFloat32 && tickets.scalar_type() == torch::kInt32, "ws/tickets dtypes");
+    rc(jla::linear_splitk(x.data_ptr(), f32, w.data_ptr(), out, m, n, k, mode, (float)rms_eps, accumulate, out_f32, qa,
+                          ptr<float>(ws), ws.numel(), ptr<int32_t>(tickets), tickets.numel(), stream()),
+       "linear_splitk");
+  } else {
+    rc(jla::linear_skinny(x.data_ptr(), f32, w.data_ptr(), out, m, n, k, mode, (float)rms_eps, accumulate, out_f32, qa,
+                          variant, stream()),
+       "linear_skinny");
+  }
+}
+
 void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, double rms_eps,
-                   bool accumulate, int64_t variant) {
+                   bool accumulate, int64_t variant, Tensor ws, Tensor tickets) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
@@ -95,16 +117,18 @@ void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_skinny: M too large");
   check_linear_out(out, m, n, mode);
-  rc(jla::linear_skinny(x.data_ptr(), x.scalar_type() == torch::kFloat32, w.data_ptr(), out.data_ptr(), m, n, k,
-                        mode, (float)rms_eps, accumulate, out.scalar_type() == torch::kFloat32, nullptr, variant,
-                        stream()),
-     "linear_skinny");
+  run_skinny(x, w, n, k, out.data_ptr(), mode, rms_eps, accumulate, out.scalar_type() == torch::kFloat32, nullptr,
+             variant, ws, tickets);
+}
+
+py::tuple skinny_workspace(int64_t m, int64_t n, int64_t k, int64_t mode) {
+  return py::make_tuple((int64_t)jla::skinny_workspace_floats(m, n, k, mode), jla::skinny_tickets(m, n, k, mode));
 }
 
 // fused qkv projection + RoPE + KV-cache write (decode / small M)
 void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions, Tensor kc,
                 Tensor vc, Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q,
-                int64_t variant) {
+                int64_t variant, Tensor ws, Tensor tickets) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   for (auto* t : {&table, &positions, &kc, &vc, &slot, &q}) check_gpu(*t, "linear_qkv arg");
@@ -136,9 +160,7 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
   qa.Dh = dh;
   qa.T = kc.size(2);
   qa.q = bf(q);
-  rc(jla::linear_skinny(x.data_ptr(), x.scalar_type() == torch::kFloat32, w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID,
-                        (float)rms_eps, 0, 0, &qa, variant, stream()),
-     "linear_qkv");
+  run_skinny(x, w, n, k, nullptr, MODE_QKV_ID, rms_eps, false, false, &qa, variant, ws, tickets);
 }
 
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate) {
@@ -263,6 +285,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_decode_splits",
         [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });
   m.def("linear_qkv", &linear_qkv);
+  m.def("skinny_workspace", &skinny_workspace);
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
         py::arg("nsplit"));

@@ -27,6 +27,13 @@ struct QKVArgs {
 
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
+// split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
+// skinny_workspace_floats / skinny_tickets (tickets zero-initialised once, self-resetting)
+size_t skinny_workspace_floats(int M, int N, int K, int mode);
+int skinny_tickets(int M, int N, int K, int mode);
+int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode, float rms_eps,
+                  int accumulate, int out_f32, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
+                  int n_tickets, hipStream_t s);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          hipStream_t s);
 

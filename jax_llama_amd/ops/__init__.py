@@ -140,8 +140,24 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate):
             x = x.to(BF16)
         e.gemm(x, w.weight, w.n, w.k, out, mode, bool(accumulate))
     else:
+        ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
-                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate), GEMV_VARIANT)
+                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate), GEMV_VARIANT, ws, tk)
+
+
+_SK_SIZES = {}
+
+
+def _skinny_ws(e, m, n, k, mode, device):
+    """Split-K partial slabs + self-resetting tickets of the skinny GEMM (shared, stream-ordered;
+    sized during the eager warm-up step so nothing is allocated under hipGraph capture)."""
+    key = (m, n, k, mode)
+    sz = _SK_SIZES.get(key)
+    if sz is None:
+        sz = _SK_SIZES[key] = tuple(e.skinny_workspace(m, n, k, mode))
+    floats, tickets = sz
+    return (workspace.get("skinny", max(1, floats), torch.float32, device),
+            workspace.get_zeroed("skinny_tickets", max(1, tickets), torch.int32, device))
 
 
 # ----------------------------------------------------------------------------------
@@ -179,9 +195,10 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
         qkv = linear(x, w, rms_eps=rms_eps)
         return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads, head_dim)
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
+    ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)
     e.linear_qkv(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
                  positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, x.device),
-                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, GEMV_VARIANT)
+                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, GEMV_VARIANT, ws, tk)
     return q
 
 

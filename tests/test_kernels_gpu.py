@@ -211,9 +211,35 @@ def test_gemv_variants_agree():
     x = torch.randn(16, 2048, device=DEV)
     w = PackedLinear.from_dense((torch.randn(512, 2048) * 0.05).to(BF16), DEV)
     outs = []
-    for v in (1, 2, 3):
+    for v in (1, 2, 3, 4):
         ops.GEMV_VARIANT = v
         outs.append(ops.linear(x, w, rms_eps=1e-5, out_dtype=torch.float32))
     ops.GEMV_VARIANT = 0
-    torch.testing.assert_close(outs[0], outs[1], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(outs[0], outs[2], rtol=1e-5, atol=1e-5)
+    for o in outs[1:]:
+        torch.testing.assert_close(outs[0], o, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("variant", [1, 4])
+@pytest.mark.parametrize("m", [1, 9, 16, 40, 64])
+def test_decode_linear_paths_all_modes(variant, m):
+    """Both decode GEMM designs, every epilogue, real-ish K (multi-split)."""
+    ops.GEMV_VARIANT = variant
+    try:
+        k, n = 4096, 768
+        x = torch.randn(m, k)
+        w, pg, pc = _mk_linear(n, k)
+        y = ops.linear(x.to(DEV), pg, rms_eps=1e-5, out_dtype=torch.float32)
+        _close(y, ref.linear(x, w, 1e-5, torch.float32), 1e-2, 1e-3)
+        xb = x.to(BF16)
+        h = torch.randn(m, n)
+        hg = h.to(DEV)
+        ops.linear_residual(xb.to(DEV), pg, hg)
+        _close(hg, ref.linear_residual(xb, w, h.clone()), 1e-2, 1e-3)
+        gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+        y2 = ops.linear_swiglu(x.to(DEV), PackedLinear.from_dense(gu, DEV), rms_eps=1e-5)
+        _close(y2, ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
+        # determinism of the split-K reduction (fixed order)
+        y_again = ops.linear(x.to(DEV), pg, rms_eps=1e-5, out_dtype=torch.float32)
+        assert torch.equal(y, y_again)
+    finally:
+        ops.GEMV_VARIANT = 0

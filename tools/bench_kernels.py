@@ -44,7 +44,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--m", type=int, nargs="+", default=[1, 16])
-    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
+    ap.add_argument("--variants", type=int, nargs="+", default=[1, 4])
     ap.add_argument("--tp", type=int, default=1)
     args = ap.parse_args()
     cfg = get_preset(args.model)

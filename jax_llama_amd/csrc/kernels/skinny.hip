@@ -22,24 +22,33 @@
 
 namespace jla {
 
-constexpr int SK_NW = 4;  // waves per workgroup
+constexpr int SK_NW = 8;  // waves per workgroup
 
-JLA_DEV void st_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-JLA_DEV float ld_wt(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Hand-counted register ring for the weight stream (same scheme as gemv.hip: tied asm loads, one
+// definition site, counted vmcnt; tools/check_asm_ring.py verifies the assembly at build time).
+JLA_DEV void sk_load_nt(u32x4& r, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "+v"(r) : "v"(p) : "memory");
 }
+template <int N>
+JLA_DEV void sk_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+JLA_DEV void sk_pin(u32x4& r) { asm volatile("" : "+v"(r)); }
+
+__device__ u32x4 g_sk_zero[64];  // zero fragment for past-the-end refills (MFMA adds 0)
 
 struct SplitArgs {
   int ksplit, kc;        // K split count, k-steps (of 32) per split
-  float* slabs;          // [groups * ksplit][NW][MT][NT][64][4] + ss [groups * ksplit][MT * 16]
-  int32_t* tickets;      // [groups], self-resetting
+  float* slabs;          // [wgs][NW][MT][NT][64][4] partial tiles, then [wgs][MT * 16] sums of squares
+  int slab_bytes;        // total bytes of the workspace (buffer descriptor range)
+  int32_t* tickets;      // [groups], zero-initialised once, reset by each group's last arriver
 };
 
 template <typename XT, int MT, int NT, int MODE, int U>
 __global__ void __launch_bounds__(SK_NW * 64)
     skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N, int K,
                   float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa, SplitArgs sa) {
-  extern __shared__ __attribute__((aligned(16))) u32x4 xs[];  // [MT][kc][64] A fragments
+  extern __shared__ __attribute__((aligned(16))) u32x4 xs[];  // [MT][kc][64] bf16 A fragments
   __shared__ float ss_l[MT * 16];
   __shared__ float inv_l[MT * 16];
   __shared__ int last_flag;
@@ -49,71 +58,32 @@ __global__ void __launch_bounds__(SK_NW * 64)
   const int KS = K >> 5, NTT = N >> 4;
   const int group = blockIdx.x / sa.ksplit, split = blockIdx.x - group * sa.ksplit;
   const int ks0 = split * sa.kc;
-  const int nk = max(0, min(KS, ks0 + sa.kc) - ks0);
-
-  // ---- stage x[:, ks0*32 : (ks0+nk)*32] -> LDS fragments (bf16), sum of squares per row
-  if (threadIdx.x < MT * 16) ss_l[threadIdx.x] = 0.f;
-  __syncthreads();
-  {
-    float ssp[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) ssp[mt] = 0.f;
-    const int npieces = nk * 64;  // per m-tile
-    for (int p = threadIdx.x; p < npieces; p += SK_NW * 64) {
-      const int j = p >> 6;  // lane of piece p == lane (p & 63) == threadIdx.x & 63
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int row = min(mt * 16 + (lane & 15), M - 1);
-        const size_t off = (size_t)row * K + (size_t)(ks0 + j) * 32 + 8 * (lane >> 4);
-        u32x4 v;
-        if constexpr (sizeof(XT) == 4) {
-          const float4* src = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off);
-          const float4 a = src[0], b = src[1];
-          ssp[mt] += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
-          v[0] = pack2bf(a.x, a.y);
-          v[1] = pack2bf(a.z, a.w);
-          v[2] = pack2bf(b.x, b.y);
-          v[3] = pack2bf(b.z, b.w);
-        } else {
-          v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(x) + off);
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) ssp[mt] += f[e] * f[e];
-        }
-        xs[(mt * nk + j) * 64 + lane] = v;
-      }
-    }
-    if (use_rms) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        float s = ssp[mt];
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        if (lane < 16) atomicAdd(&ss_l[mt * 16 + lane], s);
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- stream this wave's NT weight tiles over the chunk
+  const int nk = max(1, min(KS, ks0 + sa.kc) - ks0);
   const int tile0 = (group * SK_NW + w) * NT;
+
   const u32x4* wt[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) wt[t] = W + ((size_t)min(tile0 + t, NTT - 1) * KS + ks0) * 64 + lane;
+  const u32x4* zf = g_sk_zero + lane;
 
   f32x4 acc[MT][NT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < MT * 16) ss_l[threadIdx.x] = 0.f;
 
   u32x4 bq[U][NT] = {};
+  // Trip j0 = -U only issues k-steps 0..U-1 (the ring's single definition site), then stages x
+  // while those weight loads are in flight; every later trip consumes slot u and refills it.
   for (int j0 = -U; j0 < nk; j0 += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = j0 + u;
-      if (j >= 0 && j < nk) {
+      if (j0 >= 0) {
+        sk_wait<NT * (U - 1)>();
+#pragma unroll
+        for (int t = 0; t < NT; ++t) sk_pin(bq[u][t]);
+        const int j = min(j0 + u, nk - 1);  // past the end: zero weights, any valid x
         u32x4 af[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) af[mt] = xs[(mt * nk + j) * 64 + lane];
@@ -122,26 +92,70 @@ __global__ void __launch_bounds__(SK_NW * 64)
 #pragma unroll
           for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(af[mt], bq[u][t], acc[mt][t]);
       }
-      const int jn = j + U;
-      const bool valid = jn < nk;
+      const int jn = j0 + u + U;
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        bq[u][t] = __builtin_nontemporal_load(valid ? wt[t] + (size_t)jn * 64 : wt[t]);
+      for (int t = 0; t < NT; ++t) sk_load_nt(bq[u][t], jn < nk ? (const void*)(wt[t] + (size_t)jn * 64) : (const void*)zf);
+    }
+    if (j0 < 0) {
+      // ---- stage x[:, ks0*32 : (ks0+nk)*32] -> LDS as bf16 A fragments; RMS sums of squares
+      __syncthreads();  // ss_l zeroed
+      float ssp[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) ssp[mt] = 0.f;
+      for (int p = threadIdx.x; p < nk * 64; p += SK_NW * 64) {
+        const int j = p >> 6;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int row = min(mt * 16 + (lane & 15), M - 1);
+          const size_t off = (size_t)row * K + (size_t)(ks0 + j) * 32 + 8 * (lane >> 4);
+          u32x4 v;
+          if constexpr (sizeof(XT) == 4) {
+            const float4* src = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off);
+            const float4 a = src[0], b = src[1];
+            ssp[mt] += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
+            v[0] = pack2bf(a.x, a.y);
+            v[1] = pack2bf(a.z, a.w);
+            v[2] = pack2bf(b.x, b.y);
+            v[3] = pack2bf(b.z, b.w);
+          } else {
+            v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(x) + off);
+            float f[8];
+            unpack8(v, f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ssp[mt] += f[e] * f[e];
+          }
+          xs[(mt * nk + j) * 64 + lane] = v;
+        }
+      }
+      if (use_rms) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          float sv = ssp[mt];
+          sv += __shfl_xor(sv, 16, 64);
+          sv += __shfl_xor(sv, 32, 64);
+          if (lane < 16) atomicAdd(&ss_l[mt * 16 + lane], sv);
+        }
+      }
+      __syncthreads();
     }
   }
+  sk_wait<0>();  // retire the zero-fragment refills
 
-  // ---- split-K: publish partials, last arriver reduces (fixed split order)
+  // ---- split-K: publish partial tile (write-through sc1 stores), last arriver reduces in order
   if (sa.ksplit > 1) {
-    const size_t slab_sz = (size_t)SK_NW * MT * NT * 256;
-    float* slab = sa.slabs + (size_t)blockIdx.x * slab_sz + (size_t)w * MT * NT * 256;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(sa.slabs, 0, sa.slab_bytes, 0x00020000);
+    const int tile_bytes = SK_NW * MT * NT * 1024;
+    const int ss_base = gridDim.x * tile_bytes;
+    const int wave_off = w * MT * NT * 1024 + lane * 16;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st_wt(slab + ((mt * NT + t) * 64 + lane) * 4 + i, acc[mt][t][i]);
-    float* ss_slab = sa.slabs + (size_t)gridDim.x * slab_sz + (size_t)blockIdx.x * MT * 16;
-    if (threadIdx.x < MT * 16) st_wt(ss_slab + threadIdx.x, ss_l[threadIdx.x]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mt][t]), rs,
+                                               blockIdx.x * tile_bytes + wave_off + (mt * NT + t) * 1024, 0, 16);
+    if (threadIdx.x < MT * 16)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss_l[threadIdx.x]), rs,
+                                            ss_base + (blockIdx.x * MT * 16 + threadIdx.x) * 4, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -157,19 +171,38 @@ __global__ void __launch_bounds__(SK_NW * 64)
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < sa.ksplit; ++s) {
-      const float* sl = sa.slabs + (size_t)(b0 + s) * slab_sz + (size_t)w * MT * NT * 256;
+    int s = 0;
+    for (; s + 4 <= sa.ksplit; s += 4) {  // 4 splits' loads in flight per step
+      u32x4 v[4][MT][NT];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            v[q][mt][t] = __builtin_amdgcn_raw_buffer_load_b128(
+                rs, (b0 + s + q) * tile_bytes + wave_off + (mt * NT + t) * 1024, 0, 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[mt][t] += __builtin_bit_cast(f32x4, v[q][mt][t]);
+    }
+    for (; s < sa.ksplit; ++s)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[mt][t][i] += ld_wt(sl + ((mt * NT + t) * 64 + lane) * 4 + i);
-    }
+          acc[mt][t] += __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (b0 + s) * tile_bytes + wave_off + (mt * NT + t) * 1024,
+                                                           0, 16));
     if (threadIdx.x < MT * 16) {
-      float s = 0.f;
-      for (int sp = 0; sp < sa.ksplit; ++sp) s += ld_wt(sa.slabs + (size_t)gridDim.x * slab_sz + (size_t)(b0 + sp) * MT * 16 + threadIdx.x);
-      ss_l[threadIdx.x] = s;
+      float sum = 0.f;
+      for (int sp = 0; sp < sa.ksplit; ++sp)
+        sum += __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rs, ss_base + ((b0 + sp) * MT * 16 + threadIdx.x) * 4, 0, 16));
+      ss_l[threadIdx.x] = sum;
     }
   }
   if (threadIdx.x < MT * 16) inv_l[threadIdx.x] = use_rms ? rsqrtf(ss_l[threadIdx.x] / (float)K + eps) : 1.f;
@@ -202,7 +235,7 @@ __global__ void __launch_bounds__(SK_NW * 64)
             if (m < M && tile < NTT) {
               const int col = tile * 16 + c;
               const int head = col / qa.Dh, d = col - head * qa.Dh;
-              const int b = m / qa.S, s = m - b * qa.S;
+              const int b = m / qa.S, sq = m - b * qa.S;
               float r = v;
               if (head < qa.H + qa.Hkv) {
                 int pos = qa.positions[m];
@@ -213,7 +246,7 @@ __global__ void __launch_bounds__(SK_NW * 64)
               if (head < qa.H) {
                 qa.q[((size_t)m * qa.H + head) * qa.Dh + d] = f2bf(r);
               } else {
-                const int slot = qa.slot[0] + s;
+                const int slot = qa.slot[0] + sq;
                 if (slot < qa.T) {
                   const bool is_k = head < qa.H + qa.Hkv;
                   const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
@@ -245,18 +278,22 @@ struct SkPlan {
   int nt, groups, ksplit, kc;
 };
 
+static int sk_mt(int M) { return M <= 16 ? 1 : (M <= 32 ? 2 : 4); }  // == the kernel's MT template
+
 static SkPlan sk_plan(int M, int N, int K, int mode) {
   const int KS = K >> 5, NTT = N >> 4;
-  const int mt = (M + 15) / 16;
+  const int mt = sk_mt(M);
   SkPlan p;
-  p.nt = (mode == MODE_SWIGLU || NTT >= 8 * SK_NW) ? 2 : 1;
+  p.nt = (mode == MODE_SWIGLU || NTT >= 32 * SK_NW) ? 2 : 1;
   p.groups = (NTT + SK_NW * p.nt - 1) / (SK_NW * p.nt);
-  // LDS: MT * kc fragments of 1 KiB <= 64 KiB; target ~512 workgroups; >= 4 k-steps per split
-  const int kc_max = max(1, 64 / mt);
+  // LDS holds MT * kc A fragments of 1 KiB (<= 64 KiB); aim for ~512 workgroups, >= 8 k-steps
+  // per split, at most 8 splits unless LDS forces more.
+  const int kc_max = 64 / mt;
   int ks = (512 + p.groups - 1) / p.groups;
+  ks = min(ks, 8);
+  ks = min(ks, max(1, KS / 8));
   ks = max(ks, (KS + kc_max - 1) / kc_max);
-  ks = min(ks, max(1, KS / 4));
-  ks = max(ks, (KS + kc_max - 1) / kc_max);
+  ks = max(ks, 1);
   p.kc = (KS + ks - 1) / ks;
   p.ksplit = (KS + p.kc - 1) / p.kc;
   return p;
@@ -265,7 +302,7 @@ static SkPlan sk_plan(int M, int N, int K, int mode) {
 size_t skinny_workspace_floats(int M, int N, int K, int mode) {
   const SkPlan p = sk_plan(M, N, K, mode);
   if (p.ksplit <= 1) return 0;
-  const int mt = (M + 15) / 16;
+  const int mt = sk_mt(M);
   const size_t wgs = (size_t)p.groups * p.ksplit;
   return wgs * ((size_t)SK_NW * mt * p.nt * 256 + mt * 16);
 }
@@ -277,7 +314,7 @@ static int launch_sk(const void* x, const void* W, void* out, int M, int N, int 
                      int accumulate, int out_f32, const QKVArgs& qa, const SkPlan& p, float* ws, int32_t* tickets,
                      hipStream_t s) {
   constexpr int U = NT == 1 ? 8 : 4;
-  SplitArgs sa{p.ksplit, p.kc, ws, tickets};
+  SplitArgs sa{p.ksplit, p.kc, ws, (int)(skinny_workspace_floats(M, N, K, MODE) * 4), tickets};
   const size_t lds = (size_t)MT * p.kc * 1024;
   auto kern = &skinny_kernel<XT, MT, NT, MODE, U>;
   static bool attr_set = false;
@@ -302,7 +339,7 @@ static int sk_nt(const void* x, const void* W, void* out, int M, int N, int K, f
 }
 
 template <typename XT, int MODE>
-static int sk_mt(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms, int accumulate,
+static int sk_m(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms, int accumulate,
                  int out_f32, const QKVArgs& qa, const SkPlan& p, float* ws, int32_t* tickets, hipStream_t s) {
   if (M <= 16) return sk_nt<XT, 1, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, p, ws, tickets, s);
   if (M <= 32) return sk_nt<XT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, p, ws, tickets, s);
@@ -325,10 +362,10 @@ int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, 
 #define JLA_ARGS x, W, out, M, N, K, eps, use_rms, accumulate
 #define JLA_MODE(XT)                                                                                      \
   switch (mode) {                                                                                         \
-    case MODE_STORE: return sk_mt<XT, MODE_STORE>(JLA_ARGS, out_f32, qa, p, ws, tickets, s);              \
-    case MODE_RESIDUAL: return sk_mt<XT, MODE_RESIDUAL>(JLA_ARGS, 1, qa, p, ws, tickets, s);              \
-    case MODE_SWIGLU: return sk_mt<XT, MODE_SWIGLU>(JLA_ARGS, 0, qa, p, ws, tickets, s);                  \
-    case MODE_QKV: return sk_mt<XT, MODE_QKV>(JLA_ARGS, 0, qa, p, ws, tickets, s);                        \
+    case MODE_STORE: return sk_m<XT, MODE_STORE>(JLA_ARGS, out_f32, qa, p, ws, tickets, s);              \
+    case MODE_RESIDUAL: return sk_m<XT, MODE_RESIDUAL>(JLA_ARGS, 1, qa, p, ws, tickets, s);              \
+    case MODE_SWIGLU: return sk_m<XT, MODE_SWIGLU>(JLA_ARGS, 0, qa, p, ws, tickets, s);                  \
+    case MODE_QKV: return sk_m<XT, MODE_QKV>(JLA_ARGS, 0, qa, p, ws, tickets, s);                        \
     default: return -1;                                                                                   \
   }
   if (x_is_f32) {

@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(SK_NW * 64)
     skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N, int K,
                   float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa, SplitArgs sa) {
   extern __shared__ __attribute__((aligned(16))) u32x4 xs[];  // [MT][kc][64] bf16 A fragments
+  __shared__ float ss_w[SK_NW][MT * 16];
   __shared__ float ss_l[MT * 16];
   __shared__ float inv_l[MT * 16];
   __shared__ int last_flag;
@@ -127,16 +128,21 @@ __global__ void __launch_bounds__(SK_NW * 64)
           xs[(mt * nk + j) * 64 + lane] = v;
         }
       }
-      if (use_rms) {
+      // per-wave partials, summed in wave order below (deterministic: no LDS float atomics)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          float sv = ssp[mt];
-          sv += __shfl_xor(sv, 16, 64);
-          sv += __shfl_xor(sv, 32, 64);
-          if (lane < 16) atomicAdd(&ss_l[mt * 16 + lane], sv);
-        }
+      for (int mt = 0; mt < MT; ++mt) {
+        float sv = ssp[mt];
+        sv += __shfl_xor(sv, 16, 64);
+        sv += __shfl_xor(sv, 32, 64);
+        if (lane < 16) ss_w[w][mt * 16 + lane] = sv;
       }
       __syncthreads();
+      if (threadIdx.x < MT * 16) {
+        float sv = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < SK_NW; ++ww) sv += ss_w[ww][threadIdx.x];
+        ss_l[threadIdx.x] = sv;
+      }
     }
   }
   sk_wait<0>();  // retire the zero-fragment refills

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[1, 16])
     ap.add_argument("--variants", type=int, nargs="+", default=[1, 4])
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--ops", nargs="+", default=None, help="subset of qkv o gate_up down lm_head attn")
     args = ap.parse_args()
     cfg = get_preset(args.model)
     d, f, hd = cfg.hidden_size, cfg.intermediate_size // args.tp, cfg.head_dim
@@ -59,6 +60,8 @@ def main():
     }
     e = ops.ext()
     for name, (n, k, xdt, mode) in shapes.items():
+        if args.ops and name not in args.ops:
+            continue
         nbytes = n * k * 2
         ws = [PackedLinear.random(n, k, DEV) for _ in range(copies_for(nbytes))]
         for m in args.m:
@@ -92,6 +95,8 @@ def main():
         torch.cuda.empty_cache()
     ops.GEMV_VARIANT = 0
     # decode attention at the bench shape
+    if args.ops and "attn" not in args.ops:
+        return
     for b, t in ((16, 384), (1, 4096), (64, 1024)):
         kc = torch.randn(b, hkv, t, hd, device=DEV).to(torch.bfloat16)
         vc = torch.randn_like(kc)

@@ -126,6 +126,8 @@ def main():
         "decode_tokens_per_sec": round(replicas * args.batch * 1000.0 / decode_ms_per_token, 2),
         "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
         "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
+        "decode_kernel_choice": {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}": v
+                                 for k, v in __import__("jax_llama_amd.ops.autotune", fromlist=["x"]).table().items()},
     }
     if ctx.rank == 0:
         line = json.dumps(res)

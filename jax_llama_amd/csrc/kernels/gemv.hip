@@ -346,6 +346,13 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
                        int accumulate, int out_f32, const QKVArgs& qa, int variant, hipStream_t s) {
   // SwiGLU needs the gate/up tile pair in one workgroup; very wide outputs (lm_head, w1|w3) use
   // 2 tiles per workgroup to halve the activation re-reads.
+  // variant 5 / 6: 4 waves with 4 / 2 tiles per workgroup (x re-reads / 4, / 2) for tuning.
+  if constexpr (MT == 1) {
+    if (variant == 5 && (N & 63) == 0)
+      return launch_skinny<XT, MT, 4, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    if (variant == 6)
+      return launch_skinny<XT, MT, 2, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+  }
   if constexpr (MODE == MODE_SWIGLU) {
     return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
   } else {

@@ -14,6 +14,7 @@ from typing import Optional
 
 import torch
 
+from . import autotune
 from . import reference as ref
 from ._ext import available as ext_available  # noqa: F401
 from ._ext import ext
@@ -142,7 +143,26 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate):
     else:
         ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
-                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate), GEMV_VARIANT, ws, tk)
+                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate),
+                        _variant(e, x, w, mode), ws, tk)
+
+
+def _variant(e, x, w, mode) -> int:
+    """Decode-kernel variant for this shape: pinned (JLA_GEMV_VARIANT / ops.GEMV_VARIANT) or
+    measured once per shape on the device (ops/autotune.py)."""
+    if GEMV_VARIANT:
+        return GEMV_VARIANT
+    m = x.shape[0]
+    pmode = MODE_STORE if mode == MODE_QKV else mode  # QKV epilogue has side effects: tune as STORE
+    ws, tk = _skinny_ws(e, m, w.n, w.k, pmode, x.device)
+    ncols = w.n // 2 if pmode == MODE_SWIGLU else w.n
+    odt = torch.float32 if pmode == MODE_RESIDUAL else BF16
+    scratch = workspace.get("tune_out", m * ncols, odt, x.device).view(m, ncols)
+
+    def run(v, xx, wt):
+        e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk)
+
+    return autotune.choose(e, x, w, pmode, run)
 
 
 _SK_SIZES = {}
@@ -198,7 +218,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)
     e.linear_qkv(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
                  positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, x.device),
-                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, GEMV_VARIANT, ws, tk)
+                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, _variant(e, x, w, MODE_QKV), ws, tk)
     return q
 
 

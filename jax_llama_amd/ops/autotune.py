@@ -1,0 +1,89 @@
+"""Per-shape selection among the decode linear kernels, measured on the device at first use.
+
+Two decode GEMM designs ship (``csrc/kernels/gemv.hip`` K-split-across-waves GEMV with 1/2/4
+tiles per workgroup; ``csrc/kernels/skinny.hip`` split-K GEMM sharing x through LDS); which one
+streams the weights fastest depends on (M, N, K) in ways that are cheaper to measure than to
+model (rocprof studies: profiles/README.md). The first eager call of a shape times every
+candidate on a rotating set of scratch weights (> Infinity Cache, so each call streams from HBM,
+as in a real decode step) and caches the winner. Never runs under hipGraph capture; shapes first
+seen during capture fall back to the static heuristic.
+
+Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG,
+4 = split-K skinny GEMM. ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Tuple
+
+import torch
+
+_CACHE: Dict[Tuple, int] = {}
+ENABLED = os.environ.get("JLA_AUTOTUNE", "1") != "0"
+
+
+def m_bucket(m: int) -> int:
+    return 1 if m == 1 else (16 if m <= 16 else (32 if m <= 32 else 64))
+
+
+def heuristic(m: int, n: int, k: int, mode: int) -> int:
+    """Static choice from MI355X measurements (Llama-3-8B projections, profiles/README.md)."""
+    ntt = n // 16
+    if m > 16:
+        return 4 if n * k >= 20_000_000 else 1
+    if m <= 4:
+        return 1
+    if ntt // 4 >= 384 and n % 64 == 0:
+        return 5
+    if ntt // 2 >= 192:
+        return 6
+    return 1
+
+
+def candidates(m: int, n: int) -> Tuple[int, ...]:
+    if m > 16:
+        return (1, 4)
+    c = [1, 6, 4]
+    if n % 64 == 0:
+        c.insert(1, 5)
+    return tuple(c)
+
+
+def choose(e, x: torch.Tensor, w, mode: int, run) -> int:
+    """``run(variant, x, weight_tensor)`` launches the op once."""
+    m = x.shape[0]
+    key = (m_bucket(m), w.n, w.k, mode, x.dtype)
+    v = _CACHE.get(key)
+    if v is not None:
+        return v
+    if not ENABLED or torch.cuda.is_current_stream_capturing():
+        return heuristic(m, w.n, w.k, mode)
+    v = _measure(x, w, run, candidates(m, w.n))
+    _CACHE[key] = v
+    return v
+
+
+def _measure(x, w, run, cands) -> int:
+    nbytes = w.weight.numel() * 2
+    copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
+    ws = [torch.empty_like(w.weight).normal_(0, 0.02) for _ in range(copies)]
+    best, best_t = cands[0], float("inf")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for v in cands:
+        for i in range(2):
+            run(v, x, ws[i % copies])
+        iters = 2 * copies
+        ev0.record()
+        for i in range(iters):
+            run(v, x, ws[i % copies])
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1) / iters
+        if t < best_t:
+            best, best_t = v, t
+    del ws
+    return best
+
+
+def table() -> Dict[Tuple, int]:
+    return dict(_CACHE)

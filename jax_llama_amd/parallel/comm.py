@@ -46,9 +46,10 @@ class TPComm:
         """Returns ``[size, *t.shape]``."""
         if self.size == 1:
             return t.unsqueeze(0)
-        out = torch.empty((self.size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out
+        # flat [size * numel] buffer: the layout both RCCL and gloo accept for all_gather_into_tensor
+        out = torch.empty(self.size * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous().reshape(-1), group=self.group)
+        return out.view((self.size,) + tuple(t.shape))
 
 
 NO_COMM = TPComm()

@@ -103,6 +103,14 @@ class Encoding:
     def native(self) -> bool:
         return self._core is not None
 
+    @property
+    def mergeable_ranks(self) -> Dict[bytes, int]:
+        return self._ranks
+
+    @property
+    def special_tokens_set(self) -> AbstractSet[str]:
+        return set(self._special)
+
     def _encode_ordinary(self, text: str) -> List[int]:
         pieces = [m.encode("utf-8") for m in self._pat.findall(text)]
         if self._core is not None:

@@ -227,3 +227,73 @@ def save_meta_checkpoint(sd: Dict[str, torch.Tensor], params_json: Dict, out_dir
                 continue
             shard[k] = t.chunk(n_shards, ax)[r].clone()
         torch.save(shard, os.path.join(out_dir, f"consolidated.{r:02d}.pth"))
+
+
+# ----------------------------------------------------------------------------------
+# Per-rank loading (tensor parallel, one process per GPU)
+# ----------------------------------------------------------------------------------
+def _global_slice(pieces: List[torch.Tensor], cat_axis: int, axis: int, lo: int, hi: int) -> torch.Tensor:
+    """Rows/cols [lo, hi) along ``axis`` of ``cat(pieces, cat_axis)`` without materialising the
+    concatenation (pieces are mmapped Meta shards)."""
+    if len(pieces) == 1:
+        return pieces[0].narrow(axis, lo, hi - lo)
+    if axis != cat_axis:
+        return torch.cat([p.narrow(axis, lo, hi - lo) for p in pieces], cat_axis)
+    out, start = [], 0
+    for p in pieces:
+        n = p.shape[axis]
+        a, b = max(lo, start), min(hi, start + n)
+        if a < b:
+            out.append(p.narrow(axis, a - start, b - a))
+        start += n
+    return out[0] if len(out) == 1 else torch.cat(out, axis)
+
+
+def load_meta_rank(ckpt_dir: str, tokenizer, rank: int, size: int, max_seq_len: int = 2048,
+                   dtype: Optional[torch.dtype] = torch.bfloat16, verbose: bool = False):
+    """This TP rank's parameters straight from Meta ``consolidated.XX.pth`` shards.
+
+    Each tensor is read as the slices the rank needs (Megatron split of ``partition.py:62-78``:
+    wq/wk/wv/w1/w3/output column-parallel, wo/w2 row-parallel, embedding and norms replicated)
+    from the mmapped shards, whatever the checkpoint's own MP degree -- so 8 ranks loading a
+    70B model touch ~1/8 of the bytes each instead of 8 full host copies (the reference merges
+    everything to fp32 on the host first, convert_weights.py:66-89). Returns
+    ``(params, config)`` with ``params`` ready for ``model.load_params(params, sharded=True)``."""
+    shards, params_json = load_meta_shards(ckpt_dir, verbose)
+    vocab = tokenizer if isinstance(tokenizer, int) else len(tokenizer)
+    config = config_from_params_json(params_json, vocab, max_seq_len)
+    n = len(shards)
+    emb = [s["tok_embeddings.weight"] for s in shards]
+    if n > 1:
+        d_s, v_s = emb[0].shape[1], emb[0].shape[0]
+        emb_axis = 1 if all(e.shape[0] == v_s for e in emb) and shards[0]["norm.weight"].shape[0] == d_s * n else 0
+    else:
+        emb_axis = 0
+
+    def cvt(t):
+        return t.contiguous() if dtype is None else t.to(dtype).contiguous()
+
+    def col(key):  # [out, in] split on out
+        pieces = [s[key] for s in shards]
+        total = sum(p.shape[0] for p in pieces)
+        c = total // size
+        return cvt(_global_slice(pieces, 0, 0, rank * c, (rank + 1) * c))
+
+    def row(key):  # [out, in] split on in
+        pieces = [s[key] for s in shards]
+        total = sum(p.shape[1] for p in pieces)
+        c = total // size
+        return cvt(_global_slice(pieces, 1, 1, rank * c, (rank + 1) * c))
+
+    sd = {"tok_embeddings.weight": cvt(_cat(emb, emb_axis, None)),
+          "norm.weight": cvt(shards[0]["norm.weight"]),
+          "output.weight": col("output.weight")}
+    for i in range(config.num_hidden_layers):
+        pre = f"layers.{i}."
+        for name in _COL:
+            sd[pre + name + ".weight"] = col(pre + name + ".weight")
+        for name in _ROW:
+            sd[pre + name + ".weight"] = row(pre + name + ".weight")
+        for name in ("attention_norm", "ffn_norm"):
+            sd[pre + name + ".weight"] = cvt(shards[0][pre + name + ".weight"])
+    return meta_state_dict_to_params(sd, config.num_hidden_layers), config

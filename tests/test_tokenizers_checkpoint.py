@@ -157,6 +157,23 @@ def test_convert_meta_checkpoint(tmp_path, n_shards, vocab_parallel):
         assert torch.equal(torch.as_tensor(got).to(v.dtype), torch.as_tensor(v)), k
 
 
+@pytest.mark.parametrize("n_shards,tp", [(1, 2), (2, 2), (4, 2), (2, 4), (4, 1), (2, 1)])
+def test_load_meta_rank_equals_sharded_merge(tmp_path, n_shards, tp):
+    from jax_llama_amd.utils.checkpoint import load_meta_rank
+    cfg = tiny_config(num_key_value_heads=4, intermediate_size=96)
+    sd = random_meta_state_dict(cfg, seed=6)
+    save_meta_checkpoint(sd, params_json_for(cfg, multiple_of=32), str(tmp_path), n_shards=n_shards,
+                         vocab_parallel_embedding=(n_shards == 4))
+    full, _ = convert_llama_weights(str(tmp_path), cfg.vocab_size, max_seq_len=64)
+    for r in range(tp):
+        got, config = load_meta_rank(str(tmp_path), cfg.vocab_size, r, tp, max_seq_len=64, dtype=None)
+        want = shard_tree(full, r, tp)
+        for k, v in _flat_items(want):
+            g = torch.as_tensor(_get(got, k))
+            assert g.shape == torch.as_tensor(v).shape, k
+            assert torch.equal(g, torch.as_tensor(v)), k
+
+
 def _flat(t, pre=()):
     out = []
     for k, v in t.items():
@@ -235,3 +252,20 @@ def test_generate_from_str_semantics(llama3_tok):
     seq = gen.generate(t, (t != tok.eos_id).int(), max_gen_len=6, temperature=0.0)
     assert seq.shape == (2, s + 6)
     assert torch.equal(seq[:, :s].int(), t)
+
+
+def test_example_cli_end_to_end(tmp_path, llama3_tok):
+    """examples/generate.py main(): Meta checkpoint + tokenizer -> completions (CPU path)."""
+    import importlib.util
+    tok_path = str(tmp_path / "tokenizer.model")
+    save_tiktoken_bpe(llama3_tok.model.mergeable_ranks, tok_path)
+    cfg = tiny_config(vocab_size=len(llama3_tok), num_hidden_layers=2)
+    sd = random_meta_state_dict(cfg, seed=4)
+    save_meta_checkpoint(sd, params_json_for(cfg, multiple_of=32), str(tmp_path / "ckpt"), n_shards=2,
+                         vocab_parallel_embedding=True)
+    spec = importlib.util.spec_from_file_location("gen_example", os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "examples", "generate.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    outs = mod.main(str(tmp_path / "ckpt"), tok_path, True, max_gen_len=4, temperature=0.0)
+    assert len(outs) == 2 and outs[0].startswith("<|begin_of_text|>" + mod.PROMPTS[0])

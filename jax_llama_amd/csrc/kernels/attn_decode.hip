@@ -103,10 +103,7 @@ __global__ void __launch_bounds__(AD_WAVES * 64)
         float d = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) d += qf[h][e] * kf[e];
-        d += __shfl_xor(d, 1, 64);
-        d += __shfl_xor(d, 2, 64);
-        d += __shfl_xor(d, 4, 64);
-        d += __shfl_xor(d, 8, 64);
+        d = row16_sum(d);  // DPP: every lane of the 16-lane row gets the full dot product
         sc[h][r] = valid ? d : -INFINITY;
       }
     }
@@ -209,22 +206,49 @@ __global__ void __launch_bounds__(AD_WAVES * 64)
   __syncthreads();
   if (!last_flag) return;
 
-  // ---- last arriver: merge all splits of this (b, kv head) with sc1 loads
+  // ---- last arriver: merge all splits of this (b, kv head) with sc1 loads, in parallel:
+  // (1) every (split, head) max/sum loaded by its own thread, (2) per-head weights in LDS,
+  // (3) each (head, d) thread sums the splits' o with independent loads (8 in flight).
   const float* base = ws + ((size_t)b * Hkv + kvh) * nsplit * REP * (AD_DH + 2);
+  float* wsh = &red_o[0][0][0];  // reuse: [nsplit][REP] weights (nsplit * REP <= 4 * REP * 128)
+  for (int i = threadIdx.x; i < nsplit * REP; i += AD_WAVES * 64) wsh[i] = ld_wt(base + (size_t)i * (AD_DH + 2));
+  __syncthreads();
+  if (threadIdx.x < REP) {
+    const int h = threadIdx.x;
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, wsh[s * REP + h]);
+    red_m[0][h] = M;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nsplit * REP; i += AD_WAVES * 64) {
+    const float M = red_m[0][i % REP], m = wsh[i];
+    wsh[i] = (m == -INFINITY || M == -INFINITY) ? 0.f : __expf(m - M);
+  }
+  __syncthreads();
   for (int i = threadIdx.x; i < REP * AD_DH; i += AD_WAVES * 64) {
     const int h = i / AD_DH, d = i - h * AD_DH;
-    float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ld_wt(base + ((size_t)s * REP + h) * (AD_DH + 2)));
     float num = 0.f, den = 0.f;
-    if (M != -INFINITY) {
-      for (int s = 0; s < nsplit; ++s) {
-        const float* ps = base + ((size_t)s * REP + h) * (AD_DH + 2);
-        const float m = ld_wt(ps);
-        if (m == -INFINITY) continue;
-        const float f = __expf(m - M);
-        den += f * ld_wt(ps + 1);
-        num += f * ld_wt(ps + 2 + d);
+    int s = 0;
+    for (; s + 8 <= nsplit; s += 8) {
+      float ov[8], lv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float* ps = base + ((size_t)(s + q) * REP + h) * (AD_DH + 2);
+        lv[q] = ld_wt(ps + 1);
+        ov[q] = ld_wt(ps + 2 + d);
       }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float f = wsh[(s + q) * REP + h];
+        den += f * lv[q];
+        num += f * ov[q];
+      }
+    }
+    for (; s < nsplit; ++s) {
+      const float* ps = base + ((size_t)s * REP + h) * (AD_DH + 2);
+      const float f = wsh[s * REP + h];
+      den += f * ld_wt(ps + 1);
+      num += f * ld_wt(ps + 2 + d);
     }
     out[((size_t)b * H + h0 + h) * AD_DH + d] = f2bf(den > 0.f ? num / den : 0.f);
   }

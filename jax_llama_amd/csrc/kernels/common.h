@@ -90,6 +90,20 @@ JLA_DEV float block_sum(float v, float* red) {
 
 JLA_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 
+// DPP lane moves within a 16-lane row (no LDS traffic, unlike __shfl_xor's ds_bpermute).
+template <int CTRL>
+JLA_DEV float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of each row; every lane receives the row total.
+JLA_DEV float row16_sum(float v) {
+  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]  (xor 1)
+  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]  (xor 2)
+  v += dppf<0x141>(v);  // row_half_mirror      (other quad of the 8-lane half)
+  v += dppf<0x140>(v);  // row_mirror           (other half of the row)
+  return v;
+}
+
 // Host-side error check used by every launcher.
 #define JLA_CHECK_LAUNCH()                                                        \
   do {                                                                            \

@@ -35,7 +35,15 @@ T* ptr(const Tensor& t) {
 const jla::bf16_t* cbf(const Tensor& t) { return reinterpret_cast<const jla::bf16_t*>(t.data_ptr()); }
 jla::bf16_t* bf(const Tensor& t) { return reinterpret_cast<jla::bf16_t*>(t.data_ptr()); }
 
-void embedding(Tensor ids, Tensor table, Tensor out) {
+// optional bf16 mirror of an fp32 residual-stream tensor (same element count)
+jla::bf16_t* mirror_ptr(const c10::optional<Tensor>& mirror, int64_t numel) {
+  if (!mirror.has_value()) return nullptr;
+  check_gpu(*mirror, "mirror");
+  check(mirror->scalar_type() == torch::kBFloat16 && mirror->numel() == numel, "mirror must be bf16, same shape");
+  return bf(*mirror);
+}
+
+void embedding(Tensor ids, Tensor table, Tensor out, c10::optional<Tensor> mirror) {
   check_gpu(ids, "ids");
   check_gpu(table, "table");
   check_gpu(out, "out");
@@ -44,7 +52,9 @@ void embedding(Tensor ids, Tensor table, Tensor out) {
         "embedding dtypes");
   const int M = ids.numel(), D = table.size(1), V = table.size(0);
   check(out.numel() == (int64_t)M * D, "embedding out shape");
-  rc(jla::embedding(ptr<int32_t>(ids), cbf(table), ptr<float>(out), M, D, V, stream()), "embedding");
+  rc(jla::embedding(ptr<int32_t>(ids), cbf(table), ptr<float>(out), mirror_ptr(mirror, out.numel()), M, D, V,
+                    stream()),
+     "embedding");
 }
 
 void rms_scale(Tensor x, Tensor out, double eps) {
@@ -108,7 +118,7 @@ void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* ou
 }
 
 void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, double rms_eps,
-                   bool accumulate, int64_t variant, Tensor ws, Tensor tickets) {
+                   bool accumulate, int64_t variant, Tensor ws, Tensor tickets, c10::optional<Tensor> mirror) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
@@ -117,7 +127,9 @@ void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_skinny: M too large");
   check_linear_out(out, m, n, mode);
-  run_skinny(x, w, n, k, out.data_ptr(), mode, rms_eps, accumulate, out.scalar_type() == torch::kFloat32, nullptr,
+  jla::QKVArgs qa{};
+  qa.res_bf16 = mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr;
+  run_skinny(x, w, n, k, out.data_ptr(), mode, rms_eps, accumulate, out.scalar_type() == torch::kFloat32, &qa,
              variant, ws, tickets);
 }
 
@@ -163,14 +175,16 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
   run_skinny(x, w, n, k, nullptr, MODE_QKV_ID, rms_eps, false, false, &qa, variant, ws, tickets);
 }
 
-void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate) {
+void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate,
+          c10::optional<Tensor> mirror) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
   const int64_t m = x.size(0);
   check_linear_out(out, m, n, mode);
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-               out.scalar_type() == torch::kFloat32, stream()),
+               out.scalar_type() == torch::kFloat32, mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr,
+               stream()),
      "gemm");
 }
 
@@ -276,11 +290,15 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "jax_llama_amd gfx950 (MI355X) HIP kernels";
   m.attr("SKINNY_MAX_M") = SKINNY_MAX_M;
   m.attr("ARCH") = "gfx950";
-  m.def("embedding", &embedding);
+  m.def("embedding", &embedding, py::arg("ids"), py::arg("table"), py::arg("out"),
+        py::arg("mirror") = py::none());
   m.def("rms_scale", &rms_scale);
   m.def("rmsnorm", &rmsnorm);
-  m.def("linear_skinny", &linear_skinny);
-  m.def("gemm", &gemm);
+  m.def("linear_skinny", &linear_skinny, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"),
+        py::arg("mode"), py::arg("rms_eps"), py::arg("accumulate"), py::arg("variant"), py::arg("ws"),
+        py::arg("tickets"), py::arg("mirror") = py::none());
+  m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
+        py::arg("accumulate"), py::arg("mirror") = py::none());
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_decode_splits",
         [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });

@@ -25,7 +25,7 @@ constexpr int G_STAGE_U4 = (G_AFR + G_BFR) * 64;  // u32x4 per stage (32 KiB); 8
 template <int MODE>
 __global__ void __launch_bounds__(G_THREADS)
     gemm_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                int K, int accumulate, int out_f32) {
+                int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror) {
   __shared__ u32x4 lds[2][G_STAGE_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
@@ -144,7 +144,9 @@ __global__ void __launch_bounds__(G_THREADS)
           const float v = acc[i][j][r];
           if (MODE == MODE_RESIDUAL) {
             float* o = static_cast<float*>(out);
-            o[idx] = accumulate ? o[idx] + v : v;
+            const float nv = accumulate ? o[idx] + v : v;
+            o[idx] = nv;
+            if (mirror) mirror[idx] = f2bf(nv);
           } else if (out_f32) {
             static_cast<float*>(out)[idx] = v;
           } else {
@@ -156,16 +158,22 @@ __global__ void __launch_bounds__(G_THREADS)
 }
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
-         hipStream_t s) {
+         bf16_t* mirror, hipStream_t s) {
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M);
   const u32x4* w = static_cast<const u32x4*>(W);
   switch (mode) {
-    case MODE_STORE: gemm_kernel<MODE_STORE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32); break;
-    case MODE_RESIDUAL: gemm_kernel<MODE_RESIDUAL><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 1); break;
-    case MODE_SWIGLU: gemm_kernel<MODE_SWIGLU><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 0); break;
+    case MODE_STORE:
+      gemm_kernel<MODE_STORE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, nullptr);
+      break;
+    case MODE_RESIDUAL:
+      gemm_kernel<MODE_RESIDUAL><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 1, mirror);
+      break;
+    case MODE_SWIGLU:
+      gemm_kernel<MODE_SWIGLU><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 0, nullptr);
+      break;
     default: return -1;
   }
   JLA_CHECK_LAUNCH();

@@ -160,7 +160,10 @@ __global__ void __launch_bounds__(NW * 64)
   u32x4 bq[U][NT] = {};
   XRaw<XT> aq[U][MT] = {};
   constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
-  constexpr bool ASM = MT == 1;                  // hand-counted ring (see asm_load_nt)
+  // hand-counted ring (see asm_load_nt) where the assembly check passes: every bf16-activation
+  // variant (the decode path: the residual stream's bf16 mirror) and fp32 at MT = 1
+  // (bf16 MT = 2 with one tile fails the check: hipcc reuses in-flight ring registers there).
+  constexpr bool ASM = MT == 1 || (sizeof(XT) == 2 && !(MT == 2 && NT == 1));
   auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
     const bool valid = i < n;
     const size_t ks = (size_t)(w + i * NW);
@@ -193,7 +196,18 @@ __global__ void __launch_bounds__(NW * 64)
       issue(i0 + U + u, bq[u], aq[u]);  // refill: k-step U ahead (zero fragment past the end)
     }
   }
-  if constexpr (ASM) wait_vmcnt<0>();  // retire the past-the-end refills before the registers are reused
+  if constexpr (ASM) {
+    // retire the past-the-end refills, and keep every ring register live until then: a register
+    // the compiler thinks is dead could otherwise be reused while its load is still in flight
+    wait_vmcnt<0>();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) pin(bq[u][t]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+    }
+  }
 
   // ---- cross-wave reduction through LDS
 #pragma unroll
@@ -281,7 +295,9 @@ __global__ void __launch_bounds__(NW * 64)
         const size_t idx = (size_t)m * N + col;
         if constexpr (MODE == MODE_RESIDUAL) {
           float* o = static_cast<float*>(out);
-          o[idx] = accumulate ? o[idx] + v : v;
+          const float nv = accumulate ? o[idx] + v : v;
+          o[idx] = nv;
+          if (qa.res_bf16) qa.res_bf16[idx] = f2bf(nv);
         } else {
           if (out_f32)
             static_cast<float*>(out)[idx] = v;
@@ -299,7 +315,7 @@ static int launch_skinny(const void* x, const void* W, void* out, int M, int N, 
   // k-steps in flight per wave: 8 KiB of weights per wave at MT = 1; fp32 activations double the
   // activation registers, so MT > 1 keeps fewer steps in flight to stay spill-free.
   constexpr int U0 = (NT == 1) ? 8 : 4;
-  constexpr int UD = (sizeof(XT) == 4 && MT > 1) ? MT : (MT > 2 ? 2 : 1);
+  constexpr int UD = MT;
   constexpr int U = (U0 / UD) < 2 ? 2 : (U0 / UD);
   const int NTT = N >> 4;
   const int grid = (NTT + NT - 1) / NT;

@@ -9,7 +9,8 @@
 namespace jla {
 typedef uint16_t bf16_t;
 
-int embedding(const int32_t* ids, const bf16_t* table, float* out, int M, int D, int V, hipStream_t s);
+int embedding(const int32_t* ids, const bf16_t* table, float* out, bf16_t* mirror, int M, int D, int V,
+              hipStream_t s);
 int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
 
@@ -23,6 +24,7 @@ struct QKVArgs {
   const int32_t* slot;        // device int32[1]: cache slot of sequence position 0
   int S, H, Hkv, Dh, T;       // tokens per sequence in this call, heads, kv heads, head dim, cache len
   bf16_t* q;                  // [M, H, Dh] rotated queries
+  bf16_t* res_bf16;           // MODE_RESIDUAL: optional bf16 mirror of the updated residual (next A operand)
 };
 
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
@@ -35,7 +37,7 @@ int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, 
                   int accumulate, int out_f32, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
                   int n_tickets, hipStream_t s);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
-         hipStream_t s);
+         bf16_t* mirror, hipStream_t s);
 
 int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,

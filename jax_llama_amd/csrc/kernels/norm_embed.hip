@@ -12,24 +12,29 @@ namespace jla {
 // one block per row; 16-byte vectorised bf16 loads, fp32 stores
 __global__ void __launch_bounds__(256) embedding_kernel(const int32_t* __restrict__ ids,
                                                         const bf16_t* __restrict__ table,
-                                                        float* __restrict__ out, int D, int V) {
+                                                        float* __restrict__ out, bf16_t* __restrict__ mirror,
+                                                        int D, int V) {
   const int row = blockIdx.x;
   int id = ids[row];
   id = id < 0 ? 0 : (id >= V ? V - 1 : id);
   const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * D);
   float4* dst = reinterpret_cast<float4*>(out + (size_t)row * D);
+  u32x4* mdst = mirror ? reinterpret_cast<u32x4*>(mirror + (size_t)row * D) : nullptr;
   for (int i = threadIdx.x; i < D / 8; i += blockDim.x) {
+    const u32x4 v = src[i];
     float f[8];
-    unpack8(src[i], f);
+    unpack8(v, f);
     dst[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
     dst[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+    if (mdst) mdst[i] = v;  // bf16 mirror of the residual stream (exact: rows are bf16)
   }
 }
 
-int embedding(const int32_t* ids, const bf16_t* table, float* out, int M, int D, int V, hipStream_t s) {
+int embedding(const int32_t* ids, const bf16_t* table, float* out, bf16_t* mirror, int M, int D, int V,
+              hipStream_t s) {
   if (D % 8) return -1;
   if (M == 0) return 0;
-  embedding_kernel<<<M, 256, 0, s>>>(ids, table, out, D, V);
+  embedding_kernel<<<M, 256, 0, s>>>(ids, table, out, mirror, D, V);
   JLA_CHECK_LAUNCH();
   return 0;
 }

@@ -145,7 +145,11 @@ __global__ void __launch_bounds__(SK_NW * 64)
       }
     }
   }
-  sk_wait<0>();  // retire the zero-fragment refills
+  sk_wait<0>();  // retire the zero-fragment refills; ring registers stay live until here
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) sk_pin(bq[u][t]);
 
   // ---- split-K: publish partial tile (write-through sc1 stores), last arriver reduces in order
   if (sa.ksplit > 1) {
@@ -265,7 +269,9 @@ __global__ void __launch_bounds__(SK_NW * 64)
             const size_t idx = (size_t)m * N + tile * 16 + c;
             if constexpr (MODE == MODE_RESIDUAL) {
               float* o = static_cast<float*>(out);
-              o[idx] = accumulate ? o[idx] + v : v;
+              const float nv = accumulate ? o[idx] + v : v;
+              o[idx] = nv;
+              if (qa.res_bf16) qa.res_bf16[idx] = f2bf(nv);
             } else {
               if (out_f32)
                 static_cast<float*>(out)[idx] = v;

@@ -232,14 +232,17 @@ class LLaMAForCausalLM:
                        self.head_dim, self.device)
 
     # ------------------------------------------------------------------ core forward
-    def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor) -> None:
+    def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor, hb: torch.Tensor) -> None:
         """``h += x @ W^T`` where W is row-sharded: every rank adds its partial sum; the
-        residual is added exactly once (rank 0) before the all-reduce."""
+        residual is added exactly once (rank 0) before the all-reduce. ``hb`` is the bf16
+        mirror of ``h`` that the next projection reads (written by the GEMM epilogue at TP=1,
+        re-cast after the all-reduce otherwise)."""
         if self.comm.size == 1:
-            ops.linear_residual(x, w, h)
+            ops.linear_residual(x, w, h, mirror=hb)
         else:
             ops.linear_residual(x, w, h, accumulate=(self.comm.rank == 0))
             self.comm.all_reduce_(h)
+            hb.copy_(h)
 
     def forward_tokens(self, ids: torch.Tensor, positions: torch.Tensor, cache: KVCache, slot0,
                        kv_start: torch.Tensor, key_mask: Optional[torch.Tensor] = None,
@@ -252,13 +255,16 @@ class LLaMAForCausalLM:
         vocab shard: ``[B, V/tp]`` ("last"), ``[B*S, V/tp]`` ("all") or None ("none")."""
         b, s = ids.shape
         d = self.config.hidden_size
-        h = ops.embedding(ids.reshape(-1), self.wte)
+        # residual stream: fp32 h plus its bf16 mirror hb (the A operand of every projection
+        # that follows a norm; RMSNorm statistics are taken from these bf16 values)
+        hb = torch.empty(b * s, d, dtype=BF16, device=self.device)
+        h = ops.embedding(ids.reshape(-1), self.wte, mirror=hb)
         hidden, attns = [], []
         for i, lw in enumerate(self.layers):
             if collect_hidden:
                 hidden.append(h.reshape(b, s, d).clone())
             kc, vc = cache.layer(i)
-            q = ops.linear_qkv_rope(h, lw.qkv, self.eps, self.rope, positions, kc, vc, slot0, s,
+            q = ops.linear_qkv_rope(hb, lw.qkv, self.eps, self.rope, positions, kc, vc, slot0, s,
                                     self.n_heads, self.n_kv_heads, self.head_dim)
             q4 = q.reshape(b, s, self.n_heads, self.head_dim)
             if collect_attn:
@@ -268,13 +274,13 @@ class LLaMAForCausalLM:
                 attns.append(w)
             else:
                 a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask)
-            self._row_parallel(a, lw.o, h)
-            g = ops.linear_swiglu(h, lw.gu, rms_eps=self.eps)
-            self._row_parallel(g, lw.down, h)
+            self._row_parallel(a, lw.o, h, hb)
+            g = ops.linear_swiglu(hb, lw.gu, rms_eps=self.eps)
+            self._row_parallel(g, lw.down, h, hb)
         if logits_mode == "none":
             logits = None
         else:
-            hl = h if logits_mode == "all" else h.reshape(b, s, d)[:, -1].contiguous()
+            hl = hb if logits_mode == "all" else hb.reshape(b, s, d)[:, -1].contiguous()
             logits = ops.linear(hl, self.lm_head, rms_eps=self.eps, out_dtype=torch.float32)
         return logits, h, hidden, attns
 

@@ -67,12 +67,17 @@ workspace = _Workspace()
 
 
 # ----------------------------------------------------------------------------------
-def embedding(ids: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
-    """ids int32 [M] -> fp32 [M, D] rows of the bf16 table (residual stream is fp32)."""
+def embedding(ids: torch.Tensor, table: torch.Tensor, mirror: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ids int32 [M] -> fp32 [M, D] rows of the bf16 table (residual stream is fp32).
+    ``mirror`` (bf16 [M, D]) also receives the rows: the bf16 copy of the residual stream that
+    the next projection reads as its MFMA A operand."""
     if not _is_gpu(table):
-        return ref.embedding(ids, table)
+        out = ref.embedding(ids, table)
+        if mirror is not None:
+            mirror.copy_(out.to(BF16))
+        return out
     out = torch.empty(ids.numel(), table.shape[1], dtype=torch.float32, device=table.device)
-    ext().embedding(ids.reshape(-1).to(torch.int32), table, out)
+    ext().embedding(ids.reshape(-1).to(torch.int32), table, out, mirror)
     return out
 
 
@@ -111,11 +116,15 @@ def linear(x: torch.Tensor, w, rms_eps: Optional[float] = None, out_dtype=BF16,
 
 
 def linear_residual(x: torch.Tensor, w, residual: torch.Tensor, rms_eps: Optional[float] = None,
-                    accumulate: bool = True) -> torch.Tensor:
-    """``residual (fp32) += y`` (or ``= y`` when ``accumulate`` is False)."""
+                    accumulate: bool = True, mirror: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``residual (fp32) += y`` (or ``= y`` when ``accumulate`` is False); ``mirror`` (bf16,
+    same shape) receives ``bf16(residual)`` from the same epilogue."""
     if not _is_gpu(x):
-        return ref.linear_residual(x, w.dense(), residual, rms_eps, accumulate)
-    _gpu_linear(x, w, residual, MODE_RESIDUAL, rms_eps, accumulate)
+        ref.linear_residual(x, w.dense(), residual, rms_eps, accumulate)
+        if mirror is not None:
+            mirror.copy_(residual.to(BF16))
+        return residual
+    _gpu_linear(x, w, residual, MODE_RESIDUAL, rms_eps, accumulate, mirror)
     return residual
 
 
@@ -128,7 +137,7 @@ def linear_swiglu(x: torch.Tensor, w, rms_eps: Optional[float] = None) -> torch.
     return out
 
 
-def _gpu_linear(x, w, out, mode, rms_eps, accumulate):
+def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None):
     assert x.is_contiguous() and out.is_contiguous()
     assert x.shape[1] == w.k, (x.shape, w.k)
     m = x.shape[0]
@@ -136,15 +145,15 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate):
     if m > e.SKINNY_MAX_M:
         # Large-M (prefill) path: bf16 normalised activations, then the MFMA tiled GEMM.
         if rms_eps is not None:
-            x = rms_scale(x, rms_eps)
+            x = rms_scale(x.float() if x.dtype != torch.float32 else x, rms_eps)
         elif x.dtype != BF16:
             x = x.to(BF16)
-        e.gemm(x, w.weight, w.n, w.k, out, mode, bool(accumulate))
+        e.gemm(x, w.weight, w.n, w.k, out, mode, bool(accumulate), mirror)
     else:
         ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
                         -1.0 if rms_eps is None else float(rms_eps), bool(accumulate),
-                        _variant(e, x, w, mode), ws, tk)
+                        _variant(e, x, w, mode), ws, tk, mirror)
 
 
 def _variant(e, x, w, mode) -> int:

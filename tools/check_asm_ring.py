@@ -1,15 +1,24 @@
 #!/usr/bin/env python3
-"""Static check of the hand-counted load rings in the GEMV kernels.
+"""Static check of the hand-counted load rings (inline-asm `global_load`s) in the decode kernels.
 
-Inline-asm loads are invisible to hipcc's waitcnt bookkeeping, so a compiler-inserted copy of a
-ring register between its asm load and the covering `s_waitcnt vmcnt` would read stale data.
-This scans the device assembly of every kernel in a .s file: for each VGPR written by an asm
-`global_load_*`, any instruction that reads it before the next `s_waitcnt vmcnt(...)` (which,
-by construction of the ring, is the first wait that can cover it) is reported.
-Usage: python tools/check_asm_ring.py file.s  (exit status 1 if a hazard is found)
+Inline-asm loads are invisible to hipcc's waitcnt bookkeeping, so any compiler-generated
+instruction that touches an asm-load destination register (reads it, or writes it: the load's late
+arrival would clobber the new value) before the `s_waitcnt vmcnt(N)` that retires that load is a
+hazard (stale data / corrupted register). This scans the device assembly of every kernel:
+
+  * outstanding vector-memory ops are an ordered queue (issue order); `s_waitcnt vmcnt(N)` retires
+    all but the newest N (stores and atomics count too, as on CDNA4);
+  * control flow: the state at a label is the union of the fall-through state and the states at
+    every branch that targets it (forward branches in the same pass, back-edges from a first
+    pass); code after an unconditional `s_branch` is only entered through its label.
+
+Usage: python tools/check_asm_ring.py file.s   (exit status 1 if any hazard is found)
 """
 import re
 import sys
+
+_VMEM = ("global_load", "buffer_load", "global_store", "buffer_store", "global_atomic", "buffer_atomic",
+         "flat_load", "flat_store")
 
 
 def regs(tok):
@@ -20,15 +29,30 @@ def regs(tok):
     return {int(m.group(1))} if m else set()
 
 
+def _merge(a, b):
+    """Union of two queues (pessimistic): keep the longer one's order, add missing asm entries."""
+    if a is None:
+        return None if b is None else list(b)
+    if b is None:
+        return list(a)
+    out = list(a) if len(a) >= len(b) else list(b)
+    other = b if out is a else a
+    have = set()
+    for r, asm in out:
+        have |= r
+    for r, asm in other:
+        if asm and not (r <= have):
+            out.insert(0, (r, asm))  # oldest position: retired first, i.e. least pessimistic
+    return out
+
+
 def scan(body, seed):
-    """One linear pass over a kernel. Outstanding vector-memory ops are an ordered queue (issue
-    order); `s_waitcnt vmcnt(N)` retires all but the newest N. `seed` maps a loop label to the
-    queue at its back-edge. Returns (hazards, queue-at-backedge per label)."""
-    queue = []  # list of (set(regs) or empty, is_asm)
+    queue = []           # list of (set(regs), is_asm); None = unreachable
+    pending_in = {k: list(v) for k, v in seed.items()}
     in_asm = False
     hazards = []
     back = {}
-    labels_seen = set()
+    seen = set()
     for i, line in enumerate(body):
         s = line.strip()
         if s.startswith(";;#ASMSTART"):
@@ -39,47 +63,53 @@ def scan(body, seed):
             continue
         lm = re.match(r"^(\.LBB\w+):", s)
         if lm:
-            labels_seen.add(lm.group(1))
-            if lm.group(1) in seed:
-                queue = list(seed[lm.group(1)]) + queue
+            lab = lm.group(1)
+            seen.add(lab)
+            queue = _merge(queue, pending_in.get(lab))
             continue
         if not s or s.startswith(";") or s.startswith("."):
             continue
+        if queue is None:
+            continue  # unreachable by fall-through
         op = s.split()[0]
         args = [a.strip() for a in s[len(op):].split(",")]
         if op.startswith("s_cbranch") or op == "s_branch":
             tgt = args[0].split()[0] if args else ""
-            if tgt in labels_seen:
-                back[tgt] = list(queue)
+            if tgt in seen:
+                back[tgt] = _merge(back.get(tgt), queue)
+            else:
+                pending_in[tgt] = _merge(pending_in.get(tgt), queue)
+            if op == "s_branch":
+                queue = None
             continue
         if op.startswith("s_waitcnt") and "vmcnt" in s:
             n = int(re.search(r"vmcnt\((\d+)\)", s).group(1))
             while len(queue) > n:
                 queue.pop(0)
             continue
-        # reads of pending asm-load destinations
-        if op.startswith("global_load") or op.startswith("buffer_load"):
-            srcs = regs(args[1].split()[0]) if len(args) > 1 else set()
-        elif op.startswith("global_store") or op.startswith("buffer_store"):
-            srcs = set()
-            for a in args[:2]:
-                srcs |= regs(a.split()[0])
+        if op.startswith("s_") or op.startswith("ds_"):
+            touched = set()
+            if op.startswith("ds_"):
+                for a in args:
+                    if a:
+                        touched |= regs(a.split()[0])
         else:
-            srcs = set()
-            for a in args[1:]:
+            touched = set()
+            for a in args:
                 if a:
-                    srcs |= regs(a.split()[0])
+                    touched |= regs(a.split()[0])
+            if op.startswith(_VMEM) and in_asm:
+                touched -= regs(args[0])  # the asm load's own destination (tied operand)
         pend = set()
         for r_, asm in queue:
             if asm:
                 pend |= r_
-        hit = srcs & pend
+        hit = touched & pend
         if hit:
             hazards.append((i, s, sorted(hit)[0]))
-        if op.startswith(("global_load", "buffer_load")):
-            queue.append((regs(args[0]) if in_asm else set(), in_asm))
-        elif op.startswith(("global_store", "buffer_store", "global_atomic", "buffer_atomic")):
-            queue.append((set(), False))
+        if op.startswith(_VMEM):
+            is_load = "load" in op
+            queue.append((regs(args[0]) if (in_asm and is_load) else set(), in_asm and is_load))
     return hazards, back
 
 
@@ -89,12 +119,14 @@ def check(path):
     for km in re.finditer(r"^(_Z\S+):", text, re.M):
         name = km.group(1)
         end = text.find(".Lfunc_end", km.end())
+        if end < 0:
+            continue
         body = text[km.end():end].split("\n")
         _, back = scan(body, {})
         hazards, _ = scan(body, back)
         for i, s, r in hazards:
             bad += 1
-            print(f"{name[:90]}: line {i}: '{s}' reads asm-load dest v{r} before a vmcnt wait")
+            print(f"{name[:90]}: line {i}: '{s}' touches asm-load dest v{r} before its vmcnt wait")
     return bad
 
 

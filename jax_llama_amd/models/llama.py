@@ -33,6 +33,7 @@ from ..ops import reference as ref
 from ..parallel.comm import NO_COMM, TPComm
 from ..parallel.partition import shard_tree
 from .kv_cache import KVCache
+from .modules import LLaMABlockCollection
 from .weights import PackedLinear
 
 BF16 = torch.bfloat16
@@ -143,6 +144,7 @@ class LLaMAForCausalLM:
         self.ln_f: Optional[torch.Tensor] = None
         self.lm_head: Optional[PackedLinear] = None
         self.layers: List[LayerWeights] = [LayerWeights() for _ in range(c.num_hidden_layers)]
+        self.blocks = LLaMABlockCollection(self)  # reference FlaxLLaMABlockCollection (model.py:548)
         self._params_id = None
 
     # ------------------------------------------------------------------ weights
@@ -259,24 +261,8 @@ class LLaMAForCausalLM:
         # that follows a norm; RMSNorm statistics are taken from these bf16 values)
         hb = torch.empty(b * s, d, dtype=BF16, device=self.device)
         h = ops.embedding(ids.reshape(-1), self.wte, mirror=hb)
-        hidden, attns = [], []
-        for i, lw in enumerate(self.layers):
-            if collect_hidden:
-                hidden.append(h.reshape(b, s, d).clone())
-            kc, vc = cache.layer(i)
-            q = ops.linear_qkv_rope(hb, lw.qkv, self.eps, self.rope, positions, kc, vc, slot0, s,
-                                    self.n_heads, self.n_kv_heads, self.head_dim)
-            q4 = q.reshape(b, s, self.n_heads, self.head_dim)
-            if collect_attn:
-                s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
-                a, w = ref.attention(q4, kc, vc, s0, kv_start, key_mask, return_weights=True)
-                a = a.reshape(b * s, -1)
-                attns.append(w)
-            else:
-                a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask)
-            self._row_parallel(a, lw.o, h, hb)
-            g = ops.linear_swiglu(hb, lw.gu, rms_eps=self.eps)
-            self._row_parallel(g, lw.down, h, hb)
+        hidden, attns = self.blocks(h, hb, positions, cache, slot0, kv_start, key_mask, s,
+                                    output_hidden_states=collect_hidden, output_attentions=collect_attn)
         if logits_mode == "none":
             logits = None
         else:

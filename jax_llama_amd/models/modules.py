@@ -1,0 +1,101 @@
+"""Decoder building blocks with the reference's module structure.
+
+Reference (``/root/reference/jax_llama/model.py``): ``FlaxLLaMAAttention`` (:105-300),
+``FlaxLLaMAMLP`` (:302-340), ``FlaxLLaMABlock`` (:342-400), ``FlaxLLaMABlockCollection`` (:548-600).
+Here each block is a thin, stateless view over one layer's packed weights that issues the fused
+MI355X ops -- the parameters live in ``LLaMAForCausalLM.layers`` so TP sharding, the packed MFMA
+layout and hipGraph capture see one flat set of tensors:
+
+  attention: [RMSNorm folded] qkv GEMV/GEMM + RoPE + KV-cache write (one kernel in decode), cache
+             attention (split-KV decode / flash prefill, GQA by indexing), wo with the residual add
+             fused into its epilogue (+ TP all-reduce)                       -- model.py:383-392
+  mlp:       [RMSNorm folded] w1|w3 GEMV/GEMM with SiLU*up epilogue, w2 with the residual add
+             (+ TP all-reduce)                                               -- model.py:394-398
+
+The residual stream is ``h`` (fp32) plus its bf16 mirror ``hb`` (the A operand of the next
+projection, written by the residual epilogues).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+
+
+class LLaMAAttention:
+    def __init__(self, model, layer_idx: int):
+        self.model = model
+        self.layer_idx = layer_idx
+
+    @property
+    def weights(self):
+        return self.model.layers[self.layer_idx]
+
+    def __call__(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int,
+                 output_attentions: bool = False) -> Optional[torch.Tensor]:
+        m, lw = self.model, self.weights
+        kc, vc = cache.layer(self.layer_idx)
+        q = ops.linear_qkv_rope(hb, lw.qkv, m.eps, m.rope, positions, kc, vc, slot0, seq_len,
+                                m.n_heads, m.n_kv_heads, m.head_dim)
+        b = hb.shape[0] // seq_len
+        q4 = q.reshape(b, seq_len, m.n_heads, m.head_dim)
+        weights = None
+        if output_attentions:  # debug path: materialised softmax weights (reference :277-286)
+            s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
+            a, weights = ref.attention(q4, kc, vc, s0, kv_start, key_mask, return_weights=True)
+            a = a.reshape(b * seq_len, -1)
+        else:
+            a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask)
+        m._row_parallel(a, lw.o, h, hb)
+        return weights
+
+
+class LLaMAMLP:
+    def __init__(self, model, layer_idx: int):
+        self.model = model
+        self.layer_idx = layer_idx
+
+    def __call__(self, h, hb) -> None:
+        m, lw = self.model, self.model.layers[self.layer_idx]
+        g = ops.linear_swiglu(hb, lw.gu, rms_eps=m.eps)
+        m._row_parallel(g, lw.down, h, hb)
+
+
+class LLaMABlock:
+    """Pre-norm block: ``h += attn(norm(h)); h += mlp(norm(h))``."""
+
+    def __init__(self, model, layer_idx: int):
+        self.attention = LLaMAAttention(model, layer_idx)
+        self.feed_forward = LLaMAMLP(model, layer_idx)
+
+    def __call__(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int,
+                 output_attentions: bool = False):
+        w = self.attention(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len, output_attentions)
+        self.feed_forward(h, hb)
+        return w
+
+
+class LLaMABlockCollection:
+    """The layer loop (reference :579-595). Inside a hipGraph-captured decode step this loop is
+    recorded once and replayed per token."""
+
+    def __init__(self, model):
+        self.blocks: List[LLaMABlock] = [LLaMABlock(model, i) for i in range(len(model.layers))]
+
+    def __len__(self):
+        return len(self.blocks)
+
+    def __call__(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int,
+                 output_hidden_states: bool = False, output_attentions: bool = False):
+        hidden, attns = [], []
+        b = hb.shape[0] // seq_len
+        for blk in self.blocks:
+            if output_hidden_states:
+                hidden.append(h.reshape(b, seq_len, -1).clone())
+            w = blk(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len, output_attentions)
+            if output_attentions:
+                attns.append(w)
+        return hidden, attns

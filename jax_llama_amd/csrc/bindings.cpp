@@ -60,10 +60,15 @@ void embedding(Tensor ids, Tensor table, Tensor out, c10::optional<Tensor> mirro
 void rms_scale(Tensor x, Tensor out, double eps) {
   check_gpu(x, "x");
   check_gpu(out, "out");
-  check(x.scalar_type() == torch::kFloat32 && out.scalar_type() == torch::kBFloat16, "rms_scale dtypes");
+  check((x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16) &&
+            out.scalar_type() == torch::kBFloat16,
+        "rms_scale dtypes");
   const int D = x.size(-1), M = x.numel() / D;
   check(out.numel() == x.numel(), "rms_scale out shape");
-  rc(jla::rms_scale(ptr<float>(x), bf(out), M, D, (float)eps, stream()), "rms_scale");
+  if (x.scalar_type() == torch::kBFloat16)
+    rc(jla::rms_scale_bf16(cbf(x), bf(out), M, D, (float)eps, stream()), "rms_scale_bf16");
+  else
+    rc(jla::rms_scale(ptr<float>(x), bf(out), M, D, (float)eps, stream()), "rms_scale");
 }
 
 void rmsnorm(Tensor x, Tensor w, Tensor out, double eps) {
@@ -137,17 +142,11 @@ py::tuple skinny_workspace(int64_t m, int64_t n, int64_t k, int64_t mode) {
   return py::make_tuple((int64_t)jla::skinny_workspace_floats(m, n, k, mode), jla::skinny_tickets(m, n, k, mode));
 }
 
-// fused qkv projection + RoPE + KV-cache write (decode / small M)
-void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions, Tensor kc,
-                Tensor vc, Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q,
-                int64_t variant, Tensor ws, Tensor tickets) {
-  check_gpu(x, "x");
-  check_packed(w, n, k);
+// RoPE + KV-cache epilogue arguments of the fused qkv projection (validated here)
+jla::QKVArgs qkv_args(int64_t m, int64_t n, const Tensor& table, const Tensor& positions, const Tensor& kc,
+                      const Tensor& vc, const Tensor& slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh,
+                      const Tensor& q) {
   for (auto* t : {&table, &positions, &kc, &vc, &slot, &q}) check_gpu(*t, "linear_qkv arg");
-  check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
-  check(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16, "x must be fp32/bf16");
-  const int64_t m = x.size(0);
-  check(m <= SKINNY_MAX_M, "linear_qkv: M too large");
   check(n == (h + 2 * hkv) * dh && dh % 16 == 0, "qkv width");
   check(table.scalar_type() == torch::kFloat32 && table.dim() == 3 && table.size(1) == dh / 2 && table.size(2) == 2,
         "rope table must be fp32 [L, Dh/2, 2]");
@@ -172,20 +171,61 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
   qa.Dh = dh;
   qa.T = kc.size(2);
   qa.q = bf(q);
+  qa.res_bf16 = nullptr;
+  return qa;
+}
+
+// fused qkv projection + RoPE + KV-cache write (decode / small M)
+void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions, Tensor kc,
+                Tensor vc, Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q,
+                int64_t variant, Tensor ws, Tensor tickets) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
+  check(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16, "x must be fp32/bf16");
+  const int64_t m = x.size(0);
+  check(m <= SKINNY_MAX_M, "linear_qkv: M too large");
+  jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
   run_skinny(x, w, n, k, nullptr, MODE_QKV_ID, rms_eps, false, false, &qa, variant, ws, tickets);
 }
 
+void check_gemm_ws(const c10::optional<Tensor>& ws, int64_t ksplit, int64_t m, int64_t n) {
+  if (ksplit <= 1) return;
+  check(ws.has_value(), "gemm: split-K needs a workspace");
+  check_gpu(*ws, "gemm ws");
+  check(ws->scalar_type() == torch::kFloat32 && ws->numel() >= ksplit * m * n, "gemm ws too small");
+}
+
+// Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel.
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate,
-          c10::optional<Tensor> mirror) {
+          c10::optional<Tensor> mirror, int64_t ksplit, c10::optional<Tensor> ws) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
+  check(mode >= 0 && mode <= 2, "gemm mode");
   const int64_t m = x.size(0);
   check_linear_out(out, m, n, mode);
+  check_gemm_ws(ws, ksplit, m, n);
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-               out.scalar_type() == torch::kFloat32, mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr,
-               stream()),
+               out.scalar_type() == torch::kFloat32, mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr, nullptr,
+               ksplit > 1 ? ptr<float>(*ws) : nullptr, ksplit > 1 ? ws->numel() : 0, ksplit, stream()),
      "gemm");
+}
+
+// Tiled split-K qkv projection with the RoPE + KV-cache write in the reduce epilogue (x: rms-scaled bf16).
+void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor positions, Tensor kc, Tensor vc,
+              Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q, int64_t ksplit,
+              Tensor ws) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
+  check(ksplit >= 2, "gemm_qkv: ksplit >= 2");
+  const int64_t m = x.size(0);
+  jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
+  check_gemm_ws(ws, ksplit, m, n);
+  rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(ws), ws.numel(),
+               ksplit, stream()),
+     "gemm_qkv");
 }
 
 void rope_kv_write(Tensor qkv, Tensor table, Tensor positions, Tensor kc, Tensor vc, Tensor slot, int64_t seq_len,
@@ -298,7 +338,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("mode"), py::arg("rms_eps"), py::arg("accumulate"), py::arg("variant"), py::arg("ws"),
         py::arg("tickets"), py::arg("mirror") = py::none());
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
-        py::arg("accumulate"), py::arg("mirror") = py::none());
+        py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none());
+  m.def("gemm_qkv", &gemm_qkv);
+  m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_decode_splits",
         [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });

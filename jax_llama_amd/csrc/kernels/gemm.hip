@@ -1,8 +1,5 @@
-// Prefill linear layer (M > 64 rows): y[M, N] = epilogue( x[M, K] @ W[N, K]^T ), bf16 MFMA.
-//
-// Same epilogues as the skinny decode kernel (gemv.hip): store bf16/fp32, accumulate into the fp32
-// residual stream, or SiLU(gate)*up over the interleaved [w1;w3] weight. The RMSNorm scale is
-// applied to x beforehand (rms_scale), so x arrives as bf16.
+// Linear layer for M > 32 rows (prefill, and large-batch decode): y = epilogue(x[M, K] @ W[N, K]^T),
+// bf16 MFMA. x arrives RMS-scaled in bf16 (rms_scale) when a norm precedes the projection.
 //
 // Tiling (CDNA4): 128 x 128 output tile per 256-thread workgroup, 4 waves in 2 x 2, each wave a
 // 64 x 64 sub-tile = 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators. K advances 64 per stage. Both
@@ -11,6 +8,12 @@
 // weights are copied verbatim (each 1 KiB fragment is already contiguous in HBM). Double-buffered
 // LDS; the next stage's global loads are issued before the current stage's MFMAs and written to
 // LDS after them (issue-early / write-late), one barrier per stage.
+//
+// Decode at batch 64..512 has too few 128x128 tiles to fill 256 CUs, so K can be split over
+// gridDim.z workgroups: each writes an fp32 partial tile, and gemm_reduce_kernel sums the splits in
+// fixed order (deterministic) and runs the epilogue: store bf16/fp32, residual add (+ bf16 mirror),
+// SiLU(gate)*up over the interleaved [w1;w3] tiles, or RoPE + KV-cache write for the fused qkv
+// projection (reference ops: model.py:210/294/338/736, :58-92, :169-199, :392/:398).
 #include "common.h"
 #include "launchers.h"
 
@@ -21,37 +24,39 @@ constexpr int G_THREADS = 256;
 // fragments per stage: A 8 m-tiles x 2 k-steps, B 8 n-tiles x 2 k-steps (1 KiB each)
 constexpr int G_AFR = 16, G_BFR = 16;
 constexpr int G_STAGE_U4 = (G_AFR + G_BFR) * 64;  // u32x4 per stage (32 KiB); 8 per thread
+constexpr int MODE_PARTIAL = 7;                   // split-K: fp32 partial tile to the workspace
 
 template <int MODE>
 __global__ void __launch_bounds__(G_THREADS)
     gemm_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror) {
+                int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc) {
   __shared__ u32x4 lds[2][G_STAGE_U4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
   const int n0 = blockIdx.x * GB_N, m0 = blockIdx.y * GB_M;
   const int KS = K >> 5, NTT = N >> 4;
-  const int KT = (KS + 1) >> 1;  // stages of 2 k-steps (last may be half)
+  const int ks0 = blockIdx.z * kc;                  // this split's k-steps [ks0, ks_end)
+  const int ks_end = min(KS, ks0 + kc);
+  const int KT = (ks_end - ks0 + 1) >> 1;           // stages of 2 k-steps (last may be half)
 
-  // per-thread staging slots: fragment f = tid/64 + 4*j (j = 0..7), lane = tid & 63
-  // f in [0,16): A fragment (mt = f>>1, ks = f&1); f in [16,32): B fragment (nt = (f-16)>>1, ks = f&1)
+  // per-thread staging slots: fragment f = tid/64 + 4*j (j = 0..3), lane = tid & 63
+  // A fragments f (mt = f>>1, ks = f&1); B fragments f (nt = f>>1, ks = f&1)
   const bf16_t* asrc[4];
   const u32x4* bsrc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int f = w + 4 * j;  // 0..15 -> A
+    const int f = w + 4 * j;
     const int mt = f >> 1, ks = f & 1;
     const int row = min(m0 + mt * 16 + (lane & 15), M - 1);
-    asrc[j] = x + (size_t)row * K + ks * 32 + 8 * (lane >> 4);
-    const int fb = f;  // B fragment index 0..15
-    const int nt = min((n0 >> 4) + (fb >> 1), NTT - 1), ksb = fb & 1;
-    bsrc[j] = W + ((size_t)nt * KS + ksb) * 64 + lane;
+    asrc[j] = x + (size_t)row * K + (size_t)(ks0 + ks) * 32 + 8 * (lane >> 4);
+    const int nt = min((n0 >> 4) + (f >> 1), NTT - 1);
+    bsrc[j] = W + ((size_t)nt * KS + ks0 + ks) * 64 + lane;
   }
 
   u32x4 stage[8];
   auto gload = [&](int kt) {
     const int kbase = kt * 2;
-    if ((kbase + 1) < KS) {  // uniform branch: only the last stage of an odd-KS GEMM is half
+    if (ks0 + kbase + 1 < ks_end) {  // uniform branch: only a split's last stage can be half
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         stage[j] = *reinterpret_cast<const u32x4*>(asrc[j] + (size_t)kbase * 32);
@@ -59,13 +64,12 @@ __global__ void __launch_bounds__(G_THREADS)
       }
     } else {
       // this thread's fragments all have ks == (w & 1); ks == 1 is past the end -> zeros
-      const bool ok = (w & 1) == 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         stage[j] = u32x4{0, 0, 0, 0};
         stage[4 + j] = u32x4{0, 0, 0, 0};
       }
-      if (ok) {
+      if ((w & 1) == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           stage[j] = *reinterpret_cast<const u32x4*>(asrc[j] + (size_t)kbase * 32);
@@ -112,20 +116,20 @@ __global__ void __launch_bounds__(G_THREADS)
 
   // epilogue: lane holds C[4*(lane>>4) + r][lane & 15] of each 16x16 tile
   const int c = lane & 15;
-  if (MODE == MODE_SWIGLU) {
+  if constexpr (MODE == MODE_SWIGLU) {
     const int F = N >> 1;
     bf16_t* o = static_cast<bf16_t*>(out);
 #pragma unroll
     for (int j = 0; j < 4; j += 2) {
       const int gtile = (n0 >> 4) + wc * 4 + j;  // even
-      if (gtile + 1 >= NTT + 1) continue;
+      if (gtile >= NTT) continue;
       const int col = (gtile >> 1) * 16 + c;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = m0 + (wr * 4 + i) * 16 + 4 * (lane >> 4) + r;
-          if (row < M && gtile < NTT) o[(size_t)row * F + col] = f2bf(silu(acc[i][j][r]) * acc[i][j + 1][r]);
+          if (row < M) o[(size_t)row * F + col] = f2bf(silu(acc[i][j][r]) * acc[i][j + 1][r]);
         }
     }
   } else {
@@ -142,7 +146,9 @@ __global__ void __launch_bounds__(G_THREADS)
           if (row >= M) continue;
           const size_t idx = (size_t)row * N + col;
           const float v = acc[i][j][r];
-          if (MODE == MODE_RESIDUAL) {
+          if constexpr (MODE == MODE_PARTIAL) {
+            static_cast<float*>(out)[(size_t)blockIdx.z * M * N + idx] = v;
+          } else if constexpr (MODE == MODE_RESIDUAL) {
             float* o = static_cast<float*>(out);
             const float nv = accumulate ? o[idx] + v : v;
             o[idx] = nv;
@@ -157,22 +163,156 @@ __global__ void __launch_bounds__(G_THREADS)
   }
 }
 
+// Sum the split-K partials (fixed order) and apply the epilogue. One thread = 4 consecutive
+// columns of one row (two RoPE pairs; a 16-column tile never straddles a float4).
+template <int MODE>
+__global__ void __launch_bounds__(256)
+    gemm_reduce_kernel(const float* __restrict__ ws, int ksplit, void* __restrict__ out, int M, int N,
+                       int accumulate, int out_f32, bf16_t* __restrict__ mirror, QKVArgs qa) {
+  const size_t e4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total4 = (size_t)M * N / 4;
+  if (e4 >= total4) return;
+  const size_t idx = e4 * 4;
+  const int m = (int)(idx / N), col = (int)(idx - (size_t)m * N);
+  float4 v = reinterpret_cast<const float4*>(ws)[e4];
+  for (int s = 1; s < ksplit; ++s) {
+    const float4 p = reinterpret_cast<const float4*>(ws + (size_t)s * M * N)[e4];
+    v.x += p.x;
+    v.y += p.y;
+    v.z += p.z;
+    v.w += p.w;
+  }
+  float vv[4] = {v.x, v.y, v.z, v.w};
+  if constexpr (MODE == MODE_SWIGLU) {
+    // gate tile t = 2p holds columns [32p, 32p+16), the up tile the next 16: pair the two halves
+    const int tile = col >> 4, c0 = col & 15;
+    if ((tile & 1) == 0) {
+      const float4 u = [&] {
+        float4 a = reinterpret_cast<const float4*>(ws)[e4 + 4];
+        for (int s = 1; s < ksplit; ++s) {
+          const float4 p = reinterpret_cast<const float4*>(ws + (size_t)s * M * N)[e4 + 4];
+          a.x += p.x;
+          a.y += p.y;
+          a.z += p.z;
+          a.w += p.w;
+        }
+        return a;
+      }();
+      const float uu[4] = {u.x, u.y, u.z, u.w};
+      bf16_t* o = static_cast<bf16_t*>(out) + (size_t)m * (N >> 1) + (tile >> 1) * 16 + c0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = f2bf(silu(vv[q]) * uu[q]);
+    }
+  } else if constexpr (MODE == MODE_RESIDUAL) {
+    float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + idx);
+    float4 r = *o;
+    if (accumulate) {
+      r.x += vv[0];
+      r.y += vv[1];
+      r.z += vv[2];
+      r.w += vv[3];
+    } else {
+      r = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
+    *o = r;
+    if (mirror) *reinterpret_cast<uint2*>(mirror + idx) = make_uint2(pack2bf(r.x, r.y), pack2bf(r.z, r.w));
+  } else if constexpr (MODE == MODE_QKV) {
+    const int head = col / qa.Dh, d0 = col - head * qa.Dh;
+    const int b = m / qa.S, sq = m - b * qa.S;
+    if (head < qa.H + qa.Hkv) {
+      int pos = qa.positions[m];
+      pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d0 >> 1) + p];
+        const float xr = vv[2 * p], xi = vv[2 * p + 1];
+        vv[2 * p] = xr * cs.x - xi * cs.y;
+        vv[2 * p + 1] = xr * cs.y + xi * cs.x;
+      }
+    }
+    const uint2 packed = make_uint2(pack2bf(vv[0], vv[1]), pack2bf(vv[2], vv[3]));
+    if (head < qa.H) {
+      *reinterpret_cast<uint2*>(qa.q + ((size_t)m * qa.H + head) * qa.Dh + d0) = packed;
+    } else {
+      const int slot = qa.slot[0] + sq;
+      if (slot < qa.T) {
+        const bool is_k = head < qa.H + qa.Hkv;
+        const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
+        bf16_t* cache = is_k ? qa.kc : qa.vc;
+        *reinterpret_cast<uint2*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d0) = packed;
+      }
+    }
+  } else {
+    if (out_f32)
+      *reinterpret_cast<float4*>(static_cast<float*>(out) + idx) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    else
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + idx) =
+          make_uint2(pack2bf(vv[0], vv[1]), pack2bf(vv[2], vv[3]));
+  }
+}
+
+// split-K plan: enough workgroups to fill the chip (>= ~512), >= 8 k-steps per split
+int gemm_ksplit(int M, int N, int K) {
+  const int tiles = ((N + GB_N - 1) / GB_N) * ((M + GB_M - 1) / GB_M);
+  const int KS = K >> 5;
+  int ks = 1;
+  while (tiles * ks < 512 && KS / (ks * 2) >= 8 && ks < 16) ks *= 2;
+  return ks;
+}
+
+size_t gemm_workspace_floats(int M, int N, int K) {
+  const int ks = gemm_ksplit(M, N, K);
+  return ks > 1 ? (size_t)ks * M * N : 0;
+}
+
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
-         bf16_t* mirror, hipStream_t s) {
+         bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s) {
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
-  dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M);
+  if (mode == MODE_QKV && (!qkv || ksplit < 2)) return -1;  // qkv epilogue only in the reduce kernel
+  const int KS = K >> 5;
+  if (ksplit < 1) ksplit = 1;
+  const int kc = (KS + ksplit - 1) / ksplit;
+  ksplit = (KS + kc - 1) / kc;
   const u32x4* w = static_cast<const u32x4*>(W);
+  if (ksplit == 1) {
+    dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, 1);
+    switch (mode) {
+      case MODE_STORE:
+        gemm_kernel<MODE_STORE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc);
+        break;
+      case MODE_RESIDUAL:
+        gemm_kernel<MODE_RESIDUAL><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 1, mirror, kc);
+        break;
+      case MODE_SWIGLU:
+        gemm_kernel<MODE_SWIGLU><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 0, nullptr, kc);
+        break;
+      default: return -1;
+    }
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
+  if ((N & 3) || ws == nullptr || ws_floats < (size_t)ksplit * M * N) return -3;
+  dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
+  gemm_kernel<MODE_PARTIAL><<<grid, G_THREADS, 0, s>>>(x, w, ws, M, N, K, 0, 1, nullptr, kc);
+  JLA_CHECK_LAUNCH();
+  const size_t total4 = (size_t)M * N / 4;
+  const int rgrid = (int)((total4 + 255) / 256);
+  QKVArgs qa{};
+  if (qkv) qa = *qkv;
   switch (mode) {
     case MODE_STORE:
-      gemm_kernel<MODE_STORE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, nullptr);
+      gemm_reduce_kernel<MODE_STORE><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, out_f32, nullptr, qa);
       break;
     case MODE_RESIDUAL:
-      gemm_kernel<MODE_RESIDUAL><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 1, mirror);
+      gemm_reduce_kernel<MODE_RESIDUAL><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 1, mirror, qa);
       break;
     case MODE_SWIGLU:
-      gemm_kernel<MODE_SWIGLU><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 0, nullptr);
+      gemm_reduce_kernel<MODE_SWIGLU><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa);
+      break;
+    case MODE_QKV:
+      gemm_reduce_kernel<MODE_QKV><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa);
       break;
     default: return -1;
   }

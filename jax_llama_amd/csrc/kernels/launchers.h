@@ -12,6 +12,7 @@ typedef uint16_t bf16_t;
 int embedding(const int32_t* ids, const bf16_t* table, float* out, bf16_t* mirror, int M, int D, int V,
               hipStream_t s);
 int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
+int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
 
 // Epilogue arguments of the fused qkv projection (MODE_QKV): RoPE + KV-cache write.
@@ -36,8 +37,12 @@ int skinny_tickets(int M, int N, int K, int mode);
 int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode, float rms_eps,
                   int accumulate, int out_f32, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
                   int n_tickets, hipStream_t s);
+// 128x128-tile MFMA GEMM (gemm.hip). ksplit > 1 splits K over gridDim.z into fp32 partials
+// (ws >= gemm_workspace_floats) reduced in fixed order by an epilogue kernel; MODE_QKV needs ksplit > 1.
+int gemm_ksplit(int M, int N, int K);
+size_t gemm_workspace_floats(int M, int N, int K);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
-         bf16_t* mirror, hipStream_t s);
+         bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s);
 
 int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,

@@ -77,6 +77,39 @@ int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t 
   return 0;
 }
 
+// bf16 input (the residual mirror): statistics from the bf16 values, like the decode kernels
+__global__ void __launch_bounds__(256) rms_bf16_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
+                                                       int D, float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * D);
+  u32x4* o = reinterpret_cast<u32x4*>(out + (size_t)row * D);
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < D / 8; i += blockDim.x) {
+    float f[8];
+    unpack8(xr[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)D + eps);
+  for (int i = threadIdx.x; i < D / 8; i += blockDim.x) {
+    float f[8];
+    unpack8(xr[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= inv;
+    o[i] = pack8(f);
+  }
+}
+
+int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStream_t s) {
+  if (D % 8) return -1;
+  if (M == 0) return 0;
+  rms_bf16_kernel<<<M, 256, 0, s>>>(x, out, D, eps);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s) {
   if (D % 4) return -1;
   if (M == 0) return 0;

@@ -142,18 +142,37 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None):
     assert x.shape[1] == w.k, (x.shape, w.k)
     m = x.shape[0]
     e = ext()
-    if m > e.SKINNY_MAX_M:
-        # Large-M (prefill) path: bf16 normalised activations, then the MFMA tiled GEMM.
-        if rms_eps is not None:
-            x = rms_scale(x.float() if x.dtype != torch.float32 else x, rms_eps)
-        elif x.dtype != BF16:
-            x = x.to(BF16)
-        e.gemm(x, w.weight, w.n, w.k, out, mode, bool(accumulate), mirror)
+    v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, mode)
+    if v == TILED:
+        _tiled(e, x, w.weight, w.n, w.k, out, mode, rms_eps, accumulate, mirror)
     else:
         ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
-                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate),
-                        _variant(e, x, w, mode), ws, tk, mirror)
+                        -1.0 if rms_eps is None else float(rms_eps), bool(accumulate), v, ws, tk, mirror)
+
+
+TILED = 7  # decode-kernel "variant" id of the 128x128 MFMA GEMM (split-K for mid M)
+
+
+def _tiled_input(x, rms_eps):
+    """bf16 A operand of the tiled GEMM: rms-scaled (statistics from x's own values) or cast."""
+    if rms_eps is not None:
+        return rms_scale(x, rms_eps)
+    return x if x.dtype == BF16 else x.to(BF16)
+
+
+def _gemm_ws(e, m, n, k, device):
+    ks = e.gemm_ksplit(m, n, k)
+    ws = workspace.get("gemm_ws", ks * m * n, torch.float32, device) if ks > 1 else None
+    return ks, ws
+
+
+def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
+    """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups when the
+    output has too few 128x128 tiles to fill the chip (csrc/kernels/gemm.hip)."""
+    xb = _tiled_input(x, rms_eps)
+    ks, ws = _gemm_ws(e, x.shape[0], n, k, x.device)
+    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws)
 
 
 def _variant(e, x, w, mode) -> int:
@@ -169,7 +188,10 @@ def _variant(e, x, w, mode) -> int:
     scratch = workspace.get("tune_out", m * ncols, odt, x.device).view(m, ncols)
 
     def run(v, xx, wt):
-        e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk)
+        if v == TILED:
+            _tiled(e, xx, wt, w.n, w.k, scratch, pmode, 1e-5, True)
+        else:
+            e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk)
 
     return autotune.choose(e, x, w, pmode, run)
 
@@ -220,14 +242,23 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
                                    n_heads, n_kv_heads, head_dim)
     m = x.shape[0]
     e = ext()
-    if m > e.SKINNY_MAX_M:
-        qkv = linear(x, w, rms_eps=rms_eps)
-        return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads, head_dim)
+    v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV)
+    if v == TILED:
+        ks, ws = _gemm_ws(e, m, w.n, w.k, x.device)
+        if ks == 1:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
+            qkv = linear(x, w, rms_eps=rms_eps)
+            return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads,
+                                 head_dim)
+        q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
+        e.gemm_qkv(_tiled_input(x, rms_eps), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
+                   k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
+                   int(head_dim), q, ks, ws)
+        return q
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)
     e.linear_qkv(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
                  positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, x.device),
-                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, _variant(e, x, w, MODE_QKV), ws, tk)
+                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, v, ws, tk)
     return q
 
 

@@ -9,7 +9,8 @@ as in a real decode step) and caches the winner. Never runs under hipGraph captu
 seen during capture fall back to the static heuristic.
 
 Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG,
-4 = split-K skinny GEMM. ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
+4 = split-K skinny GEMM, 7 = 128x128 MFMA GEMM with split-K (gemm.hip; M > 32 only, always used
+for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
 """
 from __future__ import annotations
 
@@ -41,6 +42,8 @@ def heuristic(m: int, n: int, k: int, mode: int) -> int:
 
 
 def candidates(m: int, n: int) -> Tuple[int, ...]:
+    if m > 32:
+        return (1, 4, 7)
     if m > 16:
         return (1, 4)
     c = [1, 6, 4]

@@ -243,3 +243,66 @@ def test_decode_linear_paths_all_modes(variant, m):
         assert torch.equal(y, y_again)
     finally:
         ops.GEMV_VARIANT = 0
+
+
+@pytest.mark.parametrize("m", [40, 64, 96, 256])
+def test_tiled_splitk_all_modes(m):
+    """128x128 MFMA GEMM with split-K partials + fixed-order reduce epilogue (decode batches > 32)."""
+    ops.GEMV_VARIANT = ops.TILED
+    try:
+        k, n = 4096, 768
+        e = ops.ext()
+        assert e.gemm_ksplit(m, n, k) > 1
+        x = torch.randn(m, k)
+        w, pg, pc = _mk_linear(n, k)
+        y = ops.linear(x.to(DEV), pg, rms_eps=1e-5, out_dtype=torch.float32)
+        _close(y, ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+        yb = ops.linear(x.to(DEV), pg, rms_eps=1e-5)
+        _close(yb, ref.linear(x, w, 1e-5, torch.float32), 2e-2, 2e-2)
+        xb = x.to(BF16)
+        h = torch.randn(m, n)
+        hg, mir = h.to(DEV), torch.empty(m, n, dtype=BF16, device=DEV)
+        ops.linear_residual(xb.to(DEV), pg, hg, mirror=mir)
+        expect = ref.linear_residual(xb, w, h.clone())
+        _close(hg, expect, 1e-2, 1e-3)
+        torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
+        gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+        y2 = ops.linear_swiglu(x.to(DEV), PackedLinear.from_dense(gu, DEV), rms_eps=1e-5)
+        _close(y2, ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
+        y_again = ops.linear(x.to(DEV), pg, rms_eps=1e-5, out_dtype=torch.float32)
+        assert torch.equal(y, y_again)
+    finally:
+        ops.GEMV_VARIANT = 0
+
+
+@pytest.mark.parametrize("m,s", [(48, 1), (128, 1), (256, 1), (96, 2)])
+def test_qkv_rope_tiled_splitk(m, s):
+    """RoPE + KV-cache write fused into the split-K reduce epilogue."""
+    ops.GEMV_VARIANT = ops.TILED
+    try:
+        h, hkv, dh, k, t = 8, 2, 128, 4096, 80
+        b = m // s
+        n = (h + 2 * hkv) * dh
+        assert ops.ext().gemm_ksplit(m, n, k) > 1
+        w = (torch.randn(n, k) * 0.05).to(BF16)
+        x = torch.randn(m, k).to(BF16)
+        table = ref.rope_table(dh, 256, 500000.0)
+        pos = torch.randint(0, 200, (m,), dtype=torch.int32)
+        kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+        vc = torch.zeros_like(kc)
+        q = ref.linear_qkv_rope(x, w, 1e-5, table, pos, kc, vc, 11, s, h, hkv, dh)
+        kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+        pg = PackedLinear.from_dense(w, DEV)
+        qg = ops.linear_qkv_rope(x.to(DEV), pg, 1e-5, table.to(DEV), pos.to(DEV), kg, vg,
+                                 torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh)
+        _close(qg, q, 2e-2, 2e-2)
+        _close(kg, kc, 2e-2, 2e-2)
+        _close(vg, vc, 2e-2, 2e-2)
+    finally:
+        ops.GEMV_VARIANT = 0
+
+
+def test_rms_scale_bf16_input():
+    x = (torch.randn(70, 4096) * 3).to(BF16)
+    out = ops.rms_scale(x.to(DEV), 1e-5)
+    _close(out, ref.rms_scale(x.float(), 1e-5), 1e-2, 1e-2)

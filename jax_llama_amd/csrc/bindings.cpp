@@ -308,6 +308,59 @@ void argmax(Tensor logits, Tensor idx, Tensor val) {
      "argmax");
 }
 
+// stage 1 of the sampler: per-4096-chunk top-K candidates (global indices = local + idx_offset)
+void topk_chunk(Tensor logits, int64_t k, int64_t idx_offset, Tensor cv, Tensor ci) {
+  for (auto* t : {&logits, &cv, &ci}) check_gpu(*t, "topk_chunk arg");
+  check(logits.scalar_type() == torch::kFloat32 && logits.dim() == 2, "logits must be fp32 [B, V]");
+  const int64_t b = logits.size(0), v = logits.size(1);
+  check(k >= 1 && k <= 64 && k <= v, "topk_chunk: 1 <= k <= min(64, V)");
+  const int64_t c = (int64_t)jla::topk_chunks(v) * k;
+  check(cv.scalar_type() == torch::kFloat32 && ci.scalar_type() == torch::kInt32 && cv.numel() == b * c &&
+            ci.numel() == b * c,
+        "topk_chunk: candidates must be [B, chunks*k] fp32/int32");
+  rc(jla::topk_chunk(ptr<float>(logits), b, v, k, idx_offset, ptr<float>(cv), ptr<int32_t>(ci), stream()),
+     "topk_chunk");
+}
+
+// stage 2: merge [B, C] candidates -> sorted top-K (mode 0) or one sampled token per row (mode 1)
+void topk_merge(Tensor cv, Tensor ci, int64_t k, int64_t mode, c10::optional<Tensor> out_v,
+                c10::optional<Tensor> out_i, c10::optional<Tensor> nxt, double temperature, double top_p,
+                int64_t seed, c10::optional<Tensor> step) {
+  check_gpu(cv, "cv");
+  check_gpu(ci, "ci");
+  check(cv.dim() == 2 && cv.sizes() == ci.sizes() && cv.scalar_type() == torch::kFloat32 &&
+            ci.scalar_type() == torch::kInt32,
+        "topk_merge: candidates [B, C] fp32/int32");
+  const int64_t b = cv.size(0), c = cv.size(1);
+  check(k >= 1 && k <= 64 && k <= c && c <= 4096, "topk_merge: 1 <= k <= 64, k <= C <= 4096");
+  float* ov = nullptr;
+  int32_t* oi = nullptr;
+  int32_t* nx = nullptr;
+  const int32_t* st = nullptr;
+  if (mode == 0) {
+    check(out_v.has_value() && out_i.has_value(), "topk_merge mode 0 needs out_v/out_i");
+    check_gpu(*out_v, "out_v");
+    check_gpu(*out_i, "out_i");
+    check(out_v->scalar_type() == torch::kFloat32 && out_i->scalar_type() == torch::kInt32 &&
+              out_v->numel() == b * k && out_i->numel() == b * k,
+          "topk_merge outputs [B, k]");
+    ov = ptr<float>(*out_v);
+    oi = ptr<int32_t>(*out_i);
+  } else {
+    check(mode == 1 && nxt.has_value() && step.has_value(), "topk_merge mode 1 needs nxt and step");
+    check_gpu(*nxt, "nxt");
+    check_gpu(*step, "step");
+    check(nxt->scalar_type() == torch::kInt32 && nxt->numel() == b && step->scalar_type() == torch::kInt32,
+          "topk_merge nxt [B] / step [1] int32");
+    check(temperature > 0, "topk_merge: temperature > 0");
+    nx = ptr<int32_t>(*nxt);
+    st = ptr<int32_t>(*step);
+  }
+  rc(jla::topk_merge(ptr<float>(cv), ptr<int32_t>(ci), b, c, k, mode, ov, oi, nx, (float)temperature, (float)top_p,
+                     (uint64_t)seed, st, stream()),
+     "topk_merge");
+}
+
 void decode_update(Tensor nxt, Tensor finished, Tensor sequences, Tensor cur_len, Tensor tokens, Tensor positions,
                    Tensor slot, int64_t pad, int64_t eos) {
   for (auto* t : {&nxt, &finished, &sequences, &cur_len, &tokens, &positions, &slot}) {
@@ -352,5 +405,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));
   m.def("argmax", &argmax);
+  m.def("topk_chunks", [](int64_t v) { return jla::topk_chunks(v); });
+  m.def("topk_chunk", &topk_chunk);
+  m.def("topk_merge", &topk_merge, py::arg("cv"), py::arg("ci"), py::arg("k"), py::arg("mode"),
+        py::arg("out_v") = py::none(), py::arg("out_i") = py::none(), py::arg("nxt") = py::none(),
+        py::arg("temperature") = 1.0, py::arg("top_p") = 1.0, py::arg("seed") = 0, py::arg("step") = py::none());
   m.def("decode_update", &decode_update);
 }

@@ -59,6 +59,11 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
                  hipStream_t s);
 
 int argmax(const float* logits, int B, int V, int32_t* idx, float* val, hipStream_t s);
+// top-k / top-p sampler (topk_sample.hip): cv/ci [B, topk_chunks(V) * K] candidates
+int topk_chunks(int V);
+int topk_chunk(const float* logits, int B, int V, int K, int idx_offset, float* cv, int32_t* ci, hipStream_t s);
+int topk_merge(const float* cv, const int32_t* ci, int B, int C, int K, int mode, float* out_v, int32_t* out_i,
+               int32_t* nxt, float temperature, float top_p, uint64_t seed, const int32_t* step, hipStream_t s);
 int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,
                   int32_t* positions, int32_t* slot, int B, int L, int pad, int eos, hipStream_t s);
 }  // namespace jla

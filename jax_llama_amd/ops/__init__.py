@@ -310,3 +310,56 @@ def argmax(logits: torch.Tensor):
     val = torch.empty(b, dtype=torch.float32, device=logits.device)
     ext().argmax(logits, idx, val)
     return idx, val
+
+
+SAMPLER_MAX_K = 64
+
+
+def topk_candidates(logits: torch.Tensor, k: int, idx_offset: int = 0):
+    """Sorted top-``k`` (values fp32 [B, k], global indices int32 [B, k]) of fp32 logits on the
+    device: per-4096-chunk radix select + one merge (csrc/kernels/topk_sample.hip)."""
+    if not _is_gpu(logits):
+        v, i = ref.topk_sorted(logits, k)
+        return v, i + idx_offset
+    e = ext()
+    b, v = logits.shape
+    c = e.topk_chunks(v) * k
+    cv = workspace.get("topk_cv", b * c, torch.float32, logits.device).view(b, c)
+    ci = workspace.get("topk_ci", b * c, torch.int32, logits.device).view(b, c)
+    e.topk_chunk(logits, k, int(idx_offset), cv, ci)
+    out_v = torch.empty(b, k, dtype=torch.float32, device=logits.device)
+    out_i = torch.empty(b, k, dtype=torch.int32, device=logits.device)
+    e.topk_merge(cv, ci, k, 0, out_v=out_v, out_i=out_i)
+    return out_v, out_i
+
+
+def topk_sample(logits: torch.Tensor, k: int, temperature: float, top_p: float, seed: int,
+                step: torch.Tensor, comm=None) -> torch.Tensor:
+    """temperature -> top-k -> top-p -> categorical on the device, exact under vocab-parallel TP
+    (each rank's top-k is all-gathered, 2*k*4 bytes per row, and merged again; every rank draws
+    the same token from the same Philox stream). ``step`` is a device int32[1] (the decode
+    loop's cur_len) so the call is hipGraph-capturable. Returns int32 [B]."""
+    b, v = logits.shape
+    tp = comm.size if comm is not None else 1
+    if not _is_gpu(logits):
+        if tp > 1:
+            full = comm.all_gather(logits.float().contiguous()).permute(1, 0, 2).reshape(b, -1)
+        else:
+            full = logits
+        return ref.topk_sample(full, k, temperature, 1.0 if top_p is None else top_p, seed, int(step.reshape(-1)[0]))
+    e = ext()
+    kl = min(k, v)  # per-rank candidates (tp * kl >= k)
+    c = e.topk_chunks(v) * kl
+    cv = workspace.get("topk_cv", b * c, torch.float32, logits.device).view(b, c)
+    ci = workspace.get("topk_ci", b * c, torch.int32, logits.device).view(b, c)
+    e.topk_chunk(logits, kl, int(comm.rank * v) if tp > 1 else 0, cv, ci)
+    if tp > 1:
+        lv = torch.empty(b, kl, dtype=torch.float32, device=logits.device)
+        li = torch.empty(b, kl, dtype=torch.int32, device=logits.device)
+        e.topk_merge(cv, ci, kl, 0, out_v=lv, out_i=li)
+        cv = comm.all_gather(lv).permute(1, 0, 2).reshape(b, tp * kl).contiguous()
+        ci = comm.all_gather(li).permute(1, 0, 2).reshape(b, tp * kl).contiguous()
+    nxt = torch.empty(b, dtype=torch.int32, device=logits.device)
+    e.topk_merge(cv, ci, k, 1, nxt=nxt, temperature=float(temperature),
+                 top_p=1.0 if top_p is None else float(top_p), seed=int(seed) & ((1 << 63) - 1), step=step)
+    return nxt

@@ -236,3 +236,56 @@ def top_k_top_p_filter(logits: torch.Tensor, temperature: float, top_k: int, top
         vals = torch.where(keep, vals, torch.full_like(vals, float("-inf")))
         x = torch.full_like(x, float("-inf")).scatter(-1, idx, vals)
     return x
+
+
+def philox4x32_10(counter, key):
+    """Philox4x32-10 (Salmon et al., SC'11) on uint32 numpy arrays: ``counter`` [..., 4], ``key``
+    [2]. Bit-exact twin of ``philox4x32_10`` in csrc/kernels/topk_sample.hip."""
+    import numpy as np
+    c = [np.asarray(counter[..., i], dtype=np.uint64) for i in range(4)]
+    k0, k1 = np.uint64(key[0]), np.uint64(key[1])
+    m0, m1, mask = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0, p1 = m0 * c[0], m1 * c[2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c = [(hi1 ^ c[1] ^ k0) & mask, lo1, (hi0 ^ c[3] ^ k1) & mask, lo0]
+        k0 = (k0 + np.uint64(0x9E3779B9)) & mask
+        k1 = (k1 + np.uint64(0xBB67AE85)) & mask
+    return np.stack([x.astype(np.uint32) for x in c], -1)
+
+
+def topk_sorted(logits: torch.Tensor, k: int):
+    """Top-k values (descending) and indices, ties broken by the lower index (lax.top_k order)."""
+    import numpy as np
+    x = logits.float().cpu().numpy()
+    vals, idxs = [], []
+    for row in x:
+        order = np.lexsort((np.arange(row.size), -row))[:k]
+        vals.append(row[order])
+        idxs.append(order)
+    return torch.from_numpy(np.stack(vals)), torch.from_numpy(np.stack(idxs).astype(np.int32))
+
+
+def topk_sample(logits: torch.Tensor, k: int, temperature: float, top_p: float, seed: int, step: int) -> torch.Tensor:
+    """Reference of the on-device sampler: temperature -> top-k -> top-p (HF keep rule) ->
+    Gumbel-max with Philox(seed; counter = (rank-in-top-k, row, step, 0))."""
+    import numpy as np
+    vals, idx = topk_sorted(logits, k)
+    v = vals.numpy().astype(np.float32) / np.float32(temperature)
+    p = np.exp(v - v[:, :1])
+    p = p / p.sum(-1, keepdims=True)
+    excl = np.cumsum(p, -1) - p
+    keep = excl < np.float32(top_p)
+    keep[:, 0] = True
+    b = v.shape[0]
+    ctr = np.zeros((b, k, 4), dtype=np.uint32)
+    ctr[..., 0] = np.arange(k, dtype=np.uint32)[None]
+    ctr[..., 1] = np.arange(b, dtype=np.uint32)[:, None]
+    ctr[..., 2] = np.uint32(step)
+    r = philox4x32_10(ctr, (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF))[..., 0]
+    u = ((r >> 8).astype(np.float32) + np.float32(0.5)) * np.float32(1.0 / 16777216.0)
+    g = -np.log(-np.log(u))
+    score = np.where(keep, v + g, -np.inf)
+    choice = score.argmax(-1)
+    return idx[torch.arange(b), torch.from_numpy(choice)].to(torch.int32)

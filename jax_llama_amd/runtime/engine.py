@@ -71,9 +71,20 @@ def _greedy(model, logits_local: torch.Tensor) -> torch.Tensor:
     return idxs.gather(0, best[None]).squeeze(0).to(torch.int32)
 
 
-def _sample(model, logits_local: torch.Tensor, gc: GenerationConfig, gen: Optional[torch.Generator]):
-    """temperature -> top-k -> top-p -> categorical (Gumbel-max), exact under vocab sharding."""
+def _sample(model, logits_local: torch.Tensor, gc: GenerationConfig, gen: Optional[torch.Generator],
+            step: Optional[torch.Tensor] = None):
+    """temperature -> top-k -> top-p -> categorical (Gumbel-max), exact under vocab sharding.
+
+    top_k in [1, 64] (HF default 50): the on-device sampler (ops.topk_sample: radix-select top-k
+    kernels + Philox Gumbel-max keyed by (seed, step)), graph-capturable and identical on CPU.
+    Otherwise (top_k = 0 / > 64): torch sort path."""
     comm = model.comm
+    v_local = logits_local.shape[1]
+    k = min(gc.top_k or 0, v_local * comm.size)
+    if step is not None and 1 <= k <= ops.SAMPLER_MAX_K and gc.temperature and gc.temperature > 0:
+        if logits_local.device.type == "cpu" or ops.ext().topk_chunks(v_local) * min(k, v_local) <= 4096:
+            return ops.topk_sample(logits_local.float().contiguous(), k, gc.temperature, gc.top_p,
+                                   gc.seed, step, comm if comm.size > 1 else None)
     x = logits_local.float()
     if gc.temperature is not None and gc.temperature != 1.0:
         x = x / gc.temperature
@@ -134,7 +145,7 @@ class DecodeEngine:
     # ---------------------------------------------------------------------------------
     def _next_token(self, logits_local):
         if self.gc.do_sample:
-            return _sample(self.model, logits_local, self.gc, self._gen)
+            return _sample(self.model, logits_local, self.gc, self._gen, self.cur_len)
         return _greedy(self.model, logits_local)
 
     def _update(self, nxt: torch.Tensor):
@@ -186,9 +197,10 @@ class DecodeEngine:
         logits, *_ = model.forward_tokens(ids, pos_dev, self.cache, 0, self.kv_start, self.key_mask,
                                           logits_mode="last")
         self.cache.advance(s)
-        nxt = self._next_token(logits)
-        # state for the loop body: cur_len = S, token/pos of the last prompt position
+        # state for the loop body: cur_len = S (also the sampler's Philox step), token/pos of the
+        # last prompt position
         self.cur_len.fill_(s)
+        nxt = self._next_token(logits)
         self.positions.copy_(pos_dev[:, -1:])
         # _update writes sequences[:, S], advances pos (+1), slot (+1 -> S+1 ... ) and cur_len.
         # The prefill already advanced the slot by S; undo the update's +1 on the slot.

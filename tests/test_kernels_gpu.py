@@ -306,3 +306,38 @@ def test_rms_scale_bf16_input():
     x = (torch.randn(70, 4096) * 3).to(BF16)
     out = ops.rms_scale(x.to(DEV), 1e-5)
     _close(out, ref.rms_scale(x.float(), 1e-5), 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("b,v,k", [(1, 128256, 50), (16, 128256, 50), (3, 32000, 64), (5, 5000, 7), (2, 300, 64)])
+def test_topk_candidates_exact(b, v, k):
+    logits = torch.randn(b, v) * 4
+    logits[0, 17] = logits[0, 99] = logits[0].max() + 1  # ties: lower index first
+    if v > 4096:
+        logits[-1, 4000:4200] = float("-inf")
+    gv, gi = ops.topk_candidates(logits.to(DEV), k)
+    rv, ri = ref.topk_sorted(logits, k)
+    assert torch.equal(gi.cpu(), ri)
+    assert torch.equal(gv.cpu(), rv)
+
+
+@pytest.mark.parametrize("b,v,k,temp,top_p", [(16, 128256, 50, 1.0, 1.0), (8, 32000, 50, 0.7, 0.9),
+                                              (4, 1000, 64, 1.3, 0.5), (2, 50, 1, 1.0, 1.0)])
+def test_topk_sample_matches_reference(b, v, k, temp, top_p):
+    logits = torch.randn(b, v) * 2
+    for step in (5, 6):
+        st = torch.tensor([step], dtype=torch.int32, device=DEV)
+        got = ops.topk_sample(logits.to(DEV), k, temp, top_p, 1234, st)
+        want = ref.topk_sample(logits, k, temp, top_p, 1234, step)
+        assert torch.equal(got.cpu(), want)
+
+
+def test_topk_sample_graph_capturable():
+    logits = (torch.randn(4, 128256) * 2).to(DEV)
+    st = torch.tensor([9], dtype=torch.int32, device=DEV)
+    ops.topk_sample(logits, 50, 0.8, 0.95, 3, st)  # warm workspaces
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = ops.topk_sample(logits, 50, 0.8, 0.95, 3, st)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref.topk_sample(logits.cpu(), 50, 0.8, 0.95, 3, 9))

@@ -116,3 +116,41 @@ def test_sampling_is_seeded_and_valid():
     assert a.shape == (2, 12)
     assert torch.equal(a[:, :5], toks)
     assert int(a.min()) >= 0 and int(a.max()) < cfg.vocab_size
+
+
+def test_philox_known_answers():
+    """Random123 Philox4x32-10 known-answer vectors (the sampler's RNG, bit-exact with the kernel)."""
+    import numpy as np
+    from jax_llama_amd.ops.reference import philox4x32_10
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for ctr, key, want in kat:
+        got = philox4x32_10(np.array([ctr], dtype=np.uint32), key)[0]
+        assert tuple(int(x) for x in got) == want
+
+
+def test_reference_sampler_semantics():
+    from jax_llama_amd.ops import reference as ref
+    torch.manual_seed(0)
+    logits = torch.randn(64, 1000) * 3
+    # top_k = 1 and tiny top_p are greedy
+    assert torch.equal(ref.topk_sample(logits, 1, 1.0, 1.0, 5, 3), ref.argmax(logits))
+    assert torch.equal(ref.topk_sample(logits, 50, 1.0, 1e-6, 5, 3), ref.argmax(logits))
+    # sampled tokens lie in the top-k set, and change with the step / seed
+    a = ref.topk_sample(logits, 10, 0.7, 0.9, 5, 3)
+    top10 = logits.topk(10, -1).indices
+    assert bool((top10 == a[:, None].long()).any(-1).all())
+    assert not torch.equal(a, ref.topk_sample(logits, 10, 0.7, 0.9, 5, 4))
+    assert not torch.equal(a, ref.topk_sample(logits, 10, 0.7, 0.9, 6, 3))
+    # ties: lower index first
+    v, i = ref.topk_sorted(torch.tensor([[1.0, 3.0, 3.0, 2.0, 3.0]]), 3)
+    assert i.tolist() == [[1, 2, 4]]
+    # frequencies follow softmax(top-k logits / T)
+    row = torch.tensor([[2.0, 1.0, 0.5, 0.0, -1.0, -5.0]]).repeat(4000, 1)
+    s = torch.cat([ref.topk_sample(row, 4, 1.0, 1.0, 1, st) for st in range(3)])
+    freq = torch.bincount(s.long(), minlength=6).float() / s.numel()
+    p = torch.softmax(row[0, :4], -1)
+    assert freq[4:].sum() == 0
+    assert (freq[:4] - p).abs().max() < 0.02

@@ -393,6 +393,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none());
   m.def("gemm_qkv", &gemm_qkv);
+  m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
+  m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_decode_splits",

@@ -61,6 +61,18 @@ JLA_DEV f32x4 mfma16x16x32(const u32x4 a, const u32x4 b, f32x4 c) {
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
+// LDS-DMA: 16 bytes per lane from a per-lane global address into LDS at (wave-uniform base + 16*lane).
+JLA_DEV void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+// s_waitcnt vmcnt(N) only (expcnt/lgkmcnt left at their maxima)
+template <int N>
+JLA_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt(0xF70 | (N & 15) | ((N >> 4) << 14));
+}
+
 // Non-temporal 16-byte load for once-read streams (decode weights).
 JLA_DEV u32x4 load_nt(const u32x4* p) { return __builtin_nontemporal_load(p); }
 

@@ -163,6 +163,201 @@ __global__ void __launch_bounds__(G_THREADS)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// gemm2: BM x 256 tile (BM = 128 * WM), 4 * WM waves as WM(M) x 4(N), each wave a 128 x 64 sub-tile
+// (8 x 4 accumulators of 16x16, 128 fp32 registers). K advances 32 per LDS tile; 4 LDS tile buffers
+// filled by LDS-DMA (global_load_lds_dwordx4, no VGPR staging) run 3 tiles ahead of the MFMAs: at
+// the top of each K-tile a wave waits (counted vmcnt, never 0 in steady state) only for ITS part of
+// the tile it is about to read, then one raw s_barrier publishes every wave's part and retires the
+// reads of the buffer being refilled next (WAR). Both operands are stored fragment-shaped in LDS
+// (1 KiB = 16 rows x 32 k, lane-linear), so every ds_read_b128 is conflict-free: the packed weights
+// are copied verbatim, x is gathered by per-lane source addresses (16 rows x 64 B per wave-load).
+// Workgroups are remapped so consecutive tiles share an XCD (its own L2), M-grouped by 8.
+constexpr int G2_BN = 256, G2_NBUF = 4, G2_DIST = 3, G2_GROUP_M = 8;
+
+template <int MODE, int WM>
+__global__ void __launch_bounds__(256 * WM)
+    gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                 int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n) {
+  constexpr int NW = 4 * WM, BM = 128 * WM;
+  constexpr int AF = BM / 16, BF = G2_BN / 16, FR = AF + BF;  // fragments per K-tile
+  constexpr int G = FR / NW;                                   // LDS-DMA loads per wave per K-tile
+  static_assert(FR % NW == 0, "fragment split");
+  __shared__ u32x4 lds[G2_NBUF * FR * 64];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 2, wc = w & 3;
+
+  // XCD-aware bijective remap, then (split, M-grouped tile) order
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int split = wgid / tiles;
+  const int pid = wgid - split * tiles;
+  const int in_group = G2_GROUP_M * tiles_n;
+  const int first_m = (pid / in_group) * G2_GROUP_M;
+  const int gsz = min(tiles_m - first_m, G2_GROUP_M);
+  const int tm = first_m + (pid % in_group) % gsz;
+  const int tn = (pid % in_group) / gsz;
+  const int m0 = tm * BM, n0 = tn * G2_BN;
+
+  const int KS = K >> 5, NTT = N >> 4;
+  const int ks0 = split * kc;
+  const int KT = min(KS, ks0 + kc) - ks0;  // K-tiles (32 deep) of this split
+
+  // per-wave LDS-DMA sources: fragment f = w + NW*j (A fragments first, then B)
+  const char* src[G];
+  int step[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int f = w + NW * j;
+    if (f < AF) {
+      const int row = min(m0 + 16 * f + (lane & 15), M - 1);
+      src[j] = reinterpret_cast<const char*>(x + (size_t)row * K + (size_t)ks0 * 32 + 8 * (lane >> 4));
+      step[j] = 64;
+    } else {
+      const int nt = min((n0 >> 4) + (f - AF), NTT - 1);
+      src[j] = reinterpret_cast<const char*>(W + ((size_t)nt * KS + ks0) * 64 + lane);
+      step[j] = 1024;
+    }
+  }
+  auto issue = [&](int t) {
+    u32x4* buf = lds + (t & (G2_NBUF - 1)) * FR * 64;
+#pragma unroll
+    for (int j = 0; j < G; ++j) glds16(src[j] + (size_t)t * step[j], buf + (w + NW * j) * 64);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < G2_DIST; ++t)
+    if (t < KT) issue(t);
+
+  if constexpr (WM == 2) {
+    // Ping-pong: wave rows 0 and 1 (one wave of each per SIMD) run one barrier apart, so while
+    // one group issues its LDS-DMA + ds_reads (L phase) the other keeps the SIMD's MFMA pipe busy
+    // (M phase). Phase p of a wave: L_p = [issue tile p+3; wait own part of tile p+1; ds_read tile p;
+    // lgkmcnt(0)] -> barrier -> M_p (32 MFMAs) -> barrier. Group 0's L_p sits between barrier
+    // instances 2p and 2p+1, group 1's between 2p+1 and 2p+2, hence:
+    //  RAW: every wave retires its part of tile t in L_{t-1}, before instance 2t; group 0 reads t
+    //       after instance 2t, group 1 after 2t+1.
+    //  WAR: tile t+3 refills tile t-1's slot in L_t; every wave's reads of t-1 completed
+    //       (lgkmcnt(0)) in L_{t-1}, before instance 2t.
+    // Both groups call 2*KT + 2 barriers (the stagger and the closing one are balanced).
+    if (KT > 0) {
+      wait_vmcnt<0>();  // tile 0 (and the rest of the prologue) landed; simple, once per WG
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int t = 0; t < KT; ++t) {
+      if (t + G2_DIST < KT) issue(t + G2_DIST);
+      const int after = min(KT - 1, t + G2_DIST) - (t + 1);  // tiles issued after t+1
+      if (after >= 2)
+        wait_vmcnt<2 * G>();
+      else if (after == 1)
+        wait_vmcnt<G>();
+      else
+        wait_vmcnt<0>();
+      const u32x4* buf = lds + (t & (G2_NBUF - 1)) * FR * 64;
+      u32x4 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+  } else
+  for (int t = 0; t < KT; ++t) {
+    const int ahead = min(KT - 1 - t, G2_DIST - 1);  // tiles issued after t
+    if (ahead >= 2)
+      wait_vmcnt<2 * G>();
+    else if (ahead == 1)
+      wait_vmcnt<G>();
+    else
+      wait_vmcnt<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + G2_DIST < KT) issue(t + G2_DIST);  // refills the buffer read at t-1 (retired by the barrier)
+    const u32x4* buf = lds + (t & (G2_NBUF - 1)) * FR * 64;
+    u32x4 a[8], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+  }
+
+  const int c = lane & 15;
+  if constexpr (MODE == MODE_SWIGLU) {
+    const int F = N >> 1;
+    bf16_t* o = static_cast<bf16_t*>(out);
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      const int gtile = (n0 >> 4) + wc * 4 + j;  // even: gate tile, gtile + 1: its up tile
+      if (gtile >= NTT) continue;
+      const int col = (gtile >> 1) * 16 + c;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + (wr * 8 + i) * 16 + 4 * (lane >> 4) + r;
+          if (row < M) o[(size_t)row * F + col] = f2bf(silu(acc[i][j][r]) * acc[i][j + 1][r]);
+        }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tile = (n0 >> 4) + wc * 4 + j;
+      if (tile >= NTT) continue;
+      const int col = tile * 16 + c;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + (wr * 8 + i) * 16 + 4 * (lane >> 4) + r;
+          if (row >= M) continue;
+          const size_t idx = (size_t)row * N + col;
+          const float v = acc[i][j][r];
+          if constexpr (MODE == MODE_PARTIAL) {
+            static_cast<float*>(out)[(size_t)split * M * N + idx] = v;
+          } else if constexpr (MODE == MODE_RESIDUAL) {
+            float* o = static_cast<float*>(out);
+            const float nv = accumulate ? o[idx] + v : v;
+            o[idx] = nv;
+            if (mirror) mirror[idx] = f2bf(nv);
+          } else if (out_f32) {
+            static_cast<float*>(out)[idx] = v;
+          } else {
+            static_cast<bf16_t*>(out)[idx] = f2bf(v);
+          }
+        }
+    }
+  }
+}
+
 // Sum the split-K partials (fixed order) and apply the epilogue. One thread = 4 consecutive
 // columns of one row (two RoPE pairs; a 16-column tile never straddles a float4).
 template <int MODE>
@@ -251,18 +446,61 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// split-K plan: enough workgroups to fill the chip (>= ~512), >= 8 k-steps per split
+// Which tiled kernel gemm() launches: 2 = gemm2 (default), 1 = the 128x128 register-staged kernel
+// (kept for A/B measurements: tools/bench_gemm.py --impl 1).
+static int g_gemm_impl = 2;
+void gemm_set_impl(int impl) { g_gemm_impl = impl == 1 ? 1 : 2; }
+int gemm_get_impl() { return g_gemm_impl; }
+
+static int g2_wm(int M) { return M <= 128 ? 1 : 2; }
+
+// split-K plan: fill the chip with workgroups while keeping >= 4 K-tiles (gemm2: 1 WG per CU,
+// target ~256 WGs) / >= 8 k-steps (gemm v1: ~512 WGs) per split.
 int gemm_ksplit(int M, int N, int K) {
-  const int tiles = ((N + GB_N - 1) / GB_N) * ((M + GB_M - 1) / GB_M);
   const int KS = K >> 5;
-  int ks = 1;
-  while (tiles * ks < 512 && KS / (ks * 2) >= 8 && ks < 16) ks *= 2;
-  return ks;
+  if (g_gemm_impl == 1) {
+    const int tiles = ((N + GB_N - 1) / GB_N) * ((M + GB_M - 1) / GB_M);
+    int ks = 1;
+    while (tiles * ks < 512 && KS / (ks * 2) >= 8 && ks < 16) ks *= 2;
+    return ks;
+  }
+  const int bm = 128 * g2_wm(M);
+  const int tiles = ((N + G2_BN - 1) / G2_BN) * ((M + bm - 1) / bm);
+  // one WG per CU, and the fp32 partial slabs (ks * M * N * 8 bytes written + read) kept within
+  // ~2x the weight bytes (N * K * 2): measured optimum at M = 128..512 (profiles/README.md)
+  int ks = min(256 / tiles, max(1, K / (2 * M)));
+  ks = ks < 1 ? 1 : (ks > 16 ? 16 : ks);
+  while (ks > 1 && KS / ks < 4) --ks;
+  const int kc = (KS + ks - 1) / ks;
+  return (KS + kc - 1) / kc;
 }
 
 size_t gemm_workspace_floats(int M, int N, int K) {
   const int ks = gemm_ksplit(M, N, K);
   return ks > 1 ? (size_t)ks * M * N : 0;
+}
+
+template <int MODE>
+static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
+                      bf16_t* mirror, int kc, int ksplit, hipStream_t s) {
+  const int wm = g2_wm(M), bm = 128 * wm;
+  const int tm = (M + bm - 1) / bm, tn = (N + G2_BN - 1) / G2_BN;
+  const int grid = tm * tn * ksplit;
+  if (wm == 1)
+    gemm2_kernel<MODE, 1><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+  else
+    gemm2_kernel<MODE, 2><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+}
+
+template <int MODE>
+static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
+                         int out_f32, bf16_t* mirror, int kc, int ksplit, hipStream_t s) {
+  if (g_gemm_impl == 2) {
+    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, s);
+  } else {
+    dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
+    gemm_kernel<MODE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc);
+  }
 }
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
@@ -275,27 +513,20 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (ksplit < 1) ksplit = 1;
   const int kc = (KS + ksplit - 1) / ksplit;
   ksplit = (KS + kc - 1) / kc;
+  if (mode == MODE_QKV && ksplit < 2) return -1;
   const u32x4* w = static_cast<const u32x4*>(W);
   if (ksplit == 1) {
-    dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, 1);
     switch (mode) {
-      case MODE_STORE:
-        gemm_kernel<MODE_STORE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc);
-        break;
-      case MODE_RESIDUAL:
-        gemm_kernel<MODE_RESIDUAL><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 1, mirror, kc);
-        break;
-      case MODE_SWIGLU:
-        gemm_kernel<MODE_SWIGLU><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, 0, nullptr, kc);
-        break;
+      case MODE_STORE: launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, s); break;
+      case MODE_RESIDUAL: launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, s); break;
+      case MODE_SWIGLU: launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, s); break;
       default: return -1;
     }
     JLA_CHECK_LAUNCH();
     return 0;
   }
   if ((N & 3) || ws == nullptr || ws_floats < (size_t)ksplit * M * N) return -3;
-  dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
-  gemm_kernel<MODE_PARTIAL><<<grid, G_THREADS, 0, s>>>(x, w, ws, M, N, K, 0, 1, nullptr, kc);
+  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, s);
   JLA_CHECK_LAUNCH();
   const size_t total4 = (size_t)M * N / 4;
   const int rgrid = (int)((total4 + 255) / 256);

@@ -162,7 +162,7 @@ def _tiled_input(x, rms_eps):
 
 
 def _gemm_ws(e, m, n, k, device):
-    ks = e.gemm_ksplit(m, n, k)
+    ks = autotune.choose_gemm_ksplit(e, m, n, k, device)
     ws = workspace.get("gemm_ws", ks * m * n, torch.float32, device) if ks > 1 else None
     return ks, ws
 

@@ -90,3 +90,59 @@ def _measure(x, w, run, cands) -> int:
 
 def table() -> Dict[Tuple, int]:
     return dict(_CACHE)
+
+
+# ----------------------------------------------------------------------------------------------
+# Split-K factor of the tiled GEMM (csrc/kernels/gemm.hip) for decode-sized M: more K splits fill
+# more CUs but every split writes and re-reads an fp32 [M, N] slab, so the best factor depends on
+# (M, N, K) -- at M=256 it measured 8 for qkv/o (K=4096), 16 for down (K=14336), 2 for gate_up
+# (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
+_KS_CACHE: Dict[Tuple, int] = {}
+KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
+
+
+def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
+    key = (m, n, k)
+    ks = _KS_CACHE.get(key)
+    if ks is not None:
+        return ks
+    heur = e.gemm_ksplit(m, n, k)
+    if heur == 1 or not ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return heur
+    ks = _measure_ksplit(e, m, n, k, device, heur)
+    _KS_CACHE[key] = ks
+    return ks
+
+
+def _measure_ksplit(e, m, n, k, device, heur) -> int:
+    kt = k // 32
+    cands = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
+    nbytes = n * k * 2
+    copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
+    ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
+            for _ in range(copies)]
+    x = torch.randn(m, k, device=device).to(torch.bfloat16)
+    out = torch.empty(m, n, dtype=torch.bfloat16, device=device)
+    ws = torch.empty(max(cands) * m * n, dtype=torch.float32, device=device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best, best_t = heur, float("inf")
+    for c in cands:
+        def run(i):
+            e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, c, ws if c > 1 else None)
+        for i in range(2):
+            run(i)
+        iters = 2 * copies
+        ev0.record()
+        for i in range(iters):
+            run(i)
+        ev1.record()
+        ev1.synchronize()
+        t = ev0.elapsed_time(ev1) / iters
+        if t < best_t:
+            best, best_t = c, t
+    del ws_w, ws
+    return best
+
+
+def ksplit_table() -> Dict[Tuple, int]:
+    return dict(_KS_CACHE)

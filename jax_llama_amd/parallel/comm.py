@@ -29,8 +29,12 @@ class TPComm:
     def from_context(cls, ctx, use_custom: bool = True, max_bytes: int = 8 << 20) -> "TPComm":
         custom = None
         if ctx.tp_size > 1 and ctx.device.type == "cuda" and use_custom:
-            from .custom_allreduce import CustomAllReduce
-            custom = CustomAllReduce.create(ctx, max_bytes=max_bytes)
+            try:
+                from .custom_allreduce import CustomAllReduce
+            except ImportError:  # one-shot xGMI kernel not built: RCCL handles every message
+                CustomAllReduce = None
+            if CustomAllReduce is not None:
+                custom = CustomAllReduce.create(ctx, max_bytes=max_bytes)
         return cls(ctx.tp_size, ctx.tp_rank, ctx.tp_group, custom)
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Tiled MFMA GEMM (csrc/kernels/gemm.hip) vs the vendor library (torch.mm -> hipBLASLt) on the
+Llama projection shapes, for decode batches (M = 64..512) and prefill (M = B * S).
+
+Weights rotate over copies larger than the Infinity Cache so each timed call reads them from HBM.
+Prints one JSON line per (shape, impl): microseconds, TFLOP/s and weight TB/s.
+Usage: python tools/bench_gemm.py [--m 128 256 4096] [--model llama3-8b] [--ksplit 0]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from jax_llama_amd import ops  # noqa: E402
+from jax_llama_amd.config import get_preset  # noqa: E402
+from jax_llama_amd.models.weights import PackedLinear  # noqa: E402
+
+DEV = "cuda"
+
+
+def timeit(fn, iters):
+    for i in range(3):
+        fn(i)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for i in range(iters):
+        fn(i)
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) * 1000.0 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--m", type=int, nargs="+", default=[64, 128, 256, 512, 4096])
+    ap.add_argument("--ksplit", type=int, nargs="+", default=[0], help="0 = library heuristic")
+    ap.add_argument("--no-blas", action="store_true")
+    ap.add_argument("--impl", type=int, nargs="+", default=[2], help="tiled kernel generation(s) to time")
+    ap.add_argument("--ops", nargs="+", default=None)
+    args = ap.parse_args()
+    cfg = get_preset(args.model)
+    d, f, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+    h, hkv = cfg.num_attention_heads, cfg.num_key_value_heads
+    shapes = {"qkv": ((h + 2 * hkv) * hd, d), "o": (d, h * hd), "gate_up": (2 * f, d), "down": (d, f),
+              "lm_head": (cfg.vocab_size, d)}
+    e = ops.ext()
+    for name, (n, k) in shapes.items():
+        if args.ops and name not in args.ops:
+            continue
+        nbytes = n * k * 2
+        copies = max(2, int((700 << 20) // nbytes) + 1)
+        dense = [(torch.randn(n, k, device=DEV) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        packed = [PackedLinear.from_dense(w, DEV) for w in dense]
+        for m in args.m:
+            x = (torch.randn(m, k, device=DEV)).to(torch.bfloat16)
+            out = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+            flop = 2.0 * m * n * k
+            iters = max(5, min(200, int(2e13 / flop)))
+            res = {}
+            ref = None
+            for impl in args.impl:
+                e.gemm_set_impl(impl)
+                for ks in args.ksplit:
+                    kk = ks or e.gemm_ksplit(m, n, k)
+                    ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
+
+                    def run(i, kk=kk, ws=ws):
+                        e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk, ws if kk > 1 else None)
+                    res[f"v{impl}_ks{kk}"] = timeit(run, iters)
+                    run(0)
+                    got = out.float()
+                    if ref is None:
+                        ref = (x.float() @ dense[0].float().t())
+                    err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+                    assert err < 2e-2, (name, m, impl, kk, err)
+            e.gemm_set_impl(2)
+            if not args.no_blas:
+                res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)
+            for impl, us in res.items():
+                print(json.dumps({"op": name, "m": m, "n": n, "k": k, "impl": impl, "us": round(us, 2),
+                                  "tflops": round(flop / us / 1e6, 1), "weight_tbps": round(nbytes / us / 1e6, 2)}),
+                      flush=True)
+        del dense, packed
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

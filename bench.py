@@ -34,7 +34,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=16, help="sequences per replica")
+    # Serving-throughput operating point: 512 concurrent sequences per replica (KV cache 13 GB of the
+    # 288 GB HBM). Smaller batches are latency points (decode_ms_per_token): --batch 1 / 16.
+    ap.add_argument("--batch", type=int, default=512, help="sequences per replica")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count (INVALID for the metric)")

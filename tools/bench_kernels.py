@@ -97,7 +97,7 @@ def main():
     # decode attention at the bench shape
     if args.ops and "attn" not in args.ops:
         return
-    for b, t in ((16, 384), (1, 4096), (64, 1024)):
+    for b, t in ((16, 384), (1, 4096), (64, 1024), (256, 384), (512, 384), (512, 256)):
         kc = torch.randn(b, hkv, t, hd, device=DEV).to(torch.bfloat16)
         vc = torch.randn_like(kc)
         q = torch.randn(b, 1, h, hd, device=DEV).to(torch.bfloat16)

@@ -377,6 +377,46 @@ void decode_update(Tensor nxt, Tensor finished, Tensor sequences, Tensor cur_len
      "decode_update");
 }
 
+// ---- custom all-reduce (allreduce.hip) -------------------------------------------------------
+py::tuple car_alloc(int64_t max_bytes, int64_t world) {
+  void* buf = nullptr;
+  void* sig = nullptr;
+  hipIpcMemHandle_t hb, hs;
+  rc(jla::car_alloc(max_bytes, world, &buf, &sig, &hb, &hs), "car_alloc");
+  return py::make_tuple((int64_t)(uintptr_t)buf, (int64_t)(uintptr_t)sig,
+                        py::bytes(reinterpret_cast<const char*>(&hb), sizeof(hb)),
+                        py::bytes(reinterpret_cast<const char*>(&hs), sizeof(hs)));
+}
+
+int64_t car_init(int64_t rank, int64_t world, int64_t max_bytes, int64_t buf, int64_t sig, std::vector<std::string> hbufs,
+                 std::vector<std::string> hsigs) {
+  check((int64_t)hbufs.size() == world && (int64_t)hsigs.size() == world, "car_init: one handle per rank");
+  std::vector<hipIpcMemHandle_t> hb(world), hs(world);
+  for (int64_t p = 0; p < world; ++p) {
+    check(hbufs[p].size() == sizeof(hipIpcMemHandle_t) && hsigs[p].size() == sizeof(hipIpcMemHandle_t),
+          "car_init: handle size");
+    std::memcpy(&hb[p], hbufs[p].data(), sizeof(hipIpcMemHandle_t));
+    std::memcpy(&hs[p], hsigs[p].data(), sizeof(hipIpcMemHandle_t));
+  }
+  void* state = nullptr;
+  rc(jla::car_init(rank, world, max_bytes, reinterpret_cast<void*>(buf), reinterpret_cast<void*>(sig), hb.data(),
+                   hs.data(), &state),
+     "car_init");
+  return (int64_t)(uintptr_t)state;
+}
+
+void car_allreduce(int64_t state, Tensor in, Tensor out) {
+  check_gpu(in, "in");
+  check_gpu(out, "out");
+  check(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "car_allreduce in/out");
+  check(in.scalar_type() == torch::kBFloat16 || in.scalar_type() == torch::kFloat32, "car_allreduce dtype");
+  const int64_t nbytes = in.numel() * in.element_size();
+  check(nbytes % 16 == 0, "car_allreduce: bytes % 16");
+  rc(jla::car_allreduce(reinterpret_cast<void*>(state), in.data_ptr(), out.data_ptr(), nbytes,
+                        in.scalar_type() == torch::kBFloat16, stream()),
+     "car_allreduce");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -408,6 +448,11 @@ PYBIND11_MODULE(_C, m) {
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));
   m.def("argmax", &argmax);
   m.def("topk_chunks", [](int64_t v) { return jla::topk_chunks(v); });
+  m.def("car_alloc", &car_alloc);
+  m.def("car_init", &car_init);
+  m.def("car_allreduce", &car_allreduce);
+  m.def("car_error", [](int64_t st) { return jla::car_error(reinterpret_cast<void*>(st)); });
+  m.def("car_destroy", [](int64_t st) { jla::car_destroy(reinterpret_cast<void*>(st)); });
   m.def("topk_chunk", &topk_chunk);
   m.def("topk_merge", &topk_merge, py::arg("cv"), py::arg("ci"), py::arg("k"), py::arg("mode"),
         py::arg("out_v") = py::none(), py::arg("out_i") = py::none(), py::arg("nxt") = py::none(),

@@ -37,11 +37,20 @@ class TPComm:
                 custom = CustomAllReduce.create(ctx, max_bytes=max_bytes)
         return cls(ctx.tp_size, ctx.tp_rank, ctx.tp_group, custom)
 
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        # GPU tensors over a gloo group (multi-process tests sharing one GPU): stage through the host
+        return t.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
             return t
         if self.custom is not None and self.custom.can_handle(t):
             self.custom.all_reduce_(t)
+            return t
+        if self._host_staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
             return t
         dist.all_reduce(t, group=self.group)
         return t
@@ -50,9 +59,15 @@ class TPComm:
         """Returns ``[size, *t.shape]``."""
         if self.size == 1:
             return t.unsqueeze(0)
+        src = t.contiguous().reshape(-1)
+        staged = self._host_staged(t)
+        if staged:
+            src = src.cpu()
         # flat [size * numel] buffer: the layout both RCCL and gloo accept for all_gather_into_tensor
-        out = torch.empty(self.size * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t.contiguous().reshape(-1), group=self.group)
+        out = torch.empty(self.size * t.numel(), dtype=t.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src, group=self.group)
+        if staged:
+            out = out.to(t.device)
         return out.view((self.size,) + tuple(t.shape))
 
 

@@ -437,6 +437,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);
+  m.def("attn_set_impl", [](int64_t impl, int64_t waves_target) { jla::attn_set_impl(impl, waves_target); },
+        py::arg("impl"), py::arg("waves_target") = 0);
   m.def("attn_decode_splits",
         [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });
   m.def("linear_qkv", &linear_qkv);

@@ -31,7 +31,7 @@ JLA_DEV float ld_wt(const float* p) {
 
 template <int REP, int KPG>
 __global__ void __launch_bounds__(AD_WAVES * 64)
-    attn_decode_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    attn_decode_v1_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                        const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                        const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out,
                        float* __restrict__ ws, int32_t* __restrict__ tickets, int H, int Hkv, int T, int t_cap,
@@ -254,13 +254,284 @@ __global__ void __launch_bounds__(AD_WAVES * 64)
   }
 }
 
-static int kpg_for(int rep) { return rep <= 4 ? 8 : (rep == 8 ? 4 : 2); }
 
-int attn_decode_chunk(int B, int Hkv, int T, int rep) { return 16 * kpg_for(rep); }
+// ---------------------------------------------------------------------------------------------
+// v2 (default): streaming decode attention, one WAVE per work item (batch row, kv head, key split).
+//
+// v1 above gives every 128-key chunk its own workgroup (load everything, compute, merge), so a CU's
+// HBM queue drains between a workgroup's load burst and its compute/merge phases and every chunk
+// pays a merge; it held ~3-3.8 TB/s. Here each wave streams its item's keys in chunks of 4*KPG rows
+// through two register buffers (chunk c+1 in flight while chunk c is scored), keeps a running
+// (max, sum, o) per query head (online softmax), and needs no workgroup barrier at all. Splits are
+// only used when B*Hkv alone cannot fill the chip (small batch / long context): the split count
+// targets >= `waves_target` waves, and the last-arriving wave of a (b, kv head) merges the splits'
+// (m, l, o) (sc1 stores -> vmcnt(0) -> one agent-scope ticket add per wave, as in v1).
+//
+// Lane layout per chunk: lane = 16*g + li; row r of lane group g is key k0 + CK*c + 4*r + g, and
+// the lane holds dims [8*li, 8*li + 8) of it, so one wave load instruction covers 4 consecutive
+// cache rows (1 KiB contiguous). QK^T: 8 FMAs + a 16-lane DPP sum; P.V: lane-local over the group's
+// rows, summed across the 4 groups once per item.
+static int g_attn_impl = 2;
+static int g_attn_waves_target = 2048;
+static int g_attn_v2_min_pairs = 2048;
+void attn_set_impl(int impl, int waves_target);
+
+template <int REP, int KPG, int NS, bool MASK>
+__global__ void __launch_bounds__(64)
+    attn_decode_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                          const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
+                          const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out,
+                          float* __restrict__ ws, int32_t* __restrict__ tickets, int B, int H, int Hkv, int T,
+                          int t_cap, int nsplit, int split_len, float scale) {
+  constexpr int CK = 4 * KPG;        // keys per chunk
+  constexpr int SLOT = 2 * KPG * 64;  // u32x4 per ring slot: KPG K-row loads then KPG V-row loads
+  constexpr int QL = (REP + 3) / 4;  // q LDS-DMA loads (4 heads of 256 B per wave load)
+  __shared__ u32x4 ring[NS * SLOT + QL * 64];
+  u32x4* qbuf = ring + NS * SLOT;
+  const int lane = threadIdx.x;
+  const int item = blockIdx.x;
+  const int pair = item / nsplit, split = item - pair * nsplit;
+  const int kvh = pair % Hkv, b = pair / Hkv;
+  const int g = lane >> 4, li = lane & 15;
+  const int slot = slot_ptr[0];
+  const int lo = kv_start[b];
+  const int s0 = split * split_len;
+  const int k0 = max(s0, lo);
+  const int k1 = min(min(s0 + split_len, t_cap), slot + 1);  // keys [k0, k1)
+  const int h0 = kvh * REP;
+
+  float m_h[REP], l_h[REP];
+  f32x2_t o[REP][4];  // dims 8*li + 2i, 8*li + 2i + 1
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    m_h[h] = -INFINITY;
+    l_h[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[h][i] = f32x2_t{0.f, 0.f};
+  }
+
+  if (k0 < k1) {
+    const size_t head_off = ((size_t)b * Hkv + kvh) * T * AD_DH + 8 * li;
+    const bf16_t* kbase = kc + head_off;
+    const bf16_t* vbase = vc + head_off;
+    const uint8_t* mrow = MASK ? key_mask + (size_t)b * mask_len : nullptr;
+    // q rides the same LDS-DMA queue as K/V (an ordinary load beside glds makes hipcc wait
+    // vmcnt(0) at its first use, draining the ring): 16 lanes per head, 16 B each
+    const bf16_t* qrow = q + ((size_t)b * H + h0) * AD_DH;
+#pragma unroll
+    for (int i = 0; i < QL; ++i)
+      glds16(qrow + (size_t)min(4 * i + g, REP - 1) * AD_DH + 8 * li, qbuf + i * 64);
+    const int nc = (k1 - k0 + CK - 1) / CK;
+    u32x4 qp[REP];  // this lane's 8 dims of each query head, packed bf16 (v_dot2 operand)
+
+    // LDS-DMA: chunk c -> ring slot c % NS; lane l of K-row load r lands at slot + r*64 + l, i.e.
+    // exactly where the same lane reads it back (no other wave touches this ring).
+    auto issue = [&](int c) __attribute__((always_inline)) {
+      u32x4* sl = ring + (c % NS) * SLOT;
+      const int jb = k0 + c * CK + g;
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) glds16(kbase + (size_t)min(jb + 4 * r, k1 - 1) * AD_DH, sl + r * 64);
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) glds16(vbase + (size_t)min(jb + 4 * r, k1 - 1) * AD_DH, sl + (KPG + r) * 64);
+    };
+    auto compute = [&](const u32x4* kr, const u32x4* vr, int c) __attribute__((always_inline)) {
+      const int jb = k0 + c * CK + g;
+      float sc[REP][KPG];
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) {
+        const int j = jb + 4 * r;
+        bool valid = j < k1;
+        if constexpr (MASK) valid = valid && (j >= mask_len || mrow[j] != 0);
+        const bf16x8_t kv = __builtin_bit_cast(bf16x8_t, kr[r]);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          // (bit-casting single vector elements here miscompiles: every i read element 0)
+          const bf16x8_t qv = __builtin_bit_cast(bf16x8_t, qp[h]);
+          float d = 0.f;
+          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 0, 1), __builtin_shufflevector(qv, qv, 0, 1), d, false);
+          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 2, 3), __builtin_shufflevector(qv, qv, 2, 3), d, false);
+          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 4, 5), __builtin_shufflevector(qv, qv, 4, 5), d, false);
+          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 6, 7), __builtin_shufflevector(qv, qv, 6, 7), d, false);
+          d = row16_sum(d) * scale;
+          sc[h][r] = valid ? d : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < REP; ++h) {
+        float cm = sc[h][0];
+#pragma unroll
+        for (int r = 1; r < KPG; ++r) cm = fmaxf(cm, sc[h][r]);
+        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        const float mn = fmaxf(m_h[h], cm);
+        const float alpha = (m_h[h] == -INFINITY) ? 0.f : __expf(m_h[h] - mn);
+        m_h[h] = mn;
+        l_h[h] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[h][i] *= alpha;
+      }
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) {
+        f32x2_t vf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          vf[i] = f32x2_t{__uint_as_float(vr[r][i] << 16), __uint_as_float(vr[r][i] & 0xffff0000u)};
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          const float p = (sc[h][r] == -INFINITY) ? 0.f : __expf(sc[h][r] - m_h[h]);
+          l_h[h] += p;
+          const f32x2_t pp = {p, p};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[h][i] = __builtin_elementwise_fma(pp, vf[i], o[h][i]);
+        }
+      }
+    };
+
+    // ring: NS-1 chunks in flight ahead of the one being scored; waits counted by hand (the loop has
+    // no compiler-visible global loads, so hipcc inserts no vmcnt of its own)
+#pragma unroll
+    for (int c = 0; c < NS - 1; ++c)
+      if (c < nc) issue(c);
+    {  // q landed once chunk 0 has (issued before it)
+      const int ahead = min(nc - 1, NS - 2);
+      if (ahead >= 2)
+        wait_vmcnt<2 * 2 * KPG>();
+      else if (ahead == 1)
+        wait_vmcnt<2 * KPG>();
+      else
+        wait_vmcnt<0>();
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < REP; ++h) qp[h] = qbuf[(h >> 2) * 64 + (h & 3) * 16 + li];
+    for (int c = 0; c < nc; ++c) {
+      if (c + NS - 1 < nc) issue(c + NS - 1);
+      const int ahead = min(nc - 1 - c, NS - 1);  // chunks issued after c
+      if (ahead >= 3)
+        wait_vmcnt<3 * 2 * KPG>();
+      else if (ahead == 2)
+        wait_vmcnt<2 * 2 * KPG>();
+      else if (ahead == 1)
+        wait_vmcnt<2 * KPG>();
+      else
+        wait_vmcnt<0>();
+      asm volatile("" ::: "memory");
+      const u32x4* sl = ring + (c % NS) * SLOT;
+      u32x4 kr[KPG], vr[KPG];
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) kr[r] = sl[r * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) vr[r] = sl[(KPG + r) * 64 + lane];
+      compute(kr, vr, c);
+      // WAR: slot c % NS is refilled by the issue at the top of iteration c + 1; its ds_reads above
+      // were consumed by compute (lgkmcnt waited before use), so they have completed.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // across the 4 lane groups: each group summed its own rows (l is the same in its 16 lanes)
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      l_h[h] += __shfl_xor(l_h[h], 16, 64);
+      l_h[h] += __shfl_xor(l_h[h], 32, 64);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          o[h][i][e] += __shfl_xor(o[h][i][e], 16, 64);
+          o[h][i][e] += __shfl_xor(o[h][i][e], 32, 64);
+        }
+    }
+  }
+
+  if (nsplit == 1) {
+    if (g == 0) {
+#pragma unroll
+      for (int h = 0; h < REP; ++h) {
+        const float inv = l_h[h] > 0.f ? 1.f / l_h[h] : 0.f;
+        float r8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r8[e] = o[h][e >> 1][e & 1] * inv;
+        *reinterpret_cast<u32x4*>(out + ((size_t)b * H + h0 + h) * AD_DH + 8 * li) = pack8(r8);
+      }
+    }
+    return;
+  }
+
+  // ---- publish this split's (m, l, o) with write-through stores, then one ticket add per wave
+  float* part = ws + (size_t)item * REP * (AD_DH + 2);
+  if (g == 0) {
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st_wt(part + h * (AD_DH + 2) + 2 + 8 * li + e, o[h][e >> 1][e & 1]);
+      if (li == 0) {
+        st_wt(part + h * (AD_DH + 2), m_h[h]);
+        st_wt(part + h * (AD_DH + 2) + 1, l_h[h]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int last = 0;
+  if (lane == 0) {
+    int32_t* tk = tickets + pair;
+    const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == nsplit - 1;
+    if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for next replay
+  }
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+
+  // ---- last arriver (one wave): log-sum-exp merge of the pair's splits with sc1 loads
+  const float* base = ws + (size_t)pair * nsplit * REP * (AD_DH + 2);
+#pragma unroll 1
+  for (int h = 0; h < REP; ++h) {
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ld_wt(base + ((size_t)s * REP + h) * (AD_DH + 2)));
+    float num0 = 0.f, num1 = 0.f, den = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const float* ps = base + ((size_t)s * REP + h) * (AD_DH + 2);
+      const float ms = ld_wt(ps), ls = ld_wt(ps + 1);
+      const float a = ld_wt(ps + 2 + lane), c = ld_wt(ps + 2 + 64 + lane);
+      const float wgt = (ms == -INFINITY || M == -INFINITY) ? 0.f : __expf(ms - M);
+      den += wgt * ls;
+      num0 += wgt * a;
+      num1 += wgt * c;
+    }
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+    bf16_t* op = out + ((size_t)b * H + h0 + h) * AD_DH;
+    op[lane] = f2bf(num0 * inv);
+    op[64 + lane] = f2bf(num1 * inv);
+  }
+}
+
+static int kpg_v1(int rep) { return rep <= 4 ? 8 : (rep == 8 ? 4 : 2); }
+static int g_kpg_small = 4, g_ns = 3;  // v2 ring geometry for REP <= 4 (A/B: attn_set_impl)
+static int kpg_v2(int rep) { return rep <= 4 ? g_kpg_small : (rep == 8 ? 2 : 1); }
+
+// impl 1 = v1; 2 = v2 with (KPG 4, 3 slots) [default]; 3 = v2 (KPG 2, 4 slots); 4 = v2 (KPG 4, 2 slots)
+void attn_set_impl(int impl, int waves_target) {
+  g_attn_impl = impl == 1 ? 1 : 2;
+  g_kpg_small = impl == 3 ? 2 : 4;
+  g_ns = impl == 3 ? 4 : (impl == 4 ? 2 : 3);
+  if (waves_target > 0) g_attn_waves_target = waves_target;
+  g_attn_v2_min_pairs = waves_target < 0 ? -waves_target : 2048;  // < 0: force v2 down to -target pairs
+}
+
+// v2 streams whole (b, kv head) pairs; below ~2048 pairs its splits' serial merge loses to v1's
+// chunk-per-workgroup design (profiles/r1_attn_decode_v2_ab.jsonl), so small batches stay on v1.
+static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_attn_v2_min_pairs; }
+
+int attn_decode_chunk(int B, int Hkv, int T, int rep) { return use_v2(B, Hkv) ? 4 * kpg_v2(rep) : 16 * kpg_v1(rep); }
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
-  const int ch = attn_decode_chunk(B, Hkv, T, rep);
-  return (T + ch - 1) / ch;
+  if (!use_v2(B, Hkv)) {
+    const int ch = 16 * kpg_v1(rep);
+    return (T + ch - 1) / ch;
+  }
+  const int pairs = B * Hkv;
+  const int max_split = T > 64 ? (T + 63) / 64 : 1;  // >= 64 keys per split
+  int ns = (g_attn_waves_target + pairs - 1) / pairs;
+  ns = ns < 1 ? 1 : (ns > max_split ? max_split : ns);
+  return ns;
 }
 
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
@@ -271,21 +542,56 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   const int rep = H / Hkv;
   if (attn_decode_splits(B, Hkv, t_cap, rep) != nsplit) return -2;
   const float scale = 1.f / sqrtf((float)Dh);
-  dim3 grid(nsplit, Hkv, B);
+  if (!use_v2(B, Hkv)) {
+    dim3 grid(nsplit, Hkv, B);
 #define JLA_AD(R)                                                                                              \
   case R:                                                                                                     \
-    attn_decode_kernel<R, (R <= 4 ? 8 : (R == 8 ? 4 : 2))><<<grid, AD_WAVES * 64, 0, s>>>(                     \
+    attn_decode_v1_kernel<R, (R <= 4 ? 8 : (R == 8 ? 4 : 2))><<<grid, AD_WAVES * 64, 0, s>>>(                  \
         q, kc, vc, slot, kv_start, key_mask, mask_len, out, ws, tickets, H, Hkv, T, t_cap, nsplit, scale);     \
     break;
+    switch (rep) {
+      JLA_AD(1)
+      JLA_AD(2)
+      JLA_AD(4)
+      JLA_AD(8)
+      JLA_AD(16)
+      default: return -1;
+    }
+#undef JLA_AD
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
+  const int items = B * Hkv * nsplit;
+  int split_len = (t_cap + nsplit - 1) / nsplit;
+  split_len = (split_len + 31) / 32 * 32;
+#define JLA_AD2(R, KPG, NS)                                                                                          \
+  if (key_mask)                                                                                                     \
+    attn_decode_v2_kernel<R, KPG, NS, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
+                                                                 ws, tickets, B, H, Hkv, T, t_cap, nsplit, split_len, \
+                                                                 scale);                                           \
+  else                                                                                                              \
+    attn_decode_v2_kernel<R, KPG, NS, false><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
+                                                                  ws, tickets, B, H, Hkv, T, t_cap, nsplit,          \
+                                                                  split_len, scale);
+  const int geo = g_kpg_small * 10 + g_ns;
   switch (rep) {
-    JLA_AD(1)
-    JLA_AD(2)
-    JLA_AD(4)
-    JLA_AD(8)
-    JLA_AD(16)
+    case 1:
+    case 2:
+    case 4:
+      // REP <= 4 shares one body per geometry (REP only sizes the register arrays)
+      if (rep == 1) {
+        if (geo == 43) { JLA_AD2(1, 4, 3) } else if (geo == 24) { JLA_AD2(1, 2, 4) } else { JLA_AD2(1, 4, 2) }
+      } else if (rep == 2) {
+        if (geo == 43) { JLA_AD2(2, 4, 3) } else if (geo == 24) { JLA_AD2(2, 2, 4) } else { JLA_AD2(2, 4, 2) }
+      } else {
+        if (geo == 43) { JLA_AD2(4, 4, 3) } else if (geo == 24) { JLA_AD2(4, 2, 4) } else { JLA_AD2(4, 4, 2) }
+      }
+      break;
+    case 8: JLA_AD2(8, 2, 4) break;
+    case 16: JLA_AD2(16, 1, 4) break;
     default: return -1;
   }
-#undef JLA_AD
+#undef JLA_AD2
   JLA_CHECK_LAUNCH();
   return 0;
 }

@@ -51,6 +51,7 @@ int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const in
                   hipStream_t s);
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep);
+void attn_set_impl(int impl, int waves_target);  // 2 = streaming (default), 1 = v1 (A/B)
 int attn_decode_splits(int B, int Hkv, int T, int rep);
 // ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,

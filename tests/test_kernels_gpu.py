@@ -147,6 +147,34 @@ def test_attention_decode(rep, t, slot):
     assert got[2].float().abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("rep", [1, 4, 8])
+@pytest.mark.parametrize("t,slot", [(40, 17), (300, 299), (1030, 700)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_decode_streaming_v2(rep, t, slot, masked):
+    """The streaming (LDS-DMA ring, wave-per-item) decode kernel normally serves only large batches;
+    force it at small B so its split + last-arriver merge path and the key-mask path are covered."""
+    e = ops.ext()
+    b, hkv, dh = 3, 2, 128
+    h = hkv * rep
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, 1, h, dh).to(BF16)
+    kv_start = torch.tensor([0, 5, slot + 1], dtype=torch.int32)
+    mask = None
+    if masked:
+        mask = (torch.rand(b, t) > 0.3).to(torch.uint8)
+        mask[:, slot] = 1
+    expect = ref.attention(q, kc, vc, slot, kv_start, mask).reshape(b, h * dh)
+    try:
+        e.attn_set_impl(2, -1)  # v2 for any batch size
+        got = ops.attention(q.to(DEV), kc.to(DEV), vc.to(DEV), torch.tensor([slot], dtype=torch.int32, device=DEV),
+                            kv_start.to(DEV), None if mask is None else mask.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        e.attn_set_impl(2, 0)
+    _close(got, expect, 2e-2, 2e-2)
+    assert got[2].float().abs().max().item() == 0.0
+
+
 def test_attention_decode_key_mask():
     b, hkv, rep, t, dh, slot = 2, 2, 4, 96, 128, 80
     kc, vc = _cache(b, hkv, t, dh)

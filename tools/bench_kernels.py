@@ -47,7 +47,9 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[1, 4])
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ops", nargs="+", default=None, help="subset of qkv o gate_up down lm_head attn")
+    ap.add_argument("--attn-impls", default="1:0,2:4096", help="impl:waves_target pairs for attn A/B")
     args = ap.parse_args()
+    args.attn_impls = [tuple(int(v) for v in p.split(":")) for p in args.attn_impls.split(",")]
     cfg = get_preset(args.model)
     d, f, hd = cfg.hidden_size, cfg.intermediate_size // args.tp, cfg.head_dim
     h, hkv = cfg.num_attention_heads // args.tp, cfg.num_key_value_heads // args.tp
@@ -97,16 +99,25 @@ def main():
     # decode attention at the bench shape
     if args.ops and "attn" not in args.ops:
         return
-    for b, t in ((16, 384), (1, 4096), (64, 1024), (256, 384), (512, 384), (512, 256)):
+    for b, t in ((16, 384), (1, 4096), (64, 1024), (256, 384), (512, 384), (512, 256), (1024, 384)):
         kc = torch.randn(b, hkv, t, hd, device=DEV).to(torch.bfloat16)
         vc = torch.randn_like(kc)
         q = torch.randn(b, 1, h, hd, device=DEV).to(torch.bfloat16)
         slot = torch.tensor([t - 1], dtype=torch.int32, device=DEV)
         ks = torch.zeros(b, dtype=torch.int32, device=DEV)
-        us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
         nbytes = 2 * kc.numel() * 2
-        print(json.dumps({"op": "attn_decode", "b": b, "t": t, "us": round(us, 2),
-                          "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
+        ref_out = None
+        for impl, target in args.attn_impls:
+            e.attn_set_impl(impl, target)
+            us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
+            o = ops.attention(q, kc, vc, slot, ks).float()
+            ref_out = o if ref_out is None else ref_out
+            print(json.dumps({"op": "attn_decode", "impl": impl, "waves_target": target, "b": b, "t": t,
+                              "nsplit": e.attn_decode_splits(b, hkv, t, h // hkv), "us": round(us, 2),
+                              "TBps": round(nbytes / us / 1e6, 3),
+                              "max_diff_vs_first": round(float((o - ref_out).abs().max()), 5)}), flush=True)
+        e.attn_set_impl(2, 4096)
+        del kc, vc
 
 
 if __name__ == "__main__":

@@ -214,6 +214,17 @@ class LLaMAForCausalLM:
         self.lm_head = PackedLinear.random(self.vocab_local, d, dev, std, gen)
         return self
 
+    def save_pretrained(self, save_directory: str) -> str:
+        """Deployed-form safetensors checkpoint of this rank (``utils/native_ckpt.py``)."""
+        from ..utils.native_ckpt import save_pretrained
+        return save_pretrained(self, save_directory)
+
+    @classmethod
+    def from_pretrained(cls, directory: str, device="cpu", comm: Optional[TPComm] = None):
+        """Reload a ``save_pretrained`` checkpoint (same TP degree) straight into the kernel layout."""
+        from ..utils.native_ckpt import from_pretrained
+        return from_pretrained(directory, device=device, comm=comm)
+
     def weight_bytes(self) -> int:
         n = self.wte.numel() * 2 + self.lm_head.nbytes()
         for lw in self.layers:

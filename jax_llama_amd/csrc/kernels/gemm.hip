@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(G_THREADS)
 // Workgroups are remapped so consecutive tiles share an XCD (its own L2), M-grouped by 8.
 constexpr int G2_BN = 256, G2_NBUF = 4, G2_DIST = 3, G2_GROUP_M = 8;
 
-template <int MODE, int WM>
+template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n) {
@@ -183,7 +183,8 @@ __global__ void __launch_bounds__(256 * WM)
   constexpr int AF = BM / 16, BF = G2_BN / 16, FR = AF + BF;  // fragments per K-tile
   constexpr int G = FR / NW;                                   // LDS-DMA loads per wave per K-tile
   static_assert(FR % NW == 0, "fragment split");
-  __shared__ u32x4 lds[G2_NBUF * FR * 64];
+  constexpr int DIST = NBUF - 1;
+  __shared__ u32x4 lds[NBUF * FR * 64];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 2, wc = w & 3;
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(256 * WM)
     }
   }
   auto issue = [&](int t) {
-    u32x4* buf = lds + (t & (G2_NBUF - 1)) * FR * 64;
+    u32x4* buf = lds + (t % NBUF) * FR * 64;
 #pragma unroll
     for (int j = 0; j < G; ++j) glds16(src[j] + (size_t)t * step[j], buf + (w + NW * j) * 64);
   };
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(256 * WM)
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-  for (int t = 0; t < G2_DIST; ++t)
+  for (int t = 0; t < DIST; ++t)
     if (t < KT) issue(t);
 
   if constexpr (WM == 2) {
@@ -257,20 +258,27 @@ __global__ void __launch_bounds__(256 * WM)
     if (wr == 1) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     for (int t = 0; t < KT; ++t) {
-      if (t + G2_DIST < KT) issue(t + G2_DIST);
-      const int after = min(KT - 1, t + G2_DIST) - (t + 1);  // tiles issued after t+1
-      if (after >= 2)
-        wait_vmcnt<2 * G>();
-      else if (after == 1)
-        wait_vmcnt<G>();
-      else
-        wait_vmcnt<0>();
-      const u32x4* buf = lds + (t & (G2_NBUF - 1)) * FR * 64;
+      if (t + DIST < KT) issue(t + DIST);
+      const int after = min(KT - 1, t + DIST) - (t + 1);  // tiles issued after t+1
+      auto wait_next = [&]() {
+        if (after >= 3)
+          wait_vmcnt<3 * G>();
+        else if (after == 2)
+          wait_vmcnt<2 * G>();
+        else if (after == 1)
+          wait_vmcnt<G>();
+        else
+          wait_vmcnt<0>();
+      };
+      if constexpr (!LATE_WAIT) wait_next();
+      const u32x4* buf = lds + (t % NBUF) * FR * 64;
       u32x4 a[8], b[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+      // LATE_WAIT: tile t+1 only has to land before this phase's barrier, not before tile t's reads
+      if constexpr (LATE_WAIT) wait_next();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -287,8 +295,10 @@ __global__ void __launch_bounds__(256 * WM)
     if (wr == 0) __builtin_amdgcn_s_barrier();
   } else
   for (int t = 0; t < KT; ++t) {
-    const int ahead = min(KT - 1 - t, G2_DIST - 1);  // tiles issued after t
-    if (ahead >= 2)
+    const int ahead = min(KT - 1 - t, DIST - 1);  // tiles issued after t
+    if (ahead >= 3)
+      wait_vmcnt<3 * G>();
+    else if (ahead == 2)
       wait_vmcnt<2 * G>();
     else if (ahead == 1)
       wait_vmcnt<G>();
@@ -297,8 +307,8 @@ __global__ void __launch_bounds__(256 * WM)
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + G2_DIST < KT) issue(t + G2_DIST);  // refills the buffer read at t-1 (retired by the barrier)
-    const u32x4* buf = lds + (t & (G2_NBUF - 1)) * FR * 64;
+    if (t + DIST < KT) issue(t + DIST);  // refills the buffer read at t-1 (retired by the barrier)
+    const u32x4* buf = lds + (t % NBUF) * FR * 64;
     u32x4 a[8], b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
@@ -449,7 +459,13 @@ __global__ void __launch_bounds__(256)
 // Which tiled kernel gemm() launches: 2 = gemm2 (default), 1 = the 128x128 register-staged kernel
 // (kept for A/B measurements: tools/bench_gemm.py --impl 1).
 static int g_gemm_impl = 2;
-void gemm_set_impl(int impl) { g_gemm_impl = impl == 1 ? 1 : 2; }
+// gemm2 pipeline variant (A/B): 0 = 4 LDS buffers, wait before the reads; 1 = 4 buffers, wait after
+// the reads; 2 = 5 buffers (all 160 KiB of LDS at WM = 2, one more tile in flight), wait after
+static int g_g2_var = 1;
+void gemm_set_impl(int impl) {
+  g_gemm_impl = impl == 1 ? 1 : 2;
+  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 5 ? 2 : 1);  // 2/4 = default (late wait), 3 = early
+}
 int gemm_get_impl() { return g_gemm_impl; }
 
 static int g2_wm(int M) { return M <= 128 ? 1 : 2; }
@@ -488,6 +504,10 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int grid = tm * tn * ksplit;
   if (wm == 1)
     gemm2_kernel<MODE, 1><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+  else if (g_g2_var == 1)
+    gemm2_kernel<MODE, 2, 4, true><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+  else if (g_g2_var == 2)
+    gemm2_kernel<MODE, 2, 5, true><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
   else
     gemm2_kernel<MODE, 2><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
 }

@@ -65,10 +65,34 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-f
              "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__"]
 
 
+def _scratch_users(remarks: str):
+    """Kernels whose resource-usage remark reports scratch (private) memory: on these kernels that
+    means a runtime-indexed register array or a spill -- almost always a large slowdown."""
+    bad, name = [], None
+    for line in remarks.splitlines():
+        if "Function Name:" in line:
+            name = line.split("Function Name:")[1].split("[")[0].strip()
+        elif "ScratchSize [bytes/lane]:" in line and name:
+            size = int(line.split("ScratchSize [bytes/lane]:")[1].split("[")[0].strip())
+            if size > 0:
+                bad.append((name, size))
+    return bad
+
+
+# Kernels allowed to use scratch (rare shapes where a spill is accepted), by mangled-name substring.
+SCRATCH_OK = ("attn_decode_v2_kernelILi16E",)
+
+
 def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):
     if force or _stale(obj, [src, *headers]):
         obj.parent.mkdir(parents=True, exist_ok=True)
-        _run([HIPCC, *HIP_FLAGS, *extra, "-c", str(src), "-o", str(obj)])
+        out = _run([HIPCC, *HIP_FLAGS, *extra, "-Rpass-analysis=kernel-resource-usage", "-c", str(src), "-o",
+                    str(obj)])
+        bad = [(n, b) for n, b in _scratch_users(out) if not any(ok in n for ok in SCRATCH_OK)]
+        if bad:
+            obj.unlink(missing_ok=True)
+            raise SystemExit(f"{src.name}: kernels use scratch memory (runtime-indexed register array or spill): "
+                             + ", ".join(f"{n} ({b} B/lane)" for n, b in bad))
         return True
     return False
 

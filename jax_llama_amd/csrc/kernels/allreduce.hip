@@ -50,7 +50,7 @@ JLA_DEV void add4f(u32x4& acc, const u32x4 v) {
 __global__ void __launch_bounds__(CAR_THREADS)
     car_kernel(const char* __restrict__ in, char* __restrict__ out, long long nbytes, int is_bf16,
                const CarDevice* __restrict__ dev) {
-  const CarDevice d = *dev;
+  const CarDevice& d = *dev;  // by reference: a by-value copy indexed with runtime p lives in scratch
   const int b = blockIdx.x;
   const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
   if (b >= nchunks) return;

@@ -342,16 +342,9 @@ __global__ void __launch_bounds__(64)
         const int j = jb + 4 * r;
         bool valid = j < k1;
         if constexpr (MASK) valid = valid && (j >= mask_len || mrow[j] != 0);
-        const bf16x8_t kv = __builtin_bit_cast(bf16x8_t, kr[r]);
 #pragma unroll
         for (int h = 0; h < REP; ++h) {
-          // (bit-casting single vector elements here miscompiles: every i read element 0)
-          const bf16x8_t qv = __builtin_bit_cast(bf16x8_t, qp[h]);
-          float d = 0.f;
-          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 0, 1), __builtin_shufflevector(qv, qv, 0, 1), d, false);
-          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 2, 3), __builtin_shufflevector(qv, qv, 2, 3), d, false);
-          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 4, 5), __builtin_shufflevector(qv, qv, 4, 5), d, false);
-          d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(kv, kv, 6, 7), __builtin_shufflevector(qv, qv, 6, 7), d, false);
+          float d = dot8_bf16(kr[r], qp[h], 0.f);
           d = row16_sum(d) * scale;
           sc[h][r] = valid ? d : -INFINITY;
         }

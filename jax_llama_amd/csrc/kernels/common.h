@@ -56,6 +56,17 @@ JLA_DEV u32x4 pack8(const float* f) {
   return r;
 }
 
+// acc + sum_e a[e] * b[e] over the 8 bf16 of two 16-byte vectors (4 x v_dot2_f32_bf16, fp32 accumulate).
+// Whole-vector bit casts + literal shuffles: bit-casting single ext-vector elements miscompiles here.
+JLA_DEV float dot8_bf16(const u32x4 a, const u32x4 b, float acc) {
+  const bf16x8_t x = __builtin_bit_cast(bf16x8_t, a), y = __builtin_bit_cast(bf16x8_t, b);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 0, 1), __builtin_shufflevector(y, y, 0, 1), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 2, 3), __builtin_shufflevector(y, y, 2, 3), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 4, 5), __builtin_shufflevector(y, y, 4, 5), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 6, 7), __builtin_shufflevector(y, y, 6, 7), acc, false);
+  return acc;
+}
+
 JLA_DEV f32x4 mfma16x16x32(const u32x4 a, const u32x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);

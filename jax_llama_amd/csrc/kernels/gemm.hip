@@ -175,10 +175,16 @@ __global__ void __launch_bounds__(G_THREADS)
 // Workgroups are remapped so consecutive tiles share an XCD (its own L2), M-grouped by 8.
 constexpr int G2_BN = 256, G2_NBUF = 4, G2_DIST = 3, G2_GROUP_M = 8;
 
-template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false>
+// RMS (fused RMSNorm, reference model.py:28-48 with the gain folded into W): the A operand is the
+// UNscaled bf16 activation; the waves square-sum the A fragments they already read from LDS (wave wc
+// takes m-tiles 2wc, 2wc+1 of its row block, 8 v_dot2 per K-tile) and the epilogue scales each output
+// row by rsqrt(mean(x^2) + eps). Split-K: each split stores its partial sums ([split][M] after the
+// fp32 slabs) and the reduce kernel finishes the statistic. No rms_scale launch, no scaled copy of x.
+template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                 int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n) {
+                 int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
+                 float rms_eps, float* __restrict__ ssq_ws) {
   constexpr int NW = 4 * WM, BM = 128 * WM;
   constexpr int AF = BM / 16, BF = G2_BN / 16, FR = AF + BF;  // fragments per K-tile
   constexpr int G = FR / NW;                                   // LDS-DMA loads per wave per K-tile
@@ -234,6 +240,17 @@ __global__ void __launch_bounds__(256 * WM)
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss0 = 0.f, ss1 = 0.f;  // RMS: partial sums of squares of m-tiles 2wc, 2wc+1 (row lane & 15)
+  // The two fragments are re-read from LDS (2 extra ds_read_b128): selecting them out of a[] by the
+  // runtime wc makes hipcc move the fragment array to scratch.
+  auto sumsq = [&](const u32x4* buf) {
+    if constexpr (RMS) {
+      const u32x4 f0 = buf[(wr * 8 + 2 * wc) * 64 + lane];
+      const u32x4 f1 = buf[(wr * 8 + 2 * wc + 1) * 64 + lane];
+      ss0 = dot8_bf16(f0, f0, ss0);
+      ss1 = dot8_bf16(f1, f1, ss1);
+    }
+  };
 
 #pragma unroll
   for (int t = 0; t < DIST; ++t)
@@ -277,6 +294,7 @@ __global__ void __launch_bounds__(256 * WM)
       for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+      sumsq(buf);
       // LATE_WAIT: tile t+1 only has to land before this phase's barrier, not before tile t's reads
       if constexpr (LATE_WAIT) wait_next();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -314,10 +332,46 @@ __global__ void __launch_bounds__(256 * WM)
     for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+    sumsq(buf);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+  }
+
+  if constexpr (RMS) {
+    // complete each row's sum over the 4 lanes that hold its k-chunks (lane >> 4)
+    ss0 += __shfl_xor(ss0, 16, 64);
+    ss0 += __shfl_xor(ss0, 32, 64);
+    ss1 += __shfl_xor(ss1, 16, 64);
+    ss1 += __shfl_xor(ss1, 32, 64);
+    const int rA = m0 + (wr * 8 + 2 * wc) * 16 + (lane & 15), rB = rA + 16;
+    if constexpr (MODE == MODE_PARTIAL) {
+      if (lane < 16) {
+        if (rA < M) ssq_ws[(size_t)split * M + rA] = ss0;
+        if (rB < M) ssq_ws[(size_t)split * M + rB] = ss1;
+      }
+    } else {
+      // publish the row statistics through LDS (the tile buffers are free once every wave is past
+      // its last ds_read), then scale every accumulator row
+      float* rs = reinterpret_cast<float*>(lds);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (lane < 16) {
+        const float inv_k = 1.f / (float)K;
+        rs[(wr * 8 + 2 * wc) * 16 + lane] = 1.f / sqrtf(ss0 * inv_k + rms_eps);
+        rs[(wr * 8 + 2 * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 * inv_k + rms_eps);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sc = rs[(wr * 8 + i) * 16 + 4 * (lane >> 4) + r];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j][r] *= sc;
+        }
+    }
   }
 
   const int c = lane & 15;
@@ -373,7 +427,8 @@ __global__ void __launch_bounds__(256 * WM)
 template <int MODE>
 __global__ void __launch_bounds__(256)
     gemm_reduce_kernel(const float* __restrict__ ws, int ksplit, void* __restrict__ out, int M, int N,
-                       int accumulate, int out_f32, bf16_t* __restrict__ mirror, QKVArgs qa) {
+                       int accumulate, int out_f32, bf16_t* __restrict__ mirror, QKVArgs qa,
+                       const float* __restrict__ ssq, int K, float rms_eps) {
   const size_t e4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t total4 = (size_t)M * N / 4;
   if (e4 >= total4) return;
@@ -386,6 +441,16 @@ __global__ void __launch_bounds__(256)
     v.y += p.y;
     v.z += p.z;
     v.w += p.w;
+  }
+  float rs = 1.f;  // fused RMSNorm: the splits' partial sums of squares of row m (fixed order)
+  if (ssq) {
+    float t = 0.f;
+    for (int s = 0; s < ksplit; ++s) t += ssq[(size_t)s * M + m];
+    rs = 1.f / sqrtf(t / (float)K + rms_eps);
+    v.x *= rs;
+    v.y *= rs;
+    v.z *= rs;
+    v.w *= rs;
   }
   float vv[4] = {v.x, v.y, v.z, v.w};
   if constexpr (MODE == MODE_SWIGLU) {
@@ -401,6 +466,10 @@ __global__ void __launch_bounds__(256)
           a.z += p.z;
           a.w += p.w;
         }
+        a.x *= rs;
+        a.y *= rs;
+        a.z *= rs;
+        a.w *= rs;
         return a;
       }();
       const float uu[4] = {u.x, u.y, u.z, u.w};
@@ -493,30 +562,43 @@ int gemm_ksplit(int M, int N, int K) {
 
 size_t gemm_workspace_floats(int M, int N, int K) {
   const int ks = gemm_ksplit(M, N, K);
-  return ks > 1 ? (size_t)ks * M * N : 0;
+  return ks > 1 ? (size_t)ks * M * (N + 1) : 0;  // slabs + fused-RMS partial sums
 }
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                      bf16_t* mirror, int kc, int ksplit, hipStream_t s) {
+                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s) {
   const int wm = g2_wm(M), bm = 128 * wm;
   const int tm = (M + bm - 1) / bm, tn = (N + G2_BN - 1) / G2_BN;
   const int grid = tm * tn * ksplit;
+#define JLA_G2(WMV, NB, LATE, R)                                                                                   \
+  gemm2_kernel<MODE, WMV, NB, LATE, R><<<grid, 256 * WMV, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, \
+                                                                  kc, tm, tn, rms_eps, ssq)
+  if constexpr (MODE != MODE_RESIDUAL) {
+    if (rms_eps >= 0.f) {  // fused RMSNorm statistic (default pipeline variant only)
+      if (wm == 1)
+        JLA_G2(1, 4, false, true);
+      else
+        JLA_G2(2, 4, true, true);
+      return;
+    }
+  }
   if (wm == 1)
-    gemm2_kernel<MODE, 1><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+    JLA_G2(1, 4, false, false);
   else if (g_g2_var == 1)
-    gemm2_kernel<MODE, 2, 4, true><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+    JLA_G2(2, 4, true, false);
   else if (g_g2_var == 2)
-    gemm2_kernel<MODE, 2, 5, true><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+    JLA_G2(2, 5, true, false);
   else
-    gemm2_kernel<MODE, 2><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn);
+    JLA_G2(2, 4, false, false);
+#undef JLA_G2
 }
 
 template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
-                         int out_f32, bf16_t* mirror, int kc, int ksplit, hipStream_t s) {
+                         int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s) {
   if (g_gemm_impl == 2) {
-    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, s);
+    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, s);
   } else {
     dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
     gemm_kernel<MODE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc);
@@ -524,11 +606,14 @@ static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int 
 }
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
-         bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s) {
+         bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
+         float rms_eps) {
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   if (mode == MODE_QKV && (!qkv || ksplit < 2)) return -1;  // qkv epilogue only in the reduce kernel
+  const bool rms = rms_eps >= 0.f;
+  if (rms && (g_gemm_impl == 1 || mode == MODE_RESIDUAL)) return -5;  // caller pre-scales x instead
   const int KS = K >> 5;
   if (ksplit < 1) ksplit = 1;
   const int kc = (KS + ksplit - 1) / ksplit;
@@ -537,33 +622,47 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   const u32x4* w = static_cast<const u32x4*>(W);
   if (ksplit == 1) {
     switch (mode) {
-      case MODE_STORE: launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, s); break;
-      case MODE_RESIDUAL: launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, s); break;
-      case MODE_SWIGLU: launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, s); break;
+      case MODE_STORE:
+        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, s);
+        break;
+      case MODE_RESIDUAL:
+        launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, -1.f, nullptr, s);
+        break;
+      case MODE_SWIGLU:
+        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, s);
+        break;
       default: return -1;
     }
     JLA_CHECK_LAUNCH();
     return 0;
   }
-  if ((N & 3) || ws == nullptr || ws_floats < (size_t)ksplit * M * N) return -3;
-  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, s);
+  // workspace: [ksplit][M][N] fp32 partial slabs, then (fused RMS) [ksplit][M] partial sums of squares
+  const size_t need = (size_t)ksplit * M * N + (rms ? (size_t)ksplit * M : 0);
+  if ((N & 3) || ws == nullptr || ws_floats < need) return -3;
+  float* ssq = rms ? ws + (size_t)ksplit * M * N : nullptr;
+  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, rms_eps, ssq, s);
   JLA_CHECK_LAUNCH();
   const size_t total4 = (size_t)M * N / 4;
   const int rgrid = (int)((total4 + 255) / 256);
   QKVArgs qa{};
   if (qkv) qa = *qkv;
+  const float eps = rms ? rms_eps : 0.f;
   switch (mode) {
     case MODE_STORE:
-      gemm_reduce_kernel<MODE_STORE><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, out_f32, nullptr, qa);
+      gemm_reduce_kernel<MODE_STORE><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, out_f32, nullptr, qa,
+                                                           ssq, K, eps);
       break;
     case MODE_RESIDUAL:
-      gemm_reduce_kernel<MODE_RESIDUAL><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 1, mirror, qa);
+      gemm_reduce_kernel<MODE_RESIDUAL><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 1, mirror, qa,
+                                                              nullptr, K, eps);
       break;
     case MODE_SWIGLU:
-      gemm_reduce_kernel<MODE_SWIGLU><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa);
+      gemm_reduce_kernel<MODE_SWIGLU><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq,
+                                                            K, eps);
       break;
     case MODE_QKV:
-      gemm_reduce_kernel<MODE_QKV><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa);
+      gemm_reduce_kernel<MODE_QKV><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq, K,
+                                                         eps);
       break;
     default: return -1;
   }

@@ -43,8 +43,11 @@ int gemm_ksplit(int M, int N, int K);
 void gemm_set_impl(int impl);  // 2 = gemm2 (default), 1 = 128x128 v1 (A/B measurements)
 int gemm_get_impl();
 size_t gemm_workspace_floats(int M, int N, int K);
+// rms_eps >= 0: x is the UNscaled activation and each output row is scaled by rsqrt(mean(x^2) + eps)
+// (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
-         bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s);
+         bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
+         float rms_eps = -1.f);
 
 int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,

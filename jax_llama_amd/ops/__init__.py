@@ -154,25 +154,34 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None):
 TILED = 7  # decode-kernel "variant" id of the 128x128 MFMA GEMM (split-K for mid M)
 
 
-def _tiled_input(x, rms_eps):
-    """bf16 A operand of the tiled GEMM: rms-scaled (statistics from x's own values) or cast."""
-    if rms_eps is not None:
+def _fused_rms(e, mode, rms_eps) -> bool:
+    """The tiled GEMM applies RMSNorm itself (statistics from its own A-fragment reads, row scale in
+    the epilogue) except in residual mode and on the legacy 128x128 kernel."""
+    return rms_eps is not None and mode != MODE_RESIDUAL and e.gemm_get_impl() != 1
+
+
+def _tiled_input(x, rms_eps, fused=False):
+    """bf16 A operand of the tiled GEMM: unscaled when the GEMM fuses the norm, else rms-scaled
+    (statistics from x's own values) by a separate kernel."""
+    if rms_eps is not None and not fused:
         return rms_scale(x, rms_eps)
     return x if x.dtype == BF16 else x.to(BF16)
 
 
 def _gemm_ws(e, m, n, k, device):
     ks = autotune.choose_gemm_ksplit(e, m, n, k, device)
-    ws = workspace.get("gemm_ws", ks * m * n, torch.float32, device) if ks > 1 else None
+    # split-K slabs [ks][m][n] + the fused-RMS partial sums of squares [ks][m]
+    ws = workspace.get("gemm_ws", ks * m * (n + 1), torch.float32, device) if ks > 1 else None
     return ks, ws
 
 
 def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
     """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups when the
-    output has too few 128x128 tiles to fill the chip (csrc/kernels/gemm.hip)."""
-    xb = _tiled_input(x, rms_eps)
+    output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip)."""
+    fused = _fused_rms(e, mode, rms_eps)
+    xb = _tiled_input(x, rms_eps, fused)
     ks, ws = _gemm_ws(e, x.shape[0], n, k, x.device)
-    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws)
+    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0)
 
 
 def _variant(e, x, w, mode) -> int:
@@ -250,9 +259,10 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
             return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads,
                                  head_dim)
         q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
-        e.gemm_qkv(_tiled_input(x, rms_eps), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
+        fused = _fused_rms(e, MODE_QKV, rms_eps)
+        e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                    k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                   int(head_dim), q, ks, ws)
+                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0)
         return q
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)

@@ -33,15 +33,18 @@ def init_distributed(backend: Optional[str] = None, device_type: Optional[str] =
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # JLA_SINGLE_DEVICE=1 (test hook): every rank shares GPU 0, e.g. to rehearse a multi-rank
+        # launch on a one-GPU box (together with JLA_DIST_BACKEND=gloo: RCCL needs distinct GPUs)
+        dev_idx = 0 if os.environ.get("JLA_SINGLE_DEVICE", "0") == "1" else local_rank
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend is None:
-            backend = "nccl" if device_type == "cuda" else "gloo"
+            backend = os.environ.get("JLA_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
@@ -86,10 +89,19 @@ class ParallelContext:
 
     def barrier(self):
         if self.world > 1 and dist.is_initialized():
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and dist.get_backend() == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
+
+    def all_reduce_max(self, values):
+        """Element-wise max over all ranks of a list of floats (host result)."""
+        t = torch.tensor(values, dtype=torch.float64)
+        if self.world > 1 and dist.is_initialized():
+            if dist.get_backend() == "nccl":
+                t = t.to(self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t.cpu()]
 
 
 def single_process_context(device="cpu") -> ParallelContext:

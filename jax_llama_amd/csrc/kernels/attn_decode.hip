@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(AD_WAVES * 64)
 // rows, summed across the 4 groups once per item.
 static int g_attn_impl = 2;
 static int g_attn_waves_target = 2048;
-static int g_attn_v2_min_pairs = 2048;
+static int g_attn_v2_min_pairs = 4096;
 void attn_set_impl(int impl, int waves_target);
 
 template <int REP, int KPG, int NS, bool MASK>
@@ -497,20 +497,22 @@ __global__ void __launch_bounds__(64)
 }
 
 static int kpg_v1(int rep) { return rep <= 4 ? 8 : (rep == 8 ? 4 : 2); }
-static int g_kpg_small = 4, g_ns = 3;  // v2 ring geometry for REP <= 4 (A/B: attn_set_impl)
+static int g_kpg_small = 8, g_ns = 2;  // v2 ring geometry for REP <= 4 (A/B: attn_set_impl)
 static int kpg_v2(int rep) { return rep <= 4 ? g_kpg_small : (rep == 8 ? 2 : 1); }
 
-// impl 1 = v1; 2 = v2 with (KPG 4, 3 slots) [default]; 3 = v2 (KPG 2, 4 slots); 4 = v2 (KPG 4, 2 slots)
+// impl 1 = v1; 2 = v2 with (KPG 8, 2 slots) [default: profiles/r1_attn_decode_v2_geometry.jsonl];
+// 3 = v2 (KPG 2, 4 slots); 4 = v2 (KPG 4, 2 slots); 5 = same as 2; 6 = v2 (KPG 4, 4 slots); 7 = (KPG 4, 3 slots)
 void attn_set_impl(int impl, int waves_target) {
   g_attn_impl = impl == 1 ? 1 : 2;
-  g_kpg_small = impl == 3 ? 2 : 4;
-  g_ns = impl == 3 ? 4 : (impl == 4 ? 2 : 3);
+  g_kpg_small = impl == 3 ? 2 : (impl == 2 || impl == 5 ? 8 : 4);
+  g_ns = impl == 3 ? 4 : (impl == 7 ? 3 : (impl == 6 ? 4 : 2));
   if (waves_target > 0) g_attn_waves_target = waves_target;
-  g_attn_v2_min_pairs = waves_target < 0 ? -waves_target : 2048;  // < 0: force v2 down to -target pairs
+  g_attn_v2_min_pairs = waves_target < 0 ? -waves_target : 4096;  // < 0: force v2 down to -target pairs
 }
 
-// v2 streams whole (b, kv head) pairs; below ~2048 pairs its splits' serial merge loses to v1's
-// chunk-per-workgroup design (profiles/r1_attn_decode_v2_ab.jsonl), so small batches stay on v1.
+// v2 streams whole (b, kv head) pairs; below ~4096 pairs (B = 512 at 8 kv heads) v1's
+// chunk-per-workgroup design is as fast or faster (profiles/r1_attn_decode_v2_ab.jsonl,
+// r1_attn_decode_v2_geometry.jsonl), so smaller batches stay on v1.
 static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_attn_v2_min_pairs; }
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) { return use_v2(B, Hkv) ? 4 * kpg_v2(rep) : 16 * kpg_v1(rep); }
@@ -573,11 +575,21 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
     case 4:
       // REP <= 4 shares one body per geometry (REP only sizes the register arrays)
       if (rep == 1) {
-        if (geo == 43) { JLA_AD2(1, 4, 3) } else if (geo == 24) { JLA_AD2(1, 2, 4) } else { JLA_AD2(1, 4, 2) }
+        if (geo == 82) { JLA_AD2(1, 8, 2) } else { JLA_AD2(1, 4, 2) }
       } else if (rep == 2) {
-        if (geo == 43) { JLA_AD2(2, 4, 3) } else if (geo == 24) { JLA_AD2(2, 2, 4) } else { JLA_AD2(2, 4, 2) }
+        if (geo == 82) { JLA_AD2(2, 8, 2) } else { JLA_AD2(2, 4, 2) }
       } else {
-        if (geo == 43) { JLA_AD2(4, 4, 3) } else if (geo == 24) { JLA_AD2(4, 2, 4) } else { JLA_AD2(4, 4, 2) }
+        if (geo == 43) {
+          JLA_AD2(4, 4, 3)
+        } else if (geo == 24) {
+          JLA_AD2(4, 2, 4)
+        } else if (geo == 82) {
+          JLA_AD2(4, 8, 2)
+        } else if (geo == 44) {
+          JLA_AD2(4, 4, 4)
+        } else {
+          JLA_AD2(4, 4, 2)
+        }
       }
       break;
     case 8: JLA_AD2(8, 2, 4) break;

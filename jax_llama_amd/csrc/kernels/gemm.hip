@@ -567,8 +567,8 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s) {
-  const int wm = g2_wm(M), bm = 128 * wm;
+                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile_m, hipStream_t s) {
+  const int wm = tile_m == 128 ? 1 : (tile_m == 256 ? 2 : g2_wm(M)), bm = 128 * wm;
   const int tm = (M + bm - 1) / bm, tn = (N + G2_BN - 1) / G2_BN;
   const int grid = tm * tn * ksplit;
 #define JLA_G2(WMV, NB, LATE, R)                                                                                   \
@@ -596,9 +596,10 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
 
 template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
-                         int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s) {
+                         int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile_m,
+                         hipStream_t s) {
   if (g_gemm_impl == 2) {
-    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, s);
+    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile_m, s);
   } else {
     dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
     gemm_kernel<MODE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc);
@@ -607,7 +608,7 @@ static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int 
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps) {
+         float rms_eps, int tile_m) {
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
@@ -623,13 +624,13 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (ksplit == 1) {
     switch (mode) {
       case MODE_STORE:
-        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, s);
+        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile_m, s);
         break;
       case MODE_RESIDUAL:
-        launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, -1.f, nullptr, s);
+        launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, -1.f, nullptr, tile_m, s);
         break;
       case MODE_SWIGLU:
-        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, s);
+        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, tile_m, s);
         break;
       default: return -1;
     }
@@ -640,7 +641,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   const size_t need = (size_t)ksplit * M * N + (rms ? (size_t)ksplit * M : 0);
   if ((N & 3) || ws == nullptr || ws_floats < need) return -3;
   float* ssq = rms ? ws + (size_t)ksplit * M * N : nullptr;
-  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, rms_eps, ssq, s);
+  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, rms_eps, ssq, tile_m, s);
   JLA_CHECK_LAUNCH();
   const size_t total4 = (size_t)M * N / 4;
   const int rgrid = (int)((total4 + 255) / 256);

@@ -169,10 +169,10 @@ def _tiled_input(x, rms_eps, fused=False):
 
 
 def _gemm_ws(e, m, n, k, device):
-    ks = autotune.choose_gemm_ksplit(e, m, n, k, device)
+    ks, tm = autotune.choose_gemm_plan(e, m, n, k, device)
     # split-K slabs [ks][m][n] + the fused-RMS partial sums of squares [ks][m]
     ws = workspace.get("gemm_ws", ks * m * (n + 1), torch.float32, device) if ks > 1 else None
-    return ks, ws
+    return ks, tm, ws
 
 
 def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
@@ -180,8 +180,8 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
     output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip)."""
     fused = _fused_rms(e, mode, rms_eps)
     xb = _tiled_input(x, rms_eps, fused)
-    ks, ws = _gemm_ws(e, x.shape[0], n, k, x.device)
-    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0)
+    ks, tm, ws = _gemm_ws(e, x.shape[0], n, k, x.device)
+    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm)
 
 
 def _variant(e, x, w, mode) -> int:
@@ -253,7 +253,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     e = ext()
     v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV)
     if v == TILED:
-        ks, ws = _gemm_ws(e, m, w.n, w.k, x.device)
+        ks, tm, ws = _gemm_ws(e, m, w.n, w.k, x.device)
         if ks == 1:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
             qkv = linear(x, w, rms_eps=rms_eps)
             return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads,
@@ -262,7 +262,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
         fused = _fused_rms(e, MODE_QKV, rms_eps)
         e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                    k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0)
+                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm)
         return q
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)

@@ -97,38 +97,50 @@ def table() -> Dict[Tuple, int]:
 # more CUs but every split writes and re-reads an fp32 [M, N] slab, so the best factor depends on
 # (M, N, K) -- at M=256 it measured 8 for qkv/o (K=4096), 16 for down (K=14336), 2 for gate_up
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
-_KS_CACHE: Dict[Tuple, int] = {}
+_KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
+TILE_M_CANDIDATES = (256, 128)
+TUNE_MAX_M = 2048
+
+
+def choose_gemm_plan(e, m: int, n: int, k: int, device) -> Tuple[int, int]:
+    """(split-K factor, gemm2 tile rows) for this shape: measured once on the device for M > 128 (tile
+    rows 256 or 128 x every split that keeps >= 4 K-tiles per split); the C++ heuristic otherwise or
+    while a hipGraph is being captured."""
+    key = (m, n, k)
+    plan = _KS_CACHE.get(key)
+    if plan is not None:
+        return plan
+    heur = e.gemm_ksplit(m, n, k)
+    # tuned band: decode-sized M (prefill-sized M has enough 256x256 tiles; tuning it would also need
+    # multi-GB scratch outputs)
+    if m <= 128 or m > TUNE_MAX_M or not ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return heur, 0
+    plan = _measure_plan(e, m, n, k, device, heur)
+    _KS_CACHE[key] = plan
+    return plan
 
 
 def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
-    key = (m, n, k)
-    ks = _KS_CACHE.get(key)
-    if ks is not None:
-        return ks
-    heur = e.gemm_ksplit(m, n, k)
-    if heur == 1 or not ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
-        return heur
-    ks = _measure_ksplit(e, m, n, k, device, heur)
-    _KS_CACHE[key] = ks
-    return ks
+    return choose_gemm_plan(e, m, n, k, device)[0]
 
 
-def _measure_ksplit(e, m, n, k, device, heur) -> int:
+def _measure_plan(e, m, n, k, device, heur) -> Tuple[int, int]:
     kt = k // 32
-    cands = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
+    ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
+    cands = [(c, tm) for tm in TILE_M_CANDIDATES for c in ks_c]
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
             for _ in range(copies)]
     x = torch.randn(m, k, device=device).to(torch.bfloat16)
     out = torch.empty(m, n, dtype=torch.bfloat16, device=device)
-    ws = torch.empty(max(cands) * m * n, dtype=torch.float32, device=device)
+    ws = torch.empty(max(ks_c) * m * (n + 1), dtype=torch.float32, device=device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best, best_t = heur, float("inf")
-    for c in cands:
+    best, best_t = (heur, 0), float("inf")
+    for c, tm in cands:
         def run(i):
-            e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, c, ws if c > 1 else None)
+            e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, c, ws if c > 1 else None, -1.0, tm)
         for i in range(2):
             run(i)
         iters = 2 * copies
@@ -139,7 +151,7 @@ def _measure_ksplit(e, m, n, k, device, heur) -> int:
         ev1.synchronize()
         t = ev0.elapsed_time(ev1) / iters
         if t < best_t:
-            best, best_t = c, t
+            best, best_t = (c, tm), t
     del ws_w, ws
     return best
 

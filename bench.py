@@ -128,7 +128,7 @@ def main():
         "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
         "decode_kernel_choice": {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}": v
                                  for k, v in __import__("jax_llama_amd.ops.autotune", fromlist=["x"]).table().items()},
-        "gemm_plan_choice": {f"m{k[0]}_n{k[1]}_k{k[2]}": f"ks{v[0]}_tm{v[1]}" for k, v in
+        "gemm_plan_choice": {f"m{k[0]}_n{k[1]}_k{k[2]}": f"ks{v[0]}_tile{v[1]}" for k, v in
                              __import__("jax_llama_amd.ops.autotune", fromlist=["x"]).ksplit_table().items()},
     }
     if ctx.rank == 0:

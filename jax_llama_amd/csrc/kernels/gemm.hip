@@ -180,13 +180,15 @@ constexpr int G2_BN = 256, G2_NBUF = 4, G2_DIST = 3, G2_GROUP_M = 8;
 // takes m-tiles 2wc, 2wc+1 of its row block, 8 v_dot2 per K-tile) and the epilogue scales each output
 // row by rsqrt(mean(x^2) + eps). Split-K: each split stores its partial sums ([split][M] after the
 // fp32 slabs) and the reduce kernel finishes the statistic. No rms_scale launch, no scaled copy of x.
-template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false>
+template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
                  float rms_eps, float* __restrict__ ssq_ws) {
-  constexpr int NW = 4 * WM, BM = 128 * WM;
-  constexpr int AF = BM / 16, BF = G2_BN / 16, FR = AF + BF;  // fragments per K-tile
+  // wave tile: MT m-tiles x NTW n-tiles of 16x16 (128 x 64 by default; 64 x 32 for the 128 x 128 tile)
+  constexpr int NW = 4 * WM, BM = 16 * MT * WM, BN = 64 * NTW;
+  constexpr int RPW = MT / 4;  // RMS: m-tiles whose row statistics each wave accumulates
+  constexpr int AF = BM / 16, BF = BN / 16, FR = AF + BF;  // fragments per K-tile
   constexpr int G = FR / NW;                                   // LDS-DMA loads per wave per K-tile
   static_assert(FR % NW == 0, "fragment split");
   constexpr int DIST = NBUF - 1;
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(256 * WM)
   const int gsz = min(tiles_m - first_m, G2_GROUP_M);
   const int tm = first_m + (pid % in_group) % gsz;
   const int tn = (pid % in_group) / gsz;
-  const int m0 = tm * BM, n0 = tn * G2_BN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const int KS = K >> 5, NTT = N >> 4;
   const int ks0 = split * kc;
@@ -235,20 +237,22 @@ __global__ void __launch_bounds__(256 * WM)
     for (int j = 0; j < G; ++j) glds16(src[j] + (size_t)t * step[j], buf + (w + NW * j) * 64);
   };
 
-  f32x4 acc[8][4];
+  f32x4 acc[MT][NTW];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss0 = 0.f, ss1 = 0.f;  // RMS: partial sums of squares of m-tiles 2wc, 2wc+1 (row lane & 15)
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss0 = 0.f, ss1 = 0.f;  // RMS: partial sums of squares of m-tiles RPW*wc (+1) (row lane & 15)
   // The two fragments are re-read from LDS (2 extra ds_read_b128): selecting them out of a[] by the
   // runtime wc makes hipcc move the fragment array to scratch.
   auto sumsq = [&](const u32x4* buf) {
     if constexpr (RMS) {
-      const u32x4 f0 = buf[(wr * 8 + 2 * wc) * 64 + lane];
-      const u32x4 f1 = buf[(wr * 8 + 2 * wc + 1) * 64 + lane];
+      const u32x4 f0 = buf[(wr * MT + RPW * wc) * 64 + lane];
       ss0 = dot8_bf16(f0, f0, ss0);
-      ss1 = dot8_bf16(f1, f1, ss1);
+      if constexpr (RPW == 2) {
+        const u32x4 f1 = buf[(wr * MT + RPW * wc + 1) * 64 + lane];
+        ss1 = dot8_bf16(f1, f1, ss1);
+      }
     }
   };
 
@@ -289,11 +293,11 @@ __global__ void __launch_bounds__(256 * WM)
       };
       if constexpr (!LATE_WAIT) wait_next();
       const u32x4* buf = lds + (t % NBUF) * FR * 64;
-      u32x4 a[8], b[4];
+      u32x4 a[MT], b[NTW];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
+      for (int j = 0; j < NTW; ++j) b[j] = buf[(AF + wc * NTW + j) * 64 + lane];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+      for (int i = 0; i < MT; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
       sumsq(buf);
       // LATE_WAIT: tile t+1 only has to land before this phase's barrier, not before tile t's reads
       if constexpr (LATE_WAIT) wait_next();
@@ -302,9 +306,9 @@ __global__ void __launch_bounds__(256 * WM)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -327,16 +331,16 @@ __global__ void __launch_bounds__(256 * WM)
     asm volatile("" ::: "memory");
     if (t + DIST < KT) issue(t + DIST);  // refills the buffer read at t-1 (retired by the barrier)
     const u32x4* buf = lds + (t % NBUF) * FR * 64;
-    u32x4 a[8], b[4];
+    u32x4 a[MT], b[NTW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = buf[(AF + wc * 4 + j) * 64 + lane];
+    for (int j = 0; j < NTW; ++j) b[j] = buf[(AF + wc * NTW + j) * 64 + lane];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = buf[(wr * 8 + i) * 64 + lane];
+    for (int i = 0; i < MT; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
     sumsq(buf);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
   }
 
   if constexpr (RMS) {
@@ -345,11 +349,11 @@ __global__ void __launch_bounds__(256 * WM)
     ss0 += __shfl_xor(ss0, 32, 64);
     ss1 += __shfl_xor(ss1, 16, 64);
     ss1 += __shfl_xor(ss1, 32, 64);
-    const int rA = m0 + (wr * 8 + 2 * wc) * 16 + (lane & 15), rB = rA + 16;
+    const int rA = m0 + (wr * MT + RPW * wc) * 16 + (lane & 15), rB = rA + 16;
     if constexpr (MODE == MODE_PARTIAL) {
       if (lane < 16) {
         if (rA < M) ssq_ws[(size_t)split * M + rA] = ss0;
-        if (rB < M) ssq_ws[(size_t)split * M + rB] = ss1;
+        if (RPW == 2 && rB < M) ssq_ws[(size_t)split * M + rB] = ss1;
       }
     } else {
       // publish the row statistics through LDS (the tile buffers are free once every wave is past
@@ -359,17 +363,17 @@ __global__ void __launch_bounds__(256 * WM)
       __syncthreads();
       if (lane < 16) {
         const float inv_k = 1.f / (float)K;
-        rs[(wr * 8 + 2 * wc) * 16 + lane] = 1.f / sqrtf(ss0 * inv_k + rms_eps);
-        rs[(wr * 8 + 2 * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 * inv_k + rms_eps);
+        rs[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 * inv_k + rms_eps);
+        if constexpr (RPW == 2) rs[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 * inv_k + rms_eps);
       }
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float sc = rs[(wr * 8 + i) * 16 + 4 * (lane >> 4) + r];
+          const float sc = rs[(wr * MT + i) * 16 + 4 * (lane >> 4) + r];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j][r] *= sc;
+          for (int j = 0; j < NTW; ++j) acc[i][j][r] *= sc;
         }
     }
   }
@@ -379,29 +383,29 @@ __global__ void __launch_bounds__(256 * WM)
     const int F = N >> 1;
     bf16_t* o = static_cast<bf16_t*>(out);
 #pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      const int gtile = (n0 >> 4) + wc * 4 + j;  // even: gate tile, gtile + 1: its up tile
+    for (int j = 0; j < NTW; j += 2) {
+      const int gtile = (n0 >> 4) + wc * NTW + j;  // even: gate tile, gtile + 1: its up tile
       if (gtile >= NTT) continue;
       const int col = (gtile >> 1) * 16 + c;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + (wr * 8 + i) * 16 + 4 * (lane >> 4) + r;
+          const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
           if (row < M) o[(size_t)row * F + col] = f2bf(silu(acc[i][j][r]) * acc[i][j + 1][r]);
         }
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int tile = (n0 >> 4) + wc * 4 + j;
+    for (int j = 0; j < NTW; ++j) {
+      const int tile = (n0 >> 4) + wc * NTW + j;
       if (tile >= NTT) continue;
       const int col = tile * 16 + c;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + (wr * 8 + i) * 16 + 4 * (lane >> 4) + r;
+          const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
           if (row >= M) continue;
           const size_t idx = (size_t)row * N + col;
           const float v = acc[i][j][r];
@@ -537,7 +541,7 @@ void gemm_set_impl(int impl) {
 }
 int gemm_get_impl() { return g_gemm_impl; }
 
-static int g2_wm(int M) { return M <= 128 ? 1 : 2; }
+static int g2_wm(int M) { return M <= 128 ? 1 : 2; }  // default tile rows / 128
 
 // split-K plan: fill the chip with workgroups while keeping >= 4 K-tiles (gemm2: 1 WG per CU,
 // target ~256 WGs) / >= 8 k-steps (gemm v1: ~512 WGs) per split.
@@ -565,41 +569,53 @@ size_t gemm_workspace_floats(int M, int N, int K) {
   return ks > 1 ? (size_t)ks * M * (N + 1) : 0;  // slabs + fused-RMS partial sums
 }
 
+// gemm2 tile configurations (the `tile` argument of gemm(); 0 = by M):
+//   1: 256 x 256, 8 waves (two ping-pong rows) of 128 x 64;   2: 128 x 256, 4 waves of 128 x 64;
+//   3: 128 x 128, 8 waves (two ping-pong rows) of 64 x 32 -- 64 KiB of LDS, so two workgroups can share a CU;
+//      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
+static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
+
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile_m, hipStream_t s) {
-  const int wm = tile_m == 128 ? 1 : (tile_m == 256 ? 2 : g2_wm(M)), bm = 128 * wm;
-  const int tm = (M + bm - 1) / bm, tn = (N + G2_BN - 1) / G2_BN;
+                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s) {
+  const int cfg = tile_cfg(tile, M);
+  const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
+  const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
   const int grid = tm * tn * ksplit;
-#define JLA_G2(WMV, NB, LATE, R)                                                                                   \
-  gemm2_kernel<MODE, WMV, NB, LATE, R><<<grid, 256 * WMV, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, \
-                                                                  kc, tm, tn, rms_eps, ssq)
+#define JLA_G2(WMV, NB, LATE, R, MTV, NTV)                                                                  \
+  gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV><<<grid, 256 * WMV, 0, s>>>(                                \
+      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq)
+  const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   if constexpr (MODE != MODE_RESIDUAL) {
-    if (rms_eps >= 0.f) {  // fused RMSNorm statistic (default pipeline variant only)
-      if (wm == 1)
-        JLA_G2(1, 4, false, true);
+    if (rms) {  // fused RMSNorm statistic (default pipeline variant only)
+      if (cfg == 2)
+        JLA_G2(1, 4, false, true, 8, 4);
+      else if (cfg == 3)
+        JLA_G2(2, 4, true, true, 4, 2);
       else
-        JLA_G2(2, 4, true, true);
+        JLA_G2(2, 4, true, true, 8, 4);
       return;
     }
   }
-  if (wm == 1)
-    JLA_G2(1, 4, false, false);
+  if (cfg == 2)
+    JLA_G2(1, 4, false, false, 8, 4);
+  else if (cfg == 3)
+    JLA_G2(2, 4, true, false, 4, 2);
   else if (g_g2_var == 1)
-    JLA_G2(2, 4, true, false);
+    JLA_G2(2, 4, true, false, 8, 4);
   else if (g_g2_var == 2)
-    JLA_G2(2, 5, true, false);
+    JLA_G2(2, 5, true, false, 8, 4);
   else
-    JLA_G2(2, 4, false, false);
+    JLA_G2(2, 4, false, false, 8, 4);
 #undef JLA_G2
 }
 
 template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
-                         int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile_m,
+                         int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile,
                          hipStream_t s) {
   if (g_gemm_impl == 2) {
-    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile_m, s);
+    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s);
   } else {
     dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
     gemm_kernel<MODE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc);
@@ -608,7 +624,7 @@ static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int 
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps, int tile_m) {
+         float rms_eps, int tile) {
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
@@ -624,13 +640,13 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (ksplit == 1) {
     switch (mode) {
       case MODE_STORE:
-        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile_m, s);
+        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile, s);
         break;
       case MODE_RESIDUAL:
-        launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, -1.f, nullptr, tile_m, s);
+        launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, -1.f, nullptr, tile, s);
         break;
       case MODE_SWIGLU:
-        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, tile_m, s);
+        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s);
         break;
       default: return -1;
     }
@@ -641,7 +657,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   const size_t need = (size_t)ksplit * M * N + (rms ? (size_t)ksplit * M : 0);
   if ((N & 3) || ws == nullptr || ws_floats < need) return -3;
   float* ssq = rms ? ws + (size_t)ksplit * M * N : nullptr;
-  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, rms_eps, ssq, tile_m, s);
+  launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, rms_eps, ssq, tile, s);
   JLA_CHECK_LAUNCH();
   const size_t total4 = (size_t)M * N / 4;
   const int rgrid = (int)((total4 + 255) / 256);

@@ -47,7 +47,7 @@ size_t gemm_workspace_floats(int M, int N, int K);
 // (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps = -1.f, int tile_m = 0);  // tile_m: 128 / 256 rows per gemm2 tile, 0 = by M
+         float rms_eps = -1.f, int tile = 0);  // tile: gemm2 tile config 1 = 256x256, 2 = 128x256, 3 = 128x128, 0 = by M
 
 int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,

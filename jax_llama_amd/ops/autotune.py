@@ -99,14 +99,14 @@ def table() -> Dict[Tuple, int]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_M_CANDIDATES = (256, 128)
+TILE_CANDIDATES = (1, 2, 3)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg)
 TUNE_MAX_M = 2048
 
 
 def choose_gemm_plan(e, m: int, n: int, k: int, device) -> Tuple[int, int]:
-    """(split-K factor, gemm2 tile rows) for this shape: measured once on the device for M > 128 (tile
-    rows 256 or 128 x every split that keeps >= 4 K-tiles per split); the C++ heuristic otherwise or
-    while a hipGraph is being captured."""
+    """(split-K factor, gemm2 tile config) for this shape: measured once on the device for decode-sized
+    M (every tile config x every split that keeps >= 4 K-tiles per split); the C++ heuristic otherwise
+    or while a hipGraph is being captured."""
     key = (m, n, k)
     plan = _KS_CACHE.get(key)
     if plan is not None:
@@ -128,7 +128,7 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
 def _measure_plan(e, m, n, k, device, heur) -> Tuple[int, int]:
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
-    cands = [(c, tm) for tm in TILE_M_CANDIDATES for c in ks_c]
+    cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c]
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)

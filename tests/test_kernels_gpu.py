@@ -369,3 +369,33 @@ def test_topk_sample_graph_capturable():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), ref.topk_sample(logits.cpu(), 50, 0.8, 0.95, 3, 9))
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3])
+@pytest.mark.parametrize("ks", [1, 3])
+@pytest.mark.parametrize("m", [200, 512])
+def test_gemm_tile_configs(tile, ks, m):
+    """Every gemm2 tile configuration (256x256 / 128x256 / 128x128) x split-K x epilogue, with and
+    without the fused RMSNorm statistic, against the fp32 reference."""
+    e = ops.ext()
+    k, n = 1024, 768
+    x = torch.randn(m, k).to(BF16)
+    w, pg, _ = _mk_linear(n, k)
+    ws = torch.empty(ks * m * (n + 1), dtype=torch.float32, device=DEV)
+    wsa = ws if ks > 1 else None
+    xg = x.to(DEV)
+    for eps in (-1.0, 1e-5):
+        r = None if eps < 0 else eps
+        out = torch.empty(m, n, dtype=torch.float32, device=DEV)
+        e.gemm(xg, pg.weight, n, k, out, ops.MODE_STORE, True, None, ks, wsa, eps, tile)
+        _close(out, ref.linear(x, w, r, torch.float32), 1e-2, 2e-3)
+        gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+        gp = PackedLinear.from_dense(gu, DEV)
+        o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, wsa, eps, tile)
+        _close(o2, ref.linear_swiglu(x, gu, r), 3e-2, 3e-2)
+    h = torch.randn(m, n)
+    hg, mir = h.to(DEV), torch.empty(m, n, dtype=BF16, device=DEV)
+    e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, wsa, -1.0, tile)
+    _close(hg, ref.linear_residual(x, w, h.clone()), 1e-2, 1e-3)
+    torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)

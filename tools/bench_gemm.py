@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--no-blas", action="store_true")
     ap.add_argument("--impl", type=int, nargs="+", default=[2], help="tiled kernel generation(s) to time")
     ap.add_argument("--ops", nargs="+", default=None)
+    ap.add_argument("--tile", type=int, nargs="+", default=[0], help="gemm2 tile config(s): 0 auto, 1 256x256, "
+                    "2 128x256, 3 128x128")
     args = ap.parse_args()
     cfg = get_preset(args.model)
     d, f, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
@@ -69,12 +71,14 @@ def main():
             for impl in args.impl:
                 e.gemm_set_impl(impl)
                 for ks in args.ksplit:
+                  for tile in args.tile:
                     kk = ks or e.gemm_ksplit(m, n, k)
                     ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
 
-                    def run(i, kk=kk, ws=ws):
-                        e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk, ws if kk > 1 else None)
-                    res[f"v{impl}_ks{kk}"] = timeit(run, iters)
+                    def run(i, kk=kk, ws=ws, tile=tile):
+                        e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk, ws if kk > 1 else None,
+                               -1.0, tile)
+                    res[f"v{impl}_ks{kk}_t{tile}"] = timeit(run, iters)
                     run(0)
                     got = out.float()
                     if ref is None:

@@ -174,6 +174,10 @@ __global__ void __launch_bounds__(G_THREADS)
 // are copied verbatim, x is gathered by per-lane source addresses (16 rows x 64 B per wave-load).
 // Workgroups are remapped so consecutive tiles share an XCD (its own L2), M-grouped by 8.
 constexpr int G2_BN = 256, G2_NBUF = 4, G2_DIST = 3, G2_GROUP_M = 8;
+#ifdef JLA_GEMM_STAMPS
+// diagnostic build only (tools/debug/gemm_stamps.hip): per-wave cycles of the ping-pong phases
+__device__ unsigned long long g_gemm_stamps[8192 * 8 * 6];
+#endif
 
 // RMS (fused RMSNorm, reference model.py:28-48 with the gain folded into W): the A operand is the
 // UNscaled bf16 activation; the waves square-sum the A fragments they already read from LDS (wave wc
@@ -278,7 +282,17 @@ __global__ void __launch_bounds__(256 * WM)
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+    unsigned long long st_l = 0, st_b1 = 0, st_m = 0, st_b2 = 0, st_iss = 0, st_lds = 0, t0, t1;
+#define JLA_STAMP(v)                                                                     \
+  __builtin_amdgcn_sched_barrier(0);                                                     \
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");              \
+  __builtin_amdgcn_sched_barrier(0);
+#else
+#define JLA_STAMP(v)
+#endif
     for (int t = 0; t < KT; ++t) {
+      JLA_STAMP(t0)
       if (t + DIST < KT) issue(t + DIST);
       const int after = min(KT - 1, t + DIST) - (t + 1);  // tiles issued after t+1
       auto wait_next = [&]() {
@@ -292,6 +306,9 @@ __global__ void __launch_bounds__(256 * WM)
           wait_vmcnt<0>();
       };
       if constexpr (!LATE_WAIT) wait_next();
+#ifdef JLA_GEMM_STAMPS
+      JLA_STAMP(t1) st_iss += t1 - t0; t0 = t1;
+#endif
       const u32x4* buf = lds + (t % NBUF) * FR * 64;
       u32x4 a[MT], b[NTW];
 #pragma unroll
@@ -299,11 +316,20 @@ __global__ void __launch_bounds__(256 * WM)
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
       sumsq(buf);
+#ifdef JLA_GEMM_STAMPS
+      JLA_STAMP(t1) st_lds += t1 - t0; t0 = t1;
+#endif
       // LATE_WAIT: tile t+1 only has to land before this phase's barrier, not before tile t's reads
       if constexpr (LATE_WAIT) wait_next();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+      JLA_STAMP(t1) st_l += t1 - t0; t0 = t1;
+#endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+      JLA_STAMP(t1) st_b1 += t1 - t0; t0 = t1;
+#endif
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -311,10 +337,27 @@ __global__ void __launch_bounds__(256 * WM)
         for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+      JLA_STAMP(t1) st_m += t1 - t0; t0 = t1;
+#endif
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+      JLA_STAMP(t1) st_b2 += t1 - t0;
+#endif
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();
+#ifdef JLA_GEMM_STAMPS
+    if (lane == 0 && MODE == MODE_STORE) {
+      unsigned long long* d = g_gemm_stamps + ((size_t)blockIdx.x * NW + w) * 6;
+      d[0] = st_l;
+      d[1] = st_b1;
+      d[2] = st_m;
+      d[3] = st_b2;
+      d[4] = st_iss;
+      d[5] = st_lds;
+    }
+#endif
   } else
   for (int t = 0; t < KT; ++t) {
     const int ahead = min(KT - 1 - t, DIST - 1);  // tiles issued after t

@@ -184,7 +184,12 @@ __device__ unsigned long long g_gemm_stamps[8192 * 8 * 6];
 // takes m-tiles 2wc, 2wc+1 of its row block, 8 v_dot2 per K-tile) and the epilogue scales each output
 // row by rsqrt(mean(x^2) + eps). Split-K: each split stores its partial sums ([split][M] after the
 // fp32 slabs) and the reduce kernel finishes the statistic. No rms_scale launch, no scaled copy of x.
-template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4>
+// SUB = 2 (ping-pong only): each K-tile runs as two half phases per wave group -- [half the tile's
+// LDS-DMA issue + the A/B fragments of m-tiles 0..MT/2-1] -> 16 MFMAs, then [the other half of the issue +
+// the remaining A fragments + the vmcnt wait for tile t+1] -> 16 MFMAs -- so the partner group's MFMA
+// phase hides a shorter load phase (cdna_hip_programming.md T3+T4: the per-phase interleave is the lever).
+template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4,
+          int SUB = 1>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
@@ -240,6 +245,12 @@ __global__ void __launch_bounds__(256 * WM)
 #pragma unroll
     for (int j = 0; j < G; ++j) glds16(src[j] + (size_t)t * step[j], buf + (w + NW * j) * 64);
   };
+  // one half of a tile's loads (SUB = 2 issues a tile over two sub-phases)
+  auto issue_half = [&](int t, int h) {
+    u32x4* buf = lds + (t % NBUF) * FR * 64;
+#pragma unroll
+    for (int j = h * (G / 2); j < (h + 1) * (G / 2); ++j) glds16(src[j] + (size_t)t * step[j], buf + (w + NW * j) * 64);
+  };
 
   f32x4 acc[MT][NTW];
 #pragma unroll
@@ -291,6 +302,65 @@ __global__ void __launch_bounds__(256 * WM)
 #else
 #define JLA_STAMP(v)
 #endif
+    if constexpr (SUB == 2) {
+      // Barrier instances per K-tile t (group 0 / group 1 = one instance later): L0 | b | M0 | b | L1 | b | M1 | b.
+      //  RAW: each wave waits for its part of tile t+1 in L1(t) (group 0 before instance 4t+3, group 1 before
+      //       4t+4); tile t+1 is first read in L0(t+1), after instance 4t+4 (group 0) / 4t+5 (group 1).
+      //  WAR: tile t+3 refills tile t-1's buffer from L0(t) on (after instance 4t); the last reads of t-1
+      //       (group 1's L1(t-1)) retired with lgkmcnt(0) before its call of instance 4t.
+      static_assert(MT % 2 == 0 && G % 2 == 0, "SUB=2 splits the m-tiles and the loads in halves");
+      constexpr int MH = MT / 2;
+      for (int t = 0; t < KT; ++t) {
+        const u32x4* buf = lds + (t % NBUF) * FR * 64;
+        u32x4 a[MT], b[NTW];
+        // ---- L0: first half of tile t+3's loads; B fragments and the first half of A
+        if (t + DIST < KT) issue_half(t + DIST, 0);
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) b[j] = buf[(AF + wc * NTW + j) * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < MH; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MH; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // ---- L1: second half of the loads; the rest of A; wait for this wave's part of tile t+1
+        if (t + DIST < KT) issue_half(t + DIST, 1);
+#pragma unroll
+        for (int i = MH; i < MT; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
+        sumsq(buf);
+        {
+          const int after = min(KT - 1, t + DIST) - (t + 1);  // tiles issued after t+1
+          if (after >= 3)
+            wait_vmcnt<3 * G>();
+          else if (after == 2)
+            wait_vmcnt<2 * G>();
+          else if (after == 1)
+            wait_vmcnt<G>();
+          else
+            wait_vmcnt<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = MH; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    } else
     for (int t = 0; t < KT; ++t) {
       JLA_STAMP(t0)
       if (t + DIST < KT) issue(t + DIST);
@@ -576,11 +646,13 @@ __global__ void __launch_bounds__(256)
 // (kept for A/B measurements: tools/bench_gemm.py --impl 1).
 static int g_gemm_impl = 2;
 // gemm2 pipeline variant (A/B): 0 = 4 LDS buffers, wait before the reads; 1 = 4 buffers, wait after
-// the reads; 2 = 5 buffers (all 160 KiB of LDS at WM = 2, one more tile in flight), wait after
+// the reads; 2 = 5 buffers (all 160 KiB of LDS at WM = 2, one more tile in flight), wait after;
+// 3 = SUB = 2 half phases
 static int g_g2_var = 1;
 void gemm_set_impl(int impl) {
   g_gemm_impl = impl == 1 ? 1 : 2;
-  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 5 ? 2 : 1);  // 2/4 = default (late wait), 3 = early
+  // 2/4 = default (late wait), 3 = early wait, 5 = 5 buffers, 6 = two half phases per K-tile (SUB = 2)
+  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 5 ? 2 : (impl == 6 ? 3 : 1));
 }
 int gemm_get_impl() { return g_gemm_impl; }
 
@@ -625,9 +697,10 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
   const int grid = tm * tn * ksplit;
-#define JLA_G2(WMV, NB, LATE, R, MTV, NTV)                                                                  \
-  gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV><<<grid, 256 * WMV, 0, s>>>(                                \
+#define JLA_G2S(WMV, NB, LATE, R, MTV, NTV, SB)                                                             \
+  gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
       x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq)
+#define JLA_G2(WMV, NB, LATE, R, MTV, NTV) JLA_G2S(WMV, NB, LATE, R, MTV, NTV, 1)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   if constexpr (MODE != MODE_RESIDUAL) {
     if (rms) {  // fused RMSNorm statistic (default pipeline variant only)
@@ -635,6 +708,8 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
         JLA_G2(1, 4, false, true, 8, 4);
       else if (cfg == 3)
         JLA_G2(2, 4, true, true, 4, 2);
+      else if (g_g2_var == 3)
+        JLA_G2S(2, 4, true, true, 8, 4, 2);
       else
         JLA_G2(2, 4, true, true, 8, 4);
       return;
@@ -648,9 +723,12 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     JLA_G2(2, 4, true, false, 8, 4);
   else if (g_g2_var == 2)
     JLA_G2(2, 5, true, false, 8, 4);
+  else if (g_g2_var == 3)
+    JLA_G2S(2, 4, true, false, 8, 4, 2);
   else
     JLA_G2(2, 4, false, false, 8, 4);
 #undef JLA_G2
+#undef JLA_G2S
 }
 
 template <int MODE>

@@ -154,3 +154,37 @@ def test_reference_sampler_semantics():
     p = torch.softmax(row[0, :4], -1)
     assert freq[4:].sum() == 0
     assert (freq[:4] - p).abs().max() < 0.02
+
+
+def test_llama2_7b_config_two_layer_greedy_plumbing():
+    """BASELINE.json config 1: LLaMA-2 7B shapes (D 4096, 32 heads, F 11008, V 32000), 2 layers, random
+    init, greedy decode at MP=1 through the reference ``LLaMA.generate`` surface (generation.py:22-45) --
+    the jax_example.py plumbing on the CPU path. Checks the left-padded prompt, the EOS=pad convention and
+    that each cached decode token is the argmax of a full (no-cache) forward over the sequence so far."""
+    from types import SimpleNamespace
+
+    from jax_llama_amd import LLaMA
+    from jax_llama_amd.config import get_preset
+    from jax_llama_amd.models import LLaMAForCausalLM
+    cfg = get_preset("llama2-7b", num_hidden_layers=2)
+    assert (cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size, cfg.num_attention_heads) == (4096, 11008, 32000, 32)
+    model = LLaMAForCausalLM(cfg, device="cpu").init_random(seed=0)
+    tok = SimpleNamespace(eos_id=2, bos_id=1)
+    gen = LLaMA(None, model, tok)
+    g = torch.Generator().manual_seed(3)
+    tokens = torch.full((2, 6), tok.eos_id, dtype=torch.int32)
+    tokens[0] = torch.randint(3, cfg.vocab_size, (6,), generator=g)
+    tokens[1, 2:] = torch.randint(3, cfg.vocab_size, (4,), generator=g)
+    mask = (tokens != tok.eos_id).to(torch.int32)
+    out = gen.generate(tokens, mask, max_gen_len=3, temperature=0.0)
+    assert out.shape == (2, 9) and torch.equal(out[:, :6], tokens)
+    assert torch.equal(out, gen.generate(tokens, mask, max_gen_len=3, temperature=0.0))
+    for row in range(2):
+        n0 = int(mask[row].sum())
+        seq = out[row:row + 1, 6 - n0:]  # drop the left padding: positions restart at 0 either way
+        logits = model(seq).logits[0]
+        for j in range(3):
+            step = logits[n0 - 1 + j]
+            top2 = step.topk(2).values
+            if float(top2[0] - top2[1]) > 1e-3 * float(step.abs().max()):  # skip near-ties (bf16 weights)
+                assert int(step.argmax()) == int(seq[0, n0 + j]), (row, j)

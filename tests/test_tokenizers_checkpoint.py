@@ -138,15 +138,17 @@ def test_llama2_tokenizer(sp_tok):
 
 
 # ------------------------------------------------------------------ checkpoint conversion
-@pytest.mark.parametrize("n_shards,vocab_parallel", [(1, False), (2, False), (4, False), (2, True)])
+@pytest.mark.parametrize("n_shards,vocab_parallel", [(1, False), (2, False), (4, False), (2, True), (8, False)])
 def test_convert_meta_checkpoint(tmp_path, n_shards, vocab_parallel):
-    cfg = tiny_config(num_key_value_heads=4, intermediate_size=96)
+    # (8, False): the LLaMA-1 65B layout -- 8 consolidated.XX.pth shards, ParallelEmbedding split on the
+    # model dim (BASELINE.json config 5, download.sh:10-13)
+    cfg = tiny_config(num_attention_heads=8, num_key_value_heads=8, intermediate_size=96)
     sd = random_meta_state_dict(cfg, seed=5)
     pj = params_json_for(cfg, multiple_of=32)
     pj["some_future_key"] = 1  # unknown params.json keys are tolerated (reference ModelArgs rejects)
     save_meta_checkpoint(sd, pj, str(tmp_path), n_shards=n_shards, vocab_parallel_embedding=vocab_parallel)
     params, config = convert_llama_weights(str(tmp_path), cfg.vocab_size, max_seq_len=64)
-    assert config.hidden_size == cfg.hidden_size and config.num_key_value_heads == 4
+    assert config.hidden_size == cfg.hidden_size and config.num_key_value_heads == 8
     assert config.intermediate_size == 96 and config.vocab_size == cfg.vocab_size
     assert config.max_sequence_length == 64
     want = meta_state_dict_to_params(sd, cfg.num_hidden_layers)
@@ -157,10 +159,11 @@ def test_convert_meta_checkpoint(tmp_path, n_shards, vocab_parallel):
         assert torch.equal(torch.as_tensor(got).to(v.dtype), torch.as_tensor(v)), k
 
 
-@pytest.mark.parametrize("n_shards,tp", [(1, 2), (2, 2), (4, 2), (2, 4), (4, 1), (2, 1)])
+@pytest.mark.parametrize("n_shards,tp", [(1, 2), (2, 2), (4, 2), (2, 4), (4, 1), (2, 1), (8, 8), (8, 2), (1, 8)])
 def test_load_meta_rank_equals_sharded_merge(tmp_path, n_shards, tp):
+    # (8, 8): LLaMA-1 65B at MP=8 from its 8-shard checkpoint, every rank reading only its own slices
     from jax_llama_amd.utils.checkpoint import load_meta_rank
-    cfg = tiny_config(num_key_value_heads=4, intermediate_size=96)
+    cfg = tiny_config(num_attention_heads=8, num_key_value_heads=8, intermediate_size=96)
     sd = random_meta_state_dict(cfg, seed=6)
     save_meta_checkpoint(sd, params_json_for(cfg, multiple_of=32), str(tmp_path), n_shards=n_shards,
                          vocab_parallel_embedding=(n_shards == 4))

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--no-blas", action="store_true")
     ap.add_argument("--impl", type=int, nargs="+", default=[2], help="tiled kernel generation(s) to time")
     ap.add_argument("--ops", nargs="+", default=None)
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved A/B rounds of the impl list (one process)")
     ap.add_argument("--tile", type=int, nargs="+", default=[0], help="gemm2 tile config(s): 0 auto, 1 256x256, "
                     "2 128x256, 3 128x128")
     args = ap.parse_args()
@@ -68,7 +69,8 @@ def main():
             iters = max(5, min(200, int(2e13 / flop)))
             res = {}
             ref = None
-            for impl in args.impl:
+            first = {}
+            for rnd, impl in [(r, i) for r in range(args.rounds) for i in args.impl]:
                 e.gemm_set_impl(impl)
                 for ks in args.ksplit:
                   for tile in args.tile:
@@ -78,13 +80,16 @@ def main():
                     def run(i, kk=kk, ws=ws, tile=tile):
                         e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk, ws if kk > 1 else None,
                                -1.0, tile)
-                    res[f"v{impl}_ks{kk}_t{tile}"] = timeit(run, iters)
+                    res[f"v{impl}_ks{kk}_t{tile}" + (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                     run(0)
                     got = out.float()
                     if ref is None:
                         ref = (x.float() @ dense[0].float().t())
                     err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
                     assert err < 2e-2, (name, m, impl, kk, err)
+                    if impl >= 2:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
+                        f0 = first.setdefault((kk, tile), got.clone())
+                        assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
             e.gemm_set_impl(2)
             if not args.no_blas:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)

@@ -34,10 +34,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    # Serving-throughput operating point: 1024 concurrent sequences per replica (KV cache 51 GB of the
-    # 288 GB HBM; ~24 ms per decode step = ~41 tokens/s per sequence). Smaller batches are latency
-    # points (decode_ms_per_token): --batch 1 / 16 / 512.
-    ap.add_argument("--batch", type=int, default=1024, help="sequences per replica")
+    # Serving-throughput operating point: 2048 concurrent sequences per replica (KV cache 103 GB of the
+    # 288 GB HBM; ~44 ms per decode step = ~22 tokens/s per sequence; 35.1k tok/s vs 33.5k at 1024 and
+    # 33.6k at 1536 -- profiles/README.md). Smaller batches are latency points (decode_ms_per_token):
+    # --batch 1 / 16 / 512 / 1024.
+    ap.add_argument("--batch", type=int, default=2048, help="sequences per replica")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count (INVALID for the metric)")

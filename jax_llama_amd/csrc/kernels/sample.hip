@@ -64,9 +64,8 @@ __global__ void decode_update_kernel(const int32_t* __restrict__ nxt, int32_t* _
                                      int32_t* __restrict__ sequences, int32_t* __restrict__ cur_len,
                                      int32_t* __restrict__ tokens, int32_t* __restrict__ positions,
                                      int32_t* __restrict__ slot, int B, int L, int pad, int eos) {
-  const int b = threadIdx.x;
   const int cl = cur_len[0];
-  if (b < B) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {  // one workgroup: any batch size
     int t = nxt[b];
     const int fin = finished[b];
     if (fin) t = pad;
@@ -75,7 +74,7 @@ __global__ void decode_update_kernel(const int32_t* __restrict__ nxt, int32_t* _
     tokens[b] = t;
     positions[b] += 1;
   }
-  __syncthreads();
+  __syncthreads();  // every thread has read cur_len before it advances
   if (threadIdx.x == 0) {
     cur_len[0] = cl + 1;
     slot[0] += 1;
@@ -84,8 +83,8 @@ __global__ void decode_update_kernel(const int32_t* __restrict__ nxt, int32_t* _
 
 int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,
                   int32_t* positions, int32_t* slot, int B, int L, int pad, int eos, hipStream_t s) {
-  if (B > 1024) return -1;
-  decode_update_kernel<<<1, ((B + 63) / 64) * 64, 0, s>>>(nxt, finished, sequences, cur_len, tokens, positions, slot,
+  if (B <= 0) return -1;
+  decode_update_kernel<<<1, min(1024, ((B + 63) / 64) * 64), 0, s>>>(nxt, finished, sequences, cur_len, tokens, positions, slot,
                                                           B, L, pad, eos);
   JLA_CHECK_LAUNCH();
   return 0;

@@ -362,8 +362,9 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
                        int accumulate, int out_f32, const QKVArgs& qa, int variant, hipStream_t s) {
   // SwiGLU needs the gate/up tile pair in one workgroup; very wide outputs (lm_head, w1|w3) use
   // 2 tiles per workgroup to halve the activation re-reads.
-  // variant 5 / 6: 4 waves with 4 / 2 tiles per workgroup (x re-reads / 4, / 2) for tuning.
-  if constexpr (MT == 1) {
+  // variant 5 / 6: 4 waves with 4 / 2 tiles per workgroup (x re-reads / 4, / 2) for tuning; at MT > 1
+  // the activation fragments outnumber the weight fragments of a 1-tile workgroup, so these matter more.
+  {
     if (variant == 5 && (N & 63) == 0)
       return launch_skinny<XT, MT, 4, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
     if (variant == 6)

@@ -9,7 +9,7 @@ as in a real decode step) and caches the winner. Never runs under hipGraph captu
 seen during capture fall back to the static heuristic.
 
 Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG,
-4 = split-K skinny GEMM, 7 = 128x128 MFMA GEMM with split-K (gemm.hip; M > 32 only, always used
+4 = split-K skinny GEMM, 7 = tiled MFMA GEMM with split-K (gemm.hip; a candidate for M > 16, always used
 for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
 """
 from __future__ import annotations
@@ -42,14 +42,18 @@ def heuristic(m: int, n: int, k: int, mode: int) -> int:
 
 
 def candidates(m: int, n: int) -> Tuple[int, ...]:
-    if m > 32:
-        return (1, 4, 7)
-    if m > 16:
-        return (1, 4)
+    # M > 16: two or four activation m-tiles per weight fragment, so the 2/4-tile GEMV workgroups
+    # (fewer activation re-reads) and the tiled MFMA GEMM win on some shapes (M=24..64 sweep,
+    # profiles/r1_decode_m32_variants.jsonl: qkv -> 6, gate_up -> 5, down/lm_head -> 7 at M=32)
     c = [1, 6, 4]
     if n % 64 == 0:
         c.insert(1, 5)
+    if m > 16:
+        c.append(TILED_VARIANT)
     return tuple(c)
+
+
+TILED_VARIANT = 7
 
 
 def choose(e, x: torch.Tensor, w, mode: int, run) -> int:

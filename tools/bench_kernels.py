@@ -54,11 +54,12 @@ def main():
     d, f, hd = cfg.hidden_size, cfg.intermediate_size // args.tp, cfg.head_dim
     h, hkv = cfg.num_attention_heads // args.tp, cfg.num_key_value_heads // args.tp
     shapes = {
-        "qkv": ((h + 2 * hkv) * hd, d, torch.float32, ops.MODE_QKV),
+        # activations are the bf16 mirror of the residual stream in the model (every projection input)
+        "qkv": ((h + 2 * hkv) * hd, d, torch.bfloat16, ops.MODE_QKV),
         "o": (d, h * hd, torch.bfloat16, ops.MODE_RESIDUAL),
-        "gate_up": (2 * f, d, torch.float32, ops.MODE_SWIGLU),
+        "gate_up": (2 * f, d, torch.bfloat16, ops.MODE_SWIGLU),
         "down": (d, f, torch.bfloat16, ops.MODE_RESIDUAL),
-        "lm_head": (cfg.vocab_size // args.tp, d, torch.float32, ops.MODE_STORE),
+        "lm_head": (cfg.vocab_size // args.tp, d, torch.bfloat16, ops.MODE_STORE),
     }
     e = ops.ext()
     for name, (n, k, xdt, mode) in shapes.items():

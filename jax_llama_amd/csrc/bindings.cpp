@@ -197,9 +197,36 @@ void check_gemm_ws(const c10::optional<Tensor>& ws, int64_t ksplit, int64_t m, i
         "gemm ws too small");
 }
 
-// Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel.
+// stream-K tail (tile 4) workspace: slabs (float) + self-resetting tickets (int32, zeroed once)
+struct SkWs {
+  float* ws = nullptr;
+  size_t ws_floats = 0;
+  int32_t* tk = nullptr;
+  int n_tk = 0;
+};
+SkWs check_sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& tickets, int64_t m, int64_t n,
+                 int64_t k) {
+  SkWs r;
+  if (!jla::gemm_sk_active(m, n, k)) return r;
+  check(ws.has_value() && tickets.has_value(), "gemm tile 4: stream-K needs ws and tickets");
+  check_gpu(*ws, "gemm sk ws");
+  check_gpu(*tickets, "gemm sk tickets");
+  check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm_sk_workspace_floats(),
+        "gemm sk ws too small");
+  check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm_sk_tickets(m, n, k),
+        "gemm sk tickets too small");
+  r.ws = ptr<float>(*ws);
+  r.ws_floats = ws->numel();
+  r.tk = ptr<int32_t>(*tickets);
+  r.n_tk = (int)tickets->numel();
+  return r;
+}
+
+// Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel;
+// tile 4 -> data-parallel whole waves + stream-K tail (ws/tickets from gemm_sk_workspace).
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate,
-          c10::optional<Tensor> mirror, int64_t ksplit, c10::optional<Tensor> ws, double rms_eps, int64_t tile) {
+          c10::optional<Tensor> mirror, int64_t ksplit, c10::optional<Tensor> ws, double rms_eps, int64_t tile,
+          c10::optional<Tensor> tickets) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -207,9 +234,19 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   check(rms_eps < 0 || mode != 1, "gemm: fused RMS is not available in residual mode");
   const int64_t m = x.size(0);
   check_linear_out(out, m, n, mode);
+  jla::bf16_t* mir = mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr;
+  if (tile == 4) {
+    check(ksplit <= 1, "gemm tile 4: no K split");
+    const SkWs sk = check_sk_ws(ws, tickets, m, n, k);
+    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
+                 out.scalar_type() == torch::kFloat32, mir, nullptr, sk.ws, sk.ws_floats, 1, stream(),
+                 (float)rms_eps, 4, sk.tk, sk.n_tk),
+       "gemm");
+    return;
+  }
   check_gemm_ws(ws, ksplit, m, n, rms_eps >= 0);
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-               out.scalar_type() == torch::kFloat32, mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr, nullptr,
+               out.scalar_type() == torch::kFloat32, mir, nullptr,
                ksplit > 1 ? ptr<float>(*ws) : nullptr, ksplit > 1 ? ws->numel() : 0, ksplit, stream(),
                (float)rms_eps, (int)tile),
      "gemm");
@@ -219,13 +256,21 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
 // applies the fused RMSNorm statistic, otherwise x must already be scaled).
 void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor positions, Tensor kc, Tensor vc,
               Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q, int64_t ksplit,
-              Tensor ws, double rms_eps, int64_t tile) {
+              Tensor ws, double rms_eps, int64_t tile, c10::optional<Tensor> tickets) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
-  check(ksplit >= 2, "gemm_qkv: ksplit >= 2");
   const int64_t m = x.size(0);
   jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
+  if (tile == 4) {  // stream-K: the RoPE + cache-write epilogue runs in the GEMM itself
+    const SkWs sk = check_sk_ws(ws, tickets, m, n, k);
+    check(sk.ws != nullptr, "gemm_qkv tile 4: this shape has no stream-K tail");
+    rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, sk.ws, sk.ws_floats, 1,
+                 stream(), (float)rms_eps, 4, sk.tk, sk.n_tk),
+       "gemm_qkv");
+    return;
+  }
+  check(ksplit >= 2, "gemm_qkv: ksplit >= 2");
   check_gemm_ws(ws, ksplit, m, n, rms_eps >= 0);
   rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(ws), ws.numel(),
                ksplit, stream(), (float)rms_eps, (int)tile),
@@ -436,11 +481,18 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tickets"), py::arg("mirror") = py::none());
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
-        py::arg("rms_eps") = -1.0, py::arg("tile") = 0);
+        py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none());
+  m.def("gemm_sk_workspace", [](int64_t m, int64_t n, int64_t k) {
+    // (slab floats, tickets) of the stream-K tail of this shape; (0, 0) when it has none
+    if (!jla::gemm_sk_active(m, n, k)) return py::make_tuple((int64_t)0, (int64_t)0);
+    return py::make_tuple((int64_t)jla::gemm_sk_workspace_floats(), (int64_t)jla::gemm_sk_tickets(m, n, k));
+  });
+  m.def("gemm_sk_set_cus", [](int64_t n) { jla::gemm_sk_set_cus((int)n); });
+  m.def("gemm_sk_qkv_ok", [](int64_t m, int64_t n, int64_t k) { return (bool)jla::gemm_sk_qkv_ok(m, n, k); });
   m.def("gemm_qkv", &gemm_qkv, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("table"),
         py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"), py::arg("h"),
         py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("ksplit"), py::arg("ws"), py::arg("rms_eps") = -1.0,
-        py::arg("tile") = 0);
+        py::arg("tile") = 0, py::arg("tickets") = py::none());
   m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });

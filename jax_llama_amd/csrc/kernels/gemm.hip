@@ -179,6 +179,16 @@ constexpr int G2_BN = 256, G2_NBUF = 4, G2_DIST = 3, G2_GROUP_M = 8;
 __device__ unsigned long long g_gemm_stamps[8192 * 8 * 6];
 #endif
 
+// tile index (in the M-grouped launch order) -> (m tile, n tile); shared by the data-parallel launch
+// and the stream-K tail so both walk the same order
+JLA_DEV void g2_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int in_group = G2_GROUP_M * tiles_n;
+  const int first_m = (pid / in_group) * G2_GROUP_M;
+  const int gsz = min(tiles_m - first_m, G2_GROUP_M);
+  tm = first_m + (pid % in_group) % gsz;
+  tn = (pid % in_group) / gsz;
+}
+
 // RMS (fused RMSNorm, reference model.py:28-48 with the gain folded into W): the A operand is the
 // UNscaled bf16 activation; the waves square-sum the A fragments they already read from LDS (wave wc
 // takes m-tiles 2wc, 2wc+1 of its row block, 8 v_dot2 per K-tile) and the epilogue scales each output
@@ -213,11 +223,8 @@ __global__ void __launch_bounds__(256 * WM)
   const int tiles = tiles_m * tiles_n;
   const int split = wgid / tiles;
   const int pid = wgid - split * tiles;
-  const int in_group = G2_GROUP_M * tiles_n;
-  const int first_m = (pid / in_group) * G2_GROUP_M;
-  const int gsz = min(tiles_m - first_m, G2_GROUP_M);
-  const int tm = first_m + (pid % in_group) % gsz;
-  const int tn = (pid % in_group) / gsz;
+  int tm, tn;
+  g2_tile_coords(pid, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int KS = K >> 5, NTT = N >> 4;
@@ -539,6 +546,328 @@ __global__ void __launch_bounds__(256 * WM)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Stream-K tail of the 256 x 256 ping-pong GEMM (tile config 4). Decode-sized outputs rarely have a
+// multiple of 256 tiles (Llama-3-8B at M = 2048: qkv 192, o/down 128, gate_up 896 tiles), so the
+// last wave of whole tiles leaves CUs idle, and split-K pays a second kernel that re-reads fp32
+// slabs. Here the whole waves run as the ordinary data-parallel launch (gemm2_kernel, tiles
+// [0, dp_tiles)) and the remaining tiles' K-iterations (32-deep K-tiles) are dealt out evenly to one
+// persistent workgroup per CU: workgroup w owns iterations [I*w/P, I*(w+1)/P) of the tail, walking
+// (tile, K-range) segments in tile order. A segment covering a whole tile runs the epilogue directly.
+// A partial segment publishes its fp32 accumulators (and fused-RMS row sums) with write-through
+// (sc1) stores into the workgroup's own slab slot (slot 0: the segment at the start of its range,
+// slot 1: at the end), takes the tile's agent-scope ticket, and the LAST arriver -- whichever that
+// is -- sums every contributor's partial in contributor (= K) order, so results are deterministic,
+// and runs the fused epilogue (store / residual + bf16 mirror / SwiGLU / RoPE + KV-cache write).
+// Nobody waits on anybody (no co-residency assumption); tickets reset themselves
+// (cdna_hip_programming.md Guideline 16, sc1-store + agent ticket + sc1-load form).
+struct G2Sk {
+  int dp_tiles;        // tiles [0, dp_tiles) of the launch order ran in the data-parallel launch
+  int pad;
+  long long iters;     // tail K-iterations = (tiles - dp_tiles) * (K / 32)
+  float* slabs;        // [P][2][G2SK_SLAB_FLOATS]
+  int slab_bytes;      // buffer-descriptor range
+  int32_t* tickets;    // [tiles - dp_tiles]: zero-initialised once, reset by each tile's last arriver
+};
+constexpr int G2SK_ACC_BYTES = 8 * 8 * 4 * 1024;                // 8 waves x 8 x 4 fragments x 1 KiB
+constexpr int G2SK_SLAB_BYTES = G2SK_ACC_BYTES + 256 * 4;       // + 256 row sums of squares
+constexpr int G2SK_SLAB_FLOATS = G2SK_SLAB_BYTES / 4;
+
+JLA_DEV int g2sk_owner(long long it, long long iters, int P) {  // workgroup whose range holds iteration it
+  return (int)(((it + 1) * P - 1) / iters);
+}
+JLA_DEV long long g2sk_lo(int w, long long iters, int P) { return iters * w / P; }
+
+template <int MODE, bool RMS>
+__global__ void __launch_bounds__(512)
+    gemm2_sk_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                    int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int tiles_m, int tiles_n,
+                    float rms_eps, G2Sk sk, QKVArgs qa) {
+  constexpr int MT = 8, NTW = 4, NBUF = 4, DIST = 3, NW = 8, BM = 256, BN = 256;
+  constexpr int AF = 16, FR = 32, G = 4, RPW = 2;
+  // ONE __shared__ object (tile ring + row scales + last-arriver flag): with a second LDS object hipcc
+  // can no longer tell the LDS-DMA targets apart and drains vmcnt(0) before every ds_read of the ring
+  __shared__ u32x4 lds[NBUF * FR * 64 + BM / 4 + 1];
+  float* rs_sh = reinterpret_cast<float*>(lds + NBUF * FR * 64);  // fused-RMS row scales of the tile
+  int& sh_last = *reinterpret_cast<int*>(lds + NBUF * FR * 64 + BM / 4);
+  const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int KS = K >> 5, NTT = N >> 4;
+  // XCD-aware (bijective) remap: the workgroups that share an XCD (blockIdx.x = xcd mod 8) get
+  // consecutive iteration ranges, i.e. neighbouring tiles of the M-grouped order, so their A rows and
+  // weight columns are reused in that XCD's L2 (without it the tail streamed ~2x the bytes from HBM)
+  const int P = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = P >> 3, r8 = P & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const long long lo = g2sk_lo(wg, sk.iters, P), hi = g2sk_lo(wg + 1, sk.iters, P);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(sk.slabs, 0, sk.slab_bytes, 0x00020000);
+
+  for (long long it = lo; it < hi;) {
+    const int t = (int)(it / KS);                 // tail tile
+    const int kb = (int)(it - (long long)t * KS);  // this segment's K-tiles [kb, ke)
+    const int ke = (int)min((long long)KS, (long long)kb + (hi - it));
+    const int slot = it == lo ? 0 : 1;
+    it += ke - kb;
+    int tm, tn;
+    g2_tile_coords(sk.dp_tiles + t, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int KT = ke - kb;
+    // lane index laundered through an opaque move once per segment: the lane-dependent address math
+    // of the unrolled epilogue would otherwise be hoisted out of the segment loop and held in
+    // registers across the main loop (spills)
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+
+    __syncthreads();  // the previous segment's epilogue is done with LDS
+    const char* src[G];
+    int step[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int f = w + NW * j;
+      if (f < AF) {
+        const int row = min(m0 + 16 * f + (lane & 15), M - 1);
+        src[j] = reinterpret_cast<const char*>(x + (size_t)row * K + (size_t)kb * 32 + 8 * (lane >> 4));
+        step[j] = 64;
+      } else {
+        const int nt = min((n0 >> 4) + (f - AF), NTT - 1);
+        src[j] = reinterpret_cast<const char*>(W + ((size_t)nt * KS + kb) * 64 + lane);
+        step[j] = 1024;
+      }
+    }
+    auto issue = [&](int tt) {
+      u32x4* buf = lds + (tt % NBUF) * FR * 64;
+#pragma unroll
+      for (int j = 0; j < G; ++j) glds16(src[j] + (size_t)tt * step[j], buf + (w + NW * j) * 64);
+    };
+    f32x4 acc[MT][NTW];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss0 = 0.f, ss1 = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < DIST; ++tt)
+      if (tt < KT) issue(tt);
+
+    // ---- the gemm2 ping-pong main loop (see gemm2_kernel for the barrier / vmcnt accounting)
+    wait_vmcnt<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int tt = 0; tt < KT; ++tt) {
+      if (tt + DIST < KT) issue(tt + DIST);
+      const int after = min(KT - 1, tt + DIST) - (tt + 1);
+      const u32x4* buf = lds + (tt % NBUF) * FR * 64;
+      u32x4 a[MT], b[NTW];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) b[j] = buf[(AF + wc * NTW + j) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
+      if constexpr (RMS) {
+        const u32x4 f0 = buf[(wr * MT + RPW * wc) * 64 + lane];
+        ss0 = dot8_bf16(f0, f0, ss0);
+        const u32x4 f1 = buf[(wr * MT + RPW * wc + 1) * 64 + lane];
+        ss1 = dot8_bf16(f1, f1, ss1);
+      }
+      if (after >= 3)
+        wait_vmcnt<3 * G>();
+      else if (after == 2)
+        wait_vmcnt<2 * G>();
+      else if (after == 1)
+        wait_vmcnt<G>();
+      else
+        wait_vmcnt<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+    if constexpr (RMS) {  // row sums of this segment's K range (rows (wr*MT + RPW*wc [+1])*16 + lane&15)
+      ss0 += __shfl_xor(ss0, 16, 64);
+      ss0 += __shfl_xor(ss0, 32, 64);
+      ss1 += __shfl_xor(ss1, 16, 64);
+      ss1 += __shfl_xor(ss1, 32, 64);
+    }
+
+    if (!(kb == 0 && ke == KS)) {
+      // ---- partial segment: publish (sc1), ticket, last arriver sums all contributors in K order
+      const int base = (wg * 2 + slot) * G2SK_SLAB_BYTES;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                 base + ((w * MT + i) * NTW + j) * 1024 + lane * 16, 0, 16);
+      if (RMS && lane < 16) {
+        const int r0 = (wr * MT + RPW * wc) * 16 + lane;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss0), rsrc, base + G2SK_ACC_BYTES + r0 * 4, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss1), rsrc, base + G2SK_ACC_BYTES + (r0 + 16) * 4, 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const long long t_lo = (long long)t * KS, t_hi = t_lo + KS;
+      const int w_first = g2sk_owner(t_lo, sk.iters, P), w_last = g2sk_owner(t_hi - 1, sk.iters, P);
+      if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(sk.tickets + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == w_last - w_first;
+        if (last) __hip_atomic_store(sk.tickets + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh_last = last;
+      }
+      __syncthreads();
+      if (!sh_last) continue;
+      // sum the contributors' partials in contributor (= K) order, whoever arrived last: fragment by
+      // fragment, the ones before this workgroup (re-read), then its own (registers), then the rest
+      const int n_c = w_last - w_first + 1, me = wg - w_first;
+      int cb[4];  // slab byte offsets of the contributors (a tail tile never has more than 4: plan)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cw = min(w_first + q, w_last);
+        cb[q] = (cw * 2 + (g2sk_lo(cw, sk.iters, P) >= t_lo ? 0 : 1)) * G2SK_SLAB_BYTES;
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int off = ((w * MT + i) * NTW + j) * 1024 + lane * 16;
+          f32x4 tsum = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int q = 0; q < n_c; ++q)
+            tsum += q == me ? acc[i][j]
+                            : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, cb[q] + off, 0, 16));
+          acc[i][j] = tsum;
+        }
+      if constexpr (RMS) {
+        const int r0 = (wr * MT + RPW * wc) * 16 + (lane & 15);
+        float t0 = 0.f, t1 = 0.f;
+        for (int q = 0; q < n_c; ++q) {
+          t0 += q == me ? ss0 : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, cb[q] + G2SK_ACC_BYTES + r0 * 4, 0, 16));
+          t1 += q == me ? ss1 : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, cb[q] + G2SK_ACC_BYTES + (r0 + 16) * 4, 0, 16));
+        }
+        ss0 = t0;
+        ss1 = t1;
+      }
+    }
+
+    // ---- epilogue of a finished tile, staged through LDS one wave row (128 x 256 fp32) at a time so
+    // every output row is written by one wave with 16-byte-per-lane coalesced stores (columns swizzled
+    // by row group: the 4 row groups of an accumulator write land on distinct banks)
+    float* ep = reinterpret_cast<float*>(lds);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last read of the tile buffers
+    if constexpr (RMS) {
+      if (lane < 16) {
+        const float inv_k = 1.f / (float)K;
+        rs_sh[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 * inv_k + rms_eps);
+        rs_sh[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 * inv_k + rms_eps);
+      }
+    }
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      if (wr == half) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = i * 16 + 4 * (lane >> 4) + r;
+              const int col = ((wc * NTW + j) * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
+              ep[row * BN + col] = acc[i][j][r];
+            }
+      }
+      __syncthreads();
+#pragma unroll 2
+      for (int q = 0; q < 16; ++q) {
+        const int e = threadIdx.x + 512 * q;
+        const int row = e >> 6, c4 = (e & 63) * 4;
+        const int grow = m0 + half * 128 + row, gcol = n0 + c4;
+        float4 v = *reinterpret_cast<const float4*>(ep + row * BN + (c4 ^ (((row >> 2) & 3) << 4)));
+        if (grow >= M || gcol >= N) continue;
+        if constexpr (RMS) {
+          const float sc = rs_sh[half * 128 + row];
+          v.x *= sc;
+          v.y *= sc;
+          v.z *= sc;
+          v.w *= sc;
+        }
+        const size_t idx = (size_t)grow * N + gcol;
+        if constexpr (MODE == MODE_SWIGLU) {
+          if (((gcol >> 4) & 1) == 0) {  // gate tile; its up tile is the next 16 columns
+            const int uc = c4 + 16;
+            float4 u = *reinterpret_cast<const float4*>(ep + row * BN + (uc ^ (((row >> 2) & 3) << 4)));
+            if constexpr (RMS) {
+              const float sc = rs_sh[half * 128 + row];
+              u.x *= sc;
+              u.y *= sc;
+              u.z *= sc;
+              u.w *= sc;
+            }
+            bf16_t* o = static_cast<bf16_t*>(out) + (size_t)grow * (N >> 1) + (gcol >> 5) * 16 + (gcol & 15);
+            *reinterpret_cast<uint2*>(o) = make_uint2(pack2bf(silu(v.x) * u.x, silu(v.y) * u.y),
+                                                      pack2bf(silu(v.z) * u.z, silu(v.w) * u.w));
+          }
+        } else if constexpr (MODE == MODE_QKV) {
+          float vv[4] = {v.x, v.y, v.z, v.w};
+          const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
+          const int b = grow / qa.S, sq = grow - b * qa.S;
+          if (head < qa.H + qa.Hkv) {
+            int pos = qa.positions[grow];
+            pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
+#pragma unroll
+            for (int p2 = 0; p2 < 2; ++p2) {
+              const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d0 >> 1) + p2];
+              const float xr = vv[2 * p2], xi = vv[2 * p2 + 1];
+              vv[2 * p2] = xr * cs.x - xi * cs.y;
+              vv[2 * p2 + 1] = xr * cs.y + xi * cs.x;
+            }
+          }
+          const uint2 packed = make_uint2(pack2bf(vv[0], vv[1]), pack2bf(vv[2], vv[3]));
+          if (head < qa.H) {
+            *reinterpret_cast<uint2*>(qa.q + ((size_t)grow * qa.H + head) * qa.Dh + d0) = packed;
+          } else {
+            const int cslot = qa.slot[0] + sq;
+            if (cslot < qa.T) {
+              const bool is_k = head < qa.H + qa.Hkv;
+              const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
+              bf16_t* cache = is_k ? qa.kc : qa.vc;
+              *reinterpret_cast<uint2*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + cslot) * qa.Dh + d0) = packed;
+            }
+          }
+        } else if constexpr (MODE == MODE_RESIDUAL) {
+          float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + idx);
+          float4 r4 = v;
+          if (accumulate) {
+            const float4 old = *o;
+            r4.x += old.x;
+            r4.y += old.y;
+            r4.z += old.z;
+            r4.w += old.w;
+          }
+          *o = r4;
+          if (mirror)
+            *reinterpret_cast<uint2*>(mirror + idx) = make_uint2(pack2bf(r4.x, r4.y), pack2bf(r4.z, r4.w));
+        } else {
+          if (out_f32)
+            *reinterpret_cast<float4*>(static_cast<float*>(out) + idx) = v;
+          else
+            *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + idx) =
+                make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+        }
+      }
+      __syncthreads();  // the half-tile is consumed before the other wave row overwrites it
+    }
+  }
+}
+
 // Sum the split-K partials (fixed order) and apply the epilogue. One thread = 4 consecutive
 // columns of one row (two RoPE pairs; a 16-column tile never straddles a float4).
 template <int MODE>
@@ -692,11 +1021,13 @@ static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s) {
+                      bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
+                      int grid_override = 0) {
   const int cfg = tile_cfg(tile, M);
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
-  const int grid = tm * tn * ksplit;
+  // grid_override: only the first grid_override tiles of the launch order (stream-K's data-parallel part)
+  const int grid = grid_override > 0 ? grid_override : tm * tn * ksplit;
 #define JLA_G2S(WMV, NB, LATE, R, MTV, NTV, SB)                                                             \
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
       x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq)
@@ -743,15 +1074,116 @@ static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int 
   }
 }
 
+// ---- stream-K tail plan (tile config 4): whole waves of 256x256 tiles data-parallel, the rest dealt
+// out as K-iterations to one workgroup per CU
+static int g_num_cus = 0;
+static int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      g_num_cus = prop.multiProcessorCount;
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
+struct G2SkPlan {
+  int dp, sk;        // data-parallel tiles, stream-K tail tiles (sk == 0: no tail, plain launch)
+  long long iters;   // tail K-iterations
+};
+static G2SkPlan g2sk_plan(int M, int N, int K) {
+  const int P = num_cus(), KS = K >> 5;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  G2SkPlan p{tiles, 0, 0};
+  const int rem = tiles % P;
+  if (rem == 0) return p;
+  int sk = rem;
+  // a thin tail would split every tile over many contributors (each one a 256 KiB partial to publish
+  // and re-read): give the tail one more whole wave, and never let a tile have more than 4
+  // contributors (>= KS/3 K-tiles per workgroup), which the fixup's fixed-size table assumes
+  if ((long long)sk * KS < (long long)P * ((KS + 2) / 3) && tiles >= sk + P) sk += P;
+  if ((long long)sk * KS < (long long)P * ((KS + 2) / 3)) return p;  // leave it data-parallel
+  p.dp = tiles - sk;
+  p.sk = sk;
+  p.iters = (long long)sk * KS;
+  return p;
+}
+// test hook: pretend the device has n CUs (0 = query it) so small shapes get a data-parallel part + tail
+void gemm_sk_set_cus(int n) { g_num_cus = n > 0 ? n : 0; }
+size_t gemm_sk_workspace_floats() { return (size_t)num_cus() * 2 * G2SK_SLAB_FLOATS; }
+int gemm_sk_tickets(int M, int N, int K) { return max(1, g2sk_plan(M, N, K).sk); }
+int gemm_sk_active(int M, int N, int K) { return g2sk_plan(M, N, K).sk > 0; }
+int gemm_sk_qkv_ok(int M, int N, int K) {  // every tile in the tail: the RoPE/KV epilogue can run in-kernel
+  const G2SkPlan p = g2sk_plan(M, N, K);
+  return p.sk > 0 && p.dp == 0;
+}
+
+template <int MODE>
+static void launch_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
+                      bf16_t* mirror, float rms_eps, const G2Sk& sk, const QKVArgs& qa, hipStream_t s) {
+  const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+  if (MODE != MODE_RESIDUAL && rms_eps >= 0.f)
+    gemm2_sk_kernel<MODE, true><<<num_cus(), 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn,
+                                                          rms_eps, sk, qa);
+  else
+    gemm2_sk_kernel<MODE, false><<<num_cus(), 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn,
+                                                           rms_eps, sk, qa);
+}
+
+static int gemm_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int mode, int accumulate,
+                   int out_f32, bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
+                   int n_tickets, hipStream_t s, float rms_eps) {
+  const G2SkPlan p = g2sk_plan(M, N, K);
+  if (ws == nullptr || ws_floats < gemm_sk_workspace_floats() || tickets == nullptr || n_tickets < p.sk) return -3;
+  if (p.dp > 0) {
+    if (mode == MODE_QKV) return -1;  // the data-parallel kernel has no RoPE epilogue
+    switch (mode) {
+      case MODE_STORE:
+        launch_g2<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, K >> 5, 1, rms_eps, nullptr, 1, s, p.dp);
+        break;
+      case MODE_RESIDUAL:
+        launch_g2<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, K >> 5, 1, -1.f, nullptr, 1, s, p.dp);
+        break;
+      case MODE_SWIGLU:
+        launch_g2<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, K >> 5, 1, rms_eps, nullptr, 1, s, p.dp);
+        break;
+      default: return -1;
+    }
+    JLA_CHECK_LAUNCH();
+  }
+  G2Sk sk{p.dp, 0, p.iters, ws, (int)(gemm_sk_workspace_floats() * 4), tickets};
+  QKVArgs qa{};
+  if (qkv) qa = *qkv;
+  switch (mode) {
+    case MODE_STORE: launch_sk<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, rms_eps, sk, qa, s); break;
+    case MODE_RESIDUAL: launch_sk<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, -1.f, sk, qa, s); break;
+    case MODE_SWIGLU: launch_sk<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, rms_eps, sk, qa, s); break;
+    case MODE_QKV: launch_sk<MODE_QKV>(x, w, out, M, N, K, 0, 0, nullptr, rms_eps, sk, qa, s); break;
+    default: return -1;
+  }
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps, int tile) {
+         float rms_eps, int tile, int32_t* tickets, int n_tickets) {
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
-  if (mode == MODE_QKV && (!qkv || ksplit < 2)) return -1;  // qkv epilogue only in the reduce kernel
   const bool rms = rms_eps >= 0.f;
   if (rms && (g_gemm_impl == 1 || mode == MODE_RESIDUAL)) return -5;  // caller pre-scales x instead
+  if (tile == 4) {  // stream-K tail (256x256 ping-pong tiles; no K split)
+    if (g_gemm_impl != 2 || ksplit > 1) return -1;
+    if (mode == MODE_QKV && !qkv) return -1;
+    if (g2sk_plan(M, N, K).sk > 0)
+      return gemm_sk(x, static_cast<const u32x4*>(W), out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ws,
+                     ws_floats, tickets, n_tickets, s, rms_eps);
+    if (mode == MODE_QKV) return -1;
+    tile = 1;  // whole waves only: the plain data-parallel launch
+  }
+  if (mode == MODE_QKV && (!qkv || ksplit < 2)) return -1;  // qkv epilogue only in the reduce kernel
   const int KS = K >> 5;
   if (ksplit < 1) ksplit = 1;
   const int kc = (KS + ksplit - 1) / ksplit;

@@ -45,9 +45,17 @@ int gemm_get_impl();
 size_t gemm_workspace_floats(int M, int N, int K);
 // rms_eps >= 0: x is the UNscaled activation and each output row is scaled by rsqrt(mean(x^2) + eps)
 // (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
+// tile: gemm2 tile config 1 = 256x256, 2 = 128x256, 3 = 128x128, 0 = by M, 4 = 256x256 with a stream-K tail
+// (ksplit 1; ws >= gemm_sk_workspace_floats(), tickets >= gemm_sk_tickets(M, N, K) int32 zero-initialised
+// once, self-resetting; MODE_QKV supported when every tile is in the tail)
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps = -1.f, int tile = 0);  // tile: gemm2 tile config 1 = 256x256, 2 = 128x256, 3 = 128x128, 0 = by M
+         float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0);
+size_t gemm_sk_workspace_floats();
+int gemm_sk_tickets(int M, int N, int K);
+int gemm_sk_active(int M, int N, int K);
+int gemm_sk_qkv_ok(int M, int N, int K);
+void gemm_sk_set_cus(int n);
 
 int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,

@@ -168,20 +168,38 @@ def _tiled_input(x, rms_eps, fused=False):
     return x if x.dtype == BF16 else x.to(BF16)
 
 
+SK_TILE = 4          # gemm2 "tile config" of the stream-K tail plan (csrc/kernels/gemm.hip)
+SK_MAX_TICKETS = 1024  # >= 2 x CUs: one fixed-size ticket array, so hipGraphs never see a reallocation
+
+
+def sk_workspace(e, m, n, k, device):
+    """Slabs + self-resetting tickets of the stream-K tail (None, None when the shape has no tail)."""
+    floats, tickets = e.gemm_sk_workspace(m, n, k)
+    if floats == 0:
+        return None, None
+    assert tickets <= SK_MAX_TICKETS, tickets
+    return (workspace.get("gemm_sk", floats, torch.float32, device),
+            workspace.get_zeroed("gemm_sk_tickets", SK_MAX_TICKETS, torch.int32, device))
+
+
 def _gemm_ws(e, m, n, k, device):
+    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape."""
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device)
+    if tm == SK_TILE:
+        ws, tk = sk_workspace(e, m, n, k, device)
+        return 1, tm, ws, tk
     # split-K slabs [ks][m][n] + the fused-RMS partial sums of squares [ks][m]
     ws = workspace.get("gemm_ws", ks * m * (n + 1), torch.float32, device) if ks > 1 else None
-    return ks, tm, ws
+    return ks, tm, ws, None
 
 
 def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
-    """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups when the
-    output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip)."""
+    """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups, or a stream-K tail,
+    when the output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip)."""
     fused = _fused_rms(e, mode, rms_eps)
     xb = _tiled_input(x, rms_eps, fused)
-    ks, tm, ws = _gemm_ws(e, x.shape[0], n, k, x.device)
-    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm)
+    ks, tm, ws, tk = _gemm_ws(e, x.shape[0], n, k, x.device)
+    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
 
 
 def _variant(e, x, w, mode) -> int:
@@ -253,8 +271,10 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     e = ext()
     v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV)
     if v == TILED:
-        ks, tm, ws = _gemm_ws(e, m, w.n, w.k, x.device)
-        if ks == 1:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
+        ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device)
+        if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):
+            tm = 1  # the stream-K plan has a data-parallel part here: plain GEMM + RoPE kernel
+        if ks == 1 and tm != SK_TILE:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
             qkv = linear(x, w, rms_eps=rms_eps)
             return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads,
                                  head_dim)
@@ -262,7 +282,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
         fused = _fused_rms(e, MODE_QKV, rms_eps)
         e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                    k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm)
+                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
         return q
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)

@@ -74,22 +74,22 @@ def _measure(x, w, run, cands) -> int:
     nbytes = w.weight.numel() * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws = [torch.empty_like(w.weight).normal_(0, 0.02) for _ in range(copies)]
-    best, best_t = cands[0], float("inf")
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for v in cands:
         for i in range(2):
             run(v, x, ws[i % copies])
-        iters = 2 * copies
-        ev0.record()
-        for i in range(iters):
-            run(v, x, ws[i % copies])
-        ev1.record()
-        ev1.synchronize()
-        t = ev0.elapsed_time(ev1) / iters
-        if t < best_t:
-            best, best_t = v, t
+    times = {v: float("inf") for v in cands}
+    iters = 2 * copies
+    for _ in range(TUNE_ROUNDS):  # interleaved rounds, min per candidate (see _measure_plan)
+        for v in cands:
+            ev0.record()
+            for i in range(iters):
+                run(v, x, ws[i % copies])
+            ev1.record()
+            ev1.synchronize()
+            times[v] = min(times[v], ev0.elapsed_time(ev1) / iters)
     del ws
-    return best
+    return min(cands, key=times.get)
 
 
 def table() -> Dict[Tuple, int]:
@@ -103,7 +103,8 @@ def table() -> Dict[Tuple, int]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg)
+TILE_CANDIDATES = (1, 2, 3)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
+# plus (1, SK_TILE) -- 256x256 with a stream-K tail -- for shapes whose tile count is not a multiple of the CUs
 TUNE_MAX_M = 2048
 
 
@@ -129,10 +130,19 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
     return choose_gemm_plan(e, m, n, k, device)[0]
 
 
+SK_TILE = 4  # 256x256 tiles with a stream-K tail (no K split): csrc/kernels/gemm.hip gemm_sk
+SK_MARGIN = 0.97
+TUNE_ROUNDS = 3
+
+
 def _measure_plan(e, m, n, k, device, heur) -> Tuple[int, int]:
+    from . import sk_workspace
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c]
+    sk_ws, sk_tk = sk_workspace(e, m, n, k, device)
+    if sk_ws is not None:
+        cands.append((1, SK_TILE))
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
@@ -141,21 +151,32 @@ def _measure_plan(e, m, n, k, device, heur) -> Tuple[int, int]:
     out = torch.empty(m, n, dtype=torch.bfloat16, device=device)
     ws = torch.empty(max(ks_c) * m * (n + 1), dtype=torch.float32, device=device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best, best_t = (heur, 0), float("inf")
-    for c, tm in cands:
-        def run(i):
+
+    def run(c, tm, i):
+        if tm == SK_TILE:
+            e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, 1, sk_ws, -1.0, tm, sk_tk)
+        else:
             e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, c, ws if c > 1 else None, -1.0, tm)
+
+    for c, tm in cands:  # warm every variant (code objects, caches) before any timing
         for i in range(2):
-            run(i)
-        iters = 2 * copies
-        ev0.record()
-        for i in range(iters):
-            run(i)
-        ev1.record()
-        ev1.synchronize()
-        t = ev0.elapsed_time(ev1) / iters
-        if t < best_t:
-            best, best_t = (c, tm), t
+            run(c, tm, i)
+    # interleaved rounds, min per candidate: one round alone is at the mercy of DVFS drift between
+    # candidates (cdna_hip_programming.md rule 24)
+    times = {cand: float("inf") for cand in cands}
+    iters = 2 * copies
+    for _ in range(TUNE_ROUNDS):
+        for c, tm in cands:
+            ev0.record()
+            for i in range(iters):
+                run(c, tm, i)
+            ev1.record()
+            ev1.synchronize()
+            times[(c, tm)] = min(times[(c, tm)], ev0.elapsed_time(ev1) / iters)
+    best = min((cand for cand in cands if cand[1] != SK_TILE), key=times.get)
+    # the stream-K tail publishes fp32 partials in-kernel: keep it only when it clearly wins
+    if (1, SK_TILE) in times and times[(1, SK_TILE)] < SK_MARGIN * times[best]:
+        best = (1, SK_TILE)
     del ws_w, ws
     return best
 

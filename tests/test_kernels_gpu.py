@@ -399,3 +399,79 @@ def test_gemm_tile_configs(tile, ks, m):
     e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, wsa, -1.0, tile)
     _close(hg, ref.linear_residual(x, w, h.clone()), 1e-2, 1e-3)
     torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("cus,m", [(0, 768), (0, 1000), (16, 200), (16, 512)])
+def test_gemm_stream_k_tail(cus, m):
+    """256x256 tiles with a stream-K tail (tile config 4): every epilogue, with and without the fused
+    RMSNorm, against the fp32 reference; bit-identical on a re-run (fixed contributor order, tickets
+    reset themselves). cus=16 pretends a 16-CU device so the small shape gets a data-parallel part
+    (16 / 64 whole tiles) plus a tail split across workgroups; cus=0 uses the real CU count (all tail)."""
+    e = ops.ext()
+    e.gemm_sk_set_cus(cus)
+    try:
+        k, n = 1024, 256 * 37
+        assert e.gemm_sk_workspace(m, n, k)[0] > 0
+        x = torch.randn(m, k).to(BF16)
+        w, pg, _ = _mk_linear(n, k)
+        xg = x.to(DEV)
+        ws, tk = ops.sk_workspace(e, m, n, k, DEV)
+        for eps in (-1.0, 1e-5):
+            r = None if eps < 0 else eps
+            out = torch.empty(m, n, dtype=torch.float32, device=DEV)
+            e.gemm(xg, pg.weight, n, k, out, ops.MODE_STORE, True, None, 1, ws, eps, 4, tk)
+            _close(out, ref.linear(x, w, r, torch.float32), 1e-2, 2e-3)
+            again = torch.empty_like(out)
+            e.gemm(xg, pg.weight, n, k, again, ops.MODE_STORE, True, None, 1, ws, eps, 4, tk)
+            assert torch.equal(out, again)
+            ob = torch.empty(m, n, dtype=BF16, device=DEV)
+            e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, ws, eps, 4, tk)
+            torch.testing.assert_close(ob, out.to(BF16), rtol=0, atol=0)
+            gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+            gp = PackedLinear.from_dense(gu, DEV)
+            o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, ws, eps, 4, tk)
+            _close(o2, ref.linear_swiglu(x, gu, r), 3e-2, 3e-2)
+        h = torch.randn(m, n)
+        hg, mir = h.to(DEV), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, ws, -1.0, 4, tk)
+        _close(hg, ref.linear_residual(x, w, h.clone()), 1e-2, 1e-3)
+        torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
+        assert int(tk.abs().sum()) == 0  # every tail tile's last arriver reset its ticket
+    finally:
+        e.gemm_sk_set_cus(0)
+
+
+@pytest.mark.parametrize("m,s", [(512, 1), (384, 2)])
+def test_qkv_rope_stream_k(m, s):
+    """Fused qkv projection on the stream-K plan: RoPE + KV-cache write in the GEMM epilogue (a 16-CU
+    plan so this small projection has a tail)."""
+    e = ops.ext()
+    e.gemm_sk_set_cus(16)
+    try:
+        _qkv_rope_stream_k(e, m, s)
+    finally:
+        e.gemm_sk_set_cus(0)
+
+
+def _qkv_rope_stream_k(e, m, s):
+    h, hkv, dh, k, t = 8, 2, 128, 4096, 80
+    b = m // s
+    n = (h + 2 * hkv) * dh
+    assert e.gemm_sk_qkv_ok(m, n, k)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    x = torch.randn(m, k).to(BF16)
+    table = ref.rope_table(dh, 256, 500000.0)
+    pos = torch.randint(0, 200, (m,), dtype=torch.int32)
+    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+    vc = torch.zeros_like(kc)
+    q = ref.linear_qkv_rope(x, w, 1e-5, table, pos, kc, vc, 11, s, h, hkv, dh)
+    kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+    pg = PackedLinear.from_dense(w, DEV)
+    ws, tk = ops.sk_workspace(e, m, n, k, DEV)
+    qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
+    e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
+               torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, ws, 1e-5, 4, tk)
+    _close(qg, q, 2e-2, 2e-2)
+    _close(kg, kc, 2e-2, 2e-2)
+    _close(vg, vc, 2e-2, 2e-2)

@@ -75,11 +75,18 @@ def main():
                 for ks in args.ksplit:
                   for tile in args.tile:
                     kk = ks or e.gemm_ksplit(m, n, k)
-                    ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
+                    tk = None
+                    if tile == 4:  # stream-K tail plan (no K split)
+                        kk = 1
+                        ws, tk = ops.sk_workspace(e, m, n, k, DEV)
+                        if ws is None:
+                            continue
+                    else:
+                        ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
 
-                    def run(i, kk=kk, ws=ws, tile=tile):
-                        e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk, ws if kk > 1 else None,
-                               -1.0, tile)
+                    def run(i, kk=kk, ws=ws, tile=tile, tk=tk):
+                        e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk,
+                               ws if (kk > 1 or tile == 4) else None, -1.0, tile, tk)
                     res[f"v{impl}_ks{kk}_t{tile}" + (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                     run(0)
                     got = out.float()

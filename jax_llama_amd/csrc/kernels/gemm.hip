@@ -14,6 +14,8 @@
 // fixed order (deterministic) and runs the epilogue: store bf16/fp32, residual add (+ bf16 mirror),
 // SiLU(gate)*up over the interleaved [w1;w3] tiles, or RoPE + KV-cache write for the fused qkv
 // projection (reference ops: model.py:210/294/338/736, :58-92, :169-199, :392/:398).
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -198,8 +200,16 @@ JLA_DEV void g2_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn)
 // LDS-DMA issue + the A/B fragments of m-tiles 0..MT/2-1] -> 16 MFMAs, then [the other half of the issue +
 // the remaining A fragments + the vmcnt wait for tile t+1] -> 16 MFMAs -- so the partner group's MFMA
 // phase hides a shorter load phase (cdna_hip_programming.md T3+T4: the per-phase interleave is the lever).
+// FA (full-line A; 256 x 256 ping-pong only): x is staged in 8-row x 128-B pieces that cover a PAIR of
+// K-tiles (lane l of a piece loads row l>>3, 16-B chunk (l&7) ^ swz(row)), instead of 16-row x 64-B
+// fragment-shaped loads: half the cache lines per LDS-DMA instruction, so half the TA work for x
+// (cdna_hip_programming.md §5 "x through LDS in full 128-B lines"). The LDS image [row][8 chunks] is
+// XOR-swizzled (swz = (row & 15) >> 1) so the A-fragment ds_read_b128s stay conflict-free under the
+// gfx950 b128 lane groups. x pairs live in a 3-slot ring (96 KiB), weights in the usual 4-slot K-tile
+// ring (64 KiB); pair p is issued in two halves with K-tiles 2p-4 and 2p-3 (4 LDS-DMA per wave per
+// K-tile, as before), so the vmcnt accounting stays "everything issued two K-tiles back has landed".
 template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4,
-          int SUB = 1>
+          int SUB = 1, bool FA = false>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
@@ -211,7 +221,11 @@ __global__ void __launch_bounds__(256 * WM)
   constexpr int G = FR / NW;                                   // LDS-DMA loads per wave per K-tile
   static_assert(FR % NW == 0, "fragment split");
   constexpr int DIST = NBUF - 1;
-  __shared__ u32x4 lds[NBUF * FR * 64];
+  constexpr int A_SLOTS = 3, A_PIECES = BM / 8, A_RING = FA ? A_SLOTS * A_PIECES * 64 : 0;
+  static_assert(!FA || (WM == 2 && MT == 8 && NTW == 4 && SUB == 1 && NBUF == 4 && BF == 2 * NW),
+                "FA: 256 x 256 ping-pong, 2 weight fragments per wave per K-tile");
+  __shared__ u32x4 lds[FA ? A_RING + NBUF * BF * 64 : NBUF * FR * 64];
+  u32x4* const bring = lds + A_RING;  // FA: the weight ring follows the x ring
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int wr = w >> 2, wc = w & 3;
@@ -258,6 +272,50 @@ __global__ void __launch_bounds__(256 * WM)
 #pragma unroll
     for (int j = h * (G / 2); j < (h + 1) * (G / 2); ++j) glds16(src[j] + (size_t)t * step[j], buf + (w + NW * j) * 64);
   };
+  // FA sources, saddr form: one wave-uniform 64-bit base per operand (advanced by scalar adds) plus a
+  // 32-bit per-lane byte offset within the tile (< 15 MB for every Llama shape). x piece 16h + wu + 8j
+  // of a K-tile pair (h = issue half, a compile-time constant at every call), weight fragments wu + 8j.
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const char* const baseA = reinterpret_cast<const char*>(x + (size_t)m0 * K + (size_t)ks0 * 32);
+  const char* const baseB = reinterpret_cast<const char*>(W + ((size_t)(n0 >> 4) * KS + ks0) * 64);
+  unsigned offA[2][2], offAt[2][2], offB[2];
+  if constexpr (FA) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int P = 16 * h + wu + 8 * j;
+        const int row = min(m0 + 8 * P + (lane >> 3), M - 1) - m0;
+        const int c = (lane & 7) ^ ((P & 1) * 4 + (lane >> 4));  // the chunk stored at cell lane & 7
+        offA[h][j] = (unsigned)row * (unsigned)K * 2u + 16u * (unsigned)c;
+        // a pair whose second K-tile is past this split's range: re-read the first K-tile into the
+        // unused cells (never past the end of a row)
+        offAt[h][j] = offA[h][j] - (c >= 4 ? 64u : 0u);
+      }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = min((n0 >> 4) + wu + NW * j, NTT - 1) - (n0 >> 4);
+      offB[j] = (unsigned)nt * (unsigned)KS * 1024u + 16u * (unsigned)lane;
+    }
+  }
+  auto issueA = [&](int p, auto HC) {  // x pair p (K-tiles 2p, 2p+1), half HC of its pieces
+    constexpr int h = decltype(HC)::value;
+    u32x4* buf = lds + (p % A_SLOTS) * A_PIECES * 64;
+    const char* base = baseA + (size_t)p * 128;
+    if (2 * p + 1 >= KT) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) glds16(base + offAt[h][j], buf + (16 * h + wu + 8 * j) * 64);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) glds16(base + offA[h][j], buf + (16 * h + wu + 8 * j) * 64);
+    }
+  };
+  auto issueB = [&](int t) {
+    u32x4* buf = bring + (t % NBUF) * BF * 64;
+    const char* base = baseB + (size_t)t * 1024;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(base + offB[j], buf + (wu + NW * j) * 64);
+  };
 
   f32x4 acc[MT][NTW];
 #pragma unroll
@@ -278,9 +336,21 @@ __global__ void __launch_bounds__(256 * WM)
     }
   };
 
+  if constexpr (FA) {
 #pragma unroll
-  for (int t = 0; t < DIST; ++t)
-    if (t < KT) issue(t);
+    for (int p = 0; p < 2; ++p)
+      if (2 * p < KT) {
+        issueA(p, std::integral_constant<int, 0>{});
+        issueA(p, std::integral_constant<int, 1>{});
+      }
+#pragma unroll
+    for (int t = 0; t < DIST; ++t)
+      if (t < KT) issueB(t);
+  } else {
+#pragma unroll
+    for (int t = 0; t < DIST; ++t)
+      if (t < KT) issue(t);
+  }
 
   if constexpr (WM == 2) {
     // Ping-pong: wave rows 0 and 1 (one wave of each per SIMD) run one barrier apart, so while
@@ -366,6 +436,64 @@ __global__ void __launch_bounds__(256 * WM)
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+      }
+    } else if constexpr (FA) {
+      // FA main loop, unrolled by K-tile pairs so each step's x issue half (and its LDS read chunk) is a
+      // compile-time constant. Same phase/barrier structure as the loop below.
+      // vmcnt: every load of K-tile t+1 (its weights and both halves of its x pair) was issued at K-tile
+      // t-2 or earlier (or in the drained prologue); this wave's issues of K-tiles t-1 and t may stay in
+      // flight: 2 weight + 2 x loads per K-tile while there is something left to issue.
+      auto fa_cnt = [&](int s) {
+        return s < 0 ? 0 : (s + DIST < KT ? 2 : 0) + (2 * ((s >> 1) + 2) < KT ? 2 : 0);
+      };
+      auto fa_step = [&](int t, auto HC) {
+        constexpr int h = decltype(HC)::value;  // == t & 1
+        if (t + DIST < KT) issueB(t + DIST);
+        if (2 * ((t >> 1) + 2) < KT) issueA((t >> 1) + 2, HC);
+        // row r of the tile, chunk c of its 64-deep pair sits at u32x4 r * 8 + (c ^ ((r & 15) >> 1))
+        const u32x4* abuf = lds + ((t >> 1) % A_SLOTS) * A_PIECES * 64;
+        const u32x4* bbuf = bring + (t % NBUF) * BF * 64;
+        const int ab = (wr * MT * 16 + (lane & 15)) * 8 + ((4 * h + (lane >> 4)) ^ ((lane >> 1) & 7));
+        u32x4 a[MT], b[NTW];
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) b[j] = bbuf[(wc * NTW + j) * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a[i] = abuf[ab + i * 128];
+        if constexpr (RMS) {
+          const u32x4 f0 = abuf[ab + RPW * wc * 128];
+          ss0 = dot8_bf16(f0, f0, ss0);
+          if constexpr (RPW == 2) {
+            const u32x4 f1 = abuf[ab + (RPW * wc + 1) * 128];
+            ss1 = dot8_bf16(f1, f1, ss1);
+          }
+        }
+        const int n = fa_cnt(t - 1) + fa_cnt(t);
+        if (n >= 8)
+          wait_vmcnt<8>();
+        else if (n >= 6)
+          wait_vmcnt<6>();
+        else if (n >= 4)
+          wait_vmcnt<4>();
+        else if (n >= 2)
+          wait_vmcnt<2>();
+        else
+          wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      };
+      for (int t = 0; t < KT; t += 2) {
+        fa_step(t, std::integral_constant<int, 0>{});
+        if (t + 1 < KT) fa_step(t + 1, std::integral_constant<int, 1>{});
       }
     } else
     for (int t = 0; t < KT; ++t) {
@@ -976,12 +1104,14 @@ __global__ void __launch_bounds__(256)
 static int g_gemm_impl = 2;
 // gemm2 pipeline variant (A/B): 0 = 4 LDS buffers, wait before the reads; 1 = 4 buffers, wait after
 // the reads; 2 = 5 buffers (all 160 KiB of LDS at WM = 2, one more tile in flight), wait after;
-// 3 = SUB = 2 half phases
-static int g_g2_var = 1;
+// 3 = SUB = 2 half phases; 5 = full-line x staging (FA, the default: 6-21 % faster than 1 at M = 2048/4096
+// on every Llama-3-8B projection, bit-identical -- profiles/r1_gemm2_fullline_x_ab.jsonl)
+static int g_g2_var = 5;
 void gemm_set_impl(int impl) {
   g_gemm_impl = impl == 1 ? 1 : 2;
-  // 2/4 = default (late wait), 3 = early wait, 5 = 5 buffers, 6 = two half phases per K-tile (SUB = 2)
-  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 5 ? 2 : (impl == 6 ? 3 : 1));
+  // 2/8 = default (FA), 4 = fragment-shaped x (late wait), 3 = early wait, 5 = 5 buffers,
+  // 6 = two half phases per K-tile (SUB = 2)
+  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 4 ? 1 : (impl == 5 ? 2 : (impl == 6 ? 3 : 5)));
 }
 int gemm_get_impl() { return g_gemm_impl; }
 
@@ -1032,6 +1162,9 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
       x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq)
 #define JLA_G2(WMV, NB, LATE, R, MTV, NTV) JLA_G2S(WMV, NB, LATE, R, MTV, NTV, 1)
+#define JLA_G2FA(R)                                                                                       \
+  gemm2_kernel<MODE, 2, 4, true, R, 8, 4, 1, true><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, \
+                                                                       mirror, kc, tm, tn, rms_eps, ssq)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   if constexpr (MODE != MODE_RESIDUAL) {
     if (rms) {  // fused RMSNorm statistic (default pipeline variant only)
@@ -1041,6 +1174,8 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
         JLA_G2(2, 4, true, true, 4, 2);
       else if (g_g2_var == 3)
         JLA_G2S(2, 4, true, true, 8, 4, 2);
+      else if (g_g2_var == 5)
+        JLA_G2FA(true);
       else
         JLA_G2(2, 4, true, true, 8, 4);
       return;
@@ -1056,8 +1191,11 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     JLA_G2(2, 5, true, false, 8, 4);
   else if (g_g2_var == 3)
     JLA_G2S(2, 4, true, false, 8, 4, 2);
+  else if (g_g2_var == 5)
+    JLA_G2FA(false);
   else
     JLA_G2(2, 4, false, false, 8, 4);
+#undef JLA_G2FA
 #undef JLA_G2
 #undef JLA_G2S
 }

@@ -40,7 +40,7 @@ int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, 
 // 128x128-tile MFMA GEMM (gemm.hip). ksplit > 1 splits K over gridDim.z into fp32 partials
 // (ws >= gemm_workspace_floats) reduced in fixed order by an epilogue kernel; MODE_QKV needs ksplit > 1.
 int gemm_ksplit(int M, int N, int K);
-void gemm_set_impl(int impl);  // 2 = gemm2 (default), 1 = 128x128 v1 (A/B measurements)
+void gemm_set_impl(int impl);  // 2 = gemm2 (default, full-line x), 4 = gemm2 fragment-shaped x, 1 = 128x128 v1 (A/B)
 int gemm_get_impl();
 size_t gemm_workspace_floats(int M, int N, int K);
 // rms_eps >= 0: x is the UNscaled activation and each output row is scaled by rsqrt(mean(x^2) + eps)

@@ -401,6 +401,48 @@ def test_gemm_tile_configs(tile, ks, m):
     torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("m,k,ks", [(300, 1024, 1), (512, 1056, 1), (256, 992, 3), (700, 4096, 2)])
+def test_gemm_full_line_x(m, k, ks):
+    """gemm2 with x staged in full 128-B lines (the default, impl 2: K-tile pairs, swizzled LDS image) is
+    bit-identical to the fragment-shaped x pipeline (impl 4; same per-accumulator MFMA order) for every epilogue, with and without the
+    fused RMSNorm, including an odd K-tile count (half-used last pair) and split-K ranges that start and
+    end mid-pair; and matches the fp32 reference."""
+    e = ops.ext()
+    n = 768
+    x = torch.randn(m, k).to(BF16)
+    w, pg, _ = _mk_linear(n, k)
+    xg = x.to(DEV)
+    ws = torch.empty(ks * m * (n + 1), dtype=torch.float32, device=DEV) if ks > 1 else None
+    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+    gp = PackedLinear.from_dense(gu, DEV)
+    h0 = torch.randn(m, n).to(DEV)
+
+    def run():
+        outs = []
+        for eps in (-1.0, 1e-5):
+            o = torch.empty(m, n, dtype=torch.float32, device=DEV)
+            e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, 1)
+            o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, 1)
+            outs += [o, o2]
+        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, 1)
+        return outs + [hg, mir]
+
+    try:
+        e.gemm_set_impl(4)
+        base = run()
+        e.gemm_set_impl(2)
+        got = run()
+    finally:
+        e.gemm_set_impl(2)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(base, got)):
+        assert torch.equal(a, b), f"output {i} differs between the full-line-x and the fragment-shaped-x pipeline"
+    _close(got[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+    _close(got[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+
+
 @pytest.mark.parametrize("cus,m", [(0, 768), (0, 1000), (16, 200), (16, 512)])
 def test_gemm_stream_k_tail(cus, m):
     """256x256 tiles with a stream-K tail (tile config 4): every epilogue, with and without the fused

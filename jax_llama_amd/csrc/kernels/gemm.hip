@@ -209,7 +209,7 @@ JLA_DEV void g2_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn)
 // ring (64 KiB); pair p is issued in two halves with K-tiles 2p-4 and 2p-3 (4 LDS-DMA per wave per
 // K-tile, as before), so the vmcnt accounting stays "everything issued two K-tiles back has landed".
 template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4,
-          int SUB = 1, bool FA = false>
+          int SUB = 1, bool FA = false, int FAM = 0>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
@@ -298,23 +298,21 @@ __global__ void __launch_bounds__(256 * WM)
       offB[j] = (unsigned)nt * (unsigned)KS * 1024u + 16u * (unsigned)lane;
     }
   }
-  auto issueA = [&](int p, auto HC) {  // x pair p (K-tiles 2p, 2p+1), half HC of its pieces
+  auto issueA1 = [&](int p, auto HC, int j) {  // x pair p (K-tiles 2p, 2p+1), half HC of its pieces
     constexpr int h = decltype(HC)::value;
-    u32x4* buf = lds + (p % A_SLOTS) * A_PIECES * 64;
-    const char* base = baseA + (size_t)p * 128;
-    if (2 * p + 1 >= KT) {
+    glds16(baseA + (size_t)p * 128 + (2 * p + 1 >= KT ? offAt[h][j] : offA[h][j]),
+           lds + (p % A_SLOTS) * A_PIECES * 64 + (16 * h + wu + 8 * j) * 64);
+  };
+  auto issueA = [&](int p, auto HC) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(base + offAt[h][j], buf + (16 * h + wu + 8 * j) * 64);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(base + offA[h][j], buf + (16 * h + wu + 8 * j) * 64);
-    }
+    for (int j = 0; j < 2; ++j) issueA1(p, HC, j);
+  };
+  auto issueB1 = [&](int t, int j) {
+    glds16(baseB + (size_t)t * 1024 + offB[j], bring + (t % NBUF) * BF * 64 + (wu + NW * j) * 64);
   };
   auto issueB = [&](int t) {
-    u32x4* buf = bring + (t % NBUF) * BF * 64;
-    const char* base = baseB + (size_t)t * 1024;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(base + offB[j], buf + (wu + NW * j) * 64);
+    for (int j = 0; j < 2; ++j) issueB1(t, j);
   };
 
   f32x4 acc[MT][NTW];
@@ -443,13 +441,34 @@ __global__ void __launch_bounds__(256 * WM)
       // vmcnt: every load of K-tile t+1 (its weights and both halves of its x pair) was issued at K-tile
       // t-2 or earlier (or in the drained prologue); this wave's issues of K-tiles t-1 and t may stay in
       // flight: 2 weight + 2 x loads per K-tile while there is something left to issue.
-      auto fa_cnt = [&](int s) {
-        return s < 0 ? 0 : (s + DIST < KT ? 2 : 0) + (2 * ((s >> 1) + 2) < KT ? 2 : 0);
+      // FAM (0..4): that many of a K-tile's 4 loads (weights first, then x) are issued from its M phase,
+      // spread between the MFMAs, instead of at the head of its L phase (the stamps put the L phase --
+      // issue + reads + wait -- above the M phase); at the wait of K-tile t only the L-phase part of
+      // K-tile t's loads has been issued.
+      constexpr int MB = FAM < 2 ? FAM : 2, MA = FAM - MB;  // moved weight / x loads
+      auto fa_cnt = [&](int s, bool l_only) {
+        return s < 0 ? 0
+                     : (s + DIST < KT ? (l_only ? 2 - MB : 2) : 0) +
+                           (2 * ((s >> 1) + 2) < KT ? (l_only ? 2 - MA : 2) : 0);
       };
       auto fa_step = [&](int t, auto HC) {
         constexpr int h = decltype(HC)::value;  // == t & 1
-        if (t + DIST < KT) issueB(t + DIST);
-        if (2 * ((t >> 1) + 2) < KT) issueA((t >> 1) + 2, HC);
+#ifdef JLA_GEMM_STAMPS
+        unsigned long long t0, t1;
+        JLA_STAMP(t0)
+#endif
+        const bool more_b = t + DIST < KT, more_a = 2 * ((t >> 1) + 2) < KT;
+        if (more_b) {
+#pragma unroll
+          for (int j = 0; j < 2 - MB; ++j) issueB1(t + DIST, j);
+        }
+        if (more_a) {
+#pragma unroll
+          for (int j = 0; j < 2 - MA; ++j) issueA1((t >> 1) + 2, HC, j);
+        }
+#ifdef JLA_GEMM_STAMPS
+        JLA_STAMP(t1) st_iss += t1 - t0; t0 = t1;
+#endif
         // row r of the tile, chunk c of its 64-deep pair sits at u32x4 r * 8 + (c ^ ((r & 15) >> 1))
         const u32x4* abuf = lds + ((t >> 1) % A_SLOTS) * A_PIECES * 64;
         const u32x4* bbuf = bring + (t % NBUF) * BF * 64;
@@ -467,29 +486,74 @@ __global__ void __launch_bounds__(256 * WM)
             ss1 = dot8_bf16(f1, f1, ss1);
           }
         }
-        const int n = fa_cnt(t - 1) + fa_cnt(t);
-        if (n >= 8)
-          wait_vmcnt<8>();
-        else if (n >= 6)
-          wait_vmcnt<6>();
-        else if (n >= 4)
-          wait_vmcnt<4>();
-        else if (n >= 2)
-          wait_vmcnt<2>();
-        else
-          wait_vmcnt<0>();
+#ifdef JLA_GEMM_STAMPS
+        JLA_STAMP(t1) st_lds += t1 - t0; t0 = t1;
+#endif
+        if (t >= 1 && t + 4 < KT) {  // steady state: K-tiles t-1 and t issued 2 + 2 loads (t: its L part)
+          wait_vmcnt<8 - FAM>();
+        } else {
+          const int n = fa_cnt(t - 1, false) + fa_cnt(t, true);
+          if (n >= 8)
+            wait_vmcnt<8>();
+          else if (n == 7)
+            wait_vmcnt<7>();
+          else if (n == 6)
+            wait_vmcnt<6>();
+          else if (n == 5)
+            wait_vmcnt<5>();
+          else if (n == 4)
+            wait_vmcnt<4>();
+          else if (n == 3)
+            wait_vmcnt<3>();
+          else if (n == 2)
+            wait_vmcnt<2>();
+          else if (n == 1)
+            wait_vmcnt<1>();
+          else
+            wait_vmcnt<0>();
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+        JLA_STAMP(t1) st_l += t1 - t0; t0 = t1;
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+        JLA_STAMP(t1) st_b1 += t1 - t0; t0 = t1;
+#endif
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MT; ++i) {
 #pragma unroll
           for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
+          // moved load m (0..FAM-1) goes after m-tile (2m + 1) * MT / (2 FAM): weights j = 2-MB.., then x
+#pragma unroll
+          for (int m = 0; m < FAM; ++m) {
+            if (i == (2 * m + 1) * MT / (2 * FAM)) {
+              if (m < MB) {
+                if (more_b) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  issueB1(t + DIST, 2 - MB + m);
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+              } else if (more_a) {
+                __builtin_amdgcn_sched_barrier(0);
+                issueA1((t >> 1) + 2, HC, 2 - MA + (m - MB));
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+          }
+        }
         __builtin_amdgcn_s_setprio(0);
         asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+        JLA_STAMP(t1) st_m += t1 - t0; t0 = t1;
+#endif
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+#ifdef JLA_GEMM_STAMPS
+        JLA_STAMP(t1) st_b2 += t1 - t0;
+#endif
       };
       for (int t = 0; t < KT; t += 2) {
         fa_step(t, std::integral_constant<int, 0>{});
@@ -1111,7 +1175,10 @@ void gemm_set_impl(int impl) {
   g_gemm_impl = impl == 1 ? 1 : 2;
   // 2/8 = default (FA), 4 = fragment-shaped x (late wait), 3 = early wait, 5 = 5 buffers,
   // 6 = two half phases per K-tile (SUB = 2)
-  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 4 ? 1 : (impl == 5 ? 2 : (impl == 6 ? 3 : 5)));
+  // The default FA issues each K-tile's 2 weight loads from the M phase, between the MFMAs (FAM = 2); 9 = FA with all 4 issued at the head of the L phase (FAM = 0). FAM = 2 was
+  // 1-8 % faster than FAM = 0 on 15 of 20 Llama-3-8B projection shapes, FAM = 3 / 4 slower
+  // (profiles/r1_gemm2_fam_ab.jsonl).
+  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 4 ? 1 : (impl == 5 ? 2 : (impl == 6 ? 3 : (impl == 9 ? 6 : 5))));
 }
 int gemm_get_impl() { return g_gemm_impl; }
 
@@ -1162,9 +1229,9 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
       x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq)
 #define JLA_G2(WMV, NB, LATE, R, MTV, NTV) JLA_G2S(WMV, NB, LATE, R, MTV, NTV, 1)
-#define JLA_G2FA(R)                                                                                       \
-  gemm2_kernel<MODE, 2, 4, true, R, 8, 4, 1, true><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, \
-                                                                       mirror, kc, tm, tn, rms_eps, ssq)
+#define JLA_G2FA(R, FM)                                                                                      \
+  gemm2_kernel<MODE, 2, 4, true, R, 8, 4, 1, true, FM><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate,     \
+                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   if constexpr (MODE != MODE_RESIDUAL) {
     if (rms) {  // fused RMSNorm statistic (default pipeline variant only)
@@ -1175,7 +1242,9 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
       else if (g_g2_var == 3)
         JLA_G2S(2, 4, true, true, 8, 4, 2);
       else if (g_g2_var == 5)
-        JLA_G2FA(true);
+        JLA_G2FA(true, 2);
+      else if (g_g2_var == 6)
+        JLA_G2FA(true, 0);
       else
         JLA_G2(2, 4, true, true, 8, 4);
       return;
@@ -1192,7 +1261,9 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   else if (g_g2_var == 3)
     JLA_G2S(2, 4, true, false, 8, 4, 2);
   else if (g_g2_var == 5)
-    JLA_G2FA(false);
+    JLA_G2FA(false, 2);
+  else if (g_g2_var == 6)
+    JLA_G2FA(false, 0);
   else
     JLA_G2(2, 4, false, false, 8, 4);
 #undef JLA_G2FA

@@ -432,13 +432,17 @@ def test_gemm_full_line_x(m, k, ks):
     try:
         e.gemm_set_impl(4)
         base = run()
-        e.gemm_set_impl(2)
-        got = run()
+        variants = {}
+        for impl in (2, 9):  # default FA (weight loads issued between the MFMAs); FA with all loads up front
+            e.gemm_set_impl(impl)
+            variants[impl] = run()
     finally:
         e.gemm_set_impl(2)
     torch.cuda.synchronize()
-    for i, (a, b) in enumerate(zip(base, got)):
-        assert torch.equal(a, b), f"output {i} differs between the full-line-x and the fragment-shaped-x pipeline"
+    for impl, got in variants.items():
+        for i, (a, b) in enumerate(zip(base, got)):
+            assert torch.equal(a, b), f"impl {impl}: output {i} differs from the fragment-shaped-x pipeline"
+    got = variants[2]
     _close(got[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
     _close(got[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
 

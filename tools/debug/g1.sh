@@ -1,0 +1,6 @@
+#!/bin/bash
+# GPU round trip: the whole -m gpu suite, then the default bench (each step under its own time limit)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_gpu_all.log 2>&1 && \
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.log 2>&1

@@ -357,6 +357,26 @@ void argmax(Tensor logits, Tensor idx, Tensor val) {
      "argmax");
 }
 
+// Greedy lm_head: tiled GEMM (fused RMS when rms_eps >= 0) with the argmax in its epilogue; the fp32
+// logits are never written. ws: fp32 >= gemm_argmax_workspace(m, n) floats.
+void gemm_argmax(Tensor x, Tensor w, int64_t n, int64_t k, Tensor ws, double rms_eps, Tensor idx, Tensor val) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
+  const int64_t m = x.size(0);
+  check_gpu(ws, "ws");
+  check(ws.scalar_type() == torch::kFloat32 && (size_t)ws.numel() >= jla::gemm_argmax_workspace_floats(m, n),
+        "gemm_argmax ws too small");
+  check_gpu(idx, "idx");
+  check_gpu(val, "val");
+  check(idx.scalar_type() == torch::kInt32 && val.scalar_type() == torch::kFloat32 && idx.numel() == m &&
+            val.numel() == m,
+        "gemm_argmax outputs");
+  rc(jla::gemm_argmax(cbf(x), w.data_ptr(), ptr<float>(ws), ws.numel(), m, n, k, (float)rms_eps, ptr<int32_t>(idx),
+                      ptr<float>(val), stream()),
+     "gemm_argmax");
+}
+
 // stage 1 of the sampler: per-4096-chunk top-K candidates (global indices = local + idx_offset)
 void topk_chunk(Tensor logits, int64_t k, int64_t idx_offset, Tensor cv, Tensor ci) {
   for (auto* t : {&logits, &cv, &ci}) check_gpu(*t, "topk_chunk arg");
@@ -493,6 +513,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"), py::arg("h"),
         py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("ksplit"), py::arg("ws"), py::arg("rms_eps") = -1.0,
         py::arg("tile") = 0, py::arg("tickets") = py::none());
+  m.def("gemm_argmax", &gemm_argmax, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("ws"),
+        py::arg("rms_eps"), py::arg("idx"), py::arg("val"));
+  m.def("gemm_argmax_workspace", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_argmax_workspace_floats(m, n); });
   m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });

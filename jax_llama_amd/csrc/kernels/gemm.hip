@@ -27,6 +27,7 @@ constexpr int G_THREADS = 256;
 constexpr int G_AFR = 16, G_BFR = 16;
 constexpr int G_STAGE_U4 = (G_AFR + G_BFR) * 64;  // u32x4 per stage (32 KiB); 8 per thread
 constexpr int MODE_PARTIAL = 7;                   // split-K: fp32 partial tile to the workspace
+constexpr int MODE_ARGMAX = 8;                    // greedy lm_head: per-(row, 64 columns) first-max partials
 
 template <int MODE>
 __global__ void __launch_bounds__(G_THREADS)
@@ -707,6 +708,40 @@ __global__ void __launch_bounds__(256 * WM)
           if (row < M) o[(size_t)row * F + col] = f2bf(silu(acc[i][j][r]) * acc[i][j + 1][r]);
         }
     }
+  } else if constexpr (MODE == MODE_ARGMAX) {
+    // greedy lm_head: the logits never leave the registers. Per row, the first maximum over this
+    // wave's 64 columns (lane: its 4 columns in ascending order, strict >; then the 16 lanes of the
+    // row, ties to the smaller index) -> one (value, index) partial at [row][n0 / 64 + wc] of `out`;
+    // argmax_partials_kernel finishes the row (same result as argmax over the stored fp32 logits).
+    float2* o = static_cast<float2*>(out);
+    const int P = tiles_n * (BN / (16 * NTW)), slot = (n0 >> 6) + wc;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int tile = (n0 >> 4) + wc * NTW + j;
+          const float v = acc[i][j][r];
+          if (tile < NTT && v > bv) {
+            bv = v;
+            bi = tile * 16 + c;
+          }
+        }
+#pragma unroll
+        for (int sh = 1; sh < 16; sh <<= 1) {
+          const float ov = __shfl_xor(bv, sh, 64);
+          const int oi = __shfl_xor(bi, sh, 64);
+          if (ov > bv || (ov == bv && oi < bi)) {
+            bv = ov;
+            bi = oi;
+          }
+        }
+        const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
+        if (c == 0 && row < M) o[(size_t)row * P + slot] = make_float2(bv, __int_as_float(bi));
+      }
   } else {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
@@ -1445,6 +1480,61 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
       break;
     default: return -1;
   }
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- greedy lm_head: GEMM with the argmax in its epilogue (no fp32 logits round trip through HBM:
+// at M = 2048, V = 128256 that is 1 GB written + 1 GB read per decode step), then one wave per row
+// reduces the [M][P] partials. Ties go to the smaller index, so the result equals argmax_kernel's.
+__global__ void __launch_bounds__(256)
+    argmax_partials_kernel(const float2* __restrict__ part, int P, int M, int32_t* __restrict__ idx,
+                           float* __restrict__ val) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int k = lane; k < P; k += 64) {
+    const float2 e = part[(size_t)row * P + k];
+    const int ei = __float_as_int(e.y);
+    if (e.x > bv || (e.x == bv && ei < bi)) {
+      bv = e.x;
+      bi = ei;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    idx[row] = bi == 0x7fffffff ? 0 : bi;
+    val[row] = bv;
+  }
+}
+
+size_t gemm_argmax_workspace_floats(int M, int N) { return (size_t)M * ((N + G2_BN - 1) / G2_BN) * 4 * 2; }
+
+int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
+                int32_t* idx, float* val, hipStream_t s) {
+  if (M <= 0) return 0;
+  if ((N & 15) || (K & 31)) return -1;
+  if (g_gemm_impl != 2) return -1;
+  if (ws == nullptr || ws_floats < gemm_argmax_workspace_floats(M, N)) return -3;
+  const int tm = (M + 255) / 256, tn = (N + G2_BN - 1) / G2_BN;
+  const u32x4* w = static_cast<const u32x4*>(W);
+  if (rms_eps >= 0.f)
+    gemm2_kernel<MODE_ARGMAX, 2, 4, true, true, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr);
+  else
+    gemm2_kernel<MODE_ARGMAX, 2, 4, true, false, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr);
+  JLA_CHECK_LAUNCH();
+  argmax_partials_kernel<<<(M + 3) / 4, 256, 0, s>>>(reinterpret_cast<const float2*>(ws), tn * 4, M, idx, val);
   JLA_CHECK_LAUNCH();
   return 0;
 }

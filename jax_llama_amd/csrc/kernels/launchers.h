@@ -51,6 +51,10 @@ size_t gemm_workspace_floats(int M, int N, int K);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0);
+// greedy lm_head: GEMM + first-max argmax epilogue (ws >= gemm_argmax_workspace_floats(M, N) floats)
+int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
+                int32_t* idx, float* val, hipStream_t s);
+size_t gemm_argmax_workspace_floats(int M, int N);
 size_t gemm_sk_workspace_floats();
 int gemm_sk_tickets(int M, int N, int K);
 int gemm_sk_active(int M, int N, int K);

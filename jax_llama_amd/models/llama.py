@@ -265,7 +265,8 @@ class LLaMAForCausalLM:
 
         ``slot0``: int or device int32[1] tensor (graph capture). Returns
         ``(logits_local, h, hidden_states, attentions)`` where logits are this rank's
-        vocab shard: ``[B, V/tp]`` ("last"), ``[B*S, V/tp]`` ("all") or None ("none")."""
+        vocab shard: ``[B, V/tp]`` ("last"), ``[B*S, V/tp]`` ("all"), None ("none"), or the
+        shard's greedy ``(idx int32[B], val fp32[B])`` of the last position ("argmax")."""
         b, s = ids.shape
         d = self.config.hidden_size
         # residual stream: fp32 h plus its bf16 mirror hb (the A operand of every projection
@@ -276,6 +277,8 @@ class LLaMAForCausalLM:
                                     output_hidden_states=collect_hidden, output_attentions=collect_attn)
         if logits_mode == "none":
             logits = None
+        elif logits_mode == "argmax":  # greedy: (idx, val) of this rank's vocab shard, argmax fused in the GEMM
+            logits = ops.linear_argmax(hb.reshape(b, s, d)[:, -1].contiguous(), self.lm_head, rms_eps=self.eps)
         else:
             hl = hb if logits_mode == "all" else hb.reshape(b, s, d)[:, -1].contiguous()
             logits = ops.linear(hl, self.lm_head, rms_eps=self.eps, out_dtype=torch.float32)

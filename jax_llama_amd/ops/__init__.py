@@ -342,6 +342,28 @@ def argmax(logits: torch.Tensor):
     return idx, val
 
 
+ARGMAX_FUSED_MIN_M = 256  # one 256-row tile or more: the tiled GEMM is the lm_head kernel anyway
+
+
+def linear_argmax(x: torch.Tensor, w, rms_eps: Optional[float] = None):
+    """Greedy token of ``[inv_rms(x) *] x @ W^T`` (the lm_head): ``(idx int32[M], val fp32[M])``, first
+    max like ``jnp.argmax``. From ARGMAX_FUSED_MIN_M rows on the GPU the argmax runs in the GEMM
+    epilogue (``gemm_argmax``: the fp32 logits never reach HBM); otherwise ``linear`` + ``argmax``."""
+    m = x.shape[0]
+    if not _is_gpu(x) or m < ARGMAX_FUSED_MIN_M:
+        return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
+    e = ext()
+    if e.gemm_get_impl() != 2:
+        return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
+    assert x.is_contiguous() and x.shape[1] == w.k, (x.shape, w.k)
+    xb = x if x.dtype == BF16 else x.to(BF16)
+    ws = workspace.get("gemm_argmax", e.gemm_argmax_workspace(m, w.n), torch.float32, x.device)
+    idx = torch.empty(m, dtype=torch.int32, device=x.device)
+    val = torch.empty(m, dtype=torch.float32, device=x.device)
+    e.gemm_argmax(xb, w.weight, w.n, w.k, ws, -1.0 if rms_eps is None else float(rms_eps), idx, val)
+    return idx, val
+
+
 SAMPLER_MAX_K = 64
 
 

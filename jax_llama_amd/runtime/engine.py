@@ -51,6 +51,10 @@ class GenerationConfig:
     seed: int = 0
 
 
+# greedy decoding takes the argmax inside the lm_head GEMM epilogue (JLA_FUSED_ARGMAX=0: logits + argmax)
+FUSED_GREEDY = os.environ.get("JLA_FUSED_ARGMAX", "1") != "0"
+
+
 @dataclass
 class GenerateOutput:
     sequences: torch.Tensor
@@ -59,12 +63,17 @@ class GenerateOutput:
 # --------------------------------------------------------------------------------------
 # Sampling
 # --------------------------------------------------------------------------------------
-def _greedy(model, logits_local: torch.Tensor) -> torch.Tensor:
-    idx, val = ops.argmax(logits_local)
+def _greedy(model, logits_local) -> torch.Tensor:
+    """``logits_local``: this rank's ``[B, V/tp]`` logits, or its already reduced ``(idx, val)``
+    (``forward_tokens(logits_mode="argmax")``: argmax fused into the lm_head GEMM)."""
+    if isinstance(logits_local, tuple):
+        (idx, val), v_local = logits_local, model.vocab_local
+    else:
+        (idx, val), v_local = ops.argmax(logits_local), logits_local.shape[1]
     comm = model.comm
     if comm.size == 1:
         return idx
-    idx = idx + comm.rank * logits_local.shape[1]
+    idx = idx + comm.rank * v_local
     vals = comm.all_gather(val)  # [tp, B]
     idxs = comm.all_gather(idx)
     best = vals.argmax(0)  # first max in rank order == smallest global index among ties
@@ -167,9 +176,12 @@ class DecodeEngine:
         self.cache.index_t.add_(1)
         self.cur_len.add_(1)
 
+    def _logits_mode(self) -> str:
+        return "argmax" if FUSED_GREEDY and not self.gc.do_sample else "last"
+
     def _decode_step(self):
         logits, *_ = self.model.forward_tokens(self.tokens, self.positions, self.cache, self.cache.index_t,
-                                               self.kv_start, self.key_mask, logits_mode="last")
+                                               self.kv_start, self.key_mask, logits_mode=self._logits_mode())
         self._update(self._next_token(logits))
 
     # ---------------------------------------------------------------------------------
@@ -195,7 +207,7 @@ class DecodeEngine:
         self.finished.zero_()
         pos_dev = positions.to(dev)
         logits, *_ = model.forward_tokens(ids, pos_dev, self.cache, 0, self.kv_start, self.key_mask,
-                                          logits_mode="last")
+                                          logits_mode=self._logits_mode())
         self.cache.advance(s)
         # state for the loop body: cur_len = S (also the sampler's Philox step), token/pos of the
         # last prompt position

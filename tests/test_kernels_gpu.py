@@ -447,6 +447,44 @@ def test_gemm_full_line_x(m, k, ks):
     _close(got[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 1008, 512), (300, 4096, 1024), (700, 2560, 992)])
+def test_gemm_argmax_fused(m, n, k):
+    """Greedy lm_head with the argmax in the GEMM epilogue (gemm_argmax) returns exactly what the stored
+    fp32 logits + argmax_kernel return (index AND value, with and without the fused RMSNorm), including
+    a partial last column tile (n % 256 != 0), a partial row tile, and planted exact ties (first index
+    wins, across lanes, waves and workgroups)."""
+    e = ops.ext()
+    x = torch.randn(m, k).to(BF16)
+    w, pg, _ = _mk_linear(n, k)
+    # ties: 4 scaled-up rows of W, each repeated at another column (same logits bit for bit), so most
+    # row maxima are exact ties -- within a lane group (17/18), across waves (63/64) and workgroups
+    wt = w.clone()
+    for src, dst in ((3, 700 % n), (17, 18), (n - 300, n - 1), (64, 63)):
+        wt[src] = (w[src].float() * 8).to(BF16)
+        wt[dst] = wt[src]
+    pg = PackedLinear.from_dense(wt, DEV)
+    xg = x.to(DEV)
+    for eps in (-1.0, 1e-5):
+        logits = torch.empty(m, n, dtype=torch.float32, device=DEV)
+        e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, 1)
+        i0 = torch.empty(m, dtype=torch.int32, device=DEV)
+        v0 = torch.empty(m, dtype=torch.float32, device=DEV)
+        e.argmax(logits, i0, v0)
+        ws = torch.empty(e.gemm_argmax_workspace(m, n), dtype=torch.float32, device=DEV)
+        i1 = torch.empty_like(i0)
+        v1 = torch.empty_like(v0)
+        e.gemm_argmax(xg, pg.weight, n, k, ws, eps, i1, v1)
+        torch.cuda.synchronize()
+        assert torch.equal(i0.cpu(), i1.cpu()), (eps, (i0 != i1).nonzero()[:8])
+        assert torch.equal(v0.cpu(), v1.cpu())
+        r = ref.linear(x, wt, None if eps < 0 else eps, torch.float32)
+        agree = (r.argmax(-1).to(torch.int32) == i1.cpu()).float().mean().item()
+        assert agree > 0.97, agree  # bf16 rounding may flip near-ties against the fp32 reference
+    # the op-level API picks the fused path from ARGMAX_FUSED_MIN_M rows on
+    idx, val = ops.linear_argmax(xg, pg, 1e-5)
+    assert torch.equal(idx.cpu(), i1.cpu()) and torch.equal(val.cpu(), v1.cpu())
+
+
 @pytest.mark.parametrize("cus,m", [(0, 768), (0, 1000), (16, 200), (16, 512)])
 def test_gemm_stream_k_tail(cus, m):
     """256x256 tiles with a stream-K tail (tile config 4): every epilogue, with and without the fused

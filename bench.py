@@ -11,6 +11,15 @@ Multi-GPU (torchrun, one process per GPU, RCCL): the world is split into ``world
 data-parallel replicas of a ``tp``-way tensor-parallel model (default tp = 1: each GPU serves its
 own batch -> weak scaling). ``value`` = total output tokens of all replicas / max-over-ranks time.
 
+Extra keys (outside the timed region, reported alongside the headline):
+  * ``latency_points``: decode ms/token at B = 1/8/32/64 (BASELINE.md protocol: prompt 128, cache for
+    256 generated tokens, hipGraph replay, prefill excluded);
+  * ``sampled``: tokens/s of whole ``generate`` calls in the reference's default sampling mode
+    (temperature 0.8, top-p 0.95, top-k 50: jax_example.py:33, generation.py:22,34) at the headline batch;
+  * ``tp_points`` (world > 1): the second half of the metric, Llama-3-70B tensor-parallel over every
+    GPU of the job (MP = world, README.md:52-53): decode ms/token at B = 1/32/256 through the custom
+    xGMI collectives, under a watchdog so a stuck collective can never cost the headline line.
+
   python bench.py --gpus 1 --steps 3 --warmup 1
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --model llama3-70b --tp 8
 """
@@ -20,6 +29,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,13 +45,16 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
     # Serving-throughput operating point: 2048 concurrent sequences per replica (KV cache 103 GB of the
-    # 288 GB HBM; ~44 ms per decode step = ~22 tokens/s per sequence; 35.1k tok/s vs 33.5k at 1024 and
-    # 33.6k at 1536 -- profiles/README.md). Smaller batches are latency points (decode_ms_per_token):
-    # --batch 1 / 16 / 512 / 1024.
+    # 288 GB HBM; ~41 ms per decode step); latency points are reported separately.
     ap.add_argument("--batch", type=int, default=2048, help="sequences per replica")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count (INVALID for the metric)")
+    ap.add_argument("--latency-batches", type=int, nargs="*", default=[1, 8, 32, 64])
+    ap.add_argument("--no-sampled", action="store_true", help="skip the sampling-mode throughput point")
+    ap.add_argument("--tp-model", default="llama3-70b", help="model of the tensor-parallel points (world > 1)")
+    ap.add_argument("--tp-batches", type=int, nargs="*", default=[1, 32, 256])
+    ap.add_argument("--tp-timeout", type=float, default=420.0, help="watchdog (s) of the tensor-parallel points")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
 
@@ -50,7 +63,10 @@ def main():
 
     from jax_llama_amd.config import get_preset
     from jax_llama_amd.models import LLaMAForCausalLM
+    from jax_llama_amd.ops import autotune
     from jax_llama_amd.parallel import TPComm, init_distributed
+    from jax_llama_amd.runtime import engine as eng_mod
+    from jax_llama_amd.runtime.benchmark import decode_latency, generate_tokens_per_sec
     from jax_llama_amd.runtime.engine import GenerationConfig, get_engine
 
     ctx = init_distributed()
@@ -63,7 +79,7 @@ def main():
     overrides = {} if args.layers is None else {"num_hidden_layers": args.layers}
     max_len = args.prompt_len + args.gen_len
     cfg = get_preset(args.model, max_seq_len=max(2048, max_len), **overrides)
-    model = LLaMAForCausalLM(cfg, device=dev, comm=comm).init_random(seed=1234)
+    model = LLaMAForCausalLM(cfg, device=dev, comm=comm, _do_init=False).init_random(seed=1234)
     torch.cuda.synchronize(dev)
 
     gen = torch.Generator().manual_seed(100 + ctx.dp_rank)
@@ -86,7 +102,7 @@ def main():
     ctx.barrier()
     torch.cuda.synchronize(dev)
 
-    # decode-only timing (prefill excluded) on the already-captured engine: one extra run
+    # time to first token on the already-captured engine (prefill + first sampled token)
     eng = get_engine(model, args.batch, max_len)
     torch.cuda.synchronize(dev)
     tp0 = time.perf_counter()
@@ -127,21 +143,105 @@ def main():
         "decode_tokens_per_sec": round(replicas * args.batch * 1000.0 / decode_ms_per_token, 2),
         "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
         "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
-        "decode_kernel_choice": {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}": v
-                                 for k, v in __import__("jax_llama_amd.ops.autotune", fromlist=["x"]).table().items()},
-        "gemm_plan_choice": {f"m{k[0]}_n{k[1]}_k{k[2]}": f"ks{v[0]}_tile{v[1]}" for k, v in
-                             __import__("jax_llama_amd.ops.autotune", fromlist=["x"]).ksplit_table().items()},
     }
+    del out
+    eng_mod._ENGINES.clear()  # free the headline batch's KV cache before the extra points
+    torch.cuda.empty_cache()
+
+    # ---- latency points (same model, BASELINE.md protocol)
+    lat = []
+    for b in args.latency_batches:
+        lat.append(decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=7, barrier=ctx.barrier))
+    for p in lat:  # the slowest rank's number
+        p["decode_ms_per_token"] = ctx.all_reduce_max([p["decode_ms_per_token"]])[0]
+        p["decode_tokens_per_sec"] = round(p["batch"] * 1000.0 / p["decode_ms_per_token"], 2)
+    res["latency_points"] = {"model": args.model, "mp": args.tp, "prompt_len": args.prompt_len,
+                             "cache_len": max_len, "points": lat}
+    eng_mod._ENGINES.clear()
+    torch.cuda.empty_cache()
+
+    # ---- sampling mode at the headline batch (reference default: T 0.8, top-p 0.95, top-k 50)
+    if not args.no_sampled:
+        gcs = GenerationConfig(max_length=max_len, do_sample=True, temperature=0.8, top_p=0.95, top_k=50,
+                               pad_token_id=0, eos_token_id=-1, seed=0)
+        sp = generate_tokens_per_sec(model, args.batch, args.prompt_len, args.gen_len, gcs, seed=8,
+                                     barrier=ctx.barrier)
+        dt = ctx.all_reduce_max([sp["ms_per_generate"]])[0]
+        res["sampled"] = {"temperature": 0.8, "top_p": 0.95, "top_k": 50, "batch_per_replica": args.batch,
+                          "ms_per_generate": dt,
+                          "tokens_per_sec": round(replicas * args.batch * args.gen_len * 1000.0 / dt, 2)}
+        eng_mod._ENGINES.clear()
+        torch.cuda.empty_cache()
+    res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}": f"ks{v[0]}_tile{v[1]}"
+                               for k, v in autotune.ksplit_table().items()}
+
+    # ---- tensor-parallel points: 70B over every GPU of the job (world > 1), under a watchdog
+    if world > 1 and args.tp == 1 and args.tp_model and args.tp_batches:
+        del model
+        torch.cuda.empty_cache()
+        res["tp_points"] = _tp_points(args, ctx, res)
+
     if ctx.rank == 0:
-        line = json.dumps(res)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
+        _emit(res, args.json_out)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    del out
+
+
+def _emit(res, json_out):
+    line = json.dumps(res)
+    print(line, flush=True)
+    if json_out:
+        with open(json_out, "w") as f:
+            f.write(line + "\n")
+
+
+def _tp_points(args, ctx, res):
+    """Llama-3-70B at MP = world (one TP group over every GPU). A watchdog thread ends the process
+    with the headline line (and ``tp_points: timeout``) if the phase does not finish in time."""
+    import torch
+
+    from jax_llama_amd.config import get_preset
+    from jax_llama_amd.models import LLaMAForCausalLM
+    from jax_llama_amd.parallel import TPComm
+    from jax_llama_amd.runtime.benchmark import decode_latency
+
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(args.tp_timeout):
+            if ctx.rank == 0:
+                res["tp_points"] = {"status": "timeout", "timeout_s": args.tp_timeout}
+                _emit(res, args.json_out)
+            sys.stdout.flush()
+            os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    world = ctx.world
+    out = {"model": args.tp_model, "mp": world, "prompt_len": args.prompt_len, "cache_len":
+           args.prompt_len + args.gen_len}
+    try:
+        ctx.setup_mesh(tp=world)
+        comm = TPComm.from_context(ctx)
+        out["custom_allreduce"] = comm.custom is not None
+        cfg = get_preset(args.tp_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+        model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm, _do_init=False).init_random(seed=4321)
+        out["weight_gb_per_gpu"] = round(model.weight_bytes() / 1e9, 3)
+        out["hbm_roofline_ms_per_token"] = round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)
+        pts = []
+        for b in args.tp_batches:
+            p = decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=9, barrier=ctx.barrier)
+            p["decode_ms_per_token"] = ctx.all_reduce_max([p["decode_ms_per_token"]])[0]
+            p["decode_tokens_per_sec"] = round(b * 1000.0 / p["decode_ms_per_token"], 2)
+            pts.append(p)
+        out["points"] = pts
+        out["status"] = "ok"
+        del model
+        torch.cuda.empty_cache()
+    except Exception as ex:  # reported, never fatal to the headline line
+        out["status"] = f"error: {type(ex).__name__}: {str(ex)[:300]}"
+    done.set()
+    return out
 
 
 if __name__ == "__main__":

@@ -3,13 +3,14 @@
 
   * ``jax_llama_amd/_C*.so``   — the HIP kernels (``csrc/kernels/*.hip``, hipcc
     ``--offload-arch=gfx950``) + torch bindings (``csrc/bindings.cpp``);
-  * ``jax_llama_amd/_bpe*.so`` — the C++ byte-pair-merge core of the Llama-3 tokenizer;
-  * ``jax_llama_amd/_comm*.so`` — the xGMI custom all-reduce (``csrc/comm/*.hip``), if present.
+  * ``jax_llama_amd/_bpe*.so`` — the C++ byte-pair-merge core of the Llama-3 tokenizer.
+
+The xGMI custom all-reduce (``csrc/kernels/allreduce.hip``) is part of ``_C``.
 
 No hipify, no CUDA, no JIT cache: objects go to ``build/`` (incremental, mtime based) and the
 final ``.so`` files land next to the Python package so they travel with the repo snapshot.
 
-Usage: ``python build.py [-j N] [--force] [--only C|bpe|comm]``
+Usage: ``python build.py [-j N] [--force] [--only C|bpe]``
 """
 from __future__ import annotations
 
@@ -135,41 +136,12 @@ def build_bpe(force: bool) -> Path:
     return out
 
 
-def build_comm(jobs: int, force: bool):
-    cdir = CSRC / "comm"
-    srcs = sorted(cdir.glob("*.hip")) if cdir.exists() else []
-    if not srcs:
-        return None
-    headers = sorted(cdir.glob("*.h")) + sorted((CSRC / "kernels").glob("*.h"))
-    objs = [BUILD / "comm" / (s.stem + ".o") for s in srcs]
-    for s, o in zip(srcs, objs):
-        _compile_hip(s, o, headers, force)
-    bsrc = cdir / "bindings.cpp"
-    tdir, tinc, tlib = _torch_paths()
-    bobj = BUILD / "comm" / "bindings.o"
-    if force or _stale(bobj, [bsrc, *headers]):
-        inc = [f"-I{p}" for p in tinc] + [f"-I{_py_include()}", f"-I{CSRC}"]
-        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
-              "-DTORCH_EXTENSION_NAME=_comm", "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1",
-              "-Wno-deprecated-declarations", *inc, "-c", str(bsrc), "-o", str(bobj)])
-    out = PKG / f"_comm{EXT_SUFFIX}"
-    if force or _stale(out, [*objs, bobj]):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), str(bobj), "-o", str(out),
-              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-              "-lamdhip64", f"-Wl,-rpath,{tlib}"])
-    return out
-
-
 def build_all(jobs: int = 8, force: bool = False, only=None):
     outs = []
     if only in (None, "bpe"):
         outs.append(build_bpe(force))
     if only in (None, "C"):
         outs.append(build_C(jobs, force))
-    if only in (None, "comm"):
-        o = build_comm(jobs, force)
-        if o is not None:
-            outs.append(o)
     return outs
 
 
@@ -177,7 +149,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--only", choices=["C", "bpe", "comm"])
+    ap.add_argument("--only", choices=["C", "bpe"])
     a = ap.parse_args()
     for o in build_all(a.j, a.force, a.only):
         print("built", o.relative_to(ROOT))

@@ -41,7 +41,7 @@ def load(ckpt_dir: str, tokenizer_path: str, is_llama3: bool, max_seq_len: int =
     tokenizer = LLaMA3Tokenizer(tokenizer_path) if is_llama3 else LLaMA2Tokenizer(tokenizer_path)
     params, config = load_meta_rank(ckpt_dir, tokenizer, ctx.tp_rank, ctx.tp_size, max_seq_len=max_seq_len)
     config.bos_token_id, config.eos_token_id = tokenizer.bos_id, tokenizer.eos_id
-    model = LLaMAForCausalLM(config, device=ctx.device, comm=comm, **model_kwargs).load_params(params, sharded=True)
+    model = LLaMAForCausalLM(config, device=ctx.device, comm=comm, _do_init=False, **model_kwargs).load_params(params, sharded=True)
     del params
     return LLaMA(None, model, tokenizer, mesh=Mesh(dp=1, mp=ctx.tp_size, rank=ctx.rank))
 
@@ -65,7 +65,7 @@ def synthetic(model_name: str, batch: int, prompt_len: int, max_gen_len: int, te
     ctx.setup_mesh(tp=ctx.world)
     comm = TPComm.from_context(ctx)
     cfg = get_preset(model_name, max_seq_len=max(2048, prompt_len + max_gen_len))
-    model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm).init_random(seed=0)
+    model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm, _do_init=False).init_random(seed=0)
     toks = torch.randint(3, cfg.vocab_size, (batch, prompt_len), generator=torch.Generator().manual_seed(0),
                          dtype=torch.int32)
     gc = GenerationConfig(max_length=prompt_len + max_gen_len, do_sample=temperature != 0.0,

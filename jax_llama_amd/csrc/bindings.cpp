@@ -458,7 +458,7 @@ py::tuple car_alloc(int64_t max_bytes, int64_t world) {
 }
 
 int64_t car_init(int64_t rank, int64_t world, int64_t max_bytes, int64_t buf, int64_t sig, std::vector<std::string> hbufs,
-                 std::vector<std::string> hsigs) {
+                 std::vector<std::string> hsigs, double timeout_s) {
   check((int64_t)hbufs.size() == world && (int64_t)hsigs.size() == world, "car_init: one handle per rank");
   std::vector<hipIpcMemHandle_t> hb(world), hs(world);
   for (int64_t p = 0; p < world; ++p) {
@@ -469,21 +469,65 @@ int64_t car_init(int64_t rank, int64_t world, int64_t max_bytes, int64_t buf, in
   }
   void* state = nullptr;
   rc(jla::car_init(rank, world, max_bytes, reinterpret_cast<void*>(buf), reinterpret_cast<void*>(sig), hb.data(),
-                   hs.data(), &state),
+                   hs.data(), timeout_s, &state),
      "car_init");
   return (int64_t)(uintptr_t)state;
 }
 
-void car_allreduce(int64_t state, Tensor in, Tensor out) {
+// out = sum over the TP group of in (same dtype, bf16/fp32)
+void car_allreduce(int64_t state, Tensor in, Tensor out, bool two_shot) {
   check_gpu(in, "in");
   check_gpu(out, "out");
   check(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "car_allreduce in/out");
   check(in.scalar_type() == torch::kBFloat16 || in.scalar_type() == torch::kFloat32, "car_allreduce dtype");
   const int64_t nbytes = in.numel() * in.element_size();
   check(nbytes % 16 == 0, "car_allreduce: bytes % 16");
-  rc(jla::car_allreduce(reinterpret_cast<void*>(state), in.data_ptr(), out.data_ptr(), nbytes,
-                        in.scalar_type() == torch::kBFloat16, stream()),
+  rc(jla::car_reduce(reinterpret_cast<void*>(state), 0, in.data_ptr(), out.data_ptr(), nullptr, nullptr, nbytes,
+                     in.scalar_type() == torch::kBFloat16, two_shot, stream()),
      "car_allreduce");
+}
+
+// residual all-reduce of a row-parallel projection: h (fp32) += sum over ranks of partial; hb = bf16(h)
+void car_allreduce_residual(int64_t state, Tensor partial, Tensor h, Tensor hb, bool two_shot) {
+  check_gpu(partial, "partial");
+  check_gpu(h, "h");
+  check_gpu(hb, "hb");
+  check(partial.scalar_type() == torch::kBFloat16 || partial.scalar_type() == torch::kFloat32, "partial dtype");
+  check(h.scalar_type() == torch::kFloat32 && hb.scalar_type() == torch::kBFloat16, "h fp32 / hb bf16");
+  check(h.numel() == partial.numel() && hb.numel() == partial.numel(), "residual shapes");
+  const int64_t nbytes = partial.numel() * partial.element_size();
+  check(nbytes % 16 == 0, "car_allreduce_residual: bytes % 16");
+  rc(jla::car_reduce(reinterpret_cast<void*>(state), 1, partial.data_ptr(), nullptr, ptr<float>(h), bf(hb), nbytes,
+                     partial.scalar_type() == torch::kBFloat16, two_shot, stream()),
+     "car_allreduce_residual");
+}
+
+// (value fp32, index int32) all-gathers of the vocab-parallel sampler. mode 0: out_i[n] = index of the first max over
+// ranks (out_v optional); mode 1: out_v/out_i [n / k, world * k]
+void car_pairs(int64_t state, int64_t mode, Tensor vals, Tensor idx, int64_t idx_offset, int64_t k,
+               c10::optional<Tensor> out_v, Tensor out_i) {
+  check_gpu(vals, "vals");
+  check_gpu(idx, "idx");
+  check_gpu(out_i, "out_i");
+  check(vals.scalar_type() == torch::kFloat32 && idx.scalar_type() == torch::kInt32 &&
+            out_i.scalar_type() == torch::kInt32 && vals.numel() == idx.numel(),
+        "car_pairs dtypes");
+  const int64_t n = vals.numel();
+  auto* st = reinterpret_cast<void*>(state);
+  float* ov = nullptr;
+  if (out_v.has_value()) {
+    check_gpu(*out_v, "out_v");
+    check(out_v->scalar_type() == torch::kFloat32 && out_v->numel() == out_i.numel(), "out_v");
+    ov = ptr<float>(*out_v);
+  }
+  if (mode == 0) {
+    check(out_i.numel() == n, "car_pairs argmax out shape");
+  } else {
+    check(mode == 1 && ov && k > 0 && n % k == 0 && out_i.numel() == n * jla::car_world(st), "car_pairs top-k shapes");
+  }
+  rc(jla::car_pairs(st, (int)mode, ptr<float>(vals), ptr<int32_t>(idx), (int)idx_offset, n, (int)k, ov,
+                    ptr<int32_t>(out_i), stream()),
+     "car_pairs");
 }
 
 }  // namespace
@@ -535,7 +579,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("topk_chunks", [](int64_t v) { return jla::topk_chunks(v); });
   m.def("car_alloc", &car_alloc);
   m.def("car_init", &car_init);
-  m.def("car_allreduce", &car_allreduce);
+  m.def("car_allreduce", &car_allreduce, py::arg("state"), py::arg("inp"), py::arg("out"), py::arg("two_shot") = false);
+  m.def("car_allreduce_residual", &car_allreduce_residual, py::arg("state"), py::arg("partial"), py::arg("h"),
+        py::arg("hb"), py::arg("two_shot") = false);
+  m.def("car_pairs", &car_pairs, py::arg("state"), py::arg("mode"), py::arg("vals"), py::arg("idx"),
+        py::arg("idx_offset"), py::arg("k"), py::arg("out_v").none(true), py::arg("out_i"));
   m.def("car_error", [](int64_t st) { return jla::car_error(reinterpret_cast<void*>(st)); });
   m.def("car_destroy", [](int64_t st) { jla::car_destroy(reinterpret_cast<void*>(st)); });
   m.def("topk_chunk", &topk_chunk);

@@ -1,120 +1,293 @@
-// One-shot push all-reduce over xGMI for decode-sized tensor-parallel messages (SURVEY D1 / X1-X2:
-// the row-parallel wo / w2 outputs, 2 per layer per token; reference partition.py:67,70 where XLA's
-// GSPMD inserts the NCCL all-reduce).
+// Custom xGMI collectives for decode-sized tensor-parallel messages (the
+// row-parallel wo / w2 outputs, 2 per layer per token, and the vocab-parallel sampler gathers;
+// reference partition.py:67,70,77 where XLA's GSPMD inserts the NCCL collectives).
 //
-// Every rank owns one uncached (MTYPE UC, hipDeviceMallocUncached) receive buffer
-// [2 parities][world slots][max_bytes] and a signal array [64 blocks][world], both exported by
-// IPC handle and mapped by every peer. A call:
-//   1. block b copies its byte-chunks of the local input into slot `rank` of EVERY rank's buffer
-//      (remote stores go straight over the rank<->peer xGMI link; uncached, so they land in the
-//      peer's HBM), drains them (s_waitcnt vmcnt(0)), then writes its epoch into flag[b][rank] of
-//      every peer;
-//   2. waits until flag[b][p] >= epoch for every peer p (bounded spin: a missing peer sets the
-//      error word instead of hanging the GPU);
-//   3. sums slots 0..world-1 IN RANK ORDER from its local buffer -> bit-identical result on
-//      every rank.
-// Chunks map to blocks by byte offset (chunk c -> block c % 63) on every call and every rank, and
-// epochs are per block, so block b of rank r only ever pairs with block b of its peers; the parity
-// buffers make one barrier per call enough: block b overwrites a parity slot two calls later, and
-// by then it has seen every peer's block b signal the call in between (after that peer's reads).
-// Graph-capturable: all state (pointers, epochs) lives in device memory.
+// Memory: every rank owns ONE uncached allocation, exported by IPC handle and mapped by every peer:
+//   [A: 2 parities][world slots][max_bytes]     scatter / one-shot receive slots
+//   [R: 2 parities][2 * max_bytes]              two-shot fp32 result region
+// plus a small uncached signal allocation: flags [CAR_BLOCKS][CAR_MAX_WORLD], then per-block barrier
+// and call counters and the error word (local use only).
+//
+// Coherence protocol (independent of the MTYPE the importing GPU maps the peer memory with):
+//   * every byte handed to a peer is stored with sc0 sc1 (system-scope write-through) and every byte
+//     handed over is loaded with sc0 sc1 (system scope, bypasses the non-coherent caches);
+//   * producer: payload stores -> each wave s_waitcnt vmcnt(0) -> __syncthreads -> one lane per peer
+//     stores the flag (relaxed, system scope = sc0 sc1 store);
+//   * consumer: one lane per peer polls its flag (relaxed system-scope load, bounded by a wall-clock
+//     timeout that raises the error word instead of hanging), __syncthreads, then the payload loads.
+//   No release/acquire fences: the L2 write-back a system-scope release needs is both slow and subject
+//   to a known compiler hazard (the vmcnt wait after buffer_wbl2 can be dropped).
+//
+// Block b of every rank handles chunks c == b (mod CAR_GRID) of every message, so block b only ever
+// pairs with block b of its peers; barriers count per block and flags are monotonic. The parity
+// buffers make one barrier per round enough: a parity slot is overwritten two calls later, and by then
+// the writer has passed a barrier that every peer reached after finishing its reads of that slot.
+// Graph-capturable: all state (pointers, counters) lives in device memory.
+//
+// Kernels
+//   car_reduce_kernel<OP, TWO_SHOT>   sum of every rank's [n] input (bf16 or fp32, fp32 accumulation
+//       in rank order -> bit-identical on every rank and between one-shot and two-shot):
+//         OP_SUM    out = sum
+//         OP_RESID  h (fp32) += sum; hb (bf16) = h     (the residual add + bf16 mirror of the decode
+//                   step, fused: the row-parallel GEMM writes only its partial)
+//       one-shot: push the input into slot `rank` of every peer, barrier, sum the local slots;
+//       two-shot (reduce-scatter + all-gather): chunk c is owned by rank c % world; push it to the
+//       owner only, barrier, the owner sums and pushes the fp32 sum to every rank, barrier, apply OP.
+//   car_pairs_kernel<MODE>    all-gather of (fp32 value, int32 index) pairs (8-byte granules):
+//         MODE_ARGMAX  per row the first max in rank order (vocab-parallel greedy token)
+//         MODE_TOPK    per-rank top-k candidates laid out [B][world * k] for the final merge/sample
 #include "common.h"
 #include "launchers.h"
 
 namespace jla {
 
 constexpr int CAR_MAX_WORLD = 8;
-constexpr int CAR_BLOCKS = 64;   // signal rows; blocks 0..62 carry data, word 63 of the tail = error
+constexpr int CAR_BLOCKS = 64;   // signal rows (one per block)
 constexpr int CAR_GRID = 63;     // chunk c -> block c % CAR_GRID on every call (fixed mapping)
 constexpr int CAR_THREADS = 256;
-constexpr int CAR_CHUNK = CAR_THREADS * 16;  // bytes per block iteration
+constexpr int CAR_CHUNK = CAR_THREADS * 16;  // input bytes per block iteration
+constexpr int CAR_PAIR_CHUNK = CAR_THREADS;  // pairs per block iteration
+
+enum { OP_SUM = 0, OP_RESID = 1 };
+enum { PAIRS_ARGMAX = 0, PAIRS_TOPK = 1 };
 
 struct CarDevice {
-  char* buf[CAR_MAX_WORLD];     // every rank's receive buffer, mapped here
-  int* sig[CAR_MAX_WORLD];      // every rank's signal array [CAR_BLOCKS][CAR_MAX_WORLD]
-  int* epoch;                   // this rank's per-block epochs [CAR_BLOCKS] (local)
-  int* error;                   // set to 1 when a spin times out
-  long long max_bytes;
+  char* buf[CAR_MAX_WORLD];     // every rank's buffer (A then R), mapped here
+  int* sig[CAR_MAX_WORLD];      // every rank's flags [CAR_BLOCKS][CAR_MAX_WORLD]
+  int* barrier_count;           // [CAR_BLOCKS] barriers passed by block b (local)
+  int* call_count;              // [CAR_BLOCKS] calls made by block b (local; parity)
+  int* error;                   // 1 once a wait timed out
+  long long max_bytes;          // A slot size; R holds 2 * max_bytes per parity
+  long long timeout_ticks;      // wall-clock ticks (s_memrealtime, 100 MHz) before giving up
   int rank, world;
 };
 
-JLA_DEV void st_uc(u32x4* p, u32x4 v) { __builtin_nontemporal_store(v, p); }
-JLA_DEV u32x4 ld_uc(const u32x4* p) { return __builtin_nontemporal_load(p); }
+// ---- system-scope (sc0 sc1) vector accesses through buffer resources ---------------------------
+constexpr int SYS = 17;  // cache policy bits: sc0 | sc1
 
-JLA_DEV void add4f(u32x4& acc, const u32x4 v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = __float_as_uint(__uint_as_float(acc[i]) + __uint_as_float(v[i]));
+JLA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+JLA_DEV void st_sys16(__amdgpu_buffer_rsrc_t r, long long off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, SYS);
+}
+JLA_DEV u32x4 ld_sys16(__amdgpu_buffer_rsrc_t r, long long off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, SYS);
+}
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+JLA_DEV void st_sys8(__amdgpu_buffer_rsrc_t r, long long off, u32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, SYS);
+}
+JLA_DEV u32x2 ld_sys8(__amdgpu_buffer_rsrc_t r, long long off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, SYS);
 }
 
-// bf16 messages accumulate the world slots in fp32 and round once.
-__global__ void __launch_bounds__(CAR_THREADS)
-    car_kernel(const char* __restrict__ in, char* __restrict__ out, long long nbytes, int is_bf16,
-               const CarDevice* __restrict__ dev) {
-  const CarDevice& d = *dev;  // by reference: a by-value copy indexed with runtime p lives in scratch
-  const int b = blockIdx.x;
-  const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
-  if (b >= nchunks) return;
-  __shared__ int s_epoch;
+// Start of a call for block b: bump the call counter (parity) once per call.
+JLA_DEV int car_begin(const CarDevice& d, int b, int* s_word) {
   if (threadIdx.x == 0) {
-    const int e = d.epoch[b] + 1;
-    d.epoch[b] = e;
-    s_epoch = e;
+    const int c = d.call_count[b] + 1;
+    d.call_count[b] = c;
+    *s_word = c;
   }
   __syncthreads();
-  const int e = s_epoch;
-  const int parity = e & 1;
-  const long long slot_bytes = d.max_bytes;
-  const long long par_off = (long long)parity * d.world * slot_bytes;
+  return *s_word & 1;
+}
 
-  // 1. push local input into slot `rank` of every rank's buffer
-  for (long long c = b; c < nchunks; c += CAR_GRID) {
-    const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
-    if (off < nbytes) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(in + off);
-      for (int p = 0; p < d.world; ++p)
-        st_uc(reinterpret_cast<u32x4*>(d.buf[p] + par_off + (long long)d.rank * slot_bytes + off), v);
-    }
-  }
+// Barrier of block b with block b of every peer. Every wave of the block must have issued its
+// hand-off stores before calling.
+JLA_DEV void car_barrier(const CarDevice& d, int b, int* s_word) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) *s_word = d.barrier_count[b] + 1;
+  __syncthreads();
+  const int e = *s_word;
   if (threadIdx.x < d.world) {
-    int* f = d.sig[threadIdx.x] + b * CAR_MAX_WORLD + d.rank;
-    __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // 2. wait for every peer's block b
-  if (threadIdx.x < d.world) {
+    __hip_atomic_store(d.sig[threadIdx.x] + b * CAR_MAX_WORLD + d.rank, e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     const int* f = d.sig[d.rank] + b * CAR_MAX_WORLD + threadIdx.x;
-    int it = 0;
+    const long long t0 = (long long)wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      if (++it > (1 << 24)) {
+      if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
         __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
     }
   }
-  asm volatile("" ::: "memory");
   __syncthreads();
-  // 3. sum the slots in rank order (identical on every rank)
-  const char* mine = d.buf[d.rank] + par_off;
+  if (threadIdx.x == 0) d.barrier_count[b] = e;
+}
+
+// fp32 values of one 16-byte input piece (8 bf16 or 4 fp32)
+template <bool BF16>
+struct Piece {
+  static constexpr int N = BF16 ? 8 : 4;
+  float v[N];
+  JLA_DEV void set(const u32x4 x) {
+    if constexpr (BF16) {
+      unpack8(x, v);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(x[i]);
+    }
+  }
+  JLA_DEV void add(const u32x4 x) {
+    Piece<BF16> t;
+    t.set(x);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += t.v[i];
+  }
+};
+
+// Apply the op to element range [e0, e0 + N) given the fp32 sum
+template <int OP, bool BF16>
+JLA_DEV void car_epilogue(const float* sum, long long e0, void* out, float* h, bf16_t* hb) {
+  constexpr int N = BF16 ? 8 : 4;
+  if constexpr (OP == OP_SUM) {
+    if constexpr (BF16) {
+      *reinterpret_cast<u32x4*>(static_cast<bf16_t*>(out) + e0) = pack8(sum);
+    } else {
+      *reinterpret_cast<f32x4*>(static_cast<float*>(out) + e0) = f32x4{sum[0], sum[1], sum[2], sum[3]};
+    }
+  } else {
+    float r[N];
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+      f32x4 hv = *reinterpret_cast<const f32x4*>(h + e0 + 4 * q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[4 * q + i] = hv[i] + sum[4 * q + i];
+        hv[i] = r[4 * q + i];
+      }
+      *reinterpret_cast<f32x4*>(h + e0 + 4 * q) = hv;
+    }
+    if constexpr (BF16) {
+      *reinterpret_cast<u32x4*>(hb + e0) = pack8(r);
+    } else {
+      u32x2 p;
+      p[0] = pack2bf(r[0], r[1]);
+      p[1] = pack2bf(r[2], r[3]);
+      *reinterpret_cast<u32x2*>(hb + e0) = p;
+    }
+  }
+}
+
+template <int OP, bool BF16, bool TWO_SHOT>
+__global__ void __launch_bounds__(CAR_THREADS)
+    car_reduce_kernel(const char* __restrict__ in, void* __restrict__ out, float* __restrict__ h,
+                      bf16_t* __restrict__ hb, long long nbytes, const CarDevice* __restrict__ dev) {
+  const CarDevice& d = *dev;  // by reference: a by-value copy indexed with runtime p lives in scratch
+  constexpr int ESZ = BF16 ? 2 : 4;
+  constexpr int N = 16 / ESZ;
+  const int b = blockIdx.x;
+  const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
+  if (b >= nchunks) return;
+  __shared__ int s_word;
+  const int parity = car_begin(d, b, &s_word);
+  const long long slot = d.max_bytes;
+  const long long a_off = (long long)parity * d.world * slot;
+  const long long r_off = 2 * (long long)d.world * slot + (long long)parity * 2 * slot;
+  const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
+
+  // 1. push this rank's input: to every peer (one-shot) or to the chunk's owner (two-shot)
   for (long long c = b; c < nchunks; c += CAR_GRID) {
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
-    if (is_bf16) {
-      float acc[8];
-      unpack8(ld_uc(reinterpret_cast<const u32x4*>(mine + off)), acc);
-      for (int p = 1; p < d.world; ++p) {
-        float f[8];
-        unpack8(ld_uc(reinterpret_cast<const u32x4*>(mine + (long long)p * slot_bytes + off)), f);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] += f[i];
-      }
-      *reinterpret_cast<u32x4*>(out + off) = pack8(acc);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(in + off);
+    if (TWO_SHOT) {
+      const int o = (int)(c % d.world);
+      st_sys16(rsrc(d.buf[o]), a_off + (long long)d.rank * slot + off, v);
     } else {
-      u32x4 acc = ld_uc(reinterpret_cast<const u32x4*>(mine + off));
-      for (int p = 1; p < d.world; ++p)
-        add4f(acc, ld_uc(reinterpret_cast<const u32x4*>(mine + (long long)p * slot_bytes + off)));
-      *reinterpret_cast<u32x4*>(out + off) = acc;
+      for (int p = 0; p < d.world; ++p) st_sys16(rsrc(d.buf[p]), a_off + (long long)d.rank * slot + off, v);
+    }
+  }
+  car_barrier(d, b, &s_word);
+
+  if (!TWO_SHOT) {
+    // 2. sum the slots in rank order, apply the op
+    for (long long c = b; c < nchunks; c += CAR_GRID) {
+      const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
+      if (off >= nbytes) continue;
+      Piece<BF16> acc;
+      acc.set(ld_sys16(mine, a_off + off));
+      for (int p = 1; p < d.world; ++p) acc.add(ld_sys16(mine, a_off + (long long)p * slot + off));
+      car_epilogue<OP, BF16>(acc.v, off / ESZ, out, h, hb);
+    }
+    return;
+  }
+  // 2. owner: sum its chunks in rank order, push the fp32 sum to every rank's R region
+  for (long long c = b; c < nchunks; c += CAR_GRID) {
+    if ((int)(c % d.world) != d.rank) continue;
+    const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
+    if (off >= nbytes) continue;
+    Piece<BF16> acc;
+    acc.set(ld_sys16(mine, a_off + off));
+    for (int p = 1; p < d.world; ++p) acc.add(ld_sys16(mine, a_off + (long long)p * slot + off));
+    const long long roff = r_off + (off / ESZ) * 4;  // fp32 result of element off / ESZ
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+      const u32x4 v = {__float_as_uint(acc.v[4 * q]), __float_as_uint(acc.v[4 * q + 1]),
+                       __float_as_uint(acc.v[4 * q + 2]), __float_as_uint(acc.v[4 * q + 3])};
+      for (int p = 0; p < d.world; ++p) st_sys16(rsrc(d.buf[p]), roff + 16 * q, v);
+    }
+  }
+  car_barrier(d, b, &s_word);
+  // 3. every rank: apply the op to every chunk from the gathered sums
+  for (long long c = b; c < nchunks; c += CAR_GRID) {
+    const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
+    if (off >= nbytes) continue;
+    const long long roff = r_off + (off / ESZ) * 4;
+    float s[N];
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+      const u32x4 v = ld_sys16(mine, roff + 16 * q);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[4 * q + i] = __uint_as_float(v[i]);
+    }
+    car_epilogue<OP, BF16>(s, off / ESZ, out, h, hb);
+  }
+}
+
+// (value, index) pairs: granule i = (a[i], b[i] + idx_offset)
+template <int MODE>
+__global__ void __launch_bounds__(CAR_THREADS)
+    car_pairs_kernel(const float* __restrict__ a, const int32_t* __restrict__ bi, int idx_offset, long long n, int k,
+                     float* __restrict__ out_a, int32_t* __restrict__ out_b, const CarDevice* __restrict__ dev) {
+  const CarDevice& d = *dev;
+  const int blk = blockIdx.x;
+  const long long nchunks = (n + CAR_PAIR_CHUNK - 1) / CAR_PAIR_CHUNK;
+  if (blk >= nchunks) return;
+  __shared__ int s_word;
+  const int parity = car_begin(d, blk, &s_word);
+  const long long slot = d.max_bytes;
+  const long long a_off = (long long)parity * d.world * slot;
+  const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
+  for (long long c = blk; c < nchunks; c += CAR_GRID) {
+    const long long i = c * CAR_PAIR_CHUNK + threadIdx.x;
+    if (i >= n) continue;
+    const u32x2 v = {__float_as_uint(a[i]), (unsigned)(bi[i] + idx_offset)};
+    for (int p = 0; p < d.world; ++p) st_sys8(rsrc(d.buf[p]), a_off + (long long)d.rank * slot + i * 8, v);
+  }
+  car_barrier(d, blk, &s_word);
+  for (long long c = blk; c < nchunks; c += CAR_GRID) {
+    const long long i = c * CAR_PAIR_CHUNK + threadIdx.x;
+    if (i >= n) continue;
+    if (MODE == PAIRS_ARGMAX) {
+      u32x2 best = ld_sys8(mine, a_off + i * 8);
+      for (int p = 1; p < d.world; ++p) {
+        const u32x2 v = ld_sys8(mine, a_off + (long long)p * slot + i * 8);
+        if (__uint_as_float(v[0]) > __uint_as_float(best[0])) best = v;  // first max in rank order
+      }
+      if (out_a) out_a[i] = __uint_as_float(best[0]);
+      out_b[i] = (int32_t)best[1];
+    } else {
+      const long long row = i / k, j = i - row * k;
+      for (int p = 0; p < d.world; ++p) {
+        const u32x2 v = ld_sys8(mine, a_off + (long long)p * slot + i * 8);
+        const long long o = row * (long long)d.world * k + (long long)p * k + j;
+        out_a[o] = __uint_as_float(v[0]);
+        out_b[o] = (int32_t)v[1];
+      }
     }
   }
 }
@@ -129,12 +302,15 @@ struct CarHost {
   int n_opened;
 };
 
-size_t car_buffer_bytes(long long max_bytes, int world) { return (size_t)2 * world * max_bytes; }
-size_t car_signal_bytes() { return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 256; }
+size_t car_buffer_bytes(long long max_bytes, int world) {
+  return (size_t)2 * world * max_bytes + (size_t)2 * 2 * max_bytes;
+}
+size_t car_signal_bytes() { return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 1024; }
 
 int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemHandle_t* hbuf,
               hipIpcMemHandle_t* hsig) {
   if (world < 1 || world > CAR_MAX_WORLD || max_bytes <= 0 || (max_bytes & 15)) return -1;
+  if (car_buffer_bytes(max_bytes, world) >= 0x7fffffffull) return -3;  // buffer-resource offsets are 31-bit
   hipError_t e = hipExtMallocWithFlags(buf, car_buffer_bytes(max_bytes, world), hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
   e = hipExtMallocWithFlags(sig, car_signal_bytes(), hipDeviceMallocUncached);
@@ -149,7 +325,7 @@ int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemH
 
 // handles[p] for p != rank are opened; own pointers are used for p == rank
 int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_sig, const hipIpcMemHandle_t* hbufs,
-             const hipIpcMemHandle_t* hsigs, void** state) {
+             const hipIpcMemHandle_t* hsigs, double timeout_s, void** state) {
   if (world < 1 || world > CAR_MAX_WORLD || rank < 0 || rank >= world) return -1;
   CarHost* st = new CarHost();
   st->own_buf = own_buf;
@@ -158,6 +334,11 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   st->h.rank = rank;
   st->h.world = world;
   st->h.max_bytes = max_bytes;
+  int dev = 0, rate_khz = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0)
+    rate_khz = 100000;
+  st->h.timeout_ticks = (long long)(timeout_s * 1000.0 * rate_khz);
   for (int p = 0; p < world; ++p) {
     if (p == rank) {
       st->h.buf[p] = static_cast<char*>(own_buf);
@@ -175,10 +356,11 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
     st->h.buf[p] = static_cast<char*>(pb);
     st->h.sig[p] = static_cast<int*>(ps);
   }
-  // per-block epochs and the error word live after the flags in the local signal allocation
-  char* tail = static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int);
-  st->h.epoch = reinterpret_cast<int*>(tail);       // [CAR_GRID] per-block epochs
-  st->h.error = reinterpret_cast<int*>(tail) + CAR_GRID;
+  // barrier / call counters and the error word live after the flags in the local signal allocation
+  int* tail = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int));
+  st->h.barrier_count = tail;
+  st->h.call_count = tail + CAR_BLOCKS;
+  st->h.error = tail + 2 * CAR_BLOCKS;
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&st->d), sizeof(CarDevice));
   if (e != hipSuccess) return (int)e;
   e = hipMemcpy(st->d, &st->h, sizeof(CarDevice), hipMemcpyHostToDevice);
@@ -187,17 +369,55 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   return 0;
 }
 
-int car_allreduce(void* state, const void* in, void* out, long long nbytes, int is_bf16, hipStream_t s) {
+template <int OP, bool BF16>
+static void launch_reduce(int two_shot, int grid, const void* in, void* out, float* h, bf16_t* hb, long long nbytes,
+                          const CarDevice* d, hipStream_t s) {
+  if (two_shot)
+    car_reduce_kernel<OP, BF16, true><<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), out, h, hb, nbytes, d);
+  else
+    car_reduce_kernel<OP, BF16, false><<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), out, h, hb, nbytes, d);
+}
+
+// op 0: out = sum(in) (same dtype); op 1: h += sum(in), hb = bf16(h) (h fp32, hb bf16, element count of in)
+int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t* hb, long long nbytes, int is_bf16,
+               int two_shot, hipStream_t s) {
   CarHost* st = static_cast<CarHost*>(state);
   if (!st || nbytes <= 0) return nbytes == 0 ? 0 : -1;
   if (nbytes > st->h.max_bytes || (nbytes & 15)) return -2;
+  if (op == OP_RESID && (!h || !hb)) return -1;
+  if (two_shot && st->h.world == 1) two_shot = 0;
   const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
   const int grid = (int)(nchunks < CAR_GRID ? nchunks : CAR_GRID);
-  car_kernel<<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), static_cast<char*>(out), nbytes, is_bf16,
-                                          st->d);
+  if (op == OP_SUM) {
+    if (is_bf16) launch_reduce<OP_SUM, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
+    else launch_reduce<OP_SUM, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
+  } else {
+    if (is_bf16) launch_reduce<OP_RESID, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
+    else launch_reduce<OP_RESID, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
+  }
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+// mode 0 (argmax): out_b[i] = index of the first max over ranks of pair i (out_a: its value, optional)
+// mode 1 (top-k):  n = rows * k; out_a/out_b[row][p * k + j] = rank p's pair (row, j)
+int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_offset, long long n, int k,
+              float* out_a, int32_t* out_b, hipStream_t s) {
+  CarHost* st = static_cast<CarHost*>(state);
+  if (!st || n <= 0) return n == 0 ? 0 : -1;
+  if (n * 8 > st->h.max_bytes) return -2;
+  if (mode == PAIRS_TOPK && (k <= 0 || n % k || !out_a)) return -1;
+  const long long nchunks = (n + CAR_PAIR_CHUNK - 1) / CAR_PAIR_CHUNK;
+  const int grid = (int)(nchunks < CAR_GRID ? nchunks : CAR_GRID);
+  if (mode == PAIRS_ARGMAX)
+    car_pairs_kernel<PAIRS_ARGMAX><<<grid, CAR_THREADS, 0, s>>>(a, b, idx_offset, n, k, out_a, out_b, st->d);
+  else
+    car_pairs_kernel<PAIRS_TOPK><<<grid, CAR_THREADS, 0, s>>>(a, b, idx_offset, n, k, out_a, out_b, st->d);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
+int car_world(void* state) { return static_cast<CarHost*>(state)->h.world; }
 
 int car_error(void* state) {
   CarHost* st = static_cast<CarHost*>(state);

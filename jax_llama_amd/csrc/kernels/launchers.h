@@ -82,13 +82,20 @@ int topk_chunks(int V);
 int topk_chunk(const float* logits, int B, int V, int K, int idx_offset, float* cv, int32_t* ci, hipStream_t s);
 int topk_merge(const float* cv, const int32_t* ci, int B, int C, int K, int mode, float* out_v, int32_t* out_i,
                int32_t* nxt, float temperature, float top_p, uint64_t seed, const int32_t* step, hipStream_t s);
-// one-shot push all-reduce over IPC-mapped uncached buffers (allreduce.hip)
+// custom xGMI collectives over IPC-mapped uncached buffers (allreduce.hip)
 size_t car_buffer_bytes(long long max_bytes, int world);
 int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemHandle_t* hbuf, hipIpcMemHandle_t* hsig);
 int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_sig, const hipIpcMemHandle_t* hbufs,
-             const hipIpcMemHandle_t* hsigs, void** state);
-int car_allreduce(void* state, const void* in, void* out, long long nbytes, int is_bf16, hipStream_t s);
+             const hipIpcMemHandle_t* hsigs, double timeout_s, void** state);
+// op 0: out = sum over ranks of in (bf16/fp32); op 1: h (fp32) += sum, hb (bf16) = h. two_shot: reduce-scatter +
+// all-gather instead of every rank reading every peer's copy
+int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t* hb, long long nbytes, int is_bf16,
+               int two_shot, hipStream_t s);
+// all-gather of (fp32, int32 + idx_offset) pairs: mode 0 = first max over ranks per pair, mode 1 = [n/k][world*k]
+int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_offset, long long n, int k,
+              float* out_a, int32_t* out_b, hipStream_t s);
 int car_error(void* state);
+int car_world(void* state);
 void car_destroy(void* state);
 int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,
                   int32_t* positions, int32_t* slot, int B, int L, int pad, int eos, hipStream_t s);

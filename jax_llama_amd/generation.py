@@ -18,7 +18,7 @@ from typing import Any, List, Optional, Union
 
 import torch
 
-from .parallel.partition import P, Mesh, with_named_sharding_constraint
+from .parallel.partition import P, Mesh, gather_dp, with_named_sharding_constraint
 from .runtime.engine import GenerationConfig
 
 
@@ -47,7 +47,9 @@ class LLaMA:
             seed=seed,
         )
         out = self.model.generate(tokens, attention_mask=attention_mask, generation_config=gc)
-        return with_named_sharding_constraint(out.sequences, self.mesh, P("dp", None))
+        # the reference's output constraint P("dp", None) keeps the batch split across dp replicas;
+        # here every replica gets the whole batch back (all-gather over the dp group when there is one)
+        return gather_dp(out.sequences, self.mesh)
 
     def generate_from_str(self, prompts: List[str], max_gen_len: int, temperature: float = 0.8,
                           top_p: float = 0.95, seed: int = 0) -> List[str]:
@@ -59,10 +61,12 @@ class LLaMA:
             tokens[i, max_prompt - len(t):] = torch.tensor(t, dtype=torch.int32)  # left pad
         attention_mask = (tokens != tok.eos_id).to(torch.int32)
         out_tokens = self.generate(tokens, attention_mask, max_gen_len, temperature, top_p, seed)
+        # rows of this dp replica only when the outputs could not be gathered (no process group)
+        row0 = 0 if out_tokens.shape[0] == len(prompts) else self.mesh.dp_rank * out_tokens.shape[0]
         decoded = []
         for i, t in enumerate(out_tokens.tolist()):
             t = t[t.index(tok.bos_id):]
-            t = t[: len(prompt_tokens[i]) + max_gen_len]
+            t = t[: len(prompt_tokens[row0 + i]) + max_gen_len]
             try:
                 t = t[: t.index(tok.eos_id)]
             except ValueError:

@@ -94,20 +94,41 @@ def mask_to_kv_start(mask: torch.Tensor, device) -> Tuple[torch.Tensor, Optional
     (uint8, on ``device``) for the kernels' general masked path."""
     m = mask.detach().to("cpu").to(torch.int64)
     b, t = m.shape
-    starts = []
-    general = False
-    for row in m.tolist():
-        try:
-            s = row.index(1)
-        except ValueError:
-            s = t
-        if any(v == 0 for v in row[s:]):
-            general = True
-        starts.append(s)
-    kv_start = torch.tensor(starts, dtype=torch.int32, device=device)
-    if general:
+    valid = m != 0
+    first = torch.where(valid.any(1), valid.to(torch.int8).argmax(1), torch.full((b,), t, dtype=torch.int64))
+    after = torch.arange(t)[None, :] >= first[:, None]
+    if bool((after & ~valid).any()):  # a hole after the first valid key: general masked path
         return torch.zeros(b, dtype=torch.int32, device=device), m.to(torch.uint8).to(device).contiguous()
-    return kv_start, None
+    return first.to(torch.int32).to(device), None
+
+
+_DTYPE_NAMES = {"float32": torch.float32, "fp32": torch.float32, "f32": torch.float32,
+                "bfloat16": BF16, "bf16": BF16}
+
+
+def _resolve_dtype(d, default):
+    """torch dtype, a name, or a numpy / jnp-style dtype object (``jnp.float32``) -> torch dtype."""
+    if d is None:
+        return default
+    if isinstance(d, torch.dtype):
+        return d
+    name = d if isinstance(d, str) else getattr(d, "__name__", None) or getattr(d, "name", None) or str(d)
+    name = str(name).split(".")[-1].strip("'>")
+    if name not in _DTYPE_NAMES:
+        raise ValueError(f"unsupported dtype {d!r}")
+    return _DTYPE_NAMES[name]
+
+
+def _resolve_precision(p) -> str:
+    """jax.lax.Precision-like values -> 'default' | 'highest'."""
+    if p is None:
+        return "default"
+    name = str(getattr(p, "name", p)).lower().split(".")[-1]
+    if name in ("default", "fastest", "bfloat16"):
+        return "default"
+    if name in ("highest", "float32", "high", "tensorfloat32"):
+        return "highest"
+    raise ValueError(f"unsupported precision {p!r}")
 
 
 class LLaMAForCausalLM:
@@ -116,10 +137,36 @@ class LLaMAForCausalLM:
     base_model_prefix = "transformer"
     config_class = LLaMAConfig
 
-    def __init__(self, config: LLaMAConfig, device="cpu", comm: Optional[TPComm] = None,
-                 dtype: torch.dtype = BF16, rope_length: Optional[int] = None):
-        if dtype != BF16:
-            raise ValueError("compute dtype is bf16 (fp32 accumulation)")
+    def __init__(self, config: LLaMAConfig, input_shape: Tuple[int, ...] = (1, 1), seed: int = 0, dtype=None,
+                 _do_init: bool = True, precision=None, param_dtype=None, device="cpu",
+                 comm: Optional[TPComm] = None, rope_length: Optional[int] = None, **kwargs):
+        """Reference ``FlaxLLaMAPreTrainedModel.__init__(config, input_shape, seed, dtype, _do_init,
+        **kwargs)`` (``model.py:412-422``) with the module kwargs ``param_dtype`` / ``precision``
+        (``model.py:107-109``; ``jax_test.py:433`` passes ``precision='highest'``).
+
+        * ``_do_init=True`` (HF default): random-initialise the weights (``init_weights(seed)``);
+          ``_do_init=False`` (``jax_example.py:29``): weights come later (``load_params`` / ``params=``).
+        * ``dtype``: dtype of returned activations/logits. The MFMA kernels always run bf16 operands
+          with fp32 accumulation; ``float32`` (the reference default) and ``bfloat16`` are accepted.
+        * ``param_dtype``: storage dtype of the weights — bf16 (the MFMA operand); fp32 is accepted and
+          converted (the reference converts every checkpoint to fp32, ``convert_weights.py:68-88``).
+        * ``precision``: ``None``/``'default'``, or ``'highest'``/``'float32'``, which (as in the
+          reference, where only ``lm_head`` honours it, ``model.py:698``) computes the logits with fp32
+          lm_head weights and an fp32 GEMM."""
+        if kwargs:
+            unknown = sorted(kwargs)
+            raise TypeError(f"unexpected model kwargs {unknown}")
+        self.dtype = _resolve_dtype(dtype, torch.float32)
+        if self.dtype not in (torch.float32, BF16):
+            raise ValueError(f"dtype must be float32 or bfloat16, got {dtype}")
+        pd = _resolve_dtype(param_dtype, BF16)
+        if pd not in (torch.float32, BF16):
+            raise ValueError(f"param_dtype must be float32 or bfloat16, got {param_dtype}")
+        self.param_dtype = BF16  # MFMA operand dtype (fp32 parameters are converted on load)
+        self.precision = _resolve_precision(precision)
+        self.input_shape = tuple(input_shape)
+        self.seed = int(seed)
+        self._missing_keys = set()
         self.config = config
         self.device = torch.device(device)
         self.comm = comm or NO_COMM
@@ -146,6 +193,9 @@ class LLaMAForCausalLM:
         self.layers: List[LayerWeights] = [LayerWeights() for _ in range(c.num_hidden_layers)]
         self.blocks = LLaMABlockCollection(self)  # reference FlaxLLaMABlockCollection (model.py:548)
         self._params_id = None
+        self.lm_head_f32: Optional[torch.Tensor] = None  # [V/tp, D] fp32 (precision='highest')
+        if _do_init:
+            self.init_random(seed=self.seed)
 
     # ------------------------------------------------------------------ weights
     @property
@@ -185,6 +235,7 @@ class LLaMAForCausalLM:
         else:
             lm = _t(params["lm_head"]["kernel"]).t()
         self.lm_head = PackedLinear.from_dense(lm, dev, fold=self.ln_f)
+        self.lm_head_f32 = _t(lm).to(dev, torch.float32).contiguous() if self.precision == "highest" else None
         self._params_id = id(params)
         return self
 
@@ -212,7 +263,38 @@ class LLaMAForCausalLM:
             lw.gu = PackedLinear.random(2 * self.ffn, d, dev, std, gen)
             lw.down = PackedLinear.random(d, self.ffn, dev, std, gen)
         self.lm_head = PackedLinear.random(self.vocab_local, d, dev, std, gen)
+        self.lm_head_f32 = self.lm_head.dense().float().contiguous() if self.precision == "highest" else None
         return self
+
+    def init_weights(self, rng=None, input_shape: Optional[Tuple[int, ...]] = None, params: Optional[Dict] = None,
+                     std: Optional[float] = None) -> Dict:
+        """Reference ``init_weights(rng, input_shape, params=None)`` (``model.py:424-457``): a random
+        parameter tree with the reference names and Flax ``(in, out)`` kernel layout (fp32, host). With
+        ``params`` given, every key it lacks (``self._missing_keys``, or any absent leaf) is filled from
+        the random tree and the completed tree is returned. ``rng``: int seed, torch.Generator or a
+        PRNG-key-like integer array."""
+        from ..parallel.partition import flatten_tree, unflatten_tree
+        from ..utils.checkpoint import meta_state_dict_to_params, random_meta_state_dict
+        if rng is None:
+            seed = self.seed
+        elif isinstance(rng, torch.Generator):
+            seed = int(rng.initial_seed())
+        else:
+            seed = int(np.asarray(rng).reshape(-1)[-1])
+        c = self.config
+        sd = random_meta_state_dict(c, seed=seed, std=c.initializer_range if std is None else std,
+                                    dtype=torch.float32, norm_jitter=0.0)
+        rand = meta_state_dict_to_params(sd, c.num_hidden_layers)
+        if c.tie_word_embeddings:
+            rand.pop("lm_head", None)
+        if params is None:
+            return rand
+        flat_r, flat_p = flatten_tree(rand), flatten_tree(params)
+        missing = set(self._missing_keys) | (set(flat_r) - set(flat_p))
+        for k in missing:
+            flat_p[k] = flat_r[k]
+        self._missing_keys = set()
+        return unflatten_tree(flat_p)
 
     def save_pretrained(self, save_directory: str) -> str:
         """Deployed-form safetensors checkpoint of this rank (``utils/native_ckpt.py``)."""
@@ -246,16 +328,16 @@ class LLaMAForCausalLM:
 
     # ------------------------------------------------------------------ core forward
     def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor, hb: torch.Tensor) -> None:
-        """``h += x @ W^T`` where W is row-sharded: every rank adds its partial sum; the
-        residual is added exactly once (rank 0) before the all-reduce. ``hb`` is the bf16
-        mirror of ``h`` that the next projection reads (written by the GEMM epilogue at TP=1,
-        re-cast after the all-reduce otherwise)."""
+        """``h += x @ W^T`` where W is row-sharded. TP=1: the GEMM epilogue adds into the fp32 residual
+        ``h`` and writes its bf16 mirror ``hb`` (the A operand of the next projection). TP>1: the GEMM
+        writes only this rank's partial (``comm.reduce_dtype``, bf16 by default) and one collective
+        kernel sums the partials in rank order, adds them to ``h`` and rewrites ``hb``
+        (``comm.all_reduce_residual_``; reference ``partition.py:67,70``)."""
         if self.comm.size == 1:
             ops.linear_residual(x, w, h, mirror=hb)
         else:
-            ops.linear_residual(x, w, h, accumulate=(self.comm.rank == 0))
-            self.comm.all_reduce_(h)
-            hb.copy_(h)
+            part = ops.linear(x, w, out_dtype=self.comm.reduce_dtype)
+            self.comm.all_reduce_residual_(part, h, hb)
 
     def forward_tokens(self, ids: torch.Tensor, positions: torch.Tensor, cache: KVCache, slot0,
                        kv_start: torch.Tensor, key_mask: Optional[torch.Tensor] = None,
@@ -277,6 +359,11 @@ class LLaMAForCausalLM:
                                     output_hidden_states=collect_hidden, output_attentions=collect_attn)
         if logits_mode == "none":
             logits = None
+        elif self.precision == "highest":  # fp32 lm_head weights + fp32 GEMM (reference model.py:698-736)
+            hl = h if logits_mode == "all" else h.reshape(b, s, d)[:, -1].contiguous()
+            logits = self.final_norm(hl) @ self.lm_head_f32.t()
+            if logits_mode == "argmax":
+                logits = ops.argmax(logits.contiguous())
         elif logits_mode == "argmax":  # greedy: (idx, val) of this rank's vocab shard, argmax fused in the GEMM
             logits = ops.linear_argmax(hb.reshape(b, s, d)[:, -1].contiguous(), self.lm_head, rms_eps=self.eps)
         else:
@@ -347,10 +434,10 @@ class LLaMAForCausalLM:
                                                        collect_attn=oa)
         if past_key_values is not None:
             cache.advance(s)
-        logits = self.gather_logits(logits).reshape(b, s, -1)
+        logits = self.gather_logits(logits).reshape(b, s, -1).to(self.dtype)
         hs = None
         if oh:
-            hs = tuple(hidden) + (self.final_norm(h).reshape(b, s, -1),)
+            hs = tuple(x.to(self.dtype) for x in hidden) + (self.final_norm(h).reshape(b, s, -1).to(self.dtype),)
         out = CausalLMOutput(logits=logits, past_key_values=past_key_values, hidden_states=hs,
                              attentions=tuple(attns) if oa else None)
         return out if rd else out.to_tuple()
@@ -405,7 +492,7 @@ class LLaMAModel(LLaMAForCausalLM):
                                                   logits_mode="none", collect_hidden=oh, collect_attn=oa)
         if past_key_values is not None:
             cache.advance(s)
-        last = self.final_norm(h).reshape(b, s, -1)
+        last = self.final_norm(h).reshape(b, s, -1).to(self.dtype)
         return BaseModelOutput(last_hidden_state=last,
-                               hidden_states=(tuple(hidden) + (last,)) if oh else None,
+                               hidden_states=(tuple(x.to(self.dtype) for x in hidden) + (last,)) if oh else None,
                                attentions=tuple(attns) if oa else None)

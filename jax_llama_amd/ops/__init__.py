@@ -41,6 +41,9 @@ class _Workspace:
 
     def __init__(self):
         self._bufs = {}
+        # bumped on every (re)allocation: a captured hipGraph that recorded these buffers' addresses is
+        # stale once it changes (runtime/engine.py recaptures)
+        self.generation = 0
 
     def get(self, name: str, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
         key = (name, device, dtype)
@@ -48,6 +51,7 @@ class _Workspace:
         if buf is None or buf.numel() < numel:
             buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
             self._bufs[key] = buf
+            self.generation += 1
         return buf[:numel]
 
     def get_zeroed(self, name: str, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
@@ -57,10 +61,12 @@ class _Workspace:
         if buf is None or buf.numel() < numel:
             buf = torch.zeros(max(numel, 1), dtype=dtype, device=device)
             self._bufs[key] = buf
+            self.generation += 1
         return buf[:numel]
 
     def clear(self):
         self._bufs.clear()
+        self.generation += 1
 
 
 workspace = _Workspace()
@@ -409,8 +415,7 @@ def topk_sample(logits: torch.Tensor, k: int, temperature: float, top_p: float, 
         lv = torch.empty(b, kl, dtype=torch.float32, device=logits.device)
         li = torch.empty(b, kl, dtype=torch.int32, device=logits.device)
         e.topk_merge(cv, ci, kl, 0, out_v=lv, out_i=li)
-        cv = comm.all_gather(lv).permute(1, 0, 2).reshape(b, tp * kl).contiguous()
-        ci = comm.all_gather(li).permute(1, 0, 2).reshape(b, tp * kl).contiguous()
+        cv, ci = comm.gather_topk(lv, li)  # custom gather kernel (graph-capturable) on the GPU
     nxt = torch.empty(b, dtype=torch.int32, device=logits.device)
     e.topk_merge(cv, ci, k, 1, nxt=nxt, temperature=float(temperature),
                  top_p=1.0 if top_p is None else float(top_p), seed=int(seed) & ((1 << 63) - 1), step=step)

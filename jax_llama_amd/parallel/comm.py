@@ -4,43 +4,66 @@ The reference never calls a collective itself: XLA's GSPMD inserts the all-reduc
 row-parallel ``wo``/``w2`` (``partition.py:67,70``) and the gathers for the vocab-parallel
 ``lm_head`` (``partition.py:77``). Here they are explicit:
 
-  * ``all_reduce_``: sum over the TP group. On GPUs small (decode-sized) messages go through
-    the custom one-shot xGMI all-reduce (``csrc/comm/allreduce.hip``: peer-mapped IPC
-    buffers, every rank reads all peers over its direct links, graph-capturable); larger
-    messages and CPU/gloo runs use ``torch.distributed`` (RCCL / gloo).
-  * ``all_gather``: stacks every rank's tensor (sampler candidates, vocab-parallel logits).
+  * ``all_reduce_residual_(partial, h, hb)``: the row-parallel sum of a projection's partial
+    output, added to the fp32 residual stream ``h`` with its bf16 mirror ``hb`` rewritten — one
+    kernel on the custom xGMI path (``csrc/kernels/allreduce.hip``), RCCL/gloo + an add otherwise;
+  * ``argmax(val, idx, v_local)`` / ``gather_topk(vals, idx)``: the vocab-parallel sampler's
+    gathers (greedy ``(max, argmax)`` pair per row; per-rank top-k candidates);
+  * ``all_reduce_`` / ``all_gather``: generic sum / stack (prefill-sized messages, logits gathers).
+
+On GPUs every decode-sized message goes through the custom one-/two-shot kernels (graph-capturable,
+no host sync); larger messages and CPU/gloo runs use ``torch.distributed`` (RCCL / gloo).
+``reduce_dtype`` is the dtype of the row-parallel partials on the wire: bf16 (default, half the bytes;
+accumulated in fp32) or fp32 (``JLA_TP_REDUCE_DTYPE=fp32``).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
 import torch.distributed as dist
 
 
+def _default_reduce_dtype():
+    return torch.float32 if os.environ.get("JLA_TP_REDUCE_DTYPE", "bf16") == "fp32" else torch.bfloat16
+
+
 class TPComm:
-    def __init__(self, size: int = 1, rank: int = 0, group=None, custom=None):
+    def __init__(self, size: int = 1, rank: int = 0, group=None, custom=None,
+                 reduce_dtype: Optional[torch.dtype] = None):
         self.size = size
         self.rank = rank
         self.group = group
         self.custom = custom  # parallel.custom_allreduce.CustomAllReduce or None
+        self.reduce_dtype = reduce_dtype or _default_reduce_dtype()
 
     @classmethod
-    def from_context(cls, ctx, use_custom: bool = True, max_bytes: int = 8 << 20) -> "TPComm":
+    def from_context(cls, ctx, use_custom: bool = True, max_bytes: int = 16 << 20,
+                     reduce_dtype: Optional[torch.dtype] = None) -> "TPComm":
         custom = None
         if ctx.tp_size > 1 and ctx.device.type == "cuda" and use_custom:
             try:
                 from .custom_allreduce import CustomAllReduce
-            except ImportError:  # one-shot xGMI kernel not built: RCCL handles every message
+            except ImportError:  # kernels not built: RCCL handles every message
                 CustomAllReduce = None
             if CustomAllReduce is not None:
-                custom = CustomAllReduce.create(ctx, max_bytes=max_bytes)
-        return cls(ctx.tp_size, ctx.tp_rank, ctx.tp_group, custom)
+                from .custom_allreduce import CustomAllReduceError
+                try:
+                    custom = CustomAllReduce.create(ctx, max_bytes=max_bytes)
+                except CustomAllReduceError as ex:  # same verdict on every rank: all fall back to RCCL
+                    import logging
+                    logging.getLogger(__name__).warning("custom all-reduce disabled: %s", ex)
+                    custom = None
+        if reduce_dtype is None and ctx.device.type != "cuda":
+            reduce_dtype = torch.float32  # CPU (gloo) runs: the oracle-comparison path keeps fp32 partials
+        return cls(ctx.tp_size, ctx.tp_rank, ctx.tp_group, custom, reduce_dtype)
 
     def _host_staged(self, t: torch.Tensor) -> bool:
         # GPU tensors over a gloo group (multi-process tests sharing one GPU): stage through the host
         return t.is_cuda and dist.get_backend(self.group) == "gloo"
 
+    # ------------------------------------------------------------------ sums
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
             return t
@@ -54,6 +77,41 @@ class TPComm:
             return t
         dist.all_reduce(t, group=self.group)
         return t
+
+    def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: Optional[torch.Tensor]):
+        """``h (fp32) += sum over ranks of partial``; ``hb = bf16(h)`` when given."""
+        if self.size > 1 and self.custom is not None and hb is not None and self.custom.can_handle(partial):
+            self.custom.all_reduce_residual_(partial, h, hb)
+            return h
+        p = partial.float() if partial.dtype != torch.float32 else partial.clone()
+        self.all_reduce_(p)
+        h.add_(p.view_as(h))
+        if hb is not None:
+            hb.copy_(h)
+        return h
+
+    # ------------------------------------------------------------------ sampler gathers
+    def argmax(self, val: torch.Tensor, idx: torch.Tensor, v_local: int) -> torch.Tensor:
+        """Global greedy token per row from every rank's local ``(max, argmax)`` (first max in rank
+        order == smallest global index among ties, like ``jnp.argmax`` over the full vocab)."""
+        if self.size == 1:
+            return idx
+        off = self.rank * v_local
+        if self.custom is not None and val.is_cuda and self.custom.can_handle_pairs(val.numel()):
+            return self.custom.argmax_pairs(val.float(), idx.to(torch.int32), off)
+        vals = self.all_gather(val.float())  # [tp, B]
+        idxs = self.all_gather(idx.to(torch.int32) + off)
+        best = vals.argmax(0)
+        return idxs.gather(0, best[None]).squeeze(0).to(torch.int32)
+
+    def gather_topk(self, vals: torch.Tensor, idx: torch.Tensor):
+        """``[B, k]`` candidates (global indices) of every rank -> ``[B, tp * k]`` in rank order."""
+        b, k = vals.shape
+        if self.custom is not None and vals.is_cuda and self.custom.can_handle_pairs(vals.numel()):
+            return self.custom.topk_pairs(vals, idx, 0)
+        gv = self.all_gather(vals).permute(1, 0, 2).reshape(b, self.size * k).contiguous()
+        gi = self.all_gather(idx).permute(1, 0, 2).reshape(b, self.size * k).contiguous()
+        return gv, gi
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """Returns ``[size, *t.shape]``."""
@@ -69,6 +127,13 @@ class TPComm:
         if staged:
             out = out.to(t.device)
         return out.view((self.size,) + tuple(t.shape))
+
+    # ------------------------------------------------------------------ failure detection
+    def check(self):
+        """Raise if a custom collective timed out waiting for a peer (bounded spins ->
+        error). Called by the decode loop at its periodic host poll."""
+        if self.custom is not None:
+            self.custom.check()
 
 
 NO_COMM = TPComm()

@@ -1,22 +1,42 @@
-"""One-shot push all-reduce over xGMI for decode-sized tensor-parallel messages.
+"""Custom xGMI collectives for decode-sized tensor-parallel messages (``csrc/kernels/allreduce.hip``).
 
-SURVEY D1: RCCL (``torch.distributed`` backend ``nccl``) carries init, large messages and is the
-correctness oracle; the 2 row-parallel all-reduces per layer per token (reference
-``partition.py:67,70``: XLA inserts them after ``wo`` and ``w2``) are latency-bound, a few KiB to a
-few MiB, so they go through ``csrc/kernels/allreduce.hip``: every rank pushes its input into every
-peer's uncached, IPC-mapped receive slot over its direct xGMI link, raises a per-block flag, waits
-for its peers' flags and sums the slots in rank order (bit-identical on every rank). One kernel,
-no host sync, graph-capturable.
+SURVEY D1: RCCL (``torch.distributed`` backend ``nccl``) carries init, large (prefill) messages and is
+the correctness oracle. The per-token collectives of the decode step go through these kernels instead,
+so a captured decode step contains no RCCL call at all:
+
+  * ``all_reduce_residual_(partial, h, hb)`` — the 2 row-parallel sums per layer (reference
+    ``partition.py:67,70``: XLA inserts them after ``wo`` and ``w2``) with the residual add and the
+    bf16 mirror of the residual stream fused into the reduction (``h += sum``, ``hb = bf16(h)``);
+  * ``argmax_pairs(val, idx, offset)`` — vocab-parallel greedy token (``partition.py:77``): every
+    rank's (max, argmax) is all-gathered and reduced to the first max in rank order;
+  * ``topk_pairs(vals, idx, offset)`` — every rank's top-k candidates, gathered as ``[B, tp*k]``
+    for the exact distributed sampler.
+
+One-shot (every rank reads every peer's copy) for small messages; two-shot (reduce-scatter +
+all-gather of the fp32 sums) for large ones at >= 4 ranks, where it moves ``3/world`` of the bytes
+per link. Both sum in rank order in fp32, so they are bit-identical to each other and on every rank.
 
 Rendezvous: each rank allocates its buffers, the IPC handles are exchanged with
-``all_gather_object`` on the TP group, then every rank maps its peers'.
+``all_gather_object`` on the TP group, then every rank maps its peers'. A peer that never arrives
+makes the kernel give up after ``timeout_s`` and set an error word; ``check()`` raises on it.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
 
 from ..ops import ext
+
+# Two-shot above this many bytes per rank (at >= 4 ranks). One-shot moves (world-1) x bytes per rank over
+# world-1 links (bytes per link); two-shot moves 3 x bytes / world per link (bf16 partial scatter + fp32 sum
+# gather) at the price of a second barrier.
+TWO_SHOT_MIN_BYTES = int(os.environ.get("JLA_CAR_TWO_SHOT_BYTES", str(512 << 10)))
+
+
+class CustomAllReduceError(RuntimeError):
+    pass
 
 
 class CustomAllReduce:
@@ -29,11 +49,13 @@ class CustomAllReduce:
         self.max_bytes = max_bytes
 
     @classmethod
-    def create(cls, ctx, max_bytes: int = 8 << 20, group=None) -> "CustomAllReduce":
-        return cls.create_for(ctx.tp_rank, ctx.tp_size, ctx.tp_group if group is None else group, max_bytes)
+    def create(cls, ctx, max_bytes: int = 16 << 20, group=None, timeout_s: float = 10.0) -> "CustomAllReduce":
+        return cls.create_for(ctx.tp_rank, ctx.tp_size, ctx.tp_group if group is None else group, max_bytes,
+                              timeout_s)
 
     @classmethod
-    def create_for(cls, rank: int, world: int, group, max_bytes: int = 8 << 20) -> "CustomAllReduce":
+    def create_for(cls, rank: int, world: int, group, max_bytes: int = 16 << 20,
+                   timeout_s: float = 10.0) -> "CustomAllReduce":
         if world > 8:
             raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI hop)")
         max_bytes = (max_bytes + 15) // 16 * 16
@@ -41,27 +63,91 @@ class CustomAllReduce:
         buf, sig, hbuf, hsig = e.car_alloc(max_bytes, world)
         handles = [None] * world
         dist.all_gather_object(handles, (bytes(hbuf), bytes(hsig)), group=group)
-        state = e.car_init(rank, world, max_bytes, buf, sig, [h[0] for h in handles], [h[1] for h in handles])
-        dist.barrier(group=group)
-        return cls(state, rank, world, max_bytes)
+        err = None
+        try:
+            state = e.car_init(rank, world, max_bytes, buf, sig, [h[0] for h in handles], [h[1] for h in handles],
+                               float(timeout_s))
+        except RuntimeError as ex:  # e.g. the IPC import failed on this rank
+            state, err = 0, str(ex)
+        # every rank learns whether every rank mapped its peers: one rank failing must not leave the
+        # others spinning in a collective it will never join
+        oks = [None] * world
+        dist.all_gather_object(oks, err is None, group=group)
+        if not all(oks):
+            raise CustomAllReduceError(f"custom all-reduce setup failed on ranks "
+                                       f"{[r for r, ok in enumerate(oks) if not ok]}: {err}")
+        car = cls(state, rank, world, max_bytes)
+        # protocol self-test on the real links: a known sum, checked on the host by every rank
+        ok = car.self_test()
+        dist.all_gather_object(oks, ok, group=group)
+        if not all(oks):
+            car.close()
+            raise CustomAllReduceError("custom all-reduce self-test failed (wrong sums or a timeout)")
+        return car
 
+    def self_test(self) -> bool:
+        """One-shot and two-shot sums of rank-dependent data (bit-exact integers in fp32)."""
+        n = 64 * 1024
+        x = torch.arange(n, dtype=torch.float32, device="cuda") % 997 + 1000.0 * (self.rank + 1)
+        want = (torch.arange(n, dtype=torch.float32) % 997) * self.world + 1000.0 * self.world * (self.world + 1) / 2
+        ok = True
+        for ts in (False, True):
+            got = self.all_reduce(x, two_shot=ts).cpu()
+            ok = ok and torch.equal(got, want)
+        return bool(ok and self.error() == 0)
+
+    # ------------------------------------------------------------------ capability checks
     def can_handle(self, t: torch.Tensor) -> bool:
         nbytes = t.numel() * t.element_size()
         return (t.is_cuda and t.is_contiguous() and t.dtype in self.DTYPES and 0 < nbytes <= self.max_bytes
                 and nbytes % 16 == 0)
 
-    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        ext().car_allreduce(self.state, t, t)
+    def can_handle_pairs(self, n: int) -> bool:
+        return 0 < n * 8 <= self.max_bytes
+
+    def use_two_shot(self, nbytes: int) -> bool:
+        return self.world >= 4 and nbytes >= TWO_SHOT_MIN_BYTES
+
+    # ------------------------------------------------------------------ collectives
+    def all_reduce_(self, t: torch.Tensor, two_shot=None) -> torch.Tensor:
+        ts = self.use_two_shot(t.numel() * t.element_size()) if two_shot is None else bool(two_shot)
+        ext().car_allreduce(self.state, t, t, ts)
         return t
 
-    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, two_shot=None) -> torch.Tensor:
         out = torch.empty_like(t)
-        ext().car_allreduce(self.state, t, out)
+        ts = self.use_two_shot(t.numel() * t.element_size()) if two_shot is None else bool(two_shot)
+        ext().car_allreduce(self.state, t, out, ts)
         return out
 
+    def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: torch.Tensor, two_shot=None):
+        """``h += sum_ranks(partial)``; ``hb = bf16(h)`` (one kernel)."""
+        ts = self.use_two_shot(partial.numel() * partial.element_size()) if two_shot is None else bool(two_shot)
+        ext().car_allreduce_residual(self.state, partial, h, hb, ts)
+
+    def argmax_pairs(self, val: torch.Tensor, idx: torch.Tensor, idx_offset: int, out_val=None) -> torch.Tensor:
+        """First max over ranks of each row's local ``(val, idx + idx_offset)``: int32 ``[B]``."""
+        out = torch.empty(idx.numel(), dtype=torch.int32, device=idx.device)
+        ext().car_pairs(self.state, 0, val.contiguous(), idx.contiguous(), int(idx_offset), 1, out_val, out)
+        return out
+
+    def topk_pairs(self, vals: torch.Tensor, idx: torch.Tensor, idx_offset: int):
+        """``[B, k]`` local candidates of every rank -> ``(vals, idx)`` of shape ``[B, world * k]``."""
+        b, k = vals.shape
+        ov = torch.empty(b, self.world * k, dtype=torch.float32, device=vals.device)
+        oi = torch.empty(b, self.world * k, dtype=torch.int32, device=vals.device)
+        ext().car_pairs(self.state, 1, vals.contiguous(), idx.contiguous(), int(idx_offset), int(k), ov, oi)
+        return ov, oi
+
+    # ------------------------------------------------------------------ failure detection
     def error(self) -> int:
         """1 if a kernel gave up waiting for a peer (bounded spin) since creation."""
         return int(ext().car_error(self.state))
+
+    def check(self):
+        if self.state and self.error():
+            raise CustomAllReduceError(
+                "custom all-reduce: a peer did not arrive within the timeout; results since then are invalid")
 
     def close(self):
         if self.state:

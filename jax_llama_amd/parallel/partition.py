@@ -150,14 +150,37 @@ def shard_tree(params: Dict[str, Any], rank: int, size: int, fsdp: bool = False,
 class Mesh:
     """A (dp, mp) process mesh: ``dp`` replicas, each a TP group of ``mp`` ranks."""
 
-    def __init__(self, dp: int = 1, mp: int = 1, rank: int = 0):
+    def __init__(self, dp: int = 1, mp: int = 1, rank: int = 0, dp_group=None):
         self.shape = {"dp": dp, "mp": mp}
         self.dp_rank = rank // mp
         self.mp_rank = rank % mp
+        self.dp_group = dp_group  # torch.distributed group of this rank's dp peers (same mp rank)
+
+    @classmethod
+    def from_context(cls, ctx) -> "Mesh":
+        return cls(dp=ctx.dp_size, mp=ctx.tp_size, rank=ctx.rank, dp_group=ctx.dp_group)
 
     @property
     def devices(self):
         return self.shape
+
+
+def gather_dp(x, mesh: Optional[Mesh]):
+    """Inverse of the dp batch split: all-gather every dp replica's rows (dim 0) when a process
+    group is available; otherwise return this replica's rows unchanged."""
+    if mesh is None or mesh.shape["dp"] == 1 or not torch.is_tensor(x):
+        return x
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return x
+    dp = mesh.shape["dp"]
+    xs = x.contiguous()
+    staged = xs.is_cuda and dist.get_backend(mesh.dp_group) == "gloo"
+    src = xs.cpu() if staged else xs
+    out = [torch.empty_like(src) for _ in range(dp)]
+    dist.all_gather(out, src, group=mesh.dp_group)
+    full = torch.cat(out, 0)
+    return full.to(x.device) if staged else full
 
 
 def with_sharding_constraint(x, axis_resources):

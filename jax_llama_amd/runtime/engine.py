@@ -23,7 +23,9 @@ MI355X execution model (replaces XLA's compiled ``lax.while_loop``):
 """
 from __future__ import annotations
 
+import dataclasses
 import os
+from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Optional
 
@@ -55,6 +57,10 @@ class GenerationConfig:
 FUSED_GREEDY = os.environ.get("JLA_FUSED_ARGMAX", "1") != "0"
 
 
+def _fused_greedy() -> bool:
+    return FUSED_GREEDY
+
+
 @dataclass
 class GenerateOutput:
     sequences: torch.Tensor
@@ -65,19 +71,13 @@ class GenerateOutput:
 # --------------------------------------------------------------------------------------
 def _greedy(model, logits_local) -> torch.Tensor:
     """``logits_local``: this rank's ``[B, V/tp]`` logits, or its already reduced ``(idx, val)``
-    (``forward_tokens(logits_mode="argmax")``: argmax fused into the lm_head GEMM)."""
+    (``forward_tokens(logits_mode="argmax")``: argmax fused into the lm_head GEMM). Under TP the
+    per-rank ``(max, argmax)`` pairs are reduced by one custom gather kernel (``comm.argmax``)."""
     if isinstance(logits_local, tuple):
         (idx, val), v_local = logits_local, model.vocab_local
     else:
         (idx, val), v_local = ops.argmax(logits_local), logits_local.shape[1]
-    comm = model.comm
-    if comm.size == 1:
-        return idx
-    idx = idx + comm.rank * v_local
-    vals = comm.all_gather(val)  # [tp, B]
-    idxs = comm.all_gather(idx)
-    best = vals.argmax(0)  # first max in rank order == smallest global index among ties
-    return idxs.gather(0, best[None]).squeeze(0).to(torch.int32)
+    return model.comm.argmax(val, idx, v_local)
 
 
 def _sample(model, logits_local: torch.Tensor, gc: GenerationConfig, gen: Optional[torch.Generator],
@@ -100,10 +100,9 @@ def _sample(model, logits_local: torch.Tensor, gc: GenerationConfig, gen: Option
     if gc.top_k:
         k = min(gc.top_k, x.shape[1])
         vals, idx = torch.topk(x, k, dim=-1)
-        idx = idx + comm.rank * x.shape[1]
+        idx = (idx + comm.rank * x.shape[1]).to(torch.int32)
         if comm.size > 1:
-            gv = comm.all_gather(vals).permute(1, 0, 2).reshape(x.shape[0], -1)
-            gi = comm.all_gather(idx).permute(1, 0, 2).reshape(x.shape[0], -1)
+            gv, gi = comm.gather_topk(vals.contiguous(), idx.contiguous())
             vals, sel = torch.topk(gv, k, dim=-1)
             idx = gi.gather(1, sel)
     else:
@@ -177,7 +176,7 @@ class DecodeEngine:
         self.cur_len.add_(1)
 
     def _logits_mode(self) -> str:
-        return "argmax" if FUSED_GREEDY and not self.gc.do_sample else "last"
+        return "argmax" if _fused_greedy() and not self.gc.do_sample else "last"
 
     def _decode_step(self):
         logits, *_ = self.model.forward_tokens(self.tokens, self.positions, self.cache, self.cache.index_t,
@@ -226,16 +225,32 @@ class DecodeEngine:
         self.gc = gc
         return self.prefill(input_ids, attention_mask)
 
+    def _graph_state(self):
+        # the graph records buffer addresses: the scratch workspaces (ops.workspace) and the sampling mode
+        return (self.gc.do_sample, self.key_mask is not None, ops.workspace.generation, _fused_greedy(),
+                ops.ARGMAX_FUSED_MIN_M, self.model.comm.reduce_dtype)
+
     def _ensure_graph(self):
-        key = (self.gc.do_sample, self.key_mask is not None)
-        if self._graph is not None and self._graph_key == key:
+        if self._graph is not None and self._graph_key == self._graph_state():
             return
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        # Capture records kernels without executing them; state buffers are static.
-        with torch.cuda.graph(g):
-            self._decode_step()
-        self._graph, self._graph_key = g, key
+        for _ in range(3):
+            key = self._graph_state()
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            # Capture records kernels without executing them; state buffers are static.
+            with torch.cuda.graph(g):
+                self._decode_step()
+            self._graph, self._graph_key = g, key
+            if self._graph_state() == key:  # no workspace grew while capturing
+                return
+        raise RuntimeError("decode graph capture keeps reallocating workspaces")
+
+    def _poll(self) -> bool:
+        """Host poll (every ``check_every`` steps): True once every row has finished. Also raises if a
+        custom TP collective gave up waiting for a peer."""
+        done = bool(self.finished.all().item())
+        self.model.comm.check()
+        return done
 
     def run(self, input_ids, attention_mask, gc: GenerationConfig) -> torch.Tensor:
         self.gc = gc
@@ -262,28 +277,49 @@ class DecodeEngine:
             steps_left -= 1
             if steps_left <= 0:
                 break
-            if step % self.check_every == 0 and bool(self.finished.all().item()):
+            if step % self.check_every == 0 and self._poll():
                 break
+        self.model.comm.check()
         return self.sequences
 
 
-_ENGINES = {}
+_ENGINES: "OrderedDict" = OrderedDict()
+
+
+def _engine_budget(model) -> int:
+    """Bytes of KV cache the engine cache may keep alive (``JLA_ENGINE_CACHE_GB`` or 40 % of the device)."""
+    env = os.environ.get("JLA_ENGINE_CACHE_GB")
+    if env:
+        return int(float(env) * (1 << 30))
+    if model.device.type == "cuda":
+        return int(0.4 * torch.cuda.get_device_properties(model.device).total_memory)
+    return 8 << 30
 
 
 def get_engine(model, batch_size: int, max_length: int) -> DecodeEngine:
+    """Per-(model, B, max_length) engines (each owns a KV cache and a captured decode graph), kept in
+    LRU order and bounded by the bytes of their KV caches."""
     key = (id(model), batch_size, max_length)
     eng = _ENGINES.get(key)
-    if eng is None:
-        if len(_ENGINES) > 4:
-            _ENGINES.clear()
-        eng = DecodeEngine(model, batch_size, max_length)
-        _ENGINES[key] = eng
+    if eng is not None:
+        _ENGINES.move_to_end(key)
+        return eng
+    need = model.config.num_hidden_layers * 2 * batch_size * model.n_kv_heads * max_length * model.head_dim * 2
+    budget = _engine_budget(model)
+    held = sum(e.cache.nbytes() for e in _ENGINES.values())
+    while _ENGINES and held + need > budget:
+        _, old = _ENGINES.popitem(last=False)
+        held -= old.cache.nbytes()
+        del old
+    eng = DecodeEngine(model, batch_size, max_length)
+    _ENGINES[key] = eng
     return eng
 
 
 def generate(model, input_ids, attention_mask=None, generation_config: Optional[GenerationConfig] = None,
              prng_key=None, **kwargs) -> GenerateOutput:
-    gc = generation_config or GenerationConfig()
+    # never mutate the caller's config (HF semantics: generate works on a copy)
+    gc = dataclasses.replace(generation_config) if generation_config is not None else GenerationConfig()
     for k, v in kwargs.items():
         if hasattr(gc, k):
             setattr(gc, k, v)

@@ -76,7 +76,7 @@ def from_pretrained(directory: str, device="cpu", comm=None, config: Optional[LL
     if meta.get("format") != FORMAT:
         raise ValueError(f"unsupported native checkpoint format {meta.get('format')}")
     cfg = config or LLaMAConfig.from_pretrained(directory)
-    model = LLaMAForCausalLM(cfg, device=device, comm=comm)
+    model = LLaMAForCausalLM(cfg, device=device, comm=comm, _do_init=False)
     if meta["tp"] != model.tp_size:
         raise ValueError(f"checkpoint was saved at tp={meta['tp']} but this model runs tp={model.tp_size}; "
                          "re-shard through the Meta format (utils.checkpoint.save_meta_checkpoint)")

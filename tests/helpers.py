@@ -28,7 +28,7 @@ def gpu_config(**kw) -> LLaMAConfig:
 def build(config: LLaMAConfig, device="cpu", seed=0, comm=None):
     sd = random_meta_state_dict(config, seed=seed)
     params = meta_state_dict_to_params(sd, config.num_hidden_layers)
-    model = LLaMAForCausalLM(config, device=device, comm=comm).load_params(params)
+    model = LLaMAForCausalLM(config, device=device, comm=comm, _do_init=False).load_params(params)
     oracle = OracleLLaMA(sd, config.num_hidden_layers, config.num_attention_heads,
                          config.num_key_value_heads, config.rms_norm_eps, config.rope_theta)
     return model, oracle, sd, params

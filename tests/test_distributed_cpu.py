@@ -37,7 +37,7 @@ def _worker(rank, world, port, cfg_kw, toks, mask, q):
         comm = TPComm.from_context(ctx)
         cfg = tiny_config(**cfg_kw)
         _, _, _, params = build(cfg, seed=11)
-        model = LLaMAForCausalLM(cfg, comm=comm).load_params(params)
+        model = LLaMAForCausalLM(cfg, comm=comm, _do_init=False).load_params(params)
         pos = mask.cumsum(-1) - 1
         logits = model(toks, attention_mask=mask, position_ids=pos).logits
         gc = GenerationConfig(max_length=toks.shape[1] + 6, do_sample=False, pad_token_id=2, eos_token_id=2)
@@ -54,9 +54,11 @@ def _worker(rank, world, port, cfg_kw, toks, mask, q):
         q.put(("err", traceback.format_exc(), None, None))
 
 
-@pytest.mark.parametrize("world,kv", [(2, 2), (2, 4), (4, 4)])
+@pytest.mark.parametrize("world,kv", [(2, 2), (2, 4), (4, 4), (8, 8)])
 def test_tensor_parallel_matches_single_process(world, kv):
     cfg_kw = dict(num_key_value_heads=kv, intermediate_size=128, vocab_size=256)
+    if world == 8:  # 8 heads / 8 kv heads: one of each per rank (the 70B TP8 per-rank head layout has 1 kv head)
+        cfg_kw.update(num_attention_heads=8, hidden_size=64)
     cfg = tiny_config(**cfg_kw)
     ref_model, _, _, _ = build(cfg, seed=11)
     toks, mask = left_padded_batch([5, 8], 8, cfg.vocab_size, pad=2, seed=2)

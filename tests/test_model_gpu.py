@@ -15,7 +15,7 @@ DEV = "cuda"
 
 def _pair(cfg, seed=0):
     model_cpu, oracle, sd, params = build(cfg, seed=seed)
-    model_gpu = LLaMAForCausalLM(cfg, device=DEV).load_params(params)
+    model_gpu = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).load_params(params)
     return model_cpu, model_gpu, oracle
 
 
@@ -85,9 +85,62 @@ def test_random_init_8b_shapes_one_layer():
     """Synthetic path of bench.py at the real Llama-3-8B layer shapes (1 layer to keep it fast)."""
     from jax_llama_amd.config import get_preset
     cfg = get_preset("llama3-8b", num_hidden_layers=1)
-    m = LLaMAForCausalLM(cfg, device=DEV).init_random(seed=0)
+    m = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).init_random(seed=0)
     toks = torch.randint(0, cfg.vocab_size, (2, 16), dtype=torch.int32)
     gc = GenerationConfig(max_length=24, do_sample=False, pad_token_id=0, eos_token_id=-1)
     seq = m.generate(toks, generation_config=gc).sequences
     assert seq.shape == (2, 24)
     assert int(seq.min()) >= 0 and int(seq.max()) < cfg.vocab_size
+
+
+def test_graph_recaptured_after_workspace_growth():
+    """a cached decode graph must not replay with freed workspace buffers. Run,
+    run a longer prompt on ANOTHER engine (grows the shared workspaces), run the first engine again:
+    every run must equal an eager run."""
+    from jax_llama_amd import ops
+    cfg = gpu_config()
+    _, gpu, _ = _pair(cfg, seed=12)
+    gc = GenerationConfig(max_length=40, do_sample=False, pad_token_id=2, eos_token_id=-1)
+    toks, mask = left_padded_batch([4, 7], 8, cfg.vocab_size, pad=2, seed=13)
+    e1 = DecodeEngine(gpu, 2, 40, use_graph=True)
+    first = e1.run(toks, mask, gc).clone()
+    gen0 = ops.workspace.generation
+    big, bmask = left_padded_batch([30] * 24, 30, cfg.vocab_size, pad=2, seed=14)
+    DecodeEngine(gpu, 24, 40, use_graph=True).run(big, bmask, gc)
+    assert ops.workspace.generation > gen0  # the larger batch reallocated shared scratch
+    again = e1.run(toks, mask, gc).clone()
+    eager = DecodeEngine(gpu, 2, 40, use_graph=False).run(toks, mask, gc).clone()
+    assert torch.equal(first, eager) and torch.equal(again, eager)
+
+
+def test_fused_argmax_engine_path(monkeypatch):
+    """the lm_head GEMM with the argmax epilogue, forced at small M, inside the
+    captured decode step, gives the same greedy sequences as logits + argmax."""
+    from jax_llama_amd import ops
+    from jax_llama_amd.runtime import engine as eng_mod
+    cfg = gpu_config()
+    cpu, gpu, _ = _pair(cfg, seed=15)
+    toks, mask = left_padded_batch([6, 9, 9], 9, cfg.vocab_size, pad=2, seed=16)
+    gc = GenerationConfig(max_length=30, do_sample=False, pad_token_id=2, eos_token_id=-1)
+    monkeypatch.setattr(ops, "ARGMAX_FUSED_MIN_M", 1)
+    fused = DecodeEngine(gpu, 3, 30, use_graph=True).run(toks, mask, gc).clone()
+    monkeypatch.setattr(eng_mod, "FUSED_GREEDY", False)
+    plain = DecodeEngine(gpu, 3, 30, use_graph=True).run(toks, mask, gc).clone()
+    assert torch.equal(fused, plain)
+
+
+def test_precision_highest_logits():
+    """precision='highest' (jax_test.py:433): fp32 lm_head weights + fp32 GEMM; closer to the fp32
+    oracle than the default bf16 lm_head."""
+    cfg = gpu_config()
+    _, _, oracle, params = build(cfg, seed=17)
+    hi = LLaMAForCausalLM(cfg, device=DEV, _do_init=False, precision="highest").load_params(params)
+    lo = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).load_params(params)
+    toks = torch.randint(3, cfg.vocab_size, (2, 10), dtype=torch.int32)
+    want = oracle.forward(toks)
+    e_hi = rel_err(hi(toks).logits.cpu(), want)
+    e_lo = rel_err(lo(toks).logits.cpu(), want)
+    assert e_hi < 5e-2 and e_hi <= e_lo * 1.05, (e_hi, e_lo)
+    gc = GenerationConfig(max_length=16, do_sample=False, pad_token_id=0, eos_token_id=-1)
+    seq = hi.generate(toks, generation_config=gc).sequences
+    assert seq.shape == (2, 16)

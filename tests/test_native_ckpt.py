@@ -61,7 +61,7 @@ def _tp_worker(rank, world, port, path, toks, q):
         comm = TPComm.from_context(ctx)
         cfg = tiny_config(intermediate_size=128)
         _, _, _, params = build(cfg, seed=9)
-        model = LLaMAForCausalLM(cfg, comm=comm).load_params(params)
+        model = LLaMAForCausalLM(cfg, comm=comm, _do_init=False).load_params(params)
         model.save_pretrained(path)
         dist.barrier()
         again = LLaMAForCausalLM.from_pretrained(path, comm=comm)

@@ -575,6 +575,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nsplit"));
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));
+  m.def("attn_prefill_set_impl", [](int64_t impl) { jla::attn_prefill_set_impl((int)impl); });
   m.def("argmax", &argmax);
   m.def("topk_chunks", [](int64_t v) { return jla::topk_chunks(v); });
   m.def("car_alloc", &car_alloc);

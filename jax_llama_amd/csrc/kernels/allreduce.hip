@@ -74,7 +74,6 @@ JLA_DEV void st_sys16(__amdgpu_buffer_rsrc_t r, long long off, u32x4 v) {
 JLA_DEV u32x4 ld_sys16(__amdgpu_buffer_rsrc_t r, long long off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, SYS);
 }
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 JLA_DEV void st_sys8(__amdgpu_buffer_rsrc_t r, long long off, u32x2 v) {
   __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, SYS);
 }

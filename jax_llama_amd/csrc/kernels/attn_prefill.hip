@@ -173,11 +173,236 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ================================================================================================
+// v2: GQA-shared flash prefill on v_mfma_f32_32x32x16_bf16.
+//
+// Workgroup = NW waves = (batch row b, kv head, group of q heads, block of query positions); every wave
+// owns 32 query rows of ONE q head, and all NW waves read the SAME K/V tiles from LDS, so a (b, kv head)
+// K/V tile is fetched once per rep/hpw workgroups instead of once per q head (rep = H / Hkv).
+// Per 64-key tile and wave:
+//   S^T = K Q^T   (A = K fragment by ds_read_b128 from an XOR-swizzled image, B = Q^T fragments held in
+//                  VGPRs for the whole kernel): 2 key blocks x 8 dk-steps = 16 MFMAs. The C layout puts the
+//                  wave's query on the LANE (col = lane & 31) and 32 of the 64 keys in its registers, so the
+//                  online softmax is lane-local plus one exchange with lane ^ 32;
+//   O^T += V^T P^T (A = V^T by ds_read_b64_tr_b16 transposed reads of the row-major V image, B = the bf16 P
+//                  registers used in place with the permuted k order of the accumulator layout): 4 d tiles x
+//                  4 key steps = 16 MFMAs. O^T again has the query on the lane, so the rescale by
+//                  exp2(m_old - m_new) is lane-local too.
+// K/V tiles are register-staged (loads for tile t+1 issued before tile t's MFMAs, written to LDS after
+// the barrier that ends tile t). Causal: the workgroup stops at its last query's slot; a wave whose
+// queries all precede a tile skips its MFMAs; only tiles that cross the diagonal, kv_start or T are
+// masked element-wise. Heaviest (latest) query blocks launch first.
+constexpr int FA_KT = 64;  // keys per tile
+
+// byte offset of 16-byte chunk ch (0..15) of row `row` in a [rows][128 bf16] image whose XOR swizzle
+// serves both ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads without bank conflicts
+JLA_DEV int fa_off(int row, int ch) { return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+JLA_DEV f32x16 mfma32(const u32x4 a, const u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+JLA_DEV u32x2 ld_tr(const char* lds, int off) {
+  return __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                       (__attribute__((address_space(3))) s16x4*)(lds + off)));
+}
+
+template <int NW>
+__global__ void __launch_bounds__(NW * 64, 2)
+    attn_prefill_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
+                           const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int S, int H,
+                           int Hkv, int T, float scale_log2, int npb, int hgroups, int n_qb) {
+  constexpr int NT = NW * 64;
+  constexpr int TILE_BYTES = FA_KT * AP_DH * 2;            // 16 KiB
+  constexpr int CH_PER_T = FA_KT * 16 / NT;                 // 16-byte chunks per thread per tile (K or V)
+  __shared__ __attribute__((aligned(16))) char lds[2 * TILE_BYTES];
+  char* Ks = lds;
+  char* Vs = lds + TILE_BYTES;
+
+  const int qb = n_qb - 1 - (int)blockIdx.x;  // heaviest (latest) query blocks first
+  const int kvh = blockIdx.y / hgroups, hg = blockIdx.y - kvh * hgroups;
+  const int b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int hi = lane >> 5, col = lane & 31;
+  const int rep = H / Hkv, hpw = NW / npb;
+  const int r = w / npb, pb = w - r * npb;
+  const int h = kvh * rep + hg * hpw + r;
+  const int p0 = qb * 32 * npb + 32 * pb;   // first query position of this wave
+  const int pos = p0 + col;                  // this lane's query
+  const int slot0 = slot_ptr[0];
+  const int lo = kv_start[b];
+  const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
+
+  // Q^T fragments (B operand): lane holds Q[pos][16 ks + 8 hi .. +7]
+  u32x4 qf[8];
+  {
+    const bf16_t* qrow = q + (((size_t)b * S + min(pos, S - 1)) * H + h) * AP_DH + 8 * hi;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const u32x4*>(qrow + 16 * ks);
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int wg_last_pos = min(S, (qb + 1) * 32 * npb) - 1;
+  const int last_key = min(slot0 + wg_last_pos, T - 1);
+  const int t_begin = (lo / FA_KT) * FA_KT;
+  const int wave_first_slot = slot0 + p0, wave_last_slot = slot0 + min(p0 + 31, S - 1);
+  const int qslot = slot0 + pos;
+  const bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * T * AP_DH;
+  const bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * T * AP_DH;
+
+  // staging: thread handles chunks c = tid + NT * i (row = c >> 4, ch = c & 15) of each tile
+  u32x4 sk[CH_PER_T], sv[CH_PER_T];
+  auto load_tile = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < CH_PER_T; ++i) {
+      const int c = tid + NT * i, row = c >> 4, ch = c & 15;
+      const size_t src = (size_t)min(t0 + row, T - 1) * AP_DH + 8 * ch;
+      sk[i] = *reinterpret_cast<const u32x4*>(kb + src);
+      sv[i] = *reinterpret_cast<const u32x4*>(vb + src);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < CH_PER_T; ++i) {
+      const int c = tid + NT * i, row = c >> 4, ch = c & 15;
+      *reinterpret_cast<u32x4*>(Ks + fa_off(row, ch)) = sk[i];
+      *reinterpret_cast<u32x4*>(Vs + fa_off(row, ch)) = sv[i];
+    }
+  };
+  if (t_begin <= last_key) {
+    load_tile(t_begin);
+    store_tile();
+  }
+  __syncthreads();
+
+  // per-lane LDS read offsets: K row reads (key block kb, dk step ks -> chunk 2 ks + hi)
+  // V transposed reads: 16-lane group G = lane >> 4 covers d columns 16 (G & 1) .. +15 of a 32-wide d tile,
+  // lane 4q + p of the group addresses row q of the 4-key block, columns 4p .. 4p + 3.
+  const int gq = (lane & 15) >> 2, gp = lane & 3, G = lane >> 4;
+  for (int t0 = t_begin; t0 <= last_key; t0 += FA_KT) {
+    const bool has_next = t0 + FA_KT <= last_key;
+    if (has_next) load_tile(t0 + FA_KT);
+    if (t0 <= wave_last_slot) {
+      // ---- S^T = K Q^T
+      f32x16 st[2];
+#pragma unroll
+      for (int kbk = 0; kbk < 2; ++kbk) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) st[kbk][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + fa_off(32 * kbk + col, 2 * ks + hi));
+          st[kbk] = mfma32(kf, qf[ks], st[kbk]);
+        }
+      }
+      // ---- online softmax (log2 domain); element (kbk, i) is key t0 + 32 kbk + (i & 3) + 8 (i >> 2) + 4 hi
+      const bool full = !mrow && t0 >= lo && t0 + FA_KT - 1 <= wave_first_slot && t0 + FA_KT - 1 < T;
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int kbk = 0; kbk < 2; ++kbk)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float v = st[kbk][i] * scale_log2;
+          if (!full) {
+            const int j = t0 + 32 * kbk + (i & 3) + 8 * (i >> 2) + 4 * hi;
+            bool ok = j >= lo && j <= qslot && j < T;
+            if (mrow) ok = ok && j < mask_len && mrow[j] != 0;
+            v = ok ? v : -INFINITY;
+          }
+          st[kbk][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_run, tmax);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);  // m_run = -inf -> 0
+      float rs = 0.f;
+      u32x4 pf[4];  // B fragments of P^T for the 4 key steps
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          e[j] = __builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + j] - m_use);
+          rs += e[j];
+        }
+        pf[s] = pack8(e);
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      // ---- O^T += V^T P^T; A element j of lane half hi = V[key 16 s + 8 (j >> 2) + 4 hi + (j & 3)][d]
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int c0 = 4 * dt + 2 * (G & 1) + (gp >> 1);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int r0 = 16 * s + 4 * (G >> 1) + gq;
+          const u32x2 lo4 = ld_tr(Vs, fa_off(r0, c0) + 8 * (gp & 1));
+          const u32x2 hi4 = ld_tr(Vs, fa_off(r0 + 8, c0) + 8 * (gp & 1));
+          const u32x4 vf = {lo4[0], lo4[1], hi4[0], hi4[1]};
+          o[dt] = mfma32(vf, pf[s], o[dt]);
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with this tile's LDS images
+    if (has_next) {
+      store_tile();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: lane (query pos, half hi) holds d = 32 dt + 8 g + 4 hi + (0..3) in o[dt][4 g .. 4 g + 3]
+  if (pos < S) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16_t* dst = out + ((size_t)b * S + pos) * H * AP_DH + (size_t)h * AP_DH + 4 * hi;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 pk;
+        pk[0] = pack2bf(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
+        pk[1] = pack2bf(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<u32x2*>(dst + 32 * dt + 8 * g) = pk;
+      }
+  }
+}
+
+static int g_attn_prefill_impl = 2;
+void attn_prefill_set_impl(int impl) { g_attn_prefill_impl = impl; }
+
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,
                  hipStream_t s) {
   if (B <= 0 || S <= 0) return 0;
   if (Dh != AP_DH || H % Hkv) return -1;
+  const int rep = H / Hkv;
+  constexpr int NW = 4;
+  if (g_attn_prefill_impl == 2 && (rep % NW == 0 || NW % rep == 0)) {
+    const int npb = rep >= NW ? 1 : NW / rep;    // 32-query position blocks per workgroup
+    const int hpw = NW / npb;                    // q heads per workgroup
+    const int hgroups = rep / hpw;
+    const int n_qb = (S + 32 * npb - 1) / (32 * npb);
+    dim3 grid2(n_qb, Hkv * hgroups, B);
+    attn_prefill_v2_kernel<NW><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
+                                                         Hkv, T, 1.4426950408889634f / sqrtf((float)Dh), npb,
+                                                         hgroups, n_qb);
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid((S + AP_QB - 1) / AP_QB, H, B);
   attn_prefill_kernel<<<grid, 256, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H, Hkv, T,
                                            1.f / sqrtf((float)Dh));

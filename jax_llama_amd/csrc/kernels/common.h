@@ -17,6 +17,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // Linear epilogue modes (mirrors ops/__init__.py)
 #define MODE_STORE 0

@@ -204,6 +204,98 @@ def test_attention_prefill(rep, s, slot0):
     assert torch.isfinite(got.float()).all()
 
 
+def _attn_ref_gpu(q, kc, vc, slot0, kv_start, key_mask=None, chunk=512):
+    """fp32 PyTorch reference on the GPU (chunked over queries) for long sequences: query s of row b at
+    slot slot0 + s attends keys j with kv_start[b] <= j <= slot0 + s (and key_mask[b, j])."""
+    b, s, h, dh = q.shape
+    hkv, t = kc.shape[1], kc.shape[2]
+    rep = h // hkv
+    k = kc.float().repeat_interleave(rep, 1)  # [B, H, T, Dh]
+    v = vc.float().repeat_interleave(rep, 1)
+    out = torch.empty(b, s, h, dh, device=q.device)
+    j = torch.arange(t, device=q.device)
+    for c0 in range(0, s, chunk):
+        qc = q[:, c0:c0 + chunk].float().permute(0, 2, 1, 3)  # [B, H, c, Dh]
+        sc = qc @ k.transpose(-1, -2) / dh ** 0.5
+        qs = slot0 + c0 + torch.arange(qc.shape[2], device=q.device)
+        ok = (j[None, None, :] <= qs[None, :, None]) & (j[None, None, :] >= kv_start[:, None, None])
+        if key_mask is not None:
+            ok = ok & (key_mask[:, None, :t] != 0)
+        sc = sc.masked_fill(~ok[:, None], float("-inf"))
+        p = torch.softmax(sc, -1).nan_to_num(0.0)
+        out[:, c0:c0 + chunk] = (p @ v).permute(0, 2, 1, 3)
+    return out.reshape(b * s, h * dh)
+
+
+@pytest.mark.parametrize("impl", [2, 1])
+@pytest.mark.parametrize("rep", [1, 4, 8])
+@pytest.mark.parametrize("s,slot0,masked", [(7, 0, False), (130, 10, False), (512, 0, False), (300, 0, True),
+                                            (2048, 0, False)])
+def test_attention_prefill_long(impl, rep, s, slot0, masked):
+    """Prefill attention at real prompt lengths (S up to 2048) with left padding (kv_start) or a general
+    key mask, against an fp32 PyTorch reference; impl 2 = GQA-shared 32x32 MFMA kernel, 1 = v1."""
+    e = ops.ext()
+    if impl == 1 and s > 512:
+        pytest.skip("v1 is the A/B baseline; long shapes covered by impl 2")
+    b, hkv, dh = 2, 2, 128
+    h = hkv * rep
+    t = slot0 + s + 5
+    g = torch.Generator(device=DEV).manual_seed(s * 10 + rep)
+    kc = (torch.randn(b, hkv, t, dh, device=DEV, generator=g) * 0.5).to(BF16)
+    vc = torch.randn(b, hkv, t, dh, device=DEV, generator=g).to(BF16)
+    q = torch.randn(b, s, h, dh, device=DEV, generator=g).to(BF16)
+    kv_start = torch.tensor([0, slot0 + s // 3], dtype=torch.int32, device=DEV)  # row 1 left-padded
+    mask = None
+    if masked:
+        mask = (torch.rand(b, t, device=DEV, generator=g) > 0.3).to(torch.uint8)
+        kv_start.zero_()
+    slot = torch.tensor([slot0], dtype=torch.int32, device=DEV)
+    try:
+        e.attn_prefill_set_impl(impl)
+        got = ops.attention(q, kc, vc, slot, kv_start, mask)
+        torch.cuda.synchronize()
+    finally:
+        e.attn_prefill_set_impl(2)
+    want = _attn_ref_gpu(q, kc, vc, slot0, kv_start, mask)
+    assert torch.isfinite(got.float()).all()
+    err = (got.float() - want).abs().max().item()
+    assert err < 3e-2, err
+    if not masked and s // 3 > 0:  # left-pad queries of row 1 (no valid key) output exactly 0
+        assert got.reshape(b, s, h * dh)[1, : s // 3].float().abs().max().item() == 0.0
+
+
+def test_attention_prefill_8k():
+    """S = 8192 causal prefill (Llama-3 max_seq_len), rep 4, one batch row."""
+    b, hkv, rep, s, dh = 1, 2, 4, 8192, 128
+    h = hkv * rep
+    g = torch.Generator(device=DEV).manual_seed(3)
+    kc = (torch.randn(b, hkv, s, dh, device=DEV, generator=g) * 0.5).to(BF16)
+    vc = torch.randn(b, hkv, s, dh, device=DEV, generator=g).to(BF16)
+    q = torch.randn(b, s, h, dh, device=DEV, generator=g).to(BF16)
+    kv_start = torch.zeros(b, dtype=torch.int32, device=DEV)
+    got = ops.attention(q, kc, vc, torch.zeros(1, dtype=torch.int32, device=DEV), kv_start)
+    want = _attn_ref_gpu(q, kc, vc, 0, kv_start, chunk=256)
+    err = (got.float() - want).abs().max().item()
+    assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("rep", [4, 8])
+def test_attention_decode_8k(rep):
+    """Decode attention over an 8192-slot cache (long context), left padding on one row."""
+    b, hkv, t, dh = 2, 2, 8192, 128
+    h = hkv * rep
+    g = torch.Generator(device=DEV).manual_seed(rep)
+    kc = (torch.randn(b, hkv, t, dh, device=DEV, generator=g) * 0.5).to(BF16)
+    vc = torch.randn(b, hkv, t, dh, device=DEV, generator=g).to(BF16)
+    q = torch.randn(b, 1, h, dh, device=DEV, generator=g).to(BF16)
+    slot0 = t - 1
+    kv_start = torch.tensor([0, 3000], dtype=torch.int32, device=DEV)
+    got = ops.attention(q, kc, vc, torch.tensor([slot0], dtype=torch.int32, device=DEV), kv_start)
+    want = _attn_ref_gpu(q, kc, vc, slot0, kv_start)
+    err = (got.float() - want).abs().max().item()
+    assert err < 2e-2, err
+
+
 def test_argmax_first_index():
     x = torch.randn(4, 128256)
     x[1, 77] = 100.0

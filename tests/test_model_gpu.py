@@ -133,7 +133,7 @@ def test_precision_highest_logits():
     """precision='highest' (jax_test.py:433): fp32 lm_head weights + fp32 GEMM; closer to the fp32
     oracle than the default bf16 lm_head."""
     cfg = gpu_config()
-    _, _, oracle, params = build(cfg, seed=17)
+    _, oracle, _, params = build(cfg, seed=17)
     hi = LLaMAForCausalLM(cfg, device=DEV, _do_init=False, precision="highest").load_params(params)
     lo = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).load_params(params)
     toks = torch.randint(3, cfg.vocab_size, (2, 10), dtype=torch.int32)

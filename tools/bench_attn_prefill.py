@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Prefill attention throughput (causal, GQA) at real model shapes: TFLOP/s of impl 2 (GQA-shared
+32x32x16 MFMA flash kernel) vs impl 1 (v1). FLOPs counted for the causal triangle only:
+4 * B * H * Dh * S (S + 1) / 2. Prints one JSON line per (shape, impl)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from jax_llama_amd import ops  # noqa: E402
+
+SHAPES = [  # (name, B, S, H, Hkv)
+    ("8b_b1_s2048", 1, 2048, 32, 8), ("8b_b16_s2048", 16, 2048, 32, 8), ("8b_b1_s8192", 1, 8192, 32, 8),
+    ("8b_b2048_s128", 2048, 128, 32, 8), ("70b_b1_s2048", 1, 2048, 64, 8), ("7b_b16_s2048", 16, 2048, 32, 32),
+]
+
+
+def main():
+    e = ops.ext()
+    for name, b, s, h, hkv in SHAPES:
+        g = torch.Generator(device="cuda").manual_seed(0)
+        kc = torch.randn(b, hkv, s, 128, device="cuda", generator=g).to(torch.bfloat16)
+        vc = torch.randn(b, hkv, s, 128, device="cuda", generator=g).to(torch.bfloat16)
+        q = torch.randn(b, s, h, 128, device="cuda", generator=g).to(torch.bfloat16)
+        ks = torch.zeros(b, dtype=torch.int32, device="cuda")
+        slot = torch.zeros(1, dtype=torch.int32, device="cuda")
+        flops = 4.0 * b * h * 128 * s * (s + 1) / 2
+        ref = None
+        for impl in (2, 1):
+            if impl == 1 and s * s * b * h > 2048 * 2048 * 16 * 32:
+                continue
+            e.attn_prefill_set_impl(impl)
+            o = ops.attention(q, kc, vc, slot, ks)
+            torch.cuda.synchronize()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            n = 5
+            ev[0].record()
+            for _ in range(n):
+                ops.attention(q, kc, vc, slot, ks)
+            ev[1].record()
+            torch.cuda.synchronize()
+            us = ev[0].elapsed_time(ev[1]) * 1000 / n
+            diff = 0.0 if ref is None else float((o.float() - ref.float()).abs().max())
+            ref = o if ref is None else ref
+            print(json.dumps({"shape": name, "impl": impl, "us": round(us, 1),
+                              "tflops": round(flops / us / 1e6, 1), "max_diff_vs_impl2": round(diff, 5)}), flush=True)
+        e.attn_prefill_set_impl(2)
+        del kc, vc, q
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

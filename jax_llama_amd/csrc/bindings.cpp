@@ -9,6 +9,7 @@
 #include "kernels/launchers.h"
 
 #define MODE_QKV_ID 3
+#define MODE_ARGMAX_ID 8  // common.h MODE_ARGMAX
 
 namespace {
 
@@ -136,6 +137,32 @@ void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t
   qa.res_bf16 = mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr;
   run_skinny(x, w, n, k, out.data_ptr(), mode, rms_eps, accumulate, out.scalar_type() == torch::kFloat32, &qa,
              variant, ws, tickets);
+}
+
+// greedy lm_head at decode M (<= 64): GEMV with a first-max epilogue -> [M][N / 16] (value, index) partials in
+// `part`, then one wave per row picks the first maximum (the fp32 logits are never written)
+void linear_skinny_argmax(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, int64_t variant, Tensor part,
+                          Tensor idx, Tensor val) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && (x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16),
+        "x must be fp32/bf16 [M, K]");
+  const int64_t m = x.size(0);
+  check(m <= SKINNY_MAX_M, "linear_skinny_argmax: M too large");
+  check(variant == 1 || variant == 2 || variant == 3 || variant == 5 || variant == 6 || variant == 8 || variant == 9,
+        "argmax: GEMV variants only");
+  check_gpu(part, "part");
+  check(part.scalar_type() == torch::kFloat32 && part.numel() >= m * (n / 16) * 2, "argmax partials too small");
+  check_gpu(idx, "idx");
+  check_gpu(val, "val");
+  check(idx.scalar_type() == torch::kInt32 && val.scalar_type() == torch::kFloat32 && idx.numel() == m &&
+            val.numel() == m,
+        "argmax outputs");
+  jla::QKVArgs qa{};
+  rc(jla::linear_skinny(x.data_ptr(), x.scalar_type() == torch::kFloat32, w.data_ptr(), part.data_ptr(), m, n, k,
+                        MODE_ARGMAX_ID, (float)rms_eps, 0, 1, &qa, variant, stream()),
+     "linear_skinny_argmax");
+  rc(jla::argmax_partials(ptr<float>(part), n / 16, m, ptr<int32_t>(idx), ptr<float>(val), stream()), "argmax_partials");
 }
 
 py::tuple skinny_workspace(int64_t m, int64_t n, int64_t k, int64_t mode) {
@@ -570,6 +597,9 @@ PYBIND11_MODULE(_C, m) {
         [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });
   m.def("linear_qkv", &linear_qkv);
   m.def("skinny_workspace", &skinny_workspace);
+  m.def("linear_skinny_argmax", &linear_skinny_argmax);
+  m.def("attn_set_v3_max_pairs", [](int64_t n) { jla::attn_set_v3_max_pairs((int)n); });
+  m.def("attn_set_v1_min_wgs", [](int64_t n) { jla::attn_set_v1_min_wgs((int)n); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
         py::arg("nsplit"));

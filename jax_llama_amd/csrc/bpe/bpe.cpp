@@ -9,6 +9,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 #include <string>
@@ -96,9 +97,43 @@ class BPE {
   std::unordered_map<std::string_view, int, SVHash> map_;
 };
 
+// Python str.isspace() for one code point (Unicode White_Space as CPython classifies it).
+bool is_space(char32_t c) {
+  if (c == 0x20 || (c >= 0x09 && c <= 0x0d) || (c >= 0x1c && c <= 0x1f)) return true;
+  if (c < 0x85) return false;
+  return c == 0x85 || c == 0xa0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200a) || c == 0x2028 || c == 0x2029 ||
+         c == 0x202f || c == 0x205f || c == 0x3000;
+}
+
+// Boundaries (code-point offsets, ascending, including 0 and len) that cut `text` into windows of at most
+// `window` code points, and cut every maximal run of same-class characters (whitespace / non-whitespace)
+// inside a window at offsets run_start + k * max_run (k >= 1). This is the Llama-3 tokenizer's guard
+// against pathological inputs (reference llama3_tokenizer.py:131-146,178-202: 400k-char windows,
+// 25k-char same-class runs); the pieces between boundaries are encoded independently.
+std::vector<size_t> chunk_bounds(const std::u32string& text, size_t window, size_t max_run) {
+  std::vector<size_t> cuts{0};
+  const size_t n = text.size();
+  for (size_t w0 = 0; w0 < n; w0 += window) {
+    const size_t w1 = std::min(n, w0 + window);
+    if (w0 > 0) cuts.push_back(w0);
+    size_t a = w0;  // start of the current same-class run
+    while (a < w1) {
+      const bool sp = is_space(text[a]);
+      size_t b = a + 1;
+      while (b < w1 && is_space(text[b]) == sp) ++b;
+      for (size_t c = a + max_run; c < b; c += max_run) cuts.push_back(c);
+      a = b;
+    }
+  }
+  if (n > 0) cuts.push_back(n);
+  return cuts;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_bpe, m) {
+  m.def("chunk_bounds", &chunk_bounds, py::arg("text"), py::arg("window"), py::arg("max_run"));
+  m.def("is_space", [](const std::u32string& c) { return c.size() == 1 && is_space(c[0]); });
   m.doc() = "jax_llama_amd tiktoken-compatible BPE merge core";
   py::class_<BPE>(m, "BPE")
       .def(py::init<>())

@@ -256,6 +256,160 @@ __global__ void __launch_bounds__(AD_WAVES * 64)
 
 
 // ---------------------------------------------------------------------------------------------
+// v3 (small batch): ONE workgroup per (batch row, kv head) and no cross-workgroup merge.
+//
+// At B <= 64 the decode attention moves well under a MiB and v1's critical path is latency: load ->
+// score -> publish partials -> ticket -> last arriver reloads every split -> merge (~10 us at B = 1
+// whatever the split count: profiles/r2_attn_decode_small_batch_ab.jsonl). Here 8 waves split the
+// valid keys [kv_start, slot] into interleaved 16-lane rows (chunk of 32 * KPG keys per step, the next
+// chunk's K/V loads issued before the current chunk is scored), every wave keeps its own running
+// (max, sum, o) per query head (online softmax, no barrier in the loop), and the 8 waves merge once
+// through LDS. Rows with no valid key output 0.
+constexpr int AD3_WAVES = 8;
+
+template <int REP, int KPG>
+__global__ void __launch_bounds__(AD3_WAVES * 64)
+    attn_decode_v3_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                          const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
+                          const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int H,
+                          int Hkv, int T, int t_cap, float scale) {
+  constexpr int CH = AD3_WAVES * 4 * KPG;  // keys per chunk (8 waves x 4 groups x KPG rows)
+  __shared__ float sm_m[AD3_WAVES][REP];
+  __shared__ float sm_l[AD3_WAVES][REP];
+  __shared__ float sm_o[AD3_WAVES][REP][AD_DH];
+
+  const int kvh = blockIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int slot = slot_ptr[0];
+  const int lo = kv_start[b];
+  const int hi_key = min(slot + 1, t_cap);  // keys [lo, hi_key)
+  const int h0 = kvh * REP;
+  const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
+  const size_t head_off = ((size_t)b * Hkv + kvh) * T * AD_DH + 8 * li;
+
+  float qf[REP][8];
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(q + ((size_t)b * H + h0 + h) * AD_DH + 8 * li);
+    unpack8(v, qf[h]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qf[h][e] *= scale;
+  }
+  float m_h[REP], l_h[REP], o[REP][8];
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    m_h[h] = -INFINITY;
+    l_h[h] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
+  }
+
+  const int c_begin = lo - (lo % CH);
+  // row r of this lane's group in chunk c0: key c0 + 32 r + 4 w + g (one wave load = 4 consecutive rows)
+  u32x4 kr[KPG], vr[KPG];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < KPG; ++r) {
+      const int j = min(max(c0 + 32 * r + 4 * w + g, 0), hi_key - 1);
+      kr[r] = *reinterpret_cast<const u32x4*>(kc + head_off + (size_t)j * AD_DH);
+      vr[r] = *reinterpret_cast<const u32x4*>(vc + head_off + (size_t)j * AD_DH);
+    }
+  };
+  if (c_begin < hi_key && lo < hi_key) load(c_begin);
+  for (int c0 = c_begin; c0 < hi_key && lo < hi_key; c0 += CH) {
+    u32x4 kcur[KPG], vcur[KPG];
+#pragma unroll
+    for (int r = 0; r < KPG; ++r) {
+      kcur[r] = kr[r];
+      vcur[r] = vr[r];
+    }
+    if (c0 + CH < hi_key) load(c0 + CH);  // next chunk in flight while this one is scored
+    float sc[REP][KPG];
+#pragma unroll
+    for (int r = 0; r < KPG; ++r) {
+      const int j = c0 + 32 * r + 4 * w + g;
+      bool valid = j >= lo && j < hi_key;
+      if (mrow) valid = valid && j < mask_len && mrow[j] != 0;
+      float kf[8];
+      unpack8(kcur[r], kf);
+#pragma unroll
+      for (int h = 0; h < REP; ++h) {
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += qf[h][e] * kf[e];
+        d = row16_sum(d);
+        sc[h][r] = valid ? d : -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      float mx = sc[h][0];
+#pragma unroll
+      for (int r = 1; r < KPG; ++r) mx = fmaxf(mx, sc[h][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m_h[h], mx);
+      if (mn == -INFINITY) continue;  // nothing valid for this wave yet (wave-uniform)
+      const float alpha = __expf(m_h[h] - mn);  // m_h = -inf -> 0
+      l_h[h] *= alpha;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[h][e] *= alpha;
+      m_h[h] = mn;
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) {
+        const float p = sc[h][r] == -INFINITY ? 0.f : __expf(sc[h][r] - mn);
+        l_h[h] += p;  // every lane of the group adds the same p: counted once per group below
+        float vf[8];
+        unpack8(vcur[r], vf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[h][e] += p * vf[e];
+      }
+    }
+  }
+  // ---- per wave: sum the 4 groups (same max), then merge the 8 waves through LDS
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    float l = l_h[h];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = o[h][e];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      o[h][e] = v;
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm_o[w][h][8 * li + e] = o[h][e];
+      if (li == 0) {
+        sm_m[w][h] = m_h[h];
+        sm_l[w][h] = l / 16.f;  // each of the 16 lanes of a group added p once
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < REP * AD_DH; i += AD3_WAVES * 64) {
+    const int h = i / AD_DH, d = i - h * AD_DH;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < AD3_WAVES; ++ww) M = fmaxf(M, sm_m[ww][h]);
+    float num = 0.f, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < AD3_WAVES; ++ww) {
+        const float mw = sm_m[ww][h];
+        const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
+        num += f * sm_o[ww][h][d];
+        den += f * sm_l[ww][h];
+      }
+    }
+    out[((size_t)b * H + h0 + h) * AD_DH + d] = f2bf(den > 0.f ? num / den : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // v2 (default): streaming decode attention, one WAVE per work item (batch row, kv head, key split).
 //
 // v1 above gives every 128-key chunk its own workgroup (load everything, compute, merge), so a CU's
@@ -496,7 +650,16 @@ __global__ void __launch_bounds__(64)
   }
 }
 
-static int kpg_v1(int rep) { return rep <= 4 ? 8 : (rep == 8 ? 4 : 2); }
+// v1 keys per 16-lane group: the largest chunk (fewest splits to merge) that still gives the launch
+// ~256+ workgroups -- at small batch the kernel is latency-bound and more, shorter splits finish sooner
+// (B = 1, T = 384: 24 -> 96 workgroups)
+static int g_v1_min_wgs = 256;
+void attn_set_v1_min_wgs(int n) { g_v1_min_wgs = n; }
+static int kpg_v1(int rep, int B = 1 << 20, int Hkv = 1, int T = 1) {
+  int kpg = rep <= 4 ? 8 : (rep == 8 ? 4 : 2);
+  while (kpg > 2 && (long long)B * Hkv * ((T + 16 * kpg - 1) / (16 * kpg)) < g_v1_min_wgs) kpg >>= 1;
+  return kpg;
+}
 static int g_kpg_small = 8, g_ns = 2;  // v2 ring geometry for REP <= 4 (A/B: attn_set_impl)
 static int kpg_v2(int rep) { return rep <= 4 ? g_kpg_small : (rep == 8 ? 2 : 1); }
 
@@ -514,12 +677,20 @@ void attn_set_impl(int impl, int waves_target) {
 // chunk-per-workgroup design is as fast or faster (profiles/r1_attn_decode_v2_ab.jsonl,
 // r1_attn_decode_v2_geometry.jsonl), so smaller batches stay on v1.
 static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_attn_v2_min_pairs; }
+// v3 (one workgroup per (row, kv head), no split merge) below this many (row, kv head) pairs
+static int g_attn_v3_max_pairs = 1024;
+void attn_set_v3_max_pairs(int n) { g_attn_v3_max_pairs = n; }
+static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv) && B * Hkv <= g_attn_v3_max_pairs; }
 
-int attn_decode_chunk(int B, int Hkv, int T, int rep) { return use_v2(B, Hkv) ? 4 * kpg_v2(rep) : 16 * kpg_v1(rep); }
+int attn_decode_chunk(int B, int Hkv, int T, int rep) {
+  if (use_v3(B, Hkv, rep)) return T;
+  return use_v2(B, Hkv) ? 4 * kpg_v2(rep) : 16 * kpg_v1(rep, B, Hkv, T);
+}
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
+  if (use_v3(B, Hkv, rep)) return 1;
   if (!use_v2(B, Hkv)) {
-    const int ch = 16 * kpg_v1(rep);
+    const int ch = 16 * kpg_v1(rep, B, Hkv, T);
     return (T + ch - 1) / ch;
   }
   const int pairs = B * Hkv;
@@ -537,24 +708,37 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   const int rep = H / Hkv;
   if (attn_decode_splits(B, Hkv, t_cap, rep) != nsplit) return -2;
   const float scale = 1.f / sqrtf((float)Dh);
+  if (use_v3(B, Hkv, rep)) {
+    dim3 grid3(Hkv, B);
+#define JLA_AD3(R, K)                                                                                          \
+  if (rep == R) {                                                                                              \
+    attn_decode_v3_kernel<R, K><<<grid3, AD3_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, \
+                                                                 out, H, Hkv, T, t_cap, scale);                \
+    JLA_CHECK_LAUNCH();                                                                                        \
+    return 0;                                                                                                  \
+  }
+    JLA_AD3(1, 4) JLA_AD3(2, 4) JLA_AD3(4, 2) JLA_AD3(8, 1)
+#undef JLA_AD3
+    return -1;
+  }
   if (!use_v2(B, Hkv)) {
     dim3 grid(nsplit, Hkv, B);
-#define JLA_AD(R)                                                                                              \
-  case R:                                                                                                     \
-    attn_decode_v1_kernel<R, (R <= 4 ? 8 : (R == 8 ? 4 : 2))><<<grid, AD_WAVES * 64, 0, s>>>(                  \
-        q, kc, vc, slot, kv_start, key_mask, mask_len, out, ws, tickets, H, Hkv, T, t_cap, nsplit, scale);     \
-    break;
-    switch (rep) {
-      JLA_AD(1)
-      JLA_AD(2)
-      JLA_AD(4)
-      JLA_AD(8)
-      JLA_AD(16)
-      default: return -1;
-    }
+    const int kpg = kpg_v1(rep, B, Hkv, t_cap);
+#define JLA_AD(R, K)                                                                                           \
+  if (rep == R && kpg == K) {                                                                                  \
+    attn_decode_v1_kernel<R, K><<<grid, AD_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len,  \
+                                                               out, ws, tickets, H, Hkv, T, t_cap, nsplit,     \
+                                                               scale);                                         \
+    JLA_CHECK_LAUNCH();                                                                                        \
+    return 0;                                                                                                  \
+  }
+    JLA_AD(1, 8) JLA_AD(1, 4) JLA_AD(1, 2)
+    JLA_AD(2, 8) JLA_AD(2, 4) JLA_AD(2, 2)
+    JLA_AD(4, 8) JLA_AD(4, 4) JLA_AD(4, 2)
+    JLA_AD(8, 4) JLA_AD(8, 2)
+    JLA_AD(16, 2)
+    return -1;
 #undef JLA_AD
-    JLA_CHECK_LAUNCH();
-    return 0;
   }
   const int items = B * Hkv * nsplit;
   int split_len = (t_cap + nsplit - 1) / nsplit;

@@ -24,6 +24,7 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define MODE_RESIDUAL 1
 #define MODE_SWIGLU 2
 #define MODE_QKV 3
+#define MODE_ARGMAX 8  // greedy lm_head: first-max (value, index) partials instead of logits
 
 #define JLA_DEV __device__ __forceinline__
 

@@ -27,7 +27,6 @@ constexpr int G_THREADS = 256;
 constexpr int G_AFR = 16, G_BFR = 16;
 constexpr int G_STAGE_U4 = (G_AFR + G_BFR) * 64;  // u32x4 per stage (32 KiB); 8 per thread
 constexpr int MODE_PARTIAL = 7;                   // split-K: fp32 partial tile to the workspace
-constexpr int MODE_ARGMAX = 8;                    // greedy lm_head: per-(row, 64 columns) first-max partials
 
 template <int MODE>
 __global__ void __launch_bounds__(G_THREADS)
@@ -1515,6 +1514,13 @@ __global__ void __launch_bounds__(256)
     idx[row] = bi == 0x7fffffff ? 0 : bi;
     val[row] = bv;
   }
+}
+
+int argmax_partials(const float* part, int P, int M, int32_t* idx, float* val, hipStream_t s) {
+  if (M <= 0) return 0;
+  argmax_partials_kernel<<<(M + 3) / 4, 256, 0, s>>>(reinterpret_cast<const float2*>(part), P, M, idx, val);
+  JLA_CHECK_LAUNCH();
+  return 0;
 }
 
 size_t gemm_argmax_workspace_floats(int M, int N) { return (size_t)M * ((N + G2_BN - 1) / G2_BN) * 4 * 2; }

@@ -163,7 +163,9 @@ __global__ void __launch_bounds__(NW * 64)
   // hand-counted ring (see asm_load_nt) where the assembly check passes: every bf16-activation
   // variant (the decode path: the residual stream's bf16 mirror) and fp32 at MT = 1
   // (bf16 MT = 2 with one tile fails the check: hipcc reuses in-flight ring registers there).
-  constexpr bool ASM = MT == 1 || (sizeof(XT) == 2 && !(MT == 2 && NT == 1));
+  // (the 16-wave and doubled-ring variants 8/9 use compiler-counted loads: their ring fails the check)
+  constexpr int U_BASE = ((NT == 1 ? 8 : 4) / MT) < 2 ? 2 : ((NT == 1 ? 8 : 4) / MT);
+  constexpr bool ASM = (MT == 1 || (sizeof(XT) == 2 && !(MT == 2 && NT == 1))) && NW <= 8 && U <= U_BASE;
   auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
     const bool valid = i < n;
     const size_t ks = (size_t)(w + i * NW);
@@ -265,6 +267,24 @@ __global__ void __launch_bounds__(NW * 64)
       const int m = mt * 16 + ml;
       const int ln = (ml >> 2) * 16 + c, i = ml & 3;
       const int tile = nt0 + t;
+      if constexpr (MODE == MODE_ARGMAX) {
+        // first max of this (row, 16-column tile): (value, index) partial [M][N / 16]; every lane of the
+        // 16-lane group takes part in the shuffles (invalid rows/tiles compete with -inf)
+        const bool ok = m < M && tile < NTT;
+        float bv = ok ? reduced(mt, t, ln, i) * inv_rms[min(m, MT * 16 - 1)] : -INFINITY;
+        int bi = ok ? tile * 16 + c : 0x7fffffff;
+#pragma unroll
+        for (int sh = 1; sh < 16; sh <<= 1) {
+          const float ov = __shfl_xor(bv, sh, 64);
+          const int oi = __shfl_xor(bi, sh, 64);
+          if (ov > bv || (ov == bv && oi < bi)) {
+            bv = ov;
+            bi = oi;
+          }
+        }
+        if (ok && c == 0) static_cast<float2*>(out)[(size_t)m * NTT + tile] = make_float2(bv, __int_as_float(bi));
+        continue;
+      }
       if (m >= M || tile >= NTT) continue;
       const float v = reduced(mt, t, ln, i) * inv_rms[m];
       const int col = tile * 16 + c;
@@ -309,14 +329,16 @@ __global__ void __launch_bounds__(NW * 64)
   }
 }
 
-template <typename XT, int MT, int NT, int MODE, int NW>
+template <typename XT, int MT, int NT, int MODE, int NW, int DEEP = 0>
 static int launch_skinny(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
                          int accumulate, int out_f32, const QKVArgs& qa, hipStream_t s) {
   // k-steps in flight per wave: 8 KiB of weights per wave at MT = 1; fp32 activations double the
-  // activation registers, so MT > 1 keeps fewer steps in flight to stay spill-free.
+  // activation registers, so MT > 1 keeps fewer steps in flight to stay spill-free. DEEP = 1 doubles
+  // the ring (bf16 activations at M = 17..64: more bytes in flight per wave).
   constexpr int U0 = (NT == 1) ? 8 : 4;
   constexpr int UD = MT;
-  constexpr int U = (U0 / UD) < 2 ? 2 : (U0 / UD);
+  constexpr int U1 = (U0 / UD) < 2 ? 2 : (U0 / UD);
+  constexpr int U = DEEP ? 2 * U1 : U1;
   const int NTT = N >> 4;
   const int grid = (NTT + NT - 1) / NT;
   const size_t lds = sizeof(float) * (NW * MT * NT * 256 + NW * MT * 16 + MT * 16);
@@ -369,6 +391,14 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       return launch_skinny<XT, MT, 4, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
     if (variant == 6)
       return launch_skinny<XT, MT, 2, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    // variants 8 / 9 (bf16 activations, M > 16): 1 tile per workgroup, 16 waves / 8 waves with a doubled ring --
+    // more weight + activation bytes in flight per CU for the latency-bound small-N projections
+    if constexpr (MT > 1 && sizeof(XT) == 2 && MODE != MODE_SWIGLU) {
+      if (variant == 8)
+        return launch_skinny<XT, MT, 1, MODE, 16>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      if (variant == 9)
+        return launch_skinny<XT, MT, 1, MODE, 8, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    }
   }
   if constexpr (MODE == MODE_SWIGLU) {
     return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
@@ -404,6 +434,7 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
     case MODE_RESIDUAL: return dispatch_mt<XT, MODE_RESIDUAL>(JLA_ARGS, 1, qa, variant, s);          \
     case MODE_SWIGLU: return dispatch_mt<XT, MODE_SWIGLU>(JLA_ARGS, 0, qa, variant, s);              \
     case MODE_QKV: return dispatch_mt<XT, MODE_QKV>(JLA_ARGS, 0, qa, variant, s);                    \
+    case MODE_ARGMAX: return dispatch_mt<XT, MODE_ARGMAX>(JLA_ARGS, 0, qa, variant, s);              \
     default: return -1;                                                                              \
   }
   if (x_is_f32) {

@@ -55,6 +55,8 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
 int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
                 int32_t* idx, float* val, hipStream_t s);
 size_t gemm_argmax_workspace_floats(int M, int N);
+// first max per row over [M][P] (value, index) float2 partials
+int argmax_partials(const float* part, int P, int M, int32_t* idx, float* val, hipStream_t s);
 size_t gemm_sk_workspace_floats();
 int gemm_sk_tickets(int M, int N, int K);
 int gemm_sk_active(int M, int N, int K);
@@ -66,6 +68,8 @@ int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const in
                   hipStream_t s);
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep);
+void attn_set_v1_min_wgs(int n);
+void attn_set_v3_max_pairs(int n);  // single-workgroup-per-(row, kv head) decode kernel up to n pairs (0: off)  // v1 split sizing: smallest chunk giving >= n workgroups (default 256)
 void attn_set_impl(int impl, int waves_target);  // 2 = streaming (default), 1 = v1 (A/B)
 int attn_decode_splits(int B, int Hkv, int T, int rep);
 // ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)

@@ -349,14 +349,29 @@ def argmax(logits: torch.Tensor):
 
 
 ARGMAX_FUSED_MIN_M = 256  # one 256-row tile or more: the tiled GEMM is the lm_head kernel anyway
+# decode M <= 64: the argmax runs in the lm_head GEMV's epilogue (per-16-column partials); JLA_SKINNY_ARGMAX=0 off
+SKINNY_ARGMAX = os.environ.get("JLA_SKINNY_ARGMAX", "1") != "0"
 
 
 def linear_argmax(x: torch.Tensor, w, rms_eps: Optional[float] = None):
     """Greedy token of ``[inv_rms(x) *] x @ W^T`` (the lm_head): ``(idx int32[M], val fp32[M])``, first
-    max like ``jnp.argmax``. From ARGMAX_FUSED_MIN_M rows on the GPU the argmax runs in the GEMM
-    epilogue (``gemm_argmax``: the fp32 logits never reach HBM); otherwise ``linear`` + ``argmax``."""
+    max like ``jnp.argmax``. On the GPU the argmax runs in the GEMM epilogue and the fp32 logits never
+    reach HBM: in the decode GEMV's (M <= 64, ``linear_skinny_argmax``) or in the tiled GEMM's (from
+    ARGMAX_FUSED_MIN_M rows, ``gemm_argmax``); in between ``linear`` + ``argmax``."""
     m = x.shape[0]
-    if not _is_gpu(x) or m < ARGMAX_FUSED_MIN_M:
+    if not _is_gpu(x):
+        return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
+    if m <= ext().SKINNY_MAX_M and SKINNY_ARGMAX:
+        e = ext()
+        v = _variant(e, x, w, MODE_STORE)  # same main loop as the logits GEMV: the tuned variant applies
+        if v in (1, 2, 3, 5, 6, 8, 9):
+            part = workspace.get("skinny_argmax", m * (w.n // 16) * 2, torch.float32, x.device)
+            idx = torch.empty(m, dtype=torch.int32, device=x.device)
+            val = torch.empty(m, dtype=torch.float32, device=x.device)
+            e.linear_skinny_argmax(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), v, part, idx,
+                                   val)
+            return idx, val
+    if m < ARGMAX_FUSED_MIN_M:
         return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
     e = ext()
     if e.gemm_get_impl() != 2:

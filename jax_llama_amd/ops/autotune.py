@@ -8,7 +8,8 @@ candidate on a rotating set of scratch weights (> Infinity Cache, so each call s
 as in a real decode step) and caches the winner. Never runs under hipGraph capture; shapes first
 seen during capture fall back to the static heuristic.
 
-Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG,
+Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG, 8 / 9 = 1-tile GEMV
+with 16 waves / a doubled register ring (M > 16, bf16 activations),
 4 = split-K skinny GEMM, 7 = tiled MFMA GEMM with split-K (gemm.hip; a candidate for M > 16, always used
 for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
 """
@@ -41,7 +42,7 @@ def heuristic(m: int, n: int, k: int, mode: int) -> int:
     return 1
 
 
-def candidates(m: int, n: int) -> Tuple[int, ...]:
+def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tuple[int, ...]:
     # M > 16: two or four activation m-tiles per weight fragment, so the 2/4-tile GEMV workgroups
     # (fewer activation re-reads) and the tiled MFMA GEMM win on some shapes (M=24..64 sweep,
     # profiles/r1_decode_m32_variants.jsonl: qkv -> 6, gate_up -> 5, down/lm_head -> 7 at M=32)
@@ -50,6 +51,8 @@ def candidates(m: int, n: int) -> Tuple[int, ...]:
         c.insert(1, 5)
     if m > 16:
         c.append(TILED_VARIANT)
+        if not swiglu and bf16_x:
+            c += [8, 9]  # 1-tile GEMV with 16 waves / a doubled ring (bf16 activations only)
     return tuple(c)
 
 
@@ -65,7 +68,7 @@ def choose(e, x: torch.Tensor, w, mode: int, run) -> int:
         return v
     if not ENABLED or torch.cuda.is_current_stream_capturing():
         return heuristic(m, w.n, w.k, mode)
-    v = _measure(x, w, run, candidates(m, w.n))
+    v = _measure(x, w, run, candidates(m, w.n, swiglu=(mode == 2), bf16_x=(x.dtype == torch.bfloat16)))
     _CACHE[key] = v
     return v
 

@@ -228,7 +228,7 @@ class DecodeEngine:
     def _graph_state(self):
         # the graph records buffer addresses: the scratch workspaces (ops.workspace) and the sampling mode
         return (self.gc.do_sample, self.key_mask is not None, ops.workspace.generation, _fused_greedy(),
-                ops.ARGMAX_FUSED_MIN_M, self.model.comm.reduce_dtype)
+                ops.ARGMAX_FUSED_MIN_M, ops.SKINNY_ARGMAX, self.model.comm.reduce_dtype)
 
     def _ensure_graph(self):
         if self._graph is not None and self._graph_key == self._graph_state():

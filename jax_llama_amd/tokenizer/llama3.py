@@ -12,7 +12,7 @@ from __future__ import annotations
 import logging
 import os
 from pathlib import Path
-from typing import AbstractSet, Collection, Dict, Iterator, List, Literal, Sequence, TypedDict, Union
+from typing import AbstractSet, Collection, Dict, List, Literal, Sequence, TypedDict, Union
 
 from .bpe import Encoding, load_tiktoken_bpe
 
@@ -62,27 +62,25 @@ class Tokenizer:
         self.pad_id: int = -1
         self.stop_tokens = {self.special_tokens["<|end_of_text|>"], self.special_tokens["<|eot_id|>"]}
 
+    # guards against pathological inputs (reference llama3_tokenizer.py:131-146): the text is encoded in
+    # windows of at most WINDOW_CHARS code points, and a run of more than MAX_RUN_CHARS characters of one
+    # class (whitespace / non-whitespace) is cut into MAX_RUN_CHARS-sized pieces
+    WINDOW_CHARS = 400_000
+    MAX_RUN_CHARS = 25_000
+
     def encode(self, s: str, *, bos: bool, eos: bool,
                allowed_special: Union[Literal["all"], AbstractSet[str]] = set(),
                disallowed_special: Union[Literal["all"], Collection[str]] = ()) -> List[int]:
-        assert type(s) is str
-        TIKTOKEN_MAX_ENCODE_CHARS = 400_000
-        MAX_NO_WHITESPACES_CHARS = 25_000
-        substrs = (
-            substr
-            for i in range(0, len(s), TIKTOKEN_MAX_ENCODE_CHARS)
-            for substr in self._split_whitespaces_or_nonwhitespaces(
-                s[i: i + TIKTOKEN_MAX_ENCODE_CHARS], MAX_NO_WHITESPACES_CHARS)
-        )
-        t: List[int] = []
-        for substr in substrs:
-            t.extend(self.model.encode(substr, allowed_special=allowed_special,
-                                       disallowed_special=disallowed_special))
-        if bos:
-            t.insert(0, self.bos_id)
+        if not isinstance(s, str):
+            raise TypeError(f"expected str, got {type(s).__name__}")
+        bounds = chunk_bounds(s, self.WINDOW_CHARS, self.MAX_RUN_CHARS)
+        ids: List[int] = [self.bos_id] if bos else []
+        for lo, hi in zip(bounds, bounds[1:]):
+            ids += self.model.encode(s[lo:hi], allowed_special=allowed_special,
+                                     disallowed_special=disallowed_special)
         if eos:
-            t.append(self.eos_id)
-        return t
+            ids.append(self.eos_id)
+        return ids
 
     def decode(self, t: Sequence[int]) -> str:
         return self.model.decode(list(t))
@@ -90,45 +88,56 @@ class Tokenizer:
     def __len__(self) -> int:
         return self.n_words
 
-    @staticmethod
-    def _split_whitespaces_or_nonwhitespaces(s: str, max_consecutive_slice_len: int) -> Iterator[str]:
-        current_slice_len = 0
-        current_slice_is_space = s[0].isspace() if len(s) > 0 else False
-        slice_start = 0
-        for i in range(len(s)):
-            is_now_space = s[i].isspace()
-            if current_slice_is_space ^ is_now_space:
-                current_slice_len = 1
-                current_slice_is_space = is_now_space
-            else:
-                current_slice_len += 1
-                if current_slice_len > max_consecutive_slice_len:
-                    yield s[slice_start:i]
-                    slice_start = i
-                    current_slice_len = 1
-        yield s[slice_start:]
+
+def _chunk_bounds_py(text: str, window: int, max_run: int) -> List[int]:
+    """Python twin of the C++ ``chunk_bounds`` (used when the native core is not built)."""
+    cuts = [0]
+    for w0 in range(0, len(text), window):
+        w1 = min(len(text), w0 + window)
+        if w0:
+            cuts.append(w0)
+        a = w0
+        while a < w1:
+            sp = text[a].isspace()
+            b = a + 1
+            while b < w1 and text[b].isspace() == sp:
+                b += 1
+            cuts.extend(range(a + max_run, b, max_run))
+            a = b
+    if text:
+        cuts.append(len(text))
+    return cuts
+
+
+def chunk_bounds(text: str, window: int, max_run: int) -> List[int]:
+    try:
+        from .._bpe import chunk_bounds as native
+    except ImportError:
+        return _chunk_bounds_py(text, window, max_run)
+    return native(text, window, max_run)
 
 
 class ChatFormat:
+    """Llama-3 chat template (reference ``llama3_tokenizer.py:205-232``): every message is
+    ``<|start_header_id|> role <|end_header_id|> "\n\n" content.strip() <|eot_id|>``; a dialog prompt is
+    ``<|begin_of_text|>`` + its messages + an open assistant header."""
+
     def __init__(self, tokenizer: Tokenizer):
         self.tokenizer = tokenizer
 
+    def _special(self, name: str) -> int:
+        return self.tokenizer.special_tokens[f"<|{name}|>"]
+
+    def _text(self, text: str) -> List[int]:
+        return self.tokenizer.encode(text, bos=False, eos=False)
+
     def encode_header(self, message: Message) -> List[int]:
-        tokens = [self.tokenizer.special_tokens["<|start_header_id|>"]]
-        tokens.extend(self.tokenizer.encode(message["role"], bos=False, eos=False))
-        tokens.append(self.tokenizer.special_tokens["<|end_header_id|>"])
-        tokens.extend(self.tokenizer.encode("\n\n", bos=False, eos=False))
-        return tokens
+        return [self._special("start_header_id"), *self._text(message["role"]), self._special("end_header_id"),
+                *self._text("\n\n")]
 
     def encode_message(self, message: Message) -> List[int]:
-        tokens = self.encode_header(message)
-        tokens.extend(self.tokenizer.encode(message["content"].strip(), bos=False, eos=False))
-        tokens.append(self.tokenizer.special_tokens["<|eot_id|>"])
-        return tokens
+        return self.encode_header(message) + self._text(message["content"].strip()) + [self._special("eot_id")]
 
     def encode_dialog_prompt(self, dialog: Dialog) -> List[int]:
-        tokens = [self.tokenizer.special_tokens["<|begin_of_text|>"]]
-        for message in dialog:
-            tokens.extend(self.encode_message(message))
-        tokens.extend(self.encode_header({"role": "assistant", "content": ""}))
-        return tokens
+        body = [tok for m in dialog for tok in self.encode_message(m)]
+        return [self._special("begin_of_text"), *body, *self.encode_header({"role": "assistant", "content": ""})]

@@ -296,6 +296,35 @@ def test_attention_decode_8k(rep):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("m", [1, 5, 17, 40, 64])
+@pytest.mark.parametrize("variant", [1, 5, 6])
+def test_linear_skinny_argmax(m, variant):
+    """Decode lm_head with the argmax in the GEMV epilogue == stored fp32 logits + first-max argmax,
+    bit for bit (same accumulation order), including an exact tie across two 16-column tiles."""
+    e = ops.ext()
+    n, k = 2048, 512
+    w = PackedLinear.random(n, k, DEV)
+    x = torch.randn(m, k, device=DEV).to(BF16)
+    logits = torch.empty(m, n, dtype=torch.float32, device=DEV)
+    ws, tk = ops._skinny_ws(e, m, n, k, ops.MODE_STORE, x.device)
+    e.linear_skinny(x, w.weight, n, k, logits, ops.MODE_STORE, 1e-5, True, variant, ws, tk)
+    part = torch.empty(m * (n // 16) * 2, dtype=torch.float32, device=DEV)
+    idx = torch.empty(m, dtype=torch.int32, device=DEV)
+    val = torch.empty(m, dtype=torch.float32, device=DEV)
+    e.linear_skinny_argmax(x, w.weight, n, k, 1e-5, variant, part, idx, val)
+    want_v, want_i = logits.max(-1)
+    assert torch.equal(idx.long().cpu(), logits.argmax(-1).cpu())
+    assert torch.equal(val.cpu(), want_v.cpu())
+    # tie: duplicate the weight rows of columns 100 and 900 -> equal logits, first index wins
+    wd = w.dense().clone()
+    wd[900] = wd[100]
+    wt = PackedLinear.from_dense(wd.cpu(), DEV)
+    xb = torch.zeros(m, k, device=DEV).to(BF16)
+    xb[:, :] = wd[100].to(DEV)[None, :].to(BF16)  # makes column 100 (and 900) the maximum
+    e.linear_skinny_argmax(xb, wt.weight, n, k, -1.0, variant, part, idx, val)
+    assert idx.cpu().tolist() == [100] * m
+
+
 def test_argmax_first_index():
     x = torch.randn(4, 128256)
     x[1, 77] = 100.0

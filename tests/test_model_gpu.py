@@ -113,9 +113,11 @@ def test_graph_recaptured_after_workspace_growth():
     assert torch.equal(first, eager) and torch.equal(again, eager)
 
 
-def test_fused_argmax_engine_path(monkeypatch):
-    """the lm_head GEMM with the argmax epilogue, forced at small M, inside the
-    captured decode step, gives the same greedy sequences as logits + argmax."""
+@pytest.mark.parametrize("path", ["gemv", "tiled"])
+def test_fused_argmax_engine_path(monkeypatch, path):
+    """the lm_head with the argmax in its epilogue -- the decode GEMV's (M <= 64) or
+    the tiled GEMM's (forced at small M) -- inside the captured decode step gives the same greedy
+    sequences as logits + argmax."""
     from jax_llama_amd import ops
     from jax_llama_amd.runtime import engine as eng_mod
     cfg = gpu_config()
@@ -123,6 +125,7 @@ def test_fused_argmax_engine_path(monkeypatch):
     toks, mask = left_padded_batch([6, 9, 9], 9, cfg.vocab_size, pad=2, seed=16)
     gc = GenerationConfig(max_length=30, do_sample=False, pad_token_id=2, eos_token_id=-1)
     monkeypatch.setattr(ops, "ARGMAX_FUSED_MIN_M", 1)
+    monkeypatch.setattr(ops, "SKINNY_ARGMAX", path == "gemv")
     fused = DecodeEngine(gpu, 3, 30, use_graph=True).run(toks, mask, gc).clone()
     monkeypatch.setattr(eng_mod, "FUSED_GREEDY", False)
     plain = DecodeEngine(gpu, 3, 30, use_graph=True).run(toks, mask, gc).clone()

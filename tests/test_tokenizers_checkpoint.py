@@ -118,6 +118,39 @@ def test_long_whitespace_chunking(llama3_tok):
     assert llama3_tok.decode(ids) == s
 
 
+def _pieces_oracle(s, window, max_run):
+    """Chunking semantics of the reference tokenizer (llama3_tokenizer.py:131-146,178-202), written as a
+    per-character state machine: a new piece starts at every window start and whenever a same-class
+    run has reached max_run characters."""
+    out = []
+    for w0 in range(0, max(len(s), 1), window):
+        win = s[w0:w0 + window]
+        piece, run, prev = "", 0, None
+        for ch in win:
+            cls = ch.isspace()
+            run = run + 1 if cls == prev else 1
+            if run > max_run:
+                out.append(piece)
+                piece, run = "", 1
+            piece += ch
+            prev = cls
+        out.append(piece)
+    return [p for p in out if p]
+
+
+def test_chunk_bounds_native_python_oracle():
+    from jax_llama_amd.tokenizer.llama3 import _chunk_bounds_py, chunk_bounds
+    import random
+    rnd = random.Random(0)
+    alphabet = [" ", "\t", "\n", "a", "b", "\u3000", "\xa0", "\u2003", "\u200b", "1", "\x1c"]
+    for _ in range(300):
+        s = "".join(rnd.choice(alphabet) * rnd.randint(1, 9) for _ in range(rnd.randint(0, 12)))
+        window, run = rnd.randint(1, 40), rnd.randint(1, 12)
+        for fn in (chunk_bounds, _chunk_bounds_py):
+            b = fn(s, window, run)
+            assert [s[lo:hi] for lo, hi in zip(b, b[1:]) if hi > lo] == _pieces_oracle(s, window, run), (s, window, run)
+
+
 @pytest.fixture(scope="module")
 def sp_tok(tmp_path_factory):
     spm = pytest.importorskip("sentencepiece")

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""One decode latency point (hipGraph-replayed steps, prefill excluded) of a synthetic model; the
+unit to run under rocprofv3 for a per-kernel breakdown of small-batch decode.
+
+  python tools/decode_point.py --model llama3-8b --batch 1 32 --steps 64
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, nargs="+", default=[1])
+    ap.add_argument("--steps", type=int, default=64)
+    ap.add_argument("--prompt-len", type=int, default=128)
+    ap.add_argument("--gen-len", type=int, default=256)
+    ap.add_argument("--sample", action="store_true")
+    args = ap.parse_args()
+    import torch
+    from jax_llama_amd.config import get_preset
+    from jax_llama_amd.models import LLaMAForCausalLM
+    from jax_llama_amd.runtime.benchmark import decode_latency
+    cfg = get_preset(args.model, max_seq_len=2048)
+    m = LLaMAForCausalLM(cfg, device="cuda", _do_init=False).init_random(seed=1)
+    for b in args.batch:
+        r = decode_latency(m, b, args.prompt_len, args.gen_len, steps=args.steps, do_sample=args.sample)
+        r["model"] = args.model
+        r["hbm_roofline_ms"] = round(m.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)
+        print(json.dumps(r), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -359,7 +359,7 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
 #pragma unroll
       for (int r = 0; r < KPG; ++r) {
         const float p = sc[h][r] == -INFINITY ? 0.f : __expf(sc[h][r] - mn);
-        l_h[h] += p;  // every lane of the group adds the same p: counted once per group below
+        l_h[h] += p;  // the 16 lanes of a group hold the same p (and the same running sum)
         float vf[8];
         unpack8(vcur[r], vf);
 #pragma unroll
@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
       for (int e = 0; e < 8; ++e) sm_o[w][h][8 * li + e] = o[h][e];
       if (li == 0) {
         sm_m[w][h] = m_h[h];
-        sm_l[w][h] = l / 16.f;  // each of the 16 lanes of a group added p once
+        sm_l[w][h] = l;  // sum over the 4 groups (lanes li, li + 16, li + 32, li + 48)
       }
     }
   }
@@ -678,7 +678,7 @@ void attn_set_impl(int impl, int waves_target) {
 // r1_attn_decode_v2_geometry.jsonl), so smaller batches stay on v1.
 static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_attn_v2_min_pairs; }
 // v3 (one workgroup per (row, kv head), no split merge) below this many (row, kv head) pairs
-static int g_attn_v3_max_pairs = 1024;
+static int g_attn_v3_max_pairs = 4096;  // up to the v2 threshold: faster than v1 at B = 1..256 (8 kv heads)
 void attn_set_v3_max_pairs(int n) { g_attn_v3_max_pairs = n; }
 static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv) && B * Hkv <= g_attn_v3_max_pairs; }
 

@@ -51,8 +51,8 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
         c.insert(1, 5)
     if m > 16:
         c.append(TILED_VARIANT)
-        if not swiglu and bf16_x:
-            c += [8, 9]  # 1-tile GEMV with 16 waves / a doubled ring (bf16 activations only)
+        # (variants 8 / 9 -- 16 waves / a doubled ring -- measured no faster than 1/4/6/7 at M = 32:
+        # profiles/r2_decode_m32_variants_8_9.jsonl; kept as explicit choices, not tuned)
     return tuple(c)
 
 

@@ -589,6 +589,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_argmax_workspace", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_argmax_workspace_floats(m, n); });
   m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
+  m.def("gemm4_set_variant", [](int64_t v) { jla::gemm4_set_variant((int)v); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_set_impl", [](int64_t impl, int64_t waves_target) { jla::attn_set_impl(impl, waves_target); },

@@ -51,6 +51,10 @@ size_t gemm_workspace_floats(int M, int N, int K);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0);
+// gemm4 (gemm4.hip): 256x256 tile on 4 waves of 128x128 (K multiple of 64, no K split); gemm() tile config 5
+int gemm4_launch(int mode, const bf16_t* x, const void* w, void* out, int M, int N, int K, int accumulate,
+                 int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s);
+void gemm4_set_variant(int v);
 // greedy lm_head: GEMM + first-max argmax epilogue (ws >= gemm_argmax_workspace_floats(M, N) floats)
 int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
                 int32_t* idx, float* val, hipStream_t s);

@@ -14,6 +14,8 @@ own batch -> weak scaling). ``value`` = total output tokens of all replicas / ma
 Extra keys (outside the timed region, reported alongside the headline):
   * ``latency_points``: decode ms/token at B = 1/8/32/64 (BASELINE.md protocol: prompt 128, cache for
     256 generated tokens, hipGraph replay, prefill excluded);
+  * ``ttft``: time to first token of one ``--ttft-len`` (2048) token prompt at B = 1 (prefill of every layer with
+    the flash-prefill attention + last-position lm_head + greedy token);
   * ``sampled``: tokens/s of whole ``generate`` calls in the reference's default sampling mode
     (temperature 0.8, top-p 0.95, top-k 50: jax_example.py:33, generation.py:22,34) at the headline batch;
   * ``tp_points`` (world > 1): the second half of the metric, Llama-3-70B tensor-parallel over every
@@ -52,6 +54,8 @@ def main():
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count (INVALID for the metric)")
     ap.add_argument("--latency-batches", type=int, nargs="*", default=[1, 8, 32, 64])
     ap.add_argument("--no-sampled", action="store_true", help="skip the sampling-mode throughput point")
+    ap.add_argument("--ttft-len", type=int, default=2048, help="prompt length of the time-to-first-token point "
+                    "(B = 1; 0 = skip)")
     ap.add_argument("--tp-model", default="llama3-70b", help="model of the tensor-parallel points (world > 1)")
     ap.add_argument("--tp-batches", type=int, nargs="*", default=[1, 32, 256])
     ap.add_argument("--tp-timeout", type=float, default=420.0, help="watchdog (s) of the tensor-parallel points")
@@ -66,7 +70,7 @@ def main():
     from jax_llama_amd.ops import autotune
     from jax_llama_amd.parallel import TPComm, init_distributed
     from jax_llama_amd.runtime import engine as eng_mod
-    from jax_llama_amd.runtime.benchmark import decode_latency, generate_tokens_per_sec
+    from jax_llama_amd.runtime.benchmark import decode_latency, generate_tokens_per_sec, time_to_first_token
     from jax_llama_amd.runtime.engine import GenerationConfig, get_engine
 
     ctx = init_distributed()
@@ -159,6 +163,15 @@ def main():
                              "cache_len": max_len, "points": lat}
     eng_mod._ENGINES.clear()
     torch.cuda.empty_cache()
+
+    # ---- time to first token of one long prompt (prefill + first greedy token, B = 1)
+    if args.ttft_len and args.ttft_len + 8 <= 2 * cfg.max_seq_len:
+        t = time_to_first_token(model, 1, args.ttft_len, reps=3, seed=9, barrier=ctx.barrier)
+        t["ttft_ms"] = ctx.all_reduce_max([t["ttft_ms"]])[0]
+        t["prefill_tokens_per_sec"] = round(args.ttft_len * 1000.0 / t["ttft_ms"], 1)
+        res["ttft"] = t
+        eng_mod._ENGINES.clear()
+        torch.cuda.empty_cache()
 
     # ---- sampling mode at the headline batch (reference default: T 0.8, top-p 0.95, top-k 50)
     if not args.no_sampled:

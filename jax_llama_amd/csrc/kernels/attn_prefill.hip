@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(256)
 // K/V tiles are register-staged (loads for tile t+1 issued before tile t's MFMAs, written to LDS after
 // the barrier that ends tile t). Causal: the workgroup stops at its last query's slot; a wave whose
 // queries all precede a tile skips its MFMAs; only tiles that cross the diagonal, kv_start or T are
-// masked element-wise. Heaviest (latest) query blocks launch first.
+// masked element-wise. Each workgroup runs a heavy and a light query block (causal balance).
 constexpr int FA_KT = 64;  // keys per tile
 
 // byte offset of 16-byte chunk ch (0..15) of row `row` in a [rows][128 bf16] image whose XOR swizzle
@@ -223,7 +223,6 @@ __global__ void __launch_bounds__(NW * 64, 2)
   char* Ks = lds;
   char* Vs = lds + TILE_BYTES;
 
-  const int qb = n_qb - 1 - (int)blockIdx.x;  // heaviest (latest) query blocks first
   const int kvh = blockIdx.y / hgroups, hg = blockIdx.y - kvh * hgroups;
   const int b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -231,6 +230,13 @@ __global__ void __launch_bounds__(NW * 64, 2)
   const int rep = H / Hkv, hpw = NW / npb;
   const int r = w / npb, pb = w - r * npb;
   const int h = kvh * rep + hg * hpw + r;
+  // causal balance: workgroup x runs query block n_qb-1-x (heavy) and then block x (light), so every
+  // workgroup streams ~the same number of K/V tiles (with one block per workgroup, S = 2048 at B = 1 ran
+  // the heaviest workgroup ~2x longer than the average one)
+  for (int pass = 0; pass < 2; ++pass) {
+  const int qb = pass == 0 ? n_qb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  if (pass == 1 && qb >= n_qb - 1 - (int)blockIdx.x) break;  // odd n_qb: the middle block runs once
+  if (pass == 1) __syncthreads();  // every wave is done with the LDS images of the first block
   const int p0 = qb * 32 * npb + 32 * pb;   // first query position of this wave
   const int pos = p0 + col;                  // this lane's query
   const int slot0 = slot_ptr[0];
@@ -379,6 +385,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
         *reinterpret_cast<u32x2*>(dst + 32 * dt + 8 * g) = pk;
       }
   }
+  }  // pass
 }
 
 static int g_attn_prefill_impl = 2;
@@ -396,7 +403,7 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
     const int hpw = NW / npb;                    // q heads per workgroup
     const int hgroups = rep / hpw;
     const int n_qb = (S + 32 * npb - 1) / (32 * npb);
-    dim3 grid2(n_qb, Hkv * hgroups, B);
+    dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
     attn_prefill_v2_kernel<NW><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
                                                          Hkv, T, 1.4426950408889634f / sqrtf((float)Dh), npb,
                                                          hgroups, n_qb);

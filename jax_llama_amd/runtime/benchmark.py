@@ -56,6 +56,35 @@ def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256,
             "decode_tokens_per_sec": round(batch * 1000.0 / ms, 2), "prefill_ms": round(ttft_ms, 3)}
 
 
+def time_to_first_token(model, batch: int, prompt_len: int, reps: int = 3, seed: int = 0,
+                        barrier=None) -> Dict[str, float]:
+    """Prefill of ``batch`` synthetic prompts of ``prompt_len`` tokens up to the first generated token
+    (every layer's GEMMs + flash attention + KV-cache writes, last-position lm_head, greedy argmax),
+    timed with HIP events after one warm-up prefill (autotune, workspace growth). Median of ``reps``."""
+    eng = DecodeEngine(model, batch, prompt_len + 8, use_graph=False)
+    gc = GenerationConfig(max_length=prompt_len + 8, do_sample=False, pad_token_id=0, eos_token_id=-1)
+    prompts = synthetic_prompts(model.config.vocab_size, batch, prompt_len, seed)
+    dev = model.device
+    eng.prefill_only(prompts, None, gc)
+    torch.cuda.synchronize(dev)
+    if barrier is not None:
+        barrier()
+    times = []
+    for _ in range(reps):
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        eng.prefill_only(prompts, None, gc)
+        ev1.record()
+        torch.cuda.synchronize(dev)
+        times.append(ev0.elapsed_time(ev1))
+    model.comm.check()
+    del eng
+    ms = sorted(times)[len(times) // 2]
+    return {"batch": batch, "prompt_len": prompt_len, "ttft_ms": round(ms, 3),
+            "prefill_tokens_per_sec": round(batch * prompt_len * 1000.0 / ms, 1)}
+
+
 def generate_tokens_per_sec(model, batch: int, prompt_len: int, gen_len: int, gc: GenerationConfig,
                             seed: int = 0, reps: int = 1, barrier=None) -> Dict[str, float]:
     """Whole ``generate`` calls (prefill + every decode step + sampler), output tokens per second."""

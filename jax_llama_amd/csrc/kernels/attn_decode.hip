@@ -661,13 +661,19 @@ static int kpg_v1(int rep, int B = 1 << 20, int Hkv = 1, int T = 1) {
   return kpg;
 }
 static int g_kpg_small = 8, g_ns = 2;  // v2 ring geometry for REP <= 4 (A/B: attn_set_impl)
-static int kpg_v2(int rep) { return rep <= 4 ? g_kpg_small : (rep == 8 ? 2 : 1); }
+// impl 2 (default) picks the geometry by size: at >= 16384 (row, kv head) pairs (B >= 2048 at 8 kv heads) the
+// 17-KiB (KPG 4, 2 slots) ring -- 9 waves per CU instead of 4 -- streams 5.4-5.8 TB/s against 4.0-5.6 for
+// (KPG 8, 2 slots), which stays best at B = 1024 (profiles/r2_attn_decode_b2048_geometry.jsonl)
+static bool g_geo_auto = true;
+static int geo_v2(int pairs) { return (g_geo_auto && pairs >= 16384) ? 42 : g_kpg_small * 10 + g_ns; }
+static int kpg_v2(int rep, int pairs) { return rep <= 4 ? geo_v2(pairs) / 10 : (rep == 8 ? 2 : 1); }
 
 // impl 1 = v1; 2 = v2 with (KPG 8, 2 slots) [default: profiles/r1_attn_decode_v2_geometry.jsonl];
 // 3 = v2 (KPG 2, 4 slots); 4 = v2 (KPG 4, 2 slots); 5 = same as 2; 6 = v2 (KPG 4, 4 slots); 7 = (KPG 4, 3 slots)
 void attn_set_impl(int impl, int waves_target) {
   g_attn_impl = impl == 1 ? 1 : 2;
   g_kpg_small = impl == 3 ? 2 : (impl == 2 || impl == 5 ? 8 : 4);
+  g_geo_auto = impl == 2;
   g_ns = impl == 3 ? 4 : (impl == 7 ? 3 : (impl == 6 ? 4 : 2));
   if (waves_target > 0) g_attn_waves_target = waves_target;
   g_attn_v2_min_pairs = waves_target < 0 ? -waves_target : 4096;  // < 0: force v2 down to -target pairs
@@ -684,7 +690,7 @@ static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv)
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
   if (use_v3(B, Hkv, rep)) return T;
-  return use_v2(B, Hkv) ? 4 * kpg_v2(rep) : 16 * kpg_v1(rep, B, Hkv, T);
+  return use_v2(B, Hkv) ? 4 * kpg_v2(rep, B * Hkv) : 16 * kpg_v1(rep, B, Hkv, T);
 }
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
@@ -752,7 +758,7 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
     attn_decode_v2_kernel<R, KPG, NS, false><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
                                                                   ws, tickets, B, H, Hkv, T, t_cap, nsplit,          \
                                                                   split_len, scale);
-  const int geo = g_kpg_small * 10 + g_ns;
+  const int geo = geo_v2(B * Hkv);
   switch (rep) {
     case 1:
     case 2:

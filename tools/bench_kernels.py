@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ops", nargs="+", default=None, help="subset of qkv o gate_up down lm_head attn")
     ap.add_argument("--attn-impls", default="1:0,2:4096", help="impl:waves_target pairs for attn A/B")
+    ap.add_argument("--attn-shapes", nargs="*", default=None, help="BxT decode attention shapes (default: a sweep)")
     args = ap.parse_args()
     args.attn_impls = [tuple(int(v) for v in p.split(":")) for p in args.attn_impls.split(",")]
     cfg = get_preset(args.model)
@@ -100,7 +101,9 @@ def main():
     # decode attention at the bench shape
     if args.ops and "attn" not in args.ops:
         return
-    for b, t in ((16, 384), (1, 4096), (64, 1024), (256, 384), (512, 384), (512, 256), (1024, 384)):
+    ap_shapes = ((16, 384), (1, 4096), (64, 1024), (256, 384), (512, 384), (512, 256), (1024, 384), (2048, 128),
+                 (2048, 256), (2048, 384))
+    for b, t in ap_shapes if not args.attn_shapes else [tuple(int(v) for v in p.split("x")) for p in args.attn_shapes]:
         kc = torch.randn(b, hkv, t, hd, device=DEV).to(torch.bfloat16)
         vc = torch.randn_like(kc)
         q = torch.randn(b, 1, h, hd, device=DEV).to(torch.bfloat16)

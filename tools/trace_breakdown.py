@@ -5,6 +5,7 @@ Decode-step launches of one shape repeat every step, so grouping by launch geome
 prefill GEMMs from the decode GEMMs of the same kernel template (and the shapes from each other).
 
   python tools/trace_breakdown.py gpurun_out/prof/run_kernel_trace.csv [--top 40] [--json out.json]
+  python tools/trace_breakdown.py gpurun_out/prof/run_results.db     (rocprofv3's default rocpd output)
 """
 from __future__ import annotations
 
@@ -21,14 +22,27 @@ def short(name: str) -> str:
     return name[:60]
 
 
-def breakdown(path: str):
-    groups = defaultdict(lambda: [0, 0.0])
-    total = 0.0
+def _records(path: str):
+    """(name, grid, workgroup, duration_us) per dispatch, from a kernel-trace CSV or a rocpd SQLite db."""
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        for name, gx, gy, gz, wx, wy, wz, dur in con.execute(
+                "select name, grid_x, grid_y, grid_z, workgroup_x, workgroup_y, workgroup_z, duration from kernels"):
+            yield name, str(gx * gy * gz), str(wx * wy * wz), dur / 1e3
+        return
     for r in csv.DictReader(open(path)):
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # us
         grid = r.get("Grid_Size", r.get("Grid_Size_X", "?"))
         wg = r.get("Workgroup_Size", r.get("Workgroup_Size_X", "?"))
-        key = (short(r.get("Kernel_Name", "?")), grid, wg)
+        yield r.get("Kernel_Name", "?"), grid, wg, dur
+
+
+def breakdown(path: str):
+    groups = defaultdict(lambda: [0, 0.0])
+    total = 0.0
+    for name, grid, wg, dur in _records(path):
+        key = (short(name), grid, wg)
         g = groups[key]
         g[0] += 1
         g[1] += dur

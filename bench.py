@@ -185,7 +185,7 @@ def main():
                           "tokens_per_sec": round(replicas * args.batch * args.gen_len * 1000.0 / dt, 2)}
         eng_mod._ENGINES.clear()
         torch.cuda.empty_cache()
-    res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}": f"ks{v[0]}_tile{v[1]}"
+    res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}{'_rms' if k[4] else ''}": f"ks{v[0]}_tile{v[1]}"
                                for k, v in autotune.ksplit_table().items()}
 
     # ---- tensor-parallel points: 70B over every GPU of the job (world > 1), under a watchdog

@@ -188,9 +188,9 @@ def sk_workspace(e, m, n, k, device):
             workspace.get_zeroed("gemm_sk_tickets", SK_MAX_TICKETS, torch.int32, device))
 
 
-def _gemm_ws(e, m, n, k, device):
-    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape."""
-    ks, tm = autotune.choose_gemm_plan(e, m, n, k, device)
+def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
+    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue."""
+    ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, rms)
     if tm == SK_TILE:
         ws, tk = sk_workspace(e, m, n, k, device)
         return 1, tm, ws, tk
@@ -204,7 +204,7 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
     when the output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip)."""
     fused = _fused_rms(e, mode, rms_eps)
     xb = _tiled_input(x, rms_eps, fused)
-    ks, tm, ws, tk = _gemm_ws(e, x.shape[0], n, k, x.device)
+    ks, tm, ws, tk = _gemm_ws(e, x.shape[0], n, k, x.device, mode, fused)
     e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
 
 
@@ -277,7 +277,8 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     e = ext()
     v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV)
     if v == TILED:
-        ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device)
+        # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
+        ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
         if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):
             tm = 1  # the stream-K plan has a data-parallel part here: plain GEMM + RoPE kernel
         if ks == 1 and tm != SK_TILE:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel

@@ -111,11 +111,14 @@ TILE_CANDIDATES = (1, 2, 3)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kern
 TUNE_MAX_M = 2048
 
 
-def choose_gemm_plan(e, m: int, n: int, k: int, device) -> Tuple[int, int]:
-    """(split-K factor, gemm2 tile config) for this shape: measured once on the device for decode-sized
-    M (every tile config x every split that keeps >= 4 K-tiles per split); the C++ heuristic otherwise
-    or while a hipGraph is being captured."""
-    key = (m, n, k)
+def choose_gemm_plan(e, m: int, n: int, k: int, device, mode: int = 0, rms: bool = False) -> Tuple[int, int]:
+    """(split-K factor, gemm2 tile config) for this shape and epilogue: measured once on the device for
+    decode-sized M (every tile config x every split that keeps >= 4 K-tiles per split); the C++ heuristic
+    otherwise or while a hipGraph is being captured. The epilogue is part of the key: a split plan pays it
+    in the reduce kernel, and the residual epilogue (fp32 read-modify-write + bf16 mirror) costs the reduce
+    ~2x the bf16 store's, which moves the best split factor of wo / w2."""
+    mode = 0 if mode == 3 else mode  # QKV (RoPE + cache write, side effects) is tuned as a plain store
+    key = (m, n, k, mode, bool(rms))
     plan = _KS_CACHE.get(key)
     if plan is not None:
         return plan
@@ -124,7 +127,7 @@ def choose_gemm_plan(e, m: int, n: int, k: int, device) -> Tuple[int, int]:
     # multi-GB scratch outputs)
     if m <= 128 or m > TUNE_MAX_M or not ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
         return heur, 0
-    plan = _measure_plan(e, m, n, k, device, heur)
+    plan = _measure_plan(e, m, n, k, device, heur, mode, rms)
     _KS_CACHE[key] = plan
     return plan
 
@@ -138,7 +141,7 @@ SK_MARGIN = 0.97
 TUNE_ROUNDS = 3
 
 
-def _measure_plan(e, m, n, k, device, heur) -> Tuple[int, int]:
+def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int]:
     from . import sk_workspace
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
@@ -151,15 +154,22 @@ def _measure_plan(e, m, n, k, device, heur) -> Tuple[int, int]:
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
             for _ in range(copies)]
     x = torch.randn(m, k, device=device).to(torch.bfloat16)
-    out = torch.empty(m, n, dtype=torch.bfloat16, device=device)
+    # the real epilogue's output: residual (fp32 in-place + bf16 mirror), SwiGLU (N/2 bf16), store (bf16)
+    mirror = None
+    if mode == 1:
+        out = torch.zeros(m, n, dtype=torch.float32, device=device)
+        mirror = torch.empty(m, n, dtype=torch.bfloat16, device=device)
+    else:
+        out = torch.empty(m, n // 2 if mode == 2 else n, dtype=torch.bfloat16, device=device)
+    eps = 1e-5 if (rms and mode != 1) else -1.0
     ws = torch.empty(max(ks_c) * m * (n + 1), dtype=torch.float32, device=device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run(c, tm, i):
         if tm == SK_TILE:
-            e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, 1, sk_ws, -1.0, tm, sk_tk)
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, sk_ws, eps, tm, sk_tk)
         else:
-            e.gemm(x, ws_w[i % copies], n, k, out, 0, True, None, c, ws if c > 1 else None, -1.0, tm)
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm)
 
     for c, tm in cands:  # warm every variant (code objects, caches) before any timing
         for i in range(2):

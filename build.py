@@ -10,7 +10,12 @@ The xGMI custom all-reduce (``csrc/kernels/allreduce.hip``) is part of ``_C``.
 No hipify, no CUDA, no JIT cache: objects go to ``build/`` (incremental, mtime based) and the
 final ``.so`` files land next to the Python package so they travel with the repo snapshot.
 
-Usage: ``python build.py [-j N] [--force] [--only C|bpe]``
+Usage: ``python build.py [-j N] [--force] [--only C|bpe] [--debug-bounds]``
+
+``--debug-bounds`` additionally builds ``jax_llama_amd/_C_dbg*.so`` (objects in ``build/C_dbg``) with
+``-DJLA_DEBUG_BOUNDS``: every clamped / skipped out-of-range index that comes from device state (token ids,
+the KV-cache slot, RoPE positions, the sequence length) sets a bit in an error word the host can read
+(``ops.bounds_error()``). ``JLA_DEBUG_BOUNDS=1`` makes ``ops.ext()`` load it instead of ``_C``.
 """
 from __future__ import annotations
 
@@ -100,28 +105,31 @@ def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):
     return False
 
 
-def build_C(jobs: int, force: bool) -> Path:
+def build_C(jobs: int, force: bool, debug_bounds: bool = False) -> Path:
     tdir, tinc, tlib = _torch_paths()
     kdir = CSRC / "kernels"
     headers = sorted(kdir.glob("*.h"))
     srcs = sorted(kdir.glob("*.hip"))
-    objs = [BUILD / "C" / (s.stem + ".o") for s in srcs]
+    name = "_C_dbg" if debug_bounds else "_C"
+    odir = BUILD / ("C_dbg" if debug_bounds else "C")
+    extra = ["-DJLA_DEBUG_BOUNDS"] if debug_bounds else []
+    objs = [odir / (s.stem + ".o") for s in srcs]
     with ThreadPoolExecutor(max_workers=jobs) as ex:
-        rebuilt = list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force), zip(srcs, objs)))
+        rebuilt = list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force, extra), zip(srcs, objs)))
     # the GEMV's hand-counted load ring must never be read before its wait: check the assembly
     for src, did in zip(srcs, rebuilt):
         if did and src.stem == "gemv":
-            asm = BUILD / "C" / "gemv.s"
-            _run([HIPCC, *HIP_FLAGS, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
+            asm = odir / "gemv.s"
+            _run([HIPCC, *HIP_FLAGS, *extra, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
             _run([sys.executable, str(ROOT / "tools" / "check_asm_ring.py"), str(asm)])
     bsrc = CSRC / "bindings.cpp"
-    bobj = BUILD / "C" / "bindings.o"
+    bobj = odir / "bindings.o"
     if force or _stale(bobj, [bsrc, *headers]):
         inc = [f"-I{p}" for p in tinc] + [f"-I{_py_include()}", f"-I{CSRC}"]
         _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
-              "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1",
+              f"-DTORCH_EXTENSION_NAME={name}", *extra, "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1",
               "-Wno-deprecated-declarations", "-Wno-unused-result", *inc, "-c", str(bsrc), "-o", str(bobj)])
-    out = PKG / f"_C{EXT_SUFFIX}"
+    out = PKG / f"{name}{EXT_SUFFIX}"
     if force or _stale(out, [*objs, bobj]):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), str(bobj), "-o", str(out),
               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
@@ -138,12 +146,14 @@ def build_bpe(force: bool) -> Path:
     return out
 
 
-def build_all(jobs: int = 8, force: bool = False, only=None):
+def build_all(jobs: int = 8, force: bool = False, only=None, debug_bounds: bool = False):
     outs = []
     if only in (None, "bpe"):
         outs.append(build_bpe(force))
     if only in (None, "C"):
         outs.append(build_C(jobs, force))
+        if debug_bounds:
+            outs.append(build_C(jobs, force, debug_bounds=True))
     return outs
 
 
@@ -152,6 +162,7 @@ if __name__ == "__main__":
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["C", "bpe"])
+    ap.add_argument("--debug-bounds", action="store_true", help="also build the bounds-checked _C_dbg extension")
     a = ap.parse_args()
-    for o in build_all(a.j, a.force, a.only):
+    for o in build_all(a.j, a.force, a.only, a.debug_bounds):
         print("built", o.relative_to(ROOT))

@@ -559,7 +559,7 @@ void car_pairs(int64_t state, int64_t mode, Tensor vals, Tensor idx, int64_t idx
 
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-checked build
   m.doc() = "jax_llama_amd gfx950 (MI355X) HIP kernels";
   m.attr("SKINNY_MAX_M") = SKINNY_MAX_M;
   m.attr("ARCH") = "gfx950";
@@ -599,6 +599,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_qkv", &linear_qkv);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);
+  m.def("bounds_error", [](bool reset) {
+    const int r = reset ? 1 : 0;
+    return (int64_t)(jla::jla_bounds_norm_embed(r) | jla::jla_bounds_rope_kv(r) | jla::jla_bounds_sample(r) |
+                     jla::jla_bounds_gemm(r) | jla::jla_bounds_gemv(r) | jla::jla_bounds_skinny(r) |
+                     jla::jla_bounds_attn_decode(r) | jla::jla_bounds_attn_prefill(r));
+  }, "OR of the bounds-checked debug build's error words (JLA_BOUNDS_* bits); always 0 in a release build",
+        py::arg("reset") = false);
+#ifdef JLA_DEBUG_BOUNDS
+  m.attr("DEBUG_BOUNDS") = true;
+#else
+  m.attr("DEBUG_BOUNDS") = false;
+#endif
+  m.def("attn_set_diag", [](int64_t d) { jla::attn_set_diag((int)d); });
   m.def("attn_set_v3_max_pairs", [](int64_t n) { jla::attn_set_v3_max_pairs((int)n); });
   m.def("attn_set_v1_min_wgs", [](int64_t n) { jla::attn_set_v1_min_wgs((int)n); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),

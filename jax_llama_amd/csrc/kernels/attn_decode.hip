@@ -46,6 +46,7 @@ __global__ void __launch_bounds__(AD_WAVES * 64)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int slot = slot_ptr[0];
+  if (slot >= T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);  // keys past the cache are never read
   const int lo = kv_start[b];
   const int c0 = split * CH;
   const int c1 = min(c0 + CH, min(t_cap, slot + 1));  // keys [c0, c1) of this split
@@ -282,6 +283,7 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int slot = slot_ptr[0];
+  if (slot >= T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);  // keys past the cache are never read
   const int lo = kv_start[b];
   const int hi_key = min(slot + 1, t_cap);  // keys [lo, hi_key)
   const int h0 = kvh * REP;
@@ -428,6 +430,8 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
 static int g_attn_impl = 2;
 static int g_attn_waves_target = 2048;
 static int g_attn_v2_min_pairs = 4096;
+static int g_attn_diag = 0;  // tools only: 1 = v2 streams K/V without the math (wrong results)
+void attn_set_diag(int d) { g_attn_diag = d; }
 void attn_set_impl(int impl, int waves_target);
 
 template <int REP, int KPG, int NS, bool MASK>
@@ -436,7 +440,7 @@ __global__ void __launch_bounds__(64)
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                           const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out,
                           float* __restrict__ ws, int32_t* __restrict__ tickets, int B, int H, int Hkv, int T,
-                          int t_cap, int nsplit, int split_len, float scale) {
+                          int t_cap, int nsplit, int split_len, float scale, int diag) {
   constexpr int CK = 4 * KPG;        // keys per chunk
   constexpr int SLOT = 2 * KPG * 64;  // u32x4 per ring slot: KPG K-row loads then KPG V-row loads
   constexpr int QL = (REP + 3) / 4;  // q LDS-DMA loads (4 heads of 256 B per wave load)
@@ -448,6 +452,7 @@ __global__ void __launch_bounds__(64)
   const int kvh = pair % Hkv, b = pair / Hkv;
   const int g = lane >> 4, li = lane & 15;
   const int slot = slot_ptr[0];
+  if (slot >= T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);  // keys past the cache are never read
   const int lo = kv_start[b];
   const int s0 = split * split_len;
   const int k0 = max(s0, lo);
@@ -569,7 +574,12 @@ __global__ void __launch_bounds__(64)
       for (int r = 0; r < KPG; ++r) kr[r] = sl[r * 64 + lane];
 #pragma unroll
       for (int r = 0; r < KPG; ++r) vr[r] = sl[(KPG + r) * 64 + lane];
-      compute(kr, vr, c);
+      if (diag) {  // DIAGNOSTIC (wrong results): stream only, keep the chunk live, skip the math
+#pragma unroll
+        for (int r = 0; r < KPG; ++r) asm volatile("" ::"v"(kr[r]), "v"(vr[r]));
+      } else {
+        compute(kr, vr, c);
+      }
       // WAR: slot c % NS is refilled by the issue at the top of iteration c + 1; its ds_reads above
       // were consumed by compute (lgkmcnt waited before use), so they have completed.
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -753,11 +763,11 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   if (key_mask)                                                                                                     \
     attn_decode_v2_kernel<R, KPG, NS, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
                                                                  ws, tickets, B, H, Hkv, T, t_cap, nsplit, split_len, \
-                                                                 scale);                                           \
+                                                                 scale, g_attn_diag);                              \
   else                                                                                                              \
     attn_decode_v2_kernel<R, KPG, NS, false><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
                                                                   ws, tickets, B, H, Hkv, T, t_cap, nsplit,          \
-                                                                  split_len, scale);
+                                                                  split_len, scale, g_attn_diag);
   const int geo = geo_v2(B * Hkv);
   switch (rep) {
     case 1:
@@ -790,5 +800,7 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+JLA_BOUNDS_ACCESSOR(attn_decode)
 
 }  // namespace jla

@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(256)
   const int g = lane >> 4, li = lane & 15;
   const int rep = H / Hkv, kvh = h / rep;
   const int slot0 = slot_ptr[0];
+  if (slot0 + S > T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);
   const int lo = kv_start[b];
   const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
 
@@ -240,6 +241,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
   const int p0 = qb * 32 * npb + 32 * pb;   // first query position of this wave
   const int pos = p0 + col;                  // this lane's query
   const int slot0 = slot_ptr[0];
+  if (slot0 + S > T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);
   const int lo = kv_start[b];
   const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
 
@@ -416,5 +418,7 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+JLA_BOUNDS_ACCESSOR(attn_prefill)
 
 }  // namespace jla

@@ -24,7 +24,36 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define MODE_RESIDUAL 1
 #define MODE_SWIGLU 2
 #define MODE_QKV 3
-#define MODE_ARGMAX 8  // greedy lm_head: first-max (value, index) partials instead of logits
+#define MODE_ARGMAX 8
+
+// ---- bounds-checked debug build (python build.py --debug-bounds -> jax_llama_amd/_C_dbg*.so, loaded when
+// JLA_DEBUG_BOUNDS=1). The kernels clamp or skip out-of-range indices that come from device state (token ids,
+// the KV-cache slot counter, RoPE positions, the sequence length): in a release build silently, in the debug
+// build each such event also sets a bit in this translation unit's error word (a vector atomic OR), which the
+// host reads with ops.bounds_error() / raises on in ops.check_bounds(). Bit = JLA_BOUNDS_* code.
+#define JLA_BOUNDS_TOKEN 0      // token id outside [0, vocab)
+#define JLA_BOUNDS_KV_SLOT 1    // KV-cache write at slot >= T (cache full)
+#define JLA_BOUNDS_SEQ 2        // decode step past the sequence buffer
+#define JLA_BOUNDS_ATTN_T 3     // attention asked for keys past the cache (slot >= T)
+#define JLA_BOUNDS_ROPE_POS 4   // position outside the RoPE table
+#ifdef JLA_DEBUG_BOUNDS
+static __device__ unsigned int g_jla_bounds_err;
+#define JLA_FLAG(code) atomicOr(&g_jla_bounds_err, 1u << (code))
+#define JLA_BOUNDS_ACCESSOR(tu)                                                     \
+  unsigned jla_bounds_##tu(int reset) {                                             \
+    unsigned v = 0;                                                                 \
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_jla_bounds_err), sizeof(v));         \
+    if (reset) {                                                                    \
+      const unsigned z = 0;                                                         \
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_jla_bounds_err), &z, sizeof(z));         \
+    }                                                                               \
+    return v;                                                                       \
+  }
+#else
+#define JLA_FLAG(code) ((void)0)
+#define JLA_BOUNDS_ACCESSOR(tu) \
+  unsigned jla_bounds_##tu(int) { return 0; }
+#endif  // greedy lm_head: first-max (value, index) partials instead of logits
 
 #define JLA_DEV __device__ __forceinline__
 

@@ -1047,6 +1047,7 @@ __global__ void __launch_bounds__(512)
           const int b = grow / qa.S, sq = grow - b * qa.S;
           if (head < qa.H + qa.Hkv) {
             int pos = qa.positions[grow];
+            if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
             pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
 #pragma unroll
             for (int p2 = 0; p2 < 2; ++p2) {
@@ -1066,6 +1067,8 @@ __global__ void __launch_bounds__(512)
               const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
               bf16_t* cache = is_k ? qa.kc : qa.vc;
               *reinterpret_cast<uint2*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + cslot) * qa.Dh + d0) = packed;
+            } else {
+              JLA_FLAG(JLA_BOUNDS_KV_SLOT);
             }
           }
         } else if constexpr (MODE == MODE_RESIDUAL) {
@@ -1167,6 +1170,7 @@ __global__ void __launch_bounds__(256)
     const int b = m / qa.S, sq = m - b * qa.S;
     if (head < qa.H + qa.Hkv) {
       int pos = qa.positions[m];
+      if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
       pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
@@ -1186,6 +1190,8 @@ __global__ void __launch_bounds__(256)
         const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
         bf16_t* cache = is_k ? qa.kc : qa.vc;
         *reinterpret_cast<uint2*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d0) = packed;
+      } else {
+        JLA_FLAG(JLA_BOUNDS_KV_SLOT);
       }
     }
   } else {
@@ -1548,5 +1554,7 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+JLA_BOUNDS_ACCESSOR(gemm)
 
 }  // namespace jla

@@ -51,7 +51,7 @@ JLA_DEV void g4_vmcnt() {
 
 // The 8 x pieces a wave loads per K-tile pair are issued 4 + 4 with the pair's two K-tiles (issuing all 8 with the
 // even K-tile measured 2-6 % slower).
-template <int MODE, bool RMS, bool ILV>
+template <int MODE, bool RMS, bool ILV, bool NOLOAD = false>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
@@ -171,8 +171,10 @@ __global__ void __launch_bounds__(256, 1)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);  // (s_setprio bounds a scheduling region: the loads, reads and MFMAs share one)
-    issueA(min((t >> 1) + 2, last_pair), hn == 0 ? 4 : 0, 4, (t >> 1) + 2);  // hn == 0 <=> t odd: second half
-    issueB(min(t + 4, KT - 1), t + 4);
+    if constexpr (!NOLOAD) {  // NOLOAD: diagnostic build without the steady-state LDS-DMA (wrong results)
+      issueA(min((t >> 1) + 2, last_pair), hn == 0 ? 4 : 0, 4, (t >> 1) + 2);  // hn == 0 <=> t odd: second half
+      issueB(min(t + 4, KT - 1), t + 4);
+    }
     read(t + 1, HN, an, bn);  // t + 1 == KT: a harmless read of a slot that is not written any more
     if constexpr (RMS) {
 #pragma unroll
@@ -338,6 +340,13 @@ static void g4_launch(int grid, const bf16_t* x, const u32x4* w, void* out, int 
                       int out_f32, bf16_t* mirror, int kc, int tm, int tn, float rms_eps, float* ssq, hipStream_t s) {
   // variant bit 0: no MFMA / load interleave (A/B reference); bits 1-2: diagnostics (see the kernel)
   const int diag = g_g4_variant & 6;
+  if constexpr (MODE == MODE_STORE && !RMS) {
+    if (g_g4_variant & 8) {  // diagnostic: no steady-state loads
+      gemm4_kernel<MODE, RMS, true, true><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
+                                                               tn, rms_eps, ssq, diag);
+      return;
+    }
+  }
   if (g_g4_variant & 1)
     gemm4_kernel<MODE, RMS, false><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
                                                         rms_eps, ssq, diag);

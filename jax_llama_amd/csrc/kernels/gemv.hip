@@ -296,6 +296,7 @@ __global__ void __launch_bounds__(NW * 64)
         if (head < qa.H + qa.Hkv) {
           const float pv = reduced(mt, t, ln ^ 1, i) * inv_rms[m];
           int pos = qa.positions[m];
+          if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
           pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
           const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d >> 1)];
           r = (d & 1) ? (pv * cs.y + v * cs.x) : (v * cs.x - pv * cs.y);
@@ -309,6 +310,8 @@ __global__ void __launch_bounds__(NW * 64)
             const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
             bf16_t* cache = is_k ? qa.kc : qa.vc;
             cache[(((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d] = f2bf(r);
+          } else {
+            JLA_FLAG(JLA_BOUNDS_KV_SLOT);
           }
         }
       } else {
@@ -445,5 +448,7 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
 #undef JLA_MODE
 #undef JLA_ARGS
 }
+
+JLA_BOUNDS_ACCESSOR(gemv)
 
 }  // namespace jla

@@ -74,7 +74,17 @@ int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const in
 int attn_decode_chunk(int B, int Hkv, int T, int rep);
 void attn_set_v1_min_wgs(int n);
 void attn_set_v3_max_pairs(int n);  // single-workgroup-per-(row, kv head) decode kernel up to n pairs (0: off)  // v1 split sizing: smallest chunk giving >= n workgroups (default 256)
-void attn_set_impl(int impl, int waves_target);  // 2 = streaming (default), 1 = v1 (A/B)
+void attn_set_impl(int impl, int waves_target);
+void attn_set_diag(int d);
+// bounds-checked debug build: per-translation-unit error words (JLA_BOUNDS_* bits; 0 in release builds)
+unsigned jla_bounds_norm_embed(int reset);
+unsigned jla_bounds_rope_kv(int reset);
+unsigned jla_bounds_sample(int reset);
+unsigned jla_bounds_gemm(int reset);
+unsigned jla_bounds_gemv(int reset);
+unsigned jla_bounds_skinny(int reset);
+unsigned jla_bounds_attn_decode(int reset);
+unsigned jla_bounds_attn_prefill(int reset);  // DIAGNOSTIC: 1 = the streaming kernel skips its math (wrong results)  // 2 = streaming (default), 1 = v1 (A/B)
 int attn_decode_splits(int B, int Hkv, int T, int rep);
 // ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,

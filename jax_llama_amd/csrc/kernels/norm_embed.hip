@@ -16,6 +16,7 @@ __global__ void __launch_bounds__(256) embedding_kernel(const int32_t* __restric
                                                         int D, int V) {
   const int row = blockIdx.x;
   int id = ids[row];
+  if ((id < 0 || id >= V) && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_TOKEN);
   id = id < 0 ? 0 : (id >= V ? V - 1 : id);
   const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * D);
   float4* dst = reinterpret_cast<float4*>(out + (size_t)row * D);
@@ -117,5 +118,7 @@ int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps,
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+JLA_BOUNDS_ACCESSOR(norm_embed)
 
 }  // namespace jla

@@ -21,6 +21,7 @@ __global__ void __launch_bounds__(256)
   const int vec_per_head = Dh >> 3;
   const int nvec = (H + 2 * Hkv) * vec_per_head;
   int pos = positions[m];
+  if (pos < 0 || pos >= table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
   pos = pos < 0 ? 0 : (pos >= table_len ? table_len - 1 : pos);
   const int slot = slot_ptr[0] + s;
   const u32x4* row = reinterpret_cast<const u32x4*>(qkv + (size_t)m * (H + 2 * Hkv) * Dh);
@@ -46,6 +47,8 @@ __global__ void __launch_bounds__(256)
       const int kh = head < H + Hkv ? head - H : head - H - Hkv;
       bf16_t* cache = head < H + Hkv ? kc : vc;
       reinterpret_cast<u32x4*>(cache + (((size_t)b * Hkv + kh) * T + slot) * Dh + d0)[0] = val;
+    } else {
+      JLA_FLAG(JLA_BOUNDS_KV_SLOT);
     }
   }
 }
@@ -60,5 +63,7 @@ int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const in
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+JLA_BOUNDS_ACCESSOR(rope_kv)
 
 }  // namespace jla

@@ -70,7 +70,10 @@ __global__ void decode_update_kernel(const int32_t* __restrict__ nxt, int32_t* _
     const int fin = finished[b];
     if (fin) t = pad;
     finished[b] = (fin || t == eos) ? 1 : 0;
-    if (cl < L) sequences[(size_t)b * L + cl] = t;
+    if (cl < L)
+      sequences[(size_t)b * L + cl] = t;
+    else
+      JLA_FLAG(JLA_BOUNDS_SEQ);
     tokens[b] = t;
     positions[b] += 1;
   }
@@ -89,5 +92,7 @@ int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int
   JLA_CHECK_LAUNCH();
   return 0;
 }
+
+JLA_BOUNDS_ACCESSOR(sample)
 
 }  // namespace jla

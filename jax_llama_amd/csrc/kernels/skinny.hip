@@ -249,6 +249,7 @@ __global__ void __launch_bounds__(SK_NW * 64)
               float r = v;
               if (head < qa.H + qa.Hkv) {
                 int pos = qa.positions[m];
+                if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
                 pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
                 const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d >> 1)];
                 r = (d & 1) ? (pv * cs.y + v * cs.x) : (v * cs.x - pv * cs.y);
@@ -262,6 +263,8 @@ __global__ void __launch_bounds__(SK_NW * 64)
                   const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
                   bf16_t* cache = is_k ? qa.kc : qa.vc;
                   cache[(((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d] = f2bf(r);
+                } else {
+                  JLA_FLAG(JLA_BOUNDS_KV_SLOT);
                 }
               }
             }
@@ -388,5 +391,7 @@ int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, 
 #undef JLA_MODE
 #undef JLA_ARGS
 }
+
+JLA_BOUNDS_ACCESSOR(skinny)
 
 }  // namespace jla

@@ -105,6 +105,34 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------------
+# bounds-checked debug build (JLA_DEBUG_BOUNDS=1 + python build.py --debug-bounds)
+BOUNDS_CODES = {0: "token id outside the vocabulary", 1: "KV-cache write past the cache (slot >= T)",
+                2: "decode step past the sequence buffer", 3: "attention asked for keys past the cache",
+                4: "position outside the RoPE table"}
+
+
+class BoundsError(RuntimeError):
+    pass
+
+
+def bounds_error(reset: bool = False) -> int:
+    """OR of the kernels' out-of-range events since the last reset (bits of BOUNDS_CODES); always 0 unless
+    the debug build is loaded. Synchronises the device."""
+    if not ext_available():
+        return 0
+    return int(ext().bounds_error(bool(reset)))
+
+
+def check_bounds(reset: bool = True):
+    """Raise BoundsError naming every out-of-range event the debug build recorded (no-op in release)."""
+    if not ext_available() or not getattr(ext(), "DEBUG_BOUNDS", False):
+        return
+    err = bounds_error(reset)
+    if err:
+        raise BoundsError("device-side index out of range: " +
+                          "; ".join(v for k, v in BOUNDS_CODES.items() if err >> k & 1))
+
+
 def linear(x: torch.Tensor, w, rms_eps: Optional[float] = None, out_dtype=BF16,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``y = [inv_rms(x) *] x @ W^T``; ``w`` is a ``models.weights.PackedLinear``."""

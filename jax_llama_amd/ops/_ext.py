@@ -3,6 +3,8 @@
 The extension is built by ``python build.py`` (hipcc, ``--offload-arch=gfx950``). Every op
 that receives a GPU tensor goes through it; if it is missing on a GPU we raise instead of
 silently running a slower path (the CPU reference path is only used for CPU tensors).
+``JLA_DEBUG_BOUNDS=1`` loads the bounds-checked debug build ``_C_dbg`` instead
+(``python build.py --debug-bounds``; see ``ops.check_bounds``).
 """
 from __future__ import annotations
 
@@ -20,7 +22,8 @@ def _load():
         return
     try:
         import torch  # noqa: F401  (libtorch / libamdhip64 must be loaded first)
-        _EXT = importlib.import_module("jax_llama_amd._C")
+        name = "_C_dbg" if os.environ.get("JLA_DEBUG_BOUNDS", "0") == "1" else "_C"
+        _EXT = importlib.import_module("jax_llama_amd." + name)
     except BaseException as e:  # ImportError, OSError (undefined symbol), ...
         _ERR = e
 

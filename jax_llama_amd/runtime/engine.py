@@ -250,6 +250,7 @@ class DecodeEngine:
         custom TP collective gave up waiting for a peer."""
         done = bool(self.finished.all().item())
         self.model.comm.check()
+        ops.check_bounds()  # bounds-checked debug build only (JLA_DEBUG_BOUNDS=1): out-of-range device indices
         return done
 
     def run(self, input_ids, attention_mask, gc: GenerationConfig) -> torch.Tensor:

@@ -112,6 +112,8 @@ def main():
         nbytes = 2 * kc.numel() * 2
         ref_out = None
         for impl, target in args.attn_impls:
+            e.attn_set_diag(1 if impl >= 100 else 0)  # 100 + impl: diagnostic stream-only run of impl
+            impl = impl % 100
             e.attn_set_impl(impl, target)
             us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
             o = ops.attention(q, kc, vc, slot, ks).float()
@@ -120,6 +122,7 @@ def main():
                               "nsplit": e.attn_decode_splits(b, hkv, t, h // hkv), "us": round(us, 2),
                               "TBps": round(nbytes / us / 1e6, 3),
                               "max_diff_vs_first": round(float((o - ref_out).abs().max()), 5)}), flush=True)
+        e.attn_set_diag(0)
         e.attn_set_impl(2, 4096)
         del kc, vc
 

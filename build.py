@@ -116,10 +116,10 @@ def build_C(jobs: int, force: bool, debug_bounds: bool = False) -> Path:
     objs = [odir / (s.stem + ".o") for s in srcs]
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         rebuilt = list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force, extra), zip(srcs, objs)))
-    # the GEMV's hand-counted load ring must never be read before its wait: check the assembly
+    # the hand-counted load rings must never be read before their waits: check the assembly
     for src, did in zip(srcs, rebuilt):
-        if did and src.stem == "gemv":
-            asm = odir / "gemv.s"
+        if did and src.stem in ("gemv", "attn_decode"):  # (attn_decode: the v4 register ring)
+            asm = odir / (src.stem + ".s")
             _run([HIPCC, *HIP_FLAGS, *extra, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
             _run([sys.executable, str(ROOT / "tools" / "check_asm_ring.py"), str(asm)])
     bsrc = CSRC / "bindings.cpp"

@@ -430,7 +430,10 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
 static int g_attn_impl = 2;
 static int g_attn_waves_target = 2048;
 static int g_attn_v2_min_pairs = 4096;
-static int g_attn_diag = 0;  // tools only: 1 = v2 streams K/V without the math (wrong results)
+static int g_attn_diag = 0;
+// register-ring streaming kernel (v4) for one-split large batches without a key mask: 5-12 % faster than v2 at
+// B = 512-2048 (profiles/r2_attn_decode_v4_vs_v2.jsonl); impl 2 (default) / 8 use it, 3-7 pin a v2 geometry
+static bool g_attn_v4 = true;  // tools only: 1 = v2 streams K/V without the math (wrong results)
 void attn_set_diag(int d) { g_attn_diag = d; }
 void attn_set_impl(int impl, int waves_target);
 
@@ -660,6 +663,163 @@ __global__ void __launch_bounds__(64)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v4 (large batch, one split): v2's one-wave-per-(row, kv head) stream with the K/V rows loaded straight into
+// registers instead of through an LDS-DMA ring. v2 holds one 8-KiB chunk in flight per wave and its 17-33 KiB
+// LDS ring caps a CU at 4-9 waves: its stream-only diagnostic build (no math) tops out at 5.5-5.8 TB/s
+// (profiles/r2_attn_decode_b2048_geometry.jsonl). Here a U-slot register ring keeps U-1 chunks of 16 keys
+// (U-1 x 8 KiB) in flight per wave with no LDS, so occupancy is set by registers alone.
+// The loads are inline asm with hand-counted waits (the GEMV recipe, gemv.hip: hipcc's own waitcnt pass
+// would drain the ring at the loop back-edge); every ring slot is a "+v"-tied variable pinned behind its
+// wait, and build.py checks the assembly with tools/check_asm_ring.py. Chunks past the end re-load the last
+// valid row (never scored), so every iteration issues exactly L loads and the wait count is a constant.
+JLA_DEV void ad_load_nt(u32x4& r, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "+v"(r) : "v"(p) : "memory");
+}
+JLA_DEV void ad_load(u32x4& r, const void* p) { asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(r) : "v"(p) : "memory"); }
+JLA_DEV void ad_pin(u32x4& r) { asm volatile("" : "+v"(r)); }
+template <int N>
+JLA_DEV void ad_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+template <int REP, int KPG, int U>
+__global__ void __launch_bounds__(64)
+    attn_decode_v4_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                          const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
+                          bf16_t* __restrict__ out, int H, int Hkv, int T, int t_cap, float scale) {
+  constexpr int CK = 4 * KPG;  // keys per chunk
+  constexpr int L = 2 * KPG;   // loads per chunk and lane: KPG K rows + KPG V rows (16 B each)
+  const int lane = threadIdx.x;
+  const int item = blockIdx.x;
+  const int kvh = item % Hkv, b = item / Hkv;
+  const int g = lane >> 4, li = lane & 15;
+  const int slot = slot_ptr[0];
+  if (slot >= T && lane == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);  // keys past the cache are never read
+  const int k0 = kv_start[b];
+  const int k1 = min(t_cap, slot + 1);  // keys [k0, k1)
+  const int h0 = kvh * REP;
+
+  float m_h[REP], l_h[REP];
+  f32x2_t o[REP][4];  // dims 8*li + 2i, 8*li + 2i + 1
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    m_h[h] = -INFINITY;
+    l_h[h] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[h][i] = f32x2_t{0.f, 0.f};
+  }
+
+  const int nc = k1 > k0 ? (k1 - k0 + CK - 1) / CK : 0;
+  if (nc > 0) {
+    const size_t head_off = ((size_t)b * Hkv + kvh) * T * AD_DH + 8 * li;
+    const bf16_t* kbase = kc + head_off;
+    const bf16_t* vbase = vc + head_off;
+    // this lane's 8 dims of each query head (packed bf16: the v_dot2 operand), counted in the same queue
+    u32x4 qp[REP] = {};
+#pragma unroll
+    for (int h = 0; h < REP; ++h) ad_load(qp[h], q + ((size_t)b * H + h0 + h) * AD_DH + 8 * li);
+    u32x4 ring[U][L] = {};
+    auto issue = [&](int c, u32x4* sl) __attribute__((always_inline)) {
+      const int jb = k0 + c * CK + g;
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) ad_load_nt(sl[r], kbase + (size_t)min(jb + 4 * r, k1 - 1) * AD_DH);
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) ad_load_nt(sl[KPG + r], vbase + (size_t)min(jb + 4 * r, k1 - 1) * AD_DH);
+    };
+    auto compute = [&](const u32x4* kr, const u32x4* vr, int c) __attribute__((always_inline)) {
+      const int jb = k0 + c * CK + g;
+      float sc[REP][KPG];
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) {
+        const bool valid = jb + 4 * r < k1;
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          float d = dot8_bf16(kr[r], qp[h], 0.f);
+          d = row16_sum(d) * scale;
+          sc[h][r] = valid ? d : -INFINITY;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < REP; ++h) {
+        float cm = sc[h][0];
+#pragma unroll
+        for (int r = 1; r < KPG; ++r) cm = fmaxf(cm, sc[h][r]);
+        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        const float mn = fmaxf(m_h[h], cm);
+        const float alpha = (m_h[h] == -INFINITY) ? 0.f : __expf(m_h[h] - mn);
+        m_h[h] = mn;
+        l_h[h] *= alpha;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[h][i] *= alpha;
+      }
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) {
+        f32x2_t vf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          vf[i] = f32x2_t{__uint_as_float(vr[r][i] << 16), __uint_as_float(vr[r][i] & 0xffff0000u)};
+#pragma unroll
+        for (int h = 0; h < REP; ++h) {
+          const float pr = (sc[h][r] == -INFINITY) ? 0.f : __expf(sc[h][r] - m_h[h]);
+          l_h[h] += pr;
+          const f32x2_t pp = {pr, pr};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[h][i] = __builtin_elementwise_fma(pp, vf[i], o[h][i]);
+        }
+      }
+    };
+
+    // prologue: chunks 0 .. U-2 in flight (the q loads before them)
+#pragma unroll
+    for (int c = 0; c < U - 1; ++c) issue(c, ring[c]);
+    for (int c0 = 0; c0 < nc; c0 += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + u;
+        issue(c + U - 1, ring[(u + U - 1) % U]);  // refills the slot chunk c-1 was scored from
+        ad_vmcnt<L * (U - 1)>();                  // chunk c (and q) landed: U-1 newer chunks may be in flight
+#pragma unroll
+        for (int e = 0; e < L; ++e) ad_pin(ring[u][e]);
+#pragma unroll
+        for (int h = 0; h < REP; ++h) ad_pin(qp[h]);
+        if (c < nc) compute(ring[u], ring[u] + KPG, c);
+      }
+    }
+    // retire the past-the-end refills, keeping every ring register live until then
+    ad_vmcnt<0>();
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < L; ++e) ad_pin(ring[u][e]);
+    // across the 4 lane groups: each group summed its own rows
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      l_h[h] += __shfl_xor(l_h[h], 16, 64);
+      l_h[h] += __shfl_xor(l_h[h], 32, 64);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          o[h][i][e] += __shfl_xor(o[h][i][e], 16, 64);
+          o[h][i][e] += __shfl_xor(o[h][i][e], 32, 64);
+        }
+    }
+  }
+  if (g == 0) {
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      const float inv = l_h[h] > 0.f ? 1.f / l_h[h] : 0.f;
+      float r8[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r8[e] = o[h][e >> 1][e & 1] * inv;
+      *reinterpret_cast<u32x4*>(out + ((size_t)b * H + h0 + h) * AD_DH + 8 * li) = pack8(r8);
+    }
+  }
+}
+
 // v1 keys per 16-lane group: the largest chunk (fewest splits to merge) that still gives the launch
 // ~256+ workgroups -- at small batch the kernel is latency-bound and more, shorter splits finish sooner
 // (B = 1, T = 384: 24 -> 96 workgroups)
@@ -678,12 +838,13 @@ static bool g_geo_auto = true;
 static int geo_v2(int pairs) { return (g_geo_auto && pairs >= 16384) ? 42 : g_kpg_small * 10 + g_ns; }
 static int kpg_v2(int rep, int pairs) { return rep <= 4 ? geo_v2(pairs) / 10 : (rep == 8 ? 2 : 1); }
 
-// impl 1 = v1; 2 = v2 with (KPG 8, 2 slots) [default: profiles/r1_attn_decode_v2_geometry.jsonl];
+// impl 1 = v1; 2 = default (v4 where it applies, else v2 with the size-chosen geometry); 8 = same as 2;
 // 3 = v2 (KPG 2, 4 slots); 4 = v2 (KPG 4, 2 slots); 5 = same as 2; 6 = v2 (KPG 4, 4 slots); 7 = (KPG 4, 3 slots)
 void attn_set_impl(int impl, int waves_target) {
-  g_attn_impl = impl == 1 ? 1 : 2;
+  g_attn_impl = impl == 1 ? 1 : 2;  // 8: v2 dispatch with the v4 register-ring kernel where it applies
   g_kpg_small = impl == 3 ? 2 : (impl == 2 || impl == 5 ? 8 : 4);
   g_geo_auto = impl == 2;
+  g_attn_v4 = impl == 2 || impl == 8;
   g_ns = impl == 3 ? 4 : (impl == 7 ? 3 : (impl == 6 ? 4 : 2));
   if (waves_target > 0) g_attn_waves_target = waves_target;
   g_attn_v2_min_pairs = waves_target < 0 ? -waves_target : 4096;  // < 0: force v2 down to -target pairs
@@ -757,6 +918,16 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
 #undef JLA_AD
   }
   const int items = B * Hkv * nsplit;
+  if (g_attn_v4 && nsplit == 1 && !key_mask && rep <= 4) {
+#define JLA_AD4(R)                                                                                               \
+  if (rep == R) {                                                                                                \
+    attn_decode_v4_kernel<R, 4, 3><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale); \
+    JLA_CHECK_LAUNCH();                                                                                          \
+    return 0;                                                                                                    \
+  }
+    JLA_AD4(1) JLA_AD4(2) JLA_AD4(4)
+#undef JLA_AD4
+  }
   int split_len = (t_cap + nsplit - 1) / nsplit;
   split_len = (split_len + 31) / 32 * 32;
 #define JLA_AD2(R, KPG, NS)                                                                                          \

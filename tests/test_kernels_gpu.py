@@ -175,6 +175,34 @@ def test_attention_decode_streaming_v2(rep, t, slot, masked):
     assert got[2].float().abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize("rep", [1, 2, 4])
+@pytest.mark.parametrize("t,slot", [(300, 299), (520, 260)])
+def test_attention_decode_v4_large_batch(rep, t, slot):
+    """Large batch, one split, no key mask: the register-ring streaming kernel (v4) serves it; compare with the
+    fp32 reference and with the v2 LDS-DMA kernel (impl 4: same 16-key chunking -> same summation order)."""
+    e = ops.ext()
+    b, hkv, dh = 4096 // 8, 8, 128
+    h = hkv * rep
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, 1, h, dh).to(BF16)
+    g = torch.Generator().manual_seed(3)
+    kv_start = torch.randint(0, slot // 2, (b,), generator=g, dtype=torch.int32)
+    kv_start[7] = slot + 1  # a row with no valid key -> zeros
+    expect = ref.attention(q, kc, vc, slot, kv_start).reshape(b, h * dh)
+    args = (q.to(DEV), kc.to(DEV), vc.to(DEV), torch.tensor([slot], dtype=torch.int32, device=DEV), kv_start.to(DEV))
+    assert e.attn_decode_splits(b, hkv, t, rep) == 1
+    got = ops.attention(*args)
+    try:
+        e.attn_set_impl(4, 0)  # v2, (4-key group, 2 slots)
+        got_v2 = ops.attention(*args)
+        torch.cuda.synchronize()
+    finally:
+        e.attn_set_impl(2, 0)
+    _close(got, expect, 2e-2, 2e-2)
+    assert got[7].float().abs().max().item() == 0.0
+    _close(got, got_v2, 1e-2, 1e-2)
+
+
 def test_attention_decode_key_mask():
     b, hkv, rep, t, dh, slot = 2, 2, 4, 96, 128, 80
     kc, vc = _cache(b, hkv, t, dh)

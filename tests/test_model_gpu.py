@@ -147,3 +147,15 @@ def test_precision_highest_logits():
     gc = GenerationConfig(max_length=16, do_sample=False, pad_token_id=0, eos_token_id=-1)
     seq = hi.generate(toks, generation_config=gc).sequences
     assert seq.shape == (2, 16)
+
+
+def test_benchmark_helpers_at_max_sequence_length():
+    """bench.py's extra points (runtime/benchmark.py): TTFT at a prompt as long as max_sequence_length (the
+    RoPE table covers 2x) and one decode latency point, on a small random model."""
+    from jax_llama_amd.runtime.benchmark import decode_latency, time_to_first_token
+    cfg = gpu_config(max_sequence_length=64)
+    m = LLaMAForCausalLM(cfg, device="cuda", seed=0)
+    t = time_to_first_token(m, 1, cfg.max_sequence_length, reps=2)
+    assert t["ttft_ms"] > 0 and t["prompt_len"] == cfg.max_sequence_length
+    d = decode_latency(m, 2, prompt_len=8, gen_len=16, steps=4)
+    assert d["decode_ms_per_token"] > 0

@@ -86,9 +86,11 @@ def _scratch_users(remarks: str):
 
 
 # Kernels allowed to use scratch, by mangled-name substring -> max bytes/lane: rare shapes where a spill is
-# accepted, and gemm4's epilogues (a 2-3 dword spill AFTER the main loop; the loop itself is checked
+# accepted, and epilogue-only spills (2-3 dwords AFTER the main loop; the loop itself is checked
 # spill-free at this bound: its 256 accumulators + two fragment sets use the whole 512-register file).
-SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20, "gemm4_kernelILi": 16}
+SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20, "gemm4_kernelILi": 16,
+              # gemm2 FA + fused RMS: a 3-dword spill in the split-K fixup tail (after the main loop)
+              "gemm2_kernelILi0ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16, "gemm2_kernelILi2ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16}
 
 
 def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):

@@ -271,6 +271,20 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
        "gemm");
     return;
   }
+  if (ksplit > 1 && tickets.has_value() && jla::gemm_fixup_enabled()) {  // in-kernel split-K fixup
+    check(ws.has_value(), "gemm: split-K needs a workspace");
+    check_gpu(*ws, "gemm ws");
+    check_gpu(*tickets, "gemm tickets");
+    check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm_fix_workspace_floats(m, n, ksplit),
+          "gemm fixup slabs too small (gemm_fix_workspace)");
+    check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm_fix_tiles(m, n),
+          "gemm fixup tickets too small");
+    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
+                 out.scalar_type() == torch::kFloat32, mir, nullptr, ptr<float>(*ws), ws->numel(), ksplit, stream(),
+                 (float)rms_eps, (int)tile, ptr<int32_t>(*tickets), (int)tickets->numel()),
+       "gemm");
+    return;
+  }
   check_gemm_ws(ws, ksplit, m, n, rms_eps >= 0);
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
                out.scalar_type() == torch::kFloat32, mir, nullptr,
@@ -573,6 +587,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
         py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none());
+  m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
+    return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
+  }, "(slab floats, tickets) of the in-kernel split-K fixup");
+  m.def("gemm_set_fixup", [](bool on) { jla::gemm_set_fixup(on ? 1 : 0); });
+  m.def("gemm_fixup_enabled", []() { return jla::gemm_fixup_enabled() != 0; });
   m.def("gemm_sk_workspace", [](int64_t m, int64_t n, int64_t k) {
     // (slab floats, tickets) of the stream-K tail of this shape; (0, 0) when it has none
     if (!jla::gemm_sk_active(m, n, k)) return py::make_tuple((int64_t)0, (int64_t)0);

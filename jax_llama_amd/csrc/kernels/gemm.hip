@@ -208,12 +208,28 @@ JLA_DEV void g2_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn)
 // gfx950 b128 lane groups. x pairs live in a 3-slot ring (96 KiB), weights in the usual 4-slot K-tile
 // ring (64 KiB); pair p is issued in two halves with K-tiles 2p-4 and 2p-3 (4 LDS-DMA per wave per
 // K-tile, as before), so the vmcnt accounting stays "everything issued two K-tiles back has landed".
+// In-kernel split-K fixup (FA pipeline, 256 x 256 tiles): with fix.ksplit > 1 every (tile, K split) workgroup
+// publishes its fp32 accumulators in fragment layout (and the fused-RMS row sums) to its own slab with
+// write-through (sc1) stores, drains them, and takes the tile's agent-scope ticket; the LAST arriver sums the
+// splits in split order (its own from registers) with sc1 loads and runs the mode's normal epilogue. No
+// reduce kernel, no [ksplit][M][N] round trip; deterministic (fixed order); tickets reset themselves
+// (cdna_hip_programming.md Guideline 16, sc1-store + agent ticket + sc1-load form, as the stream-K tail).
+struct G2Fix {
+  float* slabs;       // [tiles][ksplit][G2FIX_SLAB_FLOATS]
+  int32_t* tickets;   // [tiles], zero-initialised once
+  int ksplit;         // 1 = no fixup (plain tile, or the MODE_PARTIAL + reduce-kernel path)
+  int pad;
+};
+constexpr int G2FIX_ACC_BYTES = 8 * 8 * 4 * 1024;           // 8 waves x 8 x 4 fragments x 1 KiB
+constexpr int G2FIX_SLAB_BYTES = G2FIX_ACC_BYTES + 256 * 4;  // + 256 row sums of squares
+constexpr int G2FIX_SLAB_FLOATS = G2FIX_SLAB_BYTES / 4;
+
 template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4,
           int SUB = 1, bool FA = false, int FAM = 0>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                 float rms_eps, float* __restrict__ ssq_ws) {
+                 float rms_eps, float* __restrict__ ssq_ws, G2Fix fix) {
   // wave tile: MT m-tiles x NTW n-tiles of 16x16 (128 x 64 by default; 64 x 32 for the 128 x 128 tile)
   constexpr int NW = 4 * WM, BM = 16 * MT * WM, BN = 64 * NTW;
   constexpr int RPW = MT / 4;  // RMS: m-tiles whose row statistics each wave accumulates
@@ -661,6 +677,65 @@ __global__ void __launch_bounds__(256 * WM)
     ss0 += __shfl_xor(ss0, 32, 64);
     ss1 += __shfl_xor(ss1, 16, 64);
     ss1 += __shfl_xor(ss1, 32, 64);
+  }
+  if constexpr (FA && MODE != MODE_PARTIAL && MODE != MODE_ARGMAX) {
+    if (fix.ksplit > 1) {
+      // ---- in-kernel split-K fixup (see G2Fix): publish, ticket, last arriver sums in split order
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          fix.slabs + (size_t)pid * fix.ksplit * G2FIX_SLAB_FLOATS, 0, fix.ksplit * G2FIX_SLAB_BYTES, 0x00020000);
+      const int base = split * G2FIX_SLAB_BYTES;
+      const int r0 = (wr * MT + RPW * wc) * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                 base + ((w * MT + i) * NTW + j) * 1024 + lane * 16, 0, 16);
+      if (RMS && lane < 16) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss0), rsrc, base + G2FIX_ACC_BYTES + r0 * 4, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss1), rsrc, base + G2FIX_ACC_BYTES + (r0 + 16) * 4, 0, 16);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __syncthreads();  // every store of the workgroup drained; every wave is past its last LDS read
+      int* sh_last = reinterpret_cast<int*>(lds);
+      if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(fix.tickets + pid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == fix.ksplit - 1;
+        if (last) __hip_atomic_store(fix.tickets + pid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *sh_last = last;
+      }
+      __syncthreads();
+      const int last = *sh_last;
+      __syncthreads();  // the flag is read before the epilogue reuses LDS
+      if (!last) return;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int off = ((w * MT + i) * NTW + j) * 1024 + lane * 16;
+          f32x4 tsum = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int q = 0; q < fix.ksplit; ++q)
+            tsum += q == split ? acc[i][j]
+                               : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                               rsrc, q * G2FIX_SLAB_BYTES + off, 0, 16));
+          acc[i][j] = tsum;
+        }
+      if constexpr (RMS) {
+        float t0 = 0.f, t1 = 0.f;
+        for (int q = 0; q < fix.ksplit; ++q) {
+          t0 += q == split ? ss0
+                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                 rsrc, q * G2FIX_SLAB_BYTES + G2FIX_ACC_BYTES + r0 * 4, 0, 16));
+          t1 += q == split ? ss1
+                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                 rsrc, q * G2FIX_SLAB_BYTES + G2FIX_ACC_BYTES + (r0 + 16) * 4, 0, 16));
+        }
+        ss0 = t0;
+        ss1 = t1;
+      }
+    }
+  }
+  if constexpr (RMS) {
     const int rA = m0 + (wr * MT + RPW * wc) * 16 + (lane & 15), rB = rA + 16;
     if constexpr (MODE == MODE_PARTIAL) {
       if (lane < 16) {
@@ -674,9 +749,10 @@ __global__ void __launch_bounds__(256 * WM)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __syncthreads();
       if (lane < 16) {
-        const float inv_k = 1.f / (float)K;
-        rs[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 * inv_k + rms_eps);
-        if constexpr (RPW == 2) rs[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 * inv_k + rms_eps);
+        // (t / K exactly as gemm_reduce_kernel: split and unsplit plans and the in-kernel fixup agree bit for bit)
+        const float fk = (float)K;
+        rs[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 / fk + rms_eps);
+        if constexpr (RPW == 2) rs[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 / fk + rms_eps);
       }
       __syncthreads();
 #pragma unroll
@@ -991,9 +1067,9 @@ __global__ void __launch_bounds__(512)
     __syncthreads();  // every wave is past its last read of the tile buffers
     if constexpr (RMS) {
       if (lane < 16) {
-        const float inv_k = 1.f / (float)K;
-        rs_sh[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 * inv_k + rms_eps);
-        rs_sh[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 * inv_k + rms_eps);
+        const float fk = (float)K;
+        rs_sh[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 / fk + rms_eps);
+        rs_sh[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 / fk + rms_eps);
       }
     }
 #pragma unroll 1
@@ -1245,6 +1321,16 @@ int gemm_ksplit(int M, int N, int K) {
   return (KS + kc - 1) / kc;
 }
 
+static bool g_gemm_fixup = true;
+void gemm_set_fixup(int on) { g_gemm_fixup = on != 0; }
+int gemm_fixup_enabled() { return g_gemm_fixup ? 1 : 0; }
+// slabs of the in-kernel split-K fixup: [tiles of 256 x 256][ksplit][acc + row sums]
+size_t gemm_fix_workspace_floats(int M, int N, int ksplit) {
+  const size_t tiles = (size_t)((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
+  return tiles * ksplit * G2FIX_SLAB_FLOATS;
+}
+int gemm_fix_tiles(int M, int N) { return ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN); }
+
 size_t gemm_workspace_floats(int M, int N, int K) {
   const int ks = gemm_ksplit(M, N, K);
   return ks > 1 ? (size_t)ks * M * (N + 1) : 0;  // slabs + fused-RMS partial sums
@@ -1259,7 +1345,7 @@ static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
-                      int grid_override = 0) {
+                      int grid_override = 0, G2Fix fix = G2Fix{}) {
   const int cfg = tile_cfg(tile, M);
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
@@ -1267,11 +1353,11 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int grid = grid_override > 0 ? grid_override : tm * tn * ksplit;
 #define JLA_G2S(WMV, NB, LATE, R, MTV, NTV, SB)                                                             \
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
-      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq)
+      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix)
 #define JLA_G2(WMV, NB, LATE, R, MTV, NTV) JLA_G2S(WMV, NB, LATE, R, MTV, NTV, 1)
 #define JLA_G2FA(R, FM)                                                                                      \
   gemm2_kernel<MODE, 2, 4, true, R, 8, 4, 1, true, FM><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate,     \
-                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq)
+                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   if constexpr (MODE != MODE_RESIDUAL) {
     if (rms) {  // fused RMSNorm statistic (default pipeline variant only)
@@ -1459,6 +1545,31 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
     JLA_CHECK_LAUNCH();
     return 0;
   }
+  // in-kernel split-K fixup (G2Fix): the default FA pipeline on 256 x 256 tiles, a tickets array from the
+  // caller and slabs of gemm_fix_workspace_floats(); otherwise the partial slabs + reduce kernel below
+  if (g_gemm_fixup && tickets != nullptr && mode != MODE_QKV && g_gemm_impl == 2 && tile_cfg(tile, M) == 1 &&
+      (g_g2_var == 5 || g_g2_var == 6) && (tile < 4)) {
+    const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
+    if (n_tickets < tiles || ws == nullptr || ws_floats < (size_t)tiles * ksplit * G2FIX_SLAB_FLOATS) return -3;
+    const G2Fix fix{ws, tickets, ksplit, 0};
+    switch (mode) {
+      case MODE_STORE:
+        launch_g2<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, ksplit, rms_eps, nullptr, tile,
+                              s, 0, fix);
+        break;
+      case MODE_RESIDUAL:
+        launch_g2<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, ksplit, -1.f, nullptr, tile, s, 0,
+                                 fix);
+        break;
+      case MODE_SWIGLU:
+        launch_g2<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, ksplit, rms_eps, nullptr, tile, s, 0,
+                               fix);
+        break;
+      default: return -1;
+    }
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
   // workspace: [ksplit][M][N] fp32 partial slabs, then (fused RMS) [ksplit][M] partial sums of squares
   const size_t need = (size_t)ksplit * M * N + (rms ? (size_t)ksplit * M : 0);
   if ((N & 3) || ws == nullptr || ws_floats < need) return -3;
@@ -1545,10 +1656,10 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   const u32x4* w = static_cast<const u32x4*>(W);
   if (rms_eps >= 0.f)
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, true, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
-        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr);
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{});
   else
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, false, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
-        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr);
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{});
   JLA_CHECK_LAUNCH();
   argmax_partials_kernel<<<(M + 3) / 4, 256, 0, s>>>(reinterpret_cast<const float2*>(ws), tn * 4, M, idx, val);
   JLA_CHECK_LAUNCH();

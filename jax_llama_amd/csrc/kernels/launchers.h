@@ -51,6 +51,12 @@ size_t gemm_workspace_floats(int M, int N, int K);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0);
+// split-K with tickets (ksplit > 1, tile 0-3, not MODE_QKV): the in-kernel fixup (no reduce kernel) on
+// ws >= gemm_fix_workspace_floats(M, N, ksplit) slabs and >= gemm_fix_tiles(M, N) zero-initialised tickets
+size_t gemm_fix_workspace_floats(int M, int N, int ksplit);
+int gemm_fix_tiles(int M, int N);
+void gemm_set_fixup(int on);  // A/B: 0 = partial slabs + reduce kernel even when tickets are given
+int gemm_fixup_enabled();
 // gemm4 (gemm4.hip): 256x256 tile on 4 waves of 128x128 (K multiple of 64, no K split); gemm() tile config 5
 int gemm4_launch(int mode, const bf16_t* x, const void* w, void* out, int M, int N, int K, int accumulate,
                  int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s);

@@ -216,12 +216,29 @@ def sk_workspace(e, m, n, k, device):
             workspace.get_zeroed("gemm_sk_tickets", SK_MAX_TICKETS, torch.int32, device))
 
 
+FIX_TICKETS = 4096  # tickets of the in-kernel split-K fixup: one fixed-size array (no reallocation under graphs)
+
+
+def fix_workspace(e, m, n, ks, device):
+    """Slabs + self-resetting tickets of the in-kernel split-K fixup (csrc/kernels/gemm.hip G2Fix): sized so
+    the same buffer also serves the partial-slab + reduce-kernel path ([ks][m][n] + [ks][m])."""
+    floats, tiles = e.gemm_fix_workspace(m, n, ks)
+    ws = workspace.get("gemm_ws", max(floats, ks * m * (n + 1)), torch.float32, device)
+    tk = workspace.get_zeroed("gemm_fix_tickets", max(FIX_TICKETS, tiles), torch.int32, device)
+    return ws, tk
+
+
 def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
-    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue."""
+    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue.
+    A split plan gets fixup tickets (the GEMM sums its splits itself) except for the QKV epilogue, whose
+    RoPE + cache write lives in the reduce kernel."""
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, rms)
     if tm == SK_TILE:
         ws, tk = sk_workspace(e, m, n, k, device)
         return 1, tm, ws, tk
+    if ks > 1 and mode != MODE_QKV and e.gemm_fixup_enabled():
+        ws, tk = fix_workspace(e, m, n, ks, device)
+        return ks, tm, ws, tk
     # split-K slabs [ks][m][n] + the fused-RMS partial sums of squares [ks][m]
     ws = workspace.get("gemm_ws", ks * m * (n + 1), torch.float32, device) if ks > 1 else None
     return ks, tm, ws, None
@@ -307,6 +324,8 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     if v == TILED:
         # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
         ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
+        if tm != SK_TILE:
+            tk = None  # split QKV: partial slabs + the RoPE / KV-write reduce kernel
         if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):
             tm = 1  # the stream-K plan has a data-parallel part here: plain GEMM + RoPE kernel
         if ks == 1 and tm != SK_TILE:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel

@@ -162,14 +162,19 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     else:
         out = torch.empty(m, n // 2 if mode == 2 else n, dtype=torch.bfloat16, device=device)
     eps = 1e-5 if (rms and mode != 1) else -1.0
-    ws = torch.empty(max(ks_c) * m * (n + 1), dtype=torch.float32, device=device)
+    # split plans run the way the model runs them: with the in-kernel fixup (tickets) where it applies
+    fix = e.gemm_fixup_enabled()
+    need = max(max(ks_c) * m * (n + 1), max(e.gemm_fix_workspace(m, n, c)[0] for c in ks_c))
+    ws = torch.empty(need, dtype=torch.float32, device=device)
+    fix_tk = torch.zeros(max(e.gemm_fix_workspace(m, n, 2)[1], 1), dtype=torch.int32, device=device) if fix else None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run(c, tm, i):
         if tm == SK_TILE:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, sk_ws, eps, tm, sk_tk)
         else:
-            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm)
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm,
+                   fix_tk if c > 1 else None)
 
     for c, tm in cands:  # warm every variant (code objects, caches) before any timing
         for i in range(2):

@@ -550,6 +550,54 @@ def test_gemm_tile_configs(tile, ks, m):
     torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("m,k,ks", [(256, 1024, 2), (700, 4096, 3), (2048, 4096, 2), (300, 992, 4)])
+def test_gemm_splitk_fixup(m, k, ks):
+    """In-kernel split-K fixup (G2Fix: sc1-published fragment slabs, agent ticket, last arriver sums in split
+    order + runs the epilogue) against the partial-slab + reduce-kernel path: bit-identical (same summation
+    order, same row-scale formula) for every epilogue with and without the fused RMSNorm; tickets reset
+    themselves (three back-to-back runs, one under a hipGraph); and the fp32 reference."""
+    e = ops.ext()
+    n = 768
+    x = torch.randn(m, k).to(BF16)
+    w, pg, _ = _mk_linear(n, k)
+    xg = x.to(DEV)
+    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+    gp = PackedLinear.from_dense(gu, DEV)
+    h0 = torch.randn(m, n).to(DEV)
+    floats, tiles = e.gemm_fix_workspace(m, n, ks)
+    ws = torch.empty(max(floats, ks * m * (n + 1)), dtype=torch.float32, device=DEV)
+    tk = torch.zeros(tiles, dtype=torch.int32, device=DEV)
+
+    def run(tickets):
+        outs = []
+        for eps in (-1.0, 1e-5):
+            o = torch.empty(m, n, dtype=torch.float32, device=DEV)
+            e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, 1, tickets)
+            o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, 1, tickets)
+            outs += [o, o2]
+        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, 1, tickets)
+        return outs + [hg, mir]
+
+    base = run(None)       # partial slabs + reduce kernel
+    fixed = run(tk)        # in-kernel fixup
+    again = run(tk)        # tickets were reset by the last arrivers
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        graphed = run(tk)
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(tk.abs().sum()) == 0
+    for i, (a, b, c, d) in enumerate(zip(base, fixed, again, graphed)):
+        assert torch.equal(b, c) and torch.equal(b, d), f"output {i}: fixup not reproducible"
+        assert torch.equal(a, b), f"output {i}: fixup differs from the reduce path"
+    _close(fixed[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+    _close(fixed[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+    _close(fixed[3], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
+    _close(fixed[4], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
+
+
 @pytest.mark.parametrize("m,k,ks", [(300, 1024, 1), (512, 1056, 1), (256, 992, 3), (700, 4096, 2)])
 def test_gemm_full_line_x(m, k, ks):
     """gemm2 with x staged in full 128-B lines (the default, impl 2: K-tile pairs, swizzled LDS image) is

@@ -137,8 +137,23 @@ def _worker(rank, world, port, kind, q):
             sr = ref.generate(toks, attention_mask=mask, generation_config=gc).sequences.cpu()
             res["err_fp32"] = rel_err(lt[m], lr[m])
             res["err_bf16"] = rel_err(lt16[m], lr[m])
-            res["greedy_eq_tp1"] = torch.equal(st_graph, sr)
+            res["greedy_eq_tp1"] = torch.equal(st_graph, sr)  # informative: K-sums split over ranks round
+            # differently, so an exact tie-break can differ; the asserted property is below
             res["greedy_bf16_first_eq"] = torch.equal(sb_graph[:, 12], sr[:, 12])
+
+            def argmax_gap(seq):
+                """Teacher-forced TP1 logits over ``seq``: per generated token, (max logit - its logit),
+                relative to the logit scale. 0 wherever the token is TP1's argmax."""
+                full_mask = torch.cat([mask, torch.ones(mask.shape[0], seq.shape[1] - mask.shape[1],
+                                                        dtype=mask.dtype)], 1)
+                full_pos = full_mask.cumsum(-1) - 1
+                lf = ref(seq, attention_mask=full_mask, position_ids=full_pos).logits.float().cpu()
+                prev = lf[:, 11:-1]  # logits that chose tokens 12 ..
+                chosen = prev.gather(-1, seq[:, 12:].long().unsqueeze(-1)).squeeze(-1)
+                return float(((prev.max(-1).values - chosen) / prev.abs().amax(-1)).max())
+
+            res["tp_argmax_gap"] = argmax_gap(st_graph)
+            res["tp1_argmax_gap"] = argmax_gap(sr)
             del ref
         dist.barrier()
         q.put(("ok", rank, res))
@@ -170,7 +185,10 @@ def test_tp_decode_matches_single_process(world, kind):
     r0 = res[0]
     assert r0["err_fp32"] < 2e-2, r0["err_fp32"]
     assert r0["err_bf16"] < 2e-2, r0["err_bf16"]
-    assert r0["greedy_eq_tp1"]
+    # every token the TP decode chose is TP1's argmax up to rounding (exact equality of whole sequences is
+    # not a property of a K-split sum: a near-tie can break the other way and the sequences then differ)
+    assert r0["tp1_argmax_gap"] < 1e-4, r0["tp1_argmax_gap"]
+    assert r0["tp_argmax_gap"] < 2e-3, (r0["tp_argmax_gap"], r0["greedy_eq_tp1"])
     assert r0["greedy_bf16_first_eq"]
     for r in range(world):
         assert res[r]["graph_eq_eager_fp32"] and res[r]["graph_eq_eager_bf16"], r

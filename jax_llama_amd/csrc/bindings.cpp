@@ -271,6 +271,21 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
        "gemm");
     return;
   }
+  if (tile == 6) {  // whole waves data-parallel + 2-way split tail with the in-kernel fixup
+    check(ksplit <= 1, "gemm tile 6: no K split of its own");
+    check(ws.has_value() && tickets.has_value(), "gemm tile 6 needs slabs and tickets");
+    check_gpu(*ws, "gemm ws");
+    check_gpu(*tickets, "gemm tickets");
+    check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm_hybrid_workspace_floats(m, n),
+          "gemm tile 6 slabs too small");
+    check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm_fix_tiles(m, n),
+          "gemm tile 6 tickets too small");
+    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
+                 out.scalar_type() == torch::kFloat32, mir, nullptr, ptr<float>(*ws), ws->numel(), 1, stream(),
+                 (float)rms_eps, 6, ptr<int32_t>(*tickets), (int)tickets->numel()),
+       "gemm");
+    return;
+  }
   if (ksplit > 1 && tickets.has_value() && jla::gemm_fixup_enabled()) {  // in-kernel split-K fixup
     check(ws.has_value(), "gemm: split-K needs a workspace");
     check_gpu(*ws, "gemm ws");
@@ -591,6 +606,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
     return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
   }, "(slab floats, tickets) of the in-kernel split-K fixup");
   m.def("gemm_set_fixup", [](bool on) { jla::gemm_set_fixup(on ? 1 : 0); });
+  m.def("gemm_hybrid_workspace", [](int64_t m, int64_t n) {
+    return py::make_tuple((int64_t)jla::gemm_hybrid_workspace_floats(m, n), (int64_t)jla::gemm_fix_tiles(m, n));
+  }, "(slab floats of the split tail, tickets) of tile config 6; 0 floats: no partial wave");
   m.def("gemm_fixup_enabled", []() { return jla::gemm_fixup_enabled() != 0; });
   m.def("gemm_sk_workspace", [](int64_t m, int64_t n, int64_t k) {
     // (slab floats, tickets) of the stream-K tail of this shape; (0, 0) when it has none

@@ -215,9 +215,11 @@ JLA_DEV void g2_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn)
 // reduce kernel, no [ksplit][M][N] round trip; deterministic (fixed order); tickets reset themselves
 // (cdna_hip_programming.md Guideline 16, sc1-store + agent ticket + sc1-load form, as the stream-K tail).
 struct G2Fix {
-  float* slabs;       // [tiles][ksplit][G2FIX_SLAB_FLOATS]
+  float* slabs;       // [tiles of this launch][ksplit][G2FIX_SLAB_FLOATS]
   int32_t* tickets;   // [tiles], zero-initialised once
   int ksplit;         // 1 = no fixup (plain tile, or the MODE_PARTIAL + reduce-kernel path)
+  int tile_base;      // tile_count > 0: this launch covers tiles [tile_base, tile_base + tile_count) of the
+  int tile_count;     //   launch order only (the split tail of tile config 6)
   int pad;
 };
 constexpr int G2FIX_ACC_BYTES = 8 * 8 * 4 * 1024;           // 8 waves x 8 x 4 fragments x 1 KiB
@@ -251,8 +253,9 @@ __global__ void __launch_bounds__(256 * WM)
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tiles = tiles_m * tiles_n;
-  const int split = wgid / tiles;
-  const int pid = wgid - split * tiles;
+  const int tcount = fix.tile_count > 0 ? fix.tile_count : tiles;  // tiles of this launch
+  const int split = wgid / tcount;
+  const int pid = wgid - split * tcount + (fix.tile_count > 0 ? fix.tile_base : 0);
   int tm, tn;
   g2_tile_coords(pid, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -682,7 +685,8 @@ __global__ void __launch_bounds__(256 * WM)
     if (fix.ksplit > 1) {
       // ---- in-kernel split-K fixup (see G2Fix): publish, ticket, last arriver sums in split order
       const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          fix.slabs + (size_t)pid * fix.ksplit * G2FIX_SLAB_FLOATS, 0, fix.ksplit * G2FIX_SLAB_BYTES, 0x00020000);
+          fix.slabs + (size_t)(pid - (fix.tile_count > 0 ? fix.tile_base : 0)) * fix.ksplit * G2FIX_SLAB_FLOATS, 0,
+          fix.ksplit * G2FIX_SLAB_BYTES, 0x00020000);
       const int base = split * G2FIX_SLAB_BYTES;
       const int r0 = (wr * MT + RPW * wc) * 16 + (lane & 15);
 #pragma unroll
@@ -1321,7 +1325,11 @@ int gemm_ksplit(int M, int N, int K) {
   return (KS + kc - 1) / kc;
 }
 
-static bool g_gemm_fixup = true;
+static int num_cus();
+// Off by default: measured slower than partial slabs + the reduce kernel on MI355X (the sc1 write-through
+// publish + vmcnt(0) round trip + one workgroup re-reading 256 KiB per split costs more than the separate pass:
+// o / down / qkv / gate_up at M = 512 / 2048, profiles/r2_gemm_splitk_fixup_ab.jsonl); kept as an option.
+static bool g_gemm_fixup = false;
 void gemm_set_fixup(int on) { g_gemm_fixup = on != 0; }
 int gemm_fixup_enabled() { return g_gemm_fixup ? 1 : 0; }
 // slabs of the in-kernel split-K fixup: [tiles of 256 x 256][ksplit][acc + row sums]
@@ -1330,6 +1338,11 @@ size_t gemm_fix_workspace_floats(int M, int N, int ksplit) {
   return tiles * ksplit * G2FIX_SLAB_FLOATS;
 }
 int gemm_fix_tiles(int M, int N) { return ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN); }
+// tile config 6 (whole waves data-parallel + 2-way split tail): slab floats of the tail (0: no tail)
+size_t gemm_hybrid_workspace_floats(int M, int N) {
+  const int tiles = gemm_fix_tiles(M, N), P = num_cus();
+  return (size_t)(tiles - (tiles / P) * P) * 2 * G2FIX_SLAB_FLOATS;
+}
 
 size_t gemm_workspace_floats(int M, int N, int K) {
   const int ks = gemm_ksplit(M, N, K);
@@ -1350,7 +1363,7 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
   // grid_override: only the first grid_override tiles of the launch order (stream-K's data-parallel part)
-  const int grid = grid_override > 0 ? grid_override : tm * tn * ksplit;
+  const int grid = grid_override > 0 ? grid_override : (fix.tile_count > 0 ? fix.tile_count : tm * tn) * ksplit;
 #define JLA_G2S(WMV, NB, LATE, R, MTV, NTV, SB)                                                             \
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
       x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix)
@@ -1513,6 +1526,30 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   const bool rms = rms_eps >= 0.f;
   if (rms && (g_gemm_impl == 1 || mode == MODE_RESIDUAL)) return -5;  // caller pre-scales x instead
+  if (tile == 6) {  // whole waves of 256x256 tiles data-parallel + the last partial wave split 2-way (fixup)
+    if (g_gemm_impl != 2 || mode == MODE_QKV || tickets == nullptr || !(g_g2_var == 5 || g_g2_var == 6)) return -1;
+    const int P = num_cus();
+    const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
+    const int dp = (tiles / P) * P, tail = tiles - dp;
+    const u32x4* wp = static_cast<const u32x4*>(W);
+    if (n_tickets < tiles || ws == nullptr || ws_floats < (size_t)tail * 2 * G2FIX_SLAB_FLOATS) return -3;
+    const int KS = K >> 5, kc2 = (KS + 1) / 2;
+    const G2Fix fix{ws, tickets, 2, dp, tail, 0};
+#define JLA_G6(MD, OF32, MIR, EPS)                                                                                \
+  {                                                                                                              \
+    if (dp > 0) launch_g2<MD>(x, wp, out, M, N, K, accumulate, OF32, MIR, KS, 1, EPS, nullptr, 1, s, dp);        \
+    if (tail > 0) launch_g2<MD>(x, wp, out, M, N, K, accumulate, OF32, MIR, kc2, 2, EPS, nullptr, 1, s, 0, fix); \
+  }
+    switch (mode) {
+      case MODE_STORE: JLA_G6(MODE_STORE, out_f32, nullptr, rms_eps) break;
+      case MODE_RESIDUAL: JLA_G6(MODE_RESIDUAL, 1, mirror, -1.f) break;
+      case MODE_SWIGLU: JLA_G6(MODE_SWIGLU, 0, nullptr, rms_eps) break;
+      default: return -1;
+    }
+#undef JLA_G6
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
   if (tile == 4) {  // stream-K tail (256x256 ping-pong tiles; no K split)
     if (g_gemm_impl != 2 || ksplit > 1) return -1;
     if (mode == MODE_QKV && !qkv) return -1;
@@ -1551,7 +1588,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
       (g_g2_var == 5 || g_g2_var == 6) && (tile < 4)) {
     const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
     if (n_tickets < tiles || ws == nullptr || ws_floats < (size_t)tiles * ksplit * G2FIX_SLAB_FLOATS) return -3;
-    const G2Fix fix{ws, tickets, ksplit, 0};
+    const G2Fix fix{ws, tickets, ksplit, 0, 0, 0};
     switch (mode) {
       case MODE_STORE:
         launch_g2<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, ksplit, rms_eps, nullptr, tile,

@@ -55,6 +55,9 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
 // ws >= gemm_fix_workspace_floats(M, N, ksplit) slabs and >= gemm_fix_tiles(M, N) zero-initialised tickets
 size_t gemm_fix_workspace_floats(int M, int N, int ksplit);
 int gemm_fix_tiles(int M, int N);
+// tile config 6: whole waves of 256x256 tiles data-parallel, the last partial wave split 2-way with the fixup
+// (ws >= gemm_hybrid_workspace_floats(M, N), tickets >= gemm_fix_tiles(M, N))
+size_t gemm_hybrid_workspace_floats(int M, int N);
 void gemm_set_fixup(int on);  // A/B: 0 = partial slabs + reduce kernel even when tickets are given
 int gemm_fixup_enabled();
 // gemm4 (gemm4.hip): 256x256 tile on 4 waves of 128x128 (K multiple of 64, no K split); gemm() tile config 5

@@ -236,6 +236,11 @@ def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
     if tm == SK_TILE:
         ws, tk = sk_workspace(e, m, n, k, device)
         return 1, tm, ws, tk
+    if tm == autotune.HYBRID_TILE:
+        floats, tiles = e.gemm_hybrid_workspace(m, n)
+        ws = workspace.get("gemm_ws", max(floats, 1), torch.float32, device)
+        tk = workspace.get_zeroed("gemm_fix_tickets", max(FIX_TICKETS, tiles), torch.int32, device)
+        return 1, tm, ws, tk
     if ks > 1 and mode != MODE_QKV and e.gemm_fixup_enabled():
         ws, tk = fix_workspace(e, m, n, ks, device)
         return ks, tm, ws, tk
@@ -324,6 +329,8 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     if v == TILED:
         # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
         ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
+        if tm == autotune.HYBRID_TILE:
+            tm = 1  # (only reached with ks == 1: the plain linear() below runs the hybrid plan itself)
         if tm != SK_TILE:
             tk = None  # split QKV: partial slabs + the RoPE / KV-write reduce kernel
         if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):

@@ -137,6 +137,7 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
 
 
 SK_TILE = 4  # 256x256 tiles with a stream-K tail (no K split): csrc/kernels/gemm.hip gemm_sk
+HYBRID_TILE = 6  # whole waves of 256x256 tiles + the partial wave split 2-way with the in-kernel fixup
 SK_MARGIN = 0.97
 TUNE_ROUNDS = 3
 
@@ -149,6 +150,9 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     sk_ws, sk_tk = sk_workspace(e, m, n, k, device)
     if sk_ws is not None:
         cands.append((1, SK_TILE))
+    hyb_floats = e.gemm_hybrid_workspace(m, n)[0] if e.gemm_fixup_enabled() else 0
+    if hyb_floats > 0:  # whole waves data-parallel + the partial wave split 2-way (in-kernel fixup)
+        cands.append((1, HYBRID_TILE))
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
@@ -164,14 +168,18 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     eps = 1e-5 if (rms and mode != 1) else -1.0
     # split plans run the way the model runs them: with the in-kernel fixup (tickets) where it applies
     fix = e.gemm_fixup_enabled()
-    need = max(max(ks_c) * m * (n + 1), max(e.gemm_fix_workspace(m, n, c)[0] for c in ks_c))
+    need = max(max(ks_c) * m * (n + 1), max(e.gemm_fix_workspace(m, n, c)[0] for c in ks_c), hyb_floats)
     ws = torch.empty(need, dtype=torch.float32, device=device)
     fix_tk = torch.zeros(max(e.gemm_fix_workspace(m, n, 2)[1], 1), dtype=torch.int32, device=device) if fix else None
+    if fix_tk is None and hyb_floats:
+        fix_tk = torch.zeros(e.gemm_fix_workspace(m, n, 2)[1], dtype=torch.int32, device=device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     def run(c, tm, i):
         if tm == SK_TILE:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, sk_ws, eps, tm, sk_tk)
+        elif tm == HYBRID_TILE:
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, ws, eps, tm, fix_tk)
         else:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm,
                    fix_tk if c > 1 else None)

@@ -581,13 +581,17 @@ def test_gemm_splitk_fixup(m, k, ks):
         return outs + [hg, mir]
 
     base = run(None)       # partial slabs + reduce kernel
-    fixed = run(tk)        # in-kernel fixup
-    again = run(tk)        # tickets were reset by the last arrivers
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        graphed = run(tk)
-    g.replay()
-    torch.cuda.synchronize()
+    e.gemm_set_fixup(True)  # (off by default: slower than the reduce kernel on MI355X)
+    try:
+        fixed = run(tk)        # in-kernel fixup
+        again = run(tk)        # tickets were reset by the last arrivers
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            graphed = run(tk)
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        e.gemm_set_fixup(False)
     assert int(tk.abs().sum()) == 0
     for i, (a, b, c, d) in enumerate(zip(base, fixed, again, graphed)):
         assert torch.equal(b, c) and torch.equal(b, d), f"output {i}: fixup not reproducible"
@@ -596,6 +600,56 @@ def test_gemm_splitk_fixup(m, k, ks):
     _close(fixed[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
     _close(fixed[3], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
     _close(fixed[4], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
+
+
+@pytest.mark.parametrize("cus,m,n", [(4, 512, 768), (8, 700, 1536), (0, 2048, 28672)])
+def test_gemm_hybrid_tail(cus, m, n):
+    """Tile config 6: whole waves of 256x256 tiles data-parallel + the last partial wave split 2-way with the
+    in-kernel fixup (two launches); every epilogue with / without the fused RMSNorm vs the fp32 reference and
+    vs the plain tile-1 plan; tickets reset (two runs identical); cus > 0 pretends a smaller chip so small
+    shapes have a tail."""
+    e = ops.ext()
+    k = 1024
+    x = torch.randn(m, k).to(BF16)
+    w, pg, _ = _mk_linear(n, k)
+    xg = x.to(DEV)
+    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+    gp = PackedLinear.from_dense(gu, DEV)
+    h0 = torch.randn(m, n).to(DEV)
+    try:
+        e.gemm_sk_set_cus(cus)
+        floats, tiles = e.gemm_hybrid_workspace(m, n)
+        assert floats > 0, "shape must have a partial wave"
+        ws = torch.empty(floats, dtype=torch.float32, device=DEV)
+        tk = torch.zeros(tiles, dtype=torch.int32, device=DEV)
+
+        def run(tile, tickets, wsp):
+            outs = []
+            for eps in (-1.0, 1e-5):
+                o = torch.empty(m, n, dtype=torch.float32, device=DEV)
+                e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, 1, wsp, eps, tile, tickets)
+                o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+                e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, wsp, eps, tile, tickets)
+                outs += [o, o2]
+            hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+            e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, wsp, -1.0, tile, tickets)
+            return outs + [hg, mir]
+
+        hyb, hyb2 = run(6, tk, ws), run(6, tk, ws)
+        plain = run(1, None, None)
+        torch.cuda.synchronize()
+    finally:
+        e.gemm_sk_set_cus(0)
+    assert int(tk.abs().sum()) == 0
+    for i, (a, b) in enumerate(zip(hyb, hyb2)):
+        assert torch.equal(a, b), f"output {i}: not reproducible"
+    for i, (a, b) in enumerate(zip(hyb, plain)):
+        _close(a, b, 2e-2, 2e-2)
+    _close(hyb[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+    _close(hyb[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+    _close(hyb[3], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
+    _close(hyb[4], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
+    torch.testing.assert_close(hyb[5].cpu(), hyb[4].cpu().to(BF16), rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("m,k,ks", [(300, 1024, 1), (512, 1056, 1), (256, 992, 3), (700, 4096, 2)])

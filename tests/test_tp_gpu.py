@@ -188,7 +188,8 @@ def test_tp_decode_matches_single_process(world, kind):
     # every token the TP decode chose is TP1's argmax up to rounding (exact equality of whole sequences is
     # not a property of a K-split sum: a near-tie can break the other way and the sequences then differ)
     assert r0["tp1_argmax_gap"] < 1e-4, r0["tp1_argmax_gap"]
-    assert r0["tp_argmax_gap"] < 2e-3, (r0["tp_argmax_gap"], r0["greedy_eq_tp1"])
+    # (a near-tie broken the other way costs at most the logits' rounding error: err_fp32 above is < 2e-2)
+    assert r0["tp_argmax_gap"] < 1e-2, (r0["tp_argmax_gap"], r0["greedy_eq_tp1"])
     assert r0["greedy_bf16_first_eq"]
     for r in range(world):
         assert res[r]["graph_eq_eager_fp32"] and res[r]["graph_eq_eager_bf16"], r

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--impl", type=int, nargs="+", default=[2], help="tiled kernel generation(s) to time")
     ap.add_argument("--ops", nargs="+", default=None)
     ap.add_argument("--rounds", type=int, default=1, help="interleaved A/B rounds of the impl list (one process)")
+    ap.add_argument("--fixup", type=int, nargs="+", default=[0], help="split-K: 0 partial slabs + reduce kernel, "
+                    "1 in-kernel fixup (tickets); tile 6 always uses the fixup")
     ap.add_argument("--tile", type=int, nargs="+", default=[0], help="gemm2 tile config(s): 0 auto, 1 256x256, "
                     "2 128x256, 3 128x128, 5 gemm4; 50 + v: gemm4 variant v")
     args = ap.parse_args()
@@ -76,32 +78,46 @@ def main():
                   for tile in args.tile:
                     kk = ks or e.gemm_ksplit(m, n, k)
                     tk = None
-                    if tile == 4:  # stream-K tail plan (no K split)
-                        kk = 1
-                        ws, tk = ops.sk_workspace(e, m, n, k, DEV)
-                        if ws is None:
-                            continue
-                    else:
-                        ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
+                    for fx in args.fixup:
+                      tk = None
+                      if tile == 4:  # stream-K tail plan (no K split)
+                          kk = 1
+                          ws, tk = ops.sk_workspace(e, m, n, k, DEV)
+                          if ws is None:
+                              continue
+                      elif tile == 6:  # whole waves + 2-way split tail (fixup)
+                          kk = 1
+                          floats, tiles = e.gemm_hybrid_workspace(m, n)
+                          if floats == 0:
+                              continue
+                          ws = torch.empty(floats, device=DEV, dtype=torch.float32)
+                          tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
+                      elif fx and kk > 1:
+                          floats, tiles = e.gemm_fix_workspace(m, n, kk)
+                          ws = torch.empty(max(floats, kk * m * n), device=DEV, dtype=torch.float32)
+                          tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
+                      else:
+                          ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
 
-                    tcfg = tile
-                    if tile >= 50:
-                        e.gemm4_set_variant(tile - 50)
-                        tcfg = 5
+                      tcfg = tile
+                      if tile >= 50:
+                          e.gemm4_set_variant(tile - 50)
+                          tcfg = 5
 
-                    def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk):
-                        e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk,
-                               ws if (kk > 1 or tile == 4) else None, -1.0, tile, tk)
-                    res[f"v{impl}_ks{kk}_t{tile}" + (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
-                    run(0)
-                    got = out.float()
-                    if ref is None:
-                        ref = (x.float() @ dense[0].float().t())
-                    err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
-                    assert err < 2e-2 or (tile >= 50 and (tile - 50) & 14), (name, m, impl, kk, err)
-                    if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
-                        f0 = first.setdefault((kk, tile), got.clone())
-                        assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
+                      def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk):
+                          e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk,
+                                 ws if (kk > 1 or tile in (4, 6)) else None, -1.0, tile, tk)
+                      res[f"v{impl}_ks{kk}_t{tile}" + ("_fix" if fx and kk > 1 else "") +
+                          (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
+                      run(0)
+                      got = out.float()
+                      if ref is None:
+                          ref = (x.float() @ dense[0].float().t())
+                      err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+                      assert err < 2e-2 or (tile >= 50 and (tile - 50) & 14), (name, m, impl, kk, err)
+                      if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
+                          f0 = first.setdefault((kk, tile), got.clone())
+                          assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
             e.gemm_set_impl(2)
             if not args.no_blas:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)

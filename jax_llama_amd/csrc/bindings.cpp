@@ -102,7 +102,8 @@ void check_linear_out(const Tensor& out, int64_t m, int64_t n, int64_t mode) {
 }
 
 // Decode linear dispatch. variant: 0 = auto (M == 1 -> K-split GEMV, else split-K skinny GEMM),
-// 1/2/3 = K-split GEMV (gemv.hip) with 4/8/16 waves, 4 = split-K skinny GEMM (skinny.hip).
+// 1/2/3 = K-split GEMV (gemv.hip) with 4/8/16 waves, 4 = split-K skinny GEMM (skinny.hip), 5/6/8-11 = GEMV
+// tile / wave / ring-depth variants (gemv.hip dispatch_nt).
 void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* out, int64_t mode, double rms_eps,
                 bool accumulate, bool out_f32, const jla::QKVArgs* qa, int64_t variant, const Tensor& ws,
                 const Tensor& tickets) {
@@ -149,7 +150,7 @@ void linear_skinny_argmax(Tensor x, Tensor w, int64_t n, int64_t k, double rms_e
         "x must be fp32/bf16 [M, K]");
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_skinny_argmax: M too large");
-  check(variant == 1 || variant == 2 || variant == 3 || variant == 5 || variant == 6 || variant == 8 || variant == 9,
+  check(variant == 1 || variant == 2 || variant == 3 || (variant >= 5 && variant <= 11 && variant != 7),
         "argmax: GEMV variants only");
   check_gpu(part, "part");
   check(part.scalar_type() == torch::kFloat32 && part.numel() >= m * (n / 16) * 2, "argmax partials too small");
@@ -626,6 +627,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm_argmax_workspace", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_argmax_workspace_floats(m, n); });
   m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
+  m.def("skinny_set_plan", [](int64_t nt, int64_t ks) { jla::skinny_set_plan((int)nt, (int)ks); });
   m.def("gemm4_set_variant", [](int64_t v) { jla::gemm4_set_variant((int)v); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);

@@ -211,8 +211,12 @@ JLA_DEV u32x2 ld_tr(const char* lds, int off) {
                                        (__attribute__((address_space(3))) s16x4*)(lds + off)));
 }
 
-template <int NW>
-__global__ void __launch_bounds__(NW * 64, 2)
+// QB query blocks of 32 per wave (QB = 2: "v3", 64 queries per wave): every K fragment (ds_read_b128) and V^T
+// fragment (2 x ds_read_b64_tr_b16) read from LDS feeds QB MFMAs instead of one. With QB = 1 four waves x two
+// workgroups re-read each 32-KiB K/V tile per 32 MFMAs per wave -- about the LDS read rate; QB = 2 halves the
+// LDS bytes per MFMA at the price of one workgroup per CU (O^T, S^T, Q^T and P for 64 queries: ~340 registers).
+template <int NW, int QB>
+__global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
     attn_prefill_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                            const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                            const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int S, int H,
@@ -220,6 +224,7 @@ __global__ void __launch_bounds__(NW * 64, 2)
   constexpr int NT = NW * 64;
   constexpr int TILE_BYTES = FA_KT * AP_DH * 2;            // 16 KiB
   constexpr int CH_PER_T = FA_KT * 16 / NT;                 // 16-byte chunks per thread per tile (K or V)
+  constexpr int QW = 32 * QB;                               // queries per wave
   __shared__ __attribute__((aligned(16))) char lds[2 * TILE_BYTES];
   char* Ks = lds;
   char* Vs = lds + TILE_BYTES;
@@ -238,32 +243,37 @@ __global__ void __launch_bounds__(NW * 64, 2)
   const int qb = pass == 0 ? n_qb - 1 - (int)blockIdx.x : (int)blockIdx.x;
   if (pass == 1 && qb >= n_qb - 1 - (int)blockIdx.x) break;  // odd n_qb: the middle block runs once
   if (pass == 1) __syncthreads();  // every wave is done with the LDS images of the first block
-  const int p0 = qb * 32 * npb + 32 * pb;   // first query position of this wave
-  const int pos = p0 + col;                  // this lane's query
+  const int p0 = qb * QW * npb + QW * pb;   // first query position of this wave
   const int slot0 = slot_ptr[0];
   if (slot0 + S > T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);
   const int lo = kv_start[b];
   const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
 
-  // Q^T fragments (B operand): lane holds Q[pos][16 ks + 8 hi .. +7]
-  u32x4 qf[8];
-  {
+  // Q^T fragments (B operand) of query block qq: lane holds Q[p0 + 32 qq + col][16 ks + 8 hi .. +7]
+  u32x4 qf[QB][8];
+#pragma unroll
+  for (int qq = 0; qq < QB; ++qq) {
+    const int pos = p0 + 32 * qq + col;
     const bf16_t* qrow = q + (((size_t)b * S + min(pos, S - 1)) * H + h) * AP_DH + 8 * hi;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) qf[ks] = *reinterpret_cast<const u32x4*>(qrow + 16 * ks);
+    for (int ks = 0; ks < 8; ++ks) qf[qq][ks] = *reinterpret_cast<const u32x4*>(qrow + 16 * ks);
   }
-  f32x16 o[4];
+  f32x16 o[QB][4];
+  float m_run[QB], l_run[QB];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt)
+  for (int qq = 0; qq < QB; ++qq) {
+    m_run[qq] = -INFINITY;
+    l_run[qq] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[qq][dt][i] = 0.f;
+  }
 
-  const int wg_last_pos = min(S, (qb + 1) * 32 * npb) - 1;
+  const int wg_last_pos = min(S, (qb + 1) * QW * npb) - 1;
   const int last_key = min(slot0 + wg_last_pos, T - 1);
   const int t_begin = (lo / FA_KT) * FA_KT;
-  const int wave_first_slot = slot0 + p0, wave_last_slot = slot0 + min(p0 + 31, S - 1);
-  const int qslot = slot0 + pos;
+  const int wave_last_slot = slot0 + min(p0 + QW - 1, S - 1);
   const bf16_t* kb = kc + ((size_t)b * Hkv + kvh) * T * AP_DH;
   const bf16_t* vb = vc + ((size_t)b * Hkv + kvh) * T * AP_DH;
 
@@ -300,58 +310,66 @@ __global__ void __launch_bounds__(NW * 64, 2)
     const bool has_next = t0 + FA_KT <= last_key;
     if (has_next) load_tile(t0 + FA_KT);
     if (t0 <= wave_last_slot) {
-      // ---- S^T = K Q^T
-      f32x16 st[2];
+      // ---- S^T = K Q^T (each K fragment feeds the QB query blocks)
+      f32x16 st[QB][2];
 #pragma unroll
       for (int kbk = 0; kbk < 2; ++kbk) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) st[kbk][i] = 0.f;
+        for (int qq = 0; qq < QB; ++qq)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) st[qq][kbk][i] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
           const u32x4 kf = *reinterpret_cast<const u32x4*>(Ks + fa_off(32 * kbk + col, 2 * ks + hi));
-          st[kbk] = mfma32(kf, qf[ks], st[kbk]);
+#pragma unroll
+          for (int qq = 0; qq < QB; ++qq) st[qq][kbk] = mfma32(kf, qf[qq][ks], st[qq][kbk]);
         }
       }
-      // ---- online softmax (log2 domain); element (kbk, i) is key t0 + 32 kbk + (i & 3) + 8 (i >> 2) + 4 hi
-      const bool full = !mrow && t0 >= lo && t0 + FA_KT - 1 <= wave_first_slot && t0 + FA_KT - 1 < T;
-      float tmax = -INFINITY;
+      // ---- online softmax per query block (log2 domain); element (kbk, i) is key
+      // t0 + 32 kbk + (i & 3) + 8 (i >> 2) + 4 hi
+      u32x4 pf[QB][4];  // B fragments of P^T for the 4 key steps
 #pragma unroll
-      for (int kbk = 0; kbk < 2; ++kbk)
+      for (int qq = 0; qq < QB; ++qq) {
+        const int qfirst = slot0 + p0 + 32 * qq, qslot = qfirst + col;
+        const bool full = !mrow && t0 >= lo && t0 + FA_KT - 1 <= qfirst && t0 + FA_KT - 1 < T;
+        float tmax = -INFINITY;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float v = st[kbk][i] * scale_log2;
-          if (!full) {
-            const int j = t0 + 32 * kbk + (i & 3) + 8 * (i >> 2) + 4 * hi;
-            bool ok = j >= lo && j <= qslot && j < T;
-            if (mrow) ok = ok && j < mask_len && mrow[j] != 0;
-            v = ok ? v : -INFINITY;
+        for (int kbk = 0; kbk < 2; ++kbk)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float v = st[qq][kbk][i] * scale_log2;
+            if (!full) {
+              const int j = t0 + 32 * kbk + (i & 3) + 8 * (i >> 2) + 4 * hi;
+              bool ok = j >= lo && j <= qslot && j < T;
+              if (mrow) ok = ok && j < mask_len && mrow[j] != 0;
+              v = ok ? v : -INFINITY;
+            }
+            st[qq][kbk][i] = v;
+            tmax = fmaxf(tmax, v);
           }
-          st[kbk][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float m_new = fmaxf(m_run, tmax);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);  // m_run = -inf -> 0
-      float rs = 0.f;
-      u32x4 pf[4];  // B fragments of P^T for the 4 key steps
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float m_new = fmaxf(m_run[qq], tmax);
+        const float m_use = m_new == -INFINITY ? 0.f : m_new;
+        const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - m_use);  // m_run = -inf -> 0
+        float rs = 0.f;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float e[8];
+        for (int s = 0; s < 4; ++s) {
+          float e[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          e[j] = __builtin_amdgcn_exp2f(st[s >> 1][8 * (s & 1) + j] - m_use);
-          rs += e[j];
+          for (int j = 0; j < 8; ++j) {
+            e[j] = __builtin_amdgcn_exp2f(st[qq][s >> 1][8 * (s & 1) + j] - m_use);
+            rs += e[j];
+          }
+          pf[qq][s] = pack8(e);
         }
-        pf[s] = pack8(e);
+        rs += __shfl_xor(rs, 32, 64);
+        l_run[qq] = l_run[qq] * alpha + rs;
+        m_run[qq] = m_new;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
       }
-      rs += __shfl_xor(rs, 32, 64);
-      l_run = l_run * alpha + rs;
-      m_run = m_new;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
       // ---- O^T += V^T P^T; A element j of lane half hi = V[key 16 s + 8 (j >> 2) + 4 hi + (j & 3)][d]
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -362,7 +380,8 @@ __global__ void __launch_bounds__(NW * 64, 2)
           const u32x2 lo4 = ld_tr(Vs, fa_off(r0, c0) + 8 * (gp & 1));
           const u32x2 hi4 = ld_tr(Vs, fa_off(r0 + 8, c0) + 8 * (gp & 1));
           const u32x4 vf = {lo4[0], lo4[1], hi4[0], hi4[1]};
-          o[dt] = mfma32(vf, pf[s], o[dt]);
+#pragma unroll
+          for (int qq = 0; qq < QB; ++qq) o[qq][dt] = mfma32(vf, pf[qq][s], o[qq][dt]);
         }
       }
     }
@@ -374,18 +393,22 @@ __global__ void __launch_bounds__(NW * 64, 2)
   }
 
   // ---- epilogue: lane (query pos, half hi) holds d = 32 dt + 8 g + 4 hi + (0..3) in o[dt][4 g .. 4 g + 3]
-  if (pos < S) {
-    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-    bf16_t* dst = out + ((size_t)b * S + pos) * H * AP_DH + (size_t)h * AP_DH + 4 * hi;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+  for (int qq = 0; qq < QB; ++qq) {
+    const int pos = p0 + 32 * qq + col;
+    if (pos < S) {
+      const float inv = l_run[qq] > 0.f ? 1.f / l_run[qq] : 0.f;
+      bf16_t* dst = out + ((size_t)b * S + pos) * H * AP_DH + (size_t)h * AP_DH + 4 * hi;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u32x2 pk;
-        pk[0] = pack2bf(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
-        pk[1] = pack2bf(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *reinterpret_cast<u32x2*>(dst + 32 * dt + 8 * g) = pk;
-      }
+      for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u32x2 pk;
+          pk[0] = pack2bf(o[qq][dt][4 * g] * inv, o[qq][dt][4 * g + 1] * inv);
+          pk[1] = pack2bf(o[qq][dt][4 * g + 2] * inv, o[qq][dt][4 * g + 3] * inv);
+          *reinterpret_cast<u32x2*>(dst + 32 * dt + 8 * g) = pk;
+        }
+    }
   }
   }  // pass
 }
@@ -400,15 +423,22 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   if (Dh != AP_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   constexpr int NW = 4;
-  if (g_attn_prefill_impl == 2 && (rep % NW == 0 || NW % rep == 0)) {
-    const int npb = rep >= NW ? 1 : NW / rep;    // 32-query position blocks per workgroup
+  if ((g_attn_prefill_impl == 2 || g_attn_prefill_impl == 3) && (rep % NW == 0 || NW % rep == 0)) {
+    const int npb = rep >= NW ? 1 : NW / rep;    // position blocks per workgroup
     const int hpw = NW / npb;                    // q heads per workgroup
     const int hgroups = rep / hpw;
-    const int n_qb = (S + 32 * npb - 1) / (32 * npb);
-    dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
-    attn_prefill_v2_kernel<NW><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
-                                                         Hkv, T, 1.4426950408889634f / sqrtf((float)Dh), npb,
-                                                         hgroups, n_qb);
+    const float sl2 = 1.4426950408889634f / sqrtf((float)Dh);
+    if (g_attn_prefill_impl == 3) {  // 64 queries per wave
+      const int n_qb = (S + 64 * npb - 1) / (64 * npb);
+      dim3 grid3((n_qb + 1) / 2, Hkv * hgroups, B);
+      attn_prefill_v2_kernel<NW, 2><<<grid3, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S,
+                                                              H, Hkv, T, sl2, npb, hgroups, n_qb);
+    } else {
+      const int n_qb = (S + 32 * npb - 1) / (32 * npb);
+      dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
+      attn_prefill_v2_kernel<NW, 1><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S,
+                                                              H, Hkv, T, sl2, npb, hgroups, n_qb);
+    }
     JLA_CHECK_LAUNCH();
     return 0;
   }

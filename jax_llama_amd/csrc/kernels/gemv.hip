@@ -110,16 +110,20 @@ struct XRaw<bf16_t> {  // 8 bf16 activations per lane (one 16-byte load)
     asm_load<ASM>(v, p);
   }
   JLA_DEV void pin_regs() { pin(v); }
+  // sum of squares straight from the packed pairs (v_dot2_f32_bf16): no unpacked temporaries, which at
+  // MT > 1 made hipcc copy in-flight ring registers (tools/check_asm_ring.py hazards) and forced the
+  // compiler-counted ring that drains at every back-edge
   JLA_DEV u32x4 frag(float& ss) const {
-    float f[8];
-    unpack8(v, f);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) ss += f[i] * f[i];
+    for (int i = 0; i < 4; ++i) {
+      const bf16x2_t p = __builtin_bit_cast(bf16x2_t, v[i]);
+      ss = __builtin_amdgcn_fdot2_f32_bf16(p, p, ss, false);
+    }
     return v;
   }
 };
 
-template <typename XT, int MT, int NT, int MODE, int NW, int U>
+template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false>
 __global__ void __launch_bounds__(NW * 64)
     linear_skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out,
                          int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa) {
@@ -141,7 +145,9 @@ __global__ void __launch_bounds__(NW * 64)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int row = min(mt * 16 + (lane & 15), M - 1);  // padding rows re-read the last row (not stored)
-    xp[mt] = x + (size_t)row * K + 8 * (lane >> 4);
+    // XP: activations pre-packed as MFMA A fragments [MT][KS][64 lanes][8] (1 KiB contiguous per k-step,
+    // like the weights) instead of row-major (16 rows x 64 B = 16 half-used cache lines per fragment)
+    xp[mt] = XP ? x + ((size_t)mt * KS * 64 + lane) * 8 : x + (size_t)row * K + 8 * (lane >> 4);
   }
   const u32x4* zfrag = g_zero_frag + lane;
   const XT* zx = reinterpret_cast<const XT*>(g_zero_frag);
@@ -161,11 +167,10 @@ __global__ void __launch_bounds__(NW * 64)
   XRaw<XT> aq[U][MT] = {};
   constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
   // hand-counted ring (see asm_load_nt) where the assembly check passes: every bf16-activation
-  // variant (the decode path: the residual stream's bf16 mirror) and fp32 at MT = 1
-  // (bf16 MT = 2 with one tile fails the check: hipcc reuses in-flight ring registers there).
-  // (the 16-wave and doubled-ring variants 8/9 use compiler-counted loads: their ring fails the check)
+  // variant (the decode path: the residual stream's bf16 mirror) up to 8 waves, single or doubled ring,
+  // and fp32 at MT = 1 (the 16-wave variant 8 uses compiler-counted loads: its ring fails the check)
   constexpr int U_BASE = ((NT == 1 ? 8 : 4) / MT) < 2 ? 2 : ((NT == 1 ? 8 : 4) / MT);
-  constexpr bool ASM = (MT == 1 || (sizeof(XT) == 2 && !(MT == 2 && NT == 1))) && NW <= 8 && U <= U_BASE;
+  constexpr bool ASM = (MT == 1 || sizeof(XT) == 2) && NW <= 8 && U <= 2 * U_BASE;
   auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
     const bool valid = i < n;
     const size_t ks = (size_t)(w + i * NW);
@@ -173,7 +178,7 @@ __global__ void __launch_bounds__(NW * 64)
     for (int t = 0; t < NT; ++t)
       asm_load_nt<ASM>(b[t], valid ? (const void*)(wt[t] + ks * 64) : (const void*)zfrag);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt].template load<ASM>(valid ? xp[mt] + ks * 32 : zx);
+    for (int mt = 0; mt < MT; ++mt) a[mt].template load<ASM>(valid ? xp[mt] + ks * (XP ? 512 : 32) : zx);
   };
   // No separate prologue: the first trip computes on the zero-initialised slots (MFMA adds 0) while
   // issuing k-steps 0..U-1, so every ring register has exactly one definition site (the tied
@@ -332,7 +337,7 @@ __global__ void __launch_bounds__(NW * 64)
   }
 }
 
-template <typename XT, int MT, int NT, int MODE, int NW, int DEEP = 0>
+template <typename XT, int MT, int NT, int MODE, int NW, int DEEP = 0, bool XP = false>
 static int launch_skinny(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
                          int accumulate, int out_f32, const QKVArgs& qa, hipStream_t s) {
   // k-steps in flight per wave: 8 KiB of weights per wave at MT = 1; fp32 activations double the
@@ -345,7 +350,7 @@ static int launch_skinny(const void* x, const void* W, void* out, int M, int N, 
   const int NTT = N >> 4;
   const int grid = (NTT + NT - 1) / NT;
   const size_t lds = sizeof(float) * (NW * MT * NT * 256 + NW * MT * 16 + MT * 16);
-  auto kern = &linear_skinny_kernel<XT, MT, NT, MODE, NW, U>;
+  auto kern = &linear_skinny_kernel<XT, MT, NT, MODE, NW, U, XP>;
   if (lds > 65536) {  // opt in to > 64 KiB of dynamic LDS once (not a stream op: capture-safe)
     static bool attr_set = false;
     if (!attr_set) {
@@ -394,13 +399,33 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       return launch_skinny<XT, MT, 4, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
     if (variant == 6)
       return launch_skinny<XT, MT, 2, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-    // variants 8 / 9 (bf16 activations, M > 16): 1 tile per workgroup, 16 waves / 8 waves with a doubled ring --
-    // more weight + activation bytes in flight per CU for the latency-bound small-N projections
-    if constexpr (MT > 1 && sizeof(XT) == 2 && MODE != MODE_SWIGLU) {
-      if (variant == 8)
-        return launch_skinny<XT, MT, 1, MODE, 16>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-      if (variant == 9)
-        return launch_skinny<XT, MT, 1, MODE, 8, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    // variants 8 / 9 / 11 (bf16 activations, M > 16): 1 tile per workgroup, 16 waves / 8 waves with a doubled
+    // ring / 4 waves with a doubled ring -- more weight + activation bytes in flight per wave for the
+    // latency-bound projections; variant 10: 2 tiles per workgroup (as 6) with a doubled ring
+    if constexpr (MT > 1 && sizeof(XT) == 2) {
+      if constexpr (MODE != MODE_SWIGLU) {
+        if (variant == 8)
+          return launch_skinny<XT, MT, 1, MODE, 16>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+        if (variant == 9)
+          return launch_skinny<XT, MT, 1, MODE, 8, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+        if (variant == 11)
+          return launch_skinny<XT, MT, 1, MODE, 4, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      }
+      if (variant == 10)
+        return launch_skinny<XT, MT, 2, MODE, 4, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      // diagnostic 12 / 13: variants 1 / 6 reading x as pre-packed fragments (TIMING ONLY: row-major input
+      // gives wrong results; M must fill its m-tiles so the packed reads stay in the buffer)
+      if (variant >= 12 && variant <= 15 && M == MT * 16) {
+        if (variant == 13)
+          return launch_skinny<XT, MT, 2, MODE, 4, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+        if (variant == 15)
+          return launch_skinny<XT, MT, 2, MODE, 4, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+        if constexpr (MODE != MODE_SWIGLU) {
+          if (variant == 14)
+            return launch_skinny<XT, MT, 1, MODE, 8, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+          return launch_skinny<XT, MT, 1, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+        }
+      }
     }
   }
   if constexpr (MODE == MODE_SWIGLU) {

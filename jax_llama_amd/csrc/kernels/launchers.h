@@ -34,6 +34,7 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
 // skinny_workspace_floats / skinny_tickets (tickets zero-initialised once, self-resetting)
 size_t skinny_workspace_floats(int M, int N, int K, int mode);
 int skinny_tickets(int M, int N, int K, int mode);
+void skinny_set_plan(int nt, int ksplit);  // split-K skinny GEMM plan override (0, 0 = heuristic)
 int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode, float rms_eps,
                   int accumulate, int out_f32, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
                   int n_tickets, hipStream_t s);

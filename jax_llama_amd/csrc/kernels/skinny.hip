@@ -72,11 +72,93 @@ __global__ void __launch_bounds__(SK_NW * 64)
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (threadIdx.x < MT * 16) ss_l[threadIdx.x] = 0.f;
+
+  // ---- stage x[:, ks0*32 : (ks0+nk)*32] -> LDS as bf16 A fragments; RMS sums of squares.
+  // Done BEFORE the weight ring is issued: the compiler's waits for these (ordinary) loads count only
+  // the loads it can see, so staging behind the hand-counted ring drained the ring once per staging
+  // round (s_waitcnt vmcnt(0) in the staging loop: ~4 serial HBM round trips per workgroup). Here the
+  // activation loads (L2-resident) are all issued up front, the waits cover only them, and the weight
+  // stream starts right after.
+  {
+    float ssp[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) ssp[mt] = 0.f;
+    const int nq = MT * nk * 64;  // (mt, j, lane) fragment pieces of 16 B
+    auto piece = [&](int q, int& mt, int& j) {
+      mt = q / (nk * 64);
+      j = (q - mt * nk * 64) >> 6;
+    };
+    if constexpr (sizeof(XT) == 2) {
+      constexpr int XL = 8;  // nk * MT <= 64 (LDS plan) -> at most 8 pieces per thread
+      u32x4 xv[XL];
+#pragma unroll
+      for (int i = 0; i < XL; ++i) {
+        const int q = threadIdx.x + SK_NW * 64 * i;
+        int mt, j;
+        piece(min(q, nq - 1), mt, j);
+        const int row = min(mt * 16 + (lane & 15), M - 1);
+        xv[i] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(x) + (size_t)row * K +
+                                                (size_t)(ks0 + j) * 32 + 8 * (lane >> 4));
+      }
+#pragma unroll
+      for (int i = 0; i < XL; ++i) {
+        const int q = threadIdx.x + SK_NW * 64 * i;
+        if (q < nq) {
+          int mt, j;
+          piece(q, mt, j);
+          float sq = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, xv[i][e]);
+            sq = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, sq, false);
+          }
+#pragma unroll
+          for (int m2 = 0; m2 < MT; ++m2)
+            if (m2 == mt) ssp[m2] += sq;
+          xs[(mt * nk + j) * 64 + lane] = xv[i];
+        }
+      }
+    } else {
+      for (int q = threadIdx.x; q < nq; q += SK_NW * 64) {
+        int mt, j;
+        piece(q, mt, j);
+        const int row = min(mt * 16 + (lane & 15), M - 1);
+        const size_t off = (size_t)row * K + (size_t)(ks0 + j) * 32 + 8 * (lane >> 4);
+        const float4* src = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off);
+        const float4 a = src[0], b = src[1];
+        const float sq =
+            a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
+#pragma unroll
+        for (int m2 = 0; m2 < MT; ++m2)
+          if (m2 == mt) ssp[m2] += sq;
+        u32x4 v;
+        v[0] = pack2bf(a.x, a.y);
+        v[1] = pack2bf(a.z, a.w);
+        v[2] = pack2bf(b.x, b.y);
+        v[3] = pack2bf(b.z, b.w);
+        xs[(mt * nk + j) * 64 + lane] = v;
+      }
+    }
+    // per-wave partials, summed in wave order below (deterministic: no LDS float atomics)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float sv = ssp[mt];
+      sv += __shfl_xor(sv, 16, 64);
+      sv += __shfl_xor(sv, 32, 64);
+      if (lane < 16) ss_w[w][mt * 16 + lane] = sv;
+    }
+    __syncthreads();
+    if (threadIdx.x < MT * 16) {
+      float sv = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < SK_NW; ++ww) sv += ss_w[ww][threadIdx.x];
+      ss_l[threadIdx.x] = sv;
+    }
+  }
 
   u32x4 bq[U][NT] = {};
-  // Trip j0 = -U only issues k-steps 0..U-1 (the ring's single definition site), then stages x
-  // while those weight loads are in flight; every later trip consumes slot u and refills it.
+  // Trip j0 = -U only issues k-steps 0..U-1 (the ring's single definition site); every later trip
+  // consumes slot u and refills it.
   for (int j0 = -U; j0 < nk; j0 += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -96,53 +178,6 @@ __global__ void __launch_bounds__(SK_NW * 64)
       const int jn = j0 + u + U;
 #pragma unroll
       for (int t = 0; t < NT; ++t) sk_load_nt(bq[u][t], jn < nk ? (const void*)(wt[t] + (size_t)jn * 64) : (const void*)zf);
-    }
-    if (j0 < 0) {
-      // ---- stage x[:, ks0*32 : (ks0+nk)*32] -> LDS as bf16 A fragments; RMS sums of squares
-      __syncthreads();  // ss_l zeroed
-      float ssp[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) ssp[mt] = 0.f;
-      for (int p = threadIdx.x; p < nk * 64; p += SK_NW * 64) {
-        const int j = p >> 6;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int row = min(mt * 16 + (lane & 15), M - 1);
-          const size_t off = (size_t)row * K + (size_t)(ks0 + j) * 32 + 8 * (lane >> 4);
-          u32x4 v;
-          if constexpr (sizeof(XT) == 4) {
-            const float4* src = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(x) + off);
-            const float4 a = src[0], b = src[1];
-            ssp[mt] += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
-            v[0] = pack2bf(a.x, a.y);
-            v[1] = pack2bf(a.z, a.w);
-            v[2] = pack2bf(b.x, b.y);
-            v[3] = pack2bf(b.z, b.w);
-          } else {
-            v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(x) + off);
-            float f[8];
-            unpack8(v, f);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ssp[mt] += f[e] * f[e];
-          }
-          xs[(mt * nk + j) * 64 + lane] = v;
-        }
-      }
-      // per-wave partials, summed in wave order below (deterministic: no LDS float atomics)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        float sv = ssp[mt];
-        sv += __shfl_xor(sv, 16, 64);
-        sv += __shfl_xor(sv, 32, 64);
-        if (lane < 16) ss_w[w][mt * 16 + lane] = sv;
-      }
-      __syncthreads();
-      if (threadIdx.x < MT * 16) {
-        float sv = 0.f;
-#pragma unroll
-        for (int ww = 0; ww < SK_NW; ++ww) sv += ss_w[ww][threadIdx.x];
-        ss_l[threadIdx.x] = sv;
-      }
     }
   }
   sk_wait<0>();  // retire the zero-fragment refills; ring registers stay live until here
@@ -295,11 +330,18 @@ struct SkPlan {
 
 static int sk_mt(int M) { return M <= 16 ? 1 : (M <= 32 ? 2 : 4); }  // == the kernel's MT template
 
+static int g_sk_nt = 0, g_sk_ks = 0;  // plan override for tuning (0 = heuristic)
+void skinny_set_plan(int nt, int ksplit) {
+  g_sk_nt = nt;
+  g_sk_ks = ksplit;
+}
+
 static SkPlan sk_plan(int M, int N, int K, int mode) {
   const int KS = K >> 5, NTT = N >> 4;
   const int mt = sk_mt(M);
   SkPlan p;
   p.nt = (mode == MODE_SWIGLU || NTT >= 32 * SK_NW) ? 2 : 1;
+  if (g_sk_nt > 0 && mode != MODE_SWIGLU) p.nt = g_sk_nt > 1 ? 2 : 1;
   p.groups = (NTT + SK_NW * p.nt - 1) / (SK_NW * p.nt);
   // LDS holds MT * kc A fragments of 1 KiB (<= 64 KiB); aim for ~512 workgroups, >= 8 k-steps
   // per split, at most 8 splits unless LDS forces more.
@@ -307,6 +349,7 @@ static SkPlan sk_plan(int M, int N, int K, int mode) {
   int ks = (512 + p.groups - 1) / p.groups;
   ks = min(ks, 8);
   ks = min(ks, max(1, KS / 8));
+  if (g_sk_ks > 0) ks = min(g_sk_ks, KS);
   ks = max(ks, (KS + kc_max - 1) / kc_max);
   ks = max(ks, 1);
   p.kc = (KS + ks - 1) / ks;

@@ -51,8 +51,12 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
         c.insert(1, 5)
     if m > 16:
         c.append(TILED_VARIANT)
-        # (variants 8 / 9 -- 16 waves / a doubled ring -- measured no faster than 1/4/6/7 at M = 32:
-        # profiles/r2_decode_m32_variants_8_9.jsonl; kept as explicit choices, not tuned)
+        if bf16_x:
+            # doubled hand-counted rings (8 / 4 waves, 1 tile; 4 waves, 2 tiles): at M > 16 the single ring
+            # keeps only 4 (or 2) k-steps in flight per wave (profiles/r2_decode_m32_asm_ring.jsonl)
+            c.extend([9, 11, 10])
+        # (variant 8 -- 16 waves -- measured no faster than 1/4/6/7 at M = 32:
+        # profiles/r2_decode_m32_variants_8_9.jsonl; kept as an explicit choice, not tuned)
     return tuple(c)
 
 

@@ -255,7 +255,7 @@ def _attn_ref_gpu(q, kc, vc, slot0, kv_start, key_mask=None, chunk=512):
     return out.reshape(b * s, h * dh)
 
 
-@pytest.mark.parametrize("impl", [2, 1])
+@pytest.mark.parametrize("impl", [3, 2, 1])
 @pytest.mark.parametrize("rep", [1, 4, 8])
 @pytest.mark.parametrize("s,slot0,masked", [(7, 0, False), (130, 10, False), (512, 0, False), (300, 0, True),
                                             (2048, 0, False)])
@@ -325,7 +325,7 @@ def test_attention_decode_8k(rep):
 
 
 @pytest.mark.parametrize("m", [1, 5, 17, 40, 64])
-@pytest.mark.parametrize("variant", [1, 5, 6])
+@pytest.mark.parametrize("variant", [1, 5, 6, 9, 10, 11])
 def test_linear_skinny_argmax(m, variant):
     """Decode lm_head with the argmax in the GEMV epilogue == stored fp32 logits + first-max argmax,
     bit for bit (same accumulation order), including an exact tie across two 16-column tiles."""
@@ -396,10 +396,11 @@ def test_gemv_variants_agree():
         torch.testing.assert_close(outs[0], o, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [1, 4])
+@pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11])
 @pytest.mark.parametrize("m", [1, 9, 16, 40, 64])
 def test_decode_linear_paths_all_modes(variant, m):
-    """Both decode GEMM designs, every epilogue, real-ish K (multi-split)."""
+    """Both decode GEMM designs (and the GEMV's tile / ring-depth variants: at M > 16 the hand-counted
+    doubled rings 9/10/11), every epilogue, real-ish K (multi-split)."""
     ops.GEMV_VARIANT = variant
     try:
         k, n = 4096, 768

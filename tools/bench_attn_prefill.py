@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Prefill attention throughput (causal, GQA) at real model shapes: TFLOP/s of impl 2 (GQA-shared
-32x32x16 MFMA flash kernel) vs impl 1 (v1). FLOPs counted for the causal triangle only:
+32x32x16 MFMA flash kernel, 32 queries per wave), impl 3 (same, 64 queries per wave) and impl 1 (v1). FLOPs counted for the causal triangle only:
 4 * B * H * Dh * S (S + 1) / 2. Prints one JSON line per (shape, impl)."""
 from __future__ import annotations
 
@@ -21,8 +21,15 @@ SHAPES = [  # (name, B, S, H, Hkv)
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default=None, help="run only this shape name (profiling)")
+    ap.add_argument("--impl", type=int, default=None, help="run only this impl (profiling)")
+    args = ap.parse_args()
     e = ops.ext()
     for name, b, s, h, hkv in SHAPES:
+        if args.shape and name != args.shape:
+            continue
         g = torch.Generator(device="cuda").manual_seed(0)
         kc = torch.randn(b, hkv, s, 128, device="cuda", generator=g).to(torch.bfloat16)
         vc = torch.randn(b, hkv, s, 128, device="cuda", generator=g).to(torch.bfloat16)
@@ -31,8 +38,10 @@ def main():
         slot = torch.zeros(1, dtype=torch.int32, device="cuda")
         flops = 4.0 * b * h * 128 * s * (s + 1) / 2
         ref = None
-        for impl in (2, 1):
+        for impl in (2, 3, 1):
             if impl == 1 and s * s * b * h > 2048 * 2048 * 16 * 32:
+                continue
+            if args.impl is not None and impl != args.impl:
                 continue
             e.attn_prefill_set_impl(impl)
             o = ops.attention(q, kc, vc, slot, ks)

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ops", nargs="+", default=None, help="subset of qkv o gate_up down lm_head attn")
     ap.add_argument("--attn-impls", default="1:0,2:4096", help="impl:waves_target pairs for attn A/B")
+    ap.add_argument("--sk-plans", nargs="*", default=None,
+                    help="variant 4 (split-K skinny GEMM) plan overrides nt:ksplit, e.g. 1:16 2:8")
     ap.add_argument("--attn-shapes", nargs="*", default=None, help="BxT decode attention shapes (default: a sweep)")
     args = ap.parse_args()
     args.attn_impls = [tuple(int(v) for v in p.split(":")) for p in args.attn_impls.split(",")]
@@ -70,8 +72,13 @@ def main():
         ws = [PackedLinear.random(n, k, DEV) for _ in range(copies_for(nbytes))]
         for m in args.m:
             x = torch.randn(m, k, device=DEV).to(xdt)
-            for var in args.variants:
+            runs = [(v, None) for v in args.variants]
+            if args.sk_plans:
+                runs += [(4, tuple(int(t) for t in p.split(":"))) for p in args.sk_plans]
+            for var, plan in runs:
                 ops.GEMV_VARIANT = var
+                e.skinny_set_plan(*(plan or (0, 0)))
+                ops._SK_SIZES.clear()
                 if mode == ops.MODE_QKV:
                     table = torch.randn(4096, hd // 2, 2, device=DEV)
                     pos = torch.zeros(m, dtype=torch.int32, device=DEV)
@@ -93,7 +100,9 @@ def main():
                     def fn(i, x=x):
                         ops.linear(x, ws[i % len(ws)], rms_eps=1e-5, out_dtype=torch.float32)
                 us = timeit(fn)
-                print(json.dumps({"op": name, "n": n, "k": k, "m": m, "variant": var, "us": round(us, 2),
+                e.skinny_set_plan(0, 0)
+                ops._SK_SIZES.clear()
+                print(json.dumps({"op": name, "n": n, "k": k, "m": m, "variant": var, "sk_plan": plan, "us": round(us, 2),
                                   "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
         del ws
         torch.cuda.empty_cache()

@@ -112,13 +112,10 @@ struct XRaw<bf16_t> {  // 8 bf16 activations per lane (one 16-byte load)
   JLA_DEV void pin_regs() { pin(v); }
   // sum of squares straight from the packed pairs (v_dot2_f32_bf16): no unpacked temporaries, which at
   // MT > 1 made hipcc copy in-flight ring registers (tools/check_asm_ring.py hazards) and forced the
-  // compiler-counted ring that drains at every back-edge
+  // compiler-counted ring that drains at every back-edge. dot8_bf16 bit-casts the WHOLE vector: casting
+  // single elements (v[i]) into the dot2 operand miscompiles to element 0 for every i.
   JLA_DEV u32x4 frag(float& ss) const {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bf16x2_t p = __builtin_bit_cast(bf16x2_t, v[i]);
-      ss = __builtin_amdgcn_fdot2_f32_bf16(p, p, ss, false);
-    }
+    ss = dot8_bf16(v, v, ss);
     return v;
   }
 };

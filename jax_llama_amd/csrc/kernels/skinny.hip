@@ -106,12 +106,7 @@ __global__ void __launch_bounds__(SK_NW * 64)
         if (q < nq) {
           int mt, j;
           piece(q, mt, j);
-          float sq = 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const bf16x2_t pr = __builtin_bit_cast(bf16x2_t, xv[i][e]);
-            sq = __builtin_amdgcn_fdot2_f32_bf16(pr, pr, sq, false);
-          }
+          const float sq = dot8_bf16(xv[i], xv[i], 0.f);  // whole-vector cast (see common.h)
 #pragma unroll
           for (int m2 = 0; m2 < MT; ++m2)
             if (m2 == mt) ssp[m2] += sq;

@@ -363,13 +363,15 @@ def test_argmax_first_index():
     torch.testing.assert_close(val.cpu(), x.max(-1).values)
 
 
-@pytest.mark.parametrize("m,s", [(1, 1), (16, 1), (48, 1), (6, 3), (130, 65)])
-def test_linear_qkv_rope_fused(m, s):
-    h, hkv, dh, k, t = 4, 2, 128, 512, 80
+@pytest.mark.parametrize("k,xdt", [(512, torch.float32), (256, BF16), (4096, BF16)])
+@pytest.mark.parametrize("m,s", [(1, 1), (16, 1), (48, 1), (6, 3), (60, 20), (130, 65)])
+def test_linear_qkv_rope_fused(m, s, k, xdt):
+    """Also at the small K and bf16 activations of the GPU whole-model tests (hidden 256, bf16 mirror)."""
+    h, hkv, dh, t = 4, 2, 128, 80
     b = m // s
     n = (h + 2 * hkv) * dh
     w = (torch.randn(n, k) * 0.05).to(BF16)
-    x = torch.randn(m, k)
+    x = torch.randn(m, k).to(xdt).float()
     table = ref.rope_table(dh, 256, 500000.0)
     pos = torch.randint(0, 200, (m,), dtype=torch.int32)
     kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
@@ -377,7 +379,7 @@ def test_linear_qkv_rope_fused(m, s):
     q = ref.linear_qkv_rope(x, w, 1e-5, table, pos, kc, vc, 7, s, h, hkv, dh)
     kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
     pg = PackedLinear.from_dense(w, DEV)
-    qg = ops.linear_qkv_rope(x.to(DEV), pg, 1e-5, table.to(DEV), pos.to(DEV), kg, vg,
+    qg = ops.linear_qkv_rope(x.to(xdt).to(DEV), pg, 1e-5, table.to(DEV), pos.to(DEV), kg, vg,
                              torch.tensor([7], dtype=torch.int32, device=DEV), s, h, hkv, dh)
     _close(qg, q, 2e-2, 2e-2)
     _close(kg, kc, 2e-2, 2e-2)
@@ -396,19 +398,22 @@ def test_gemv_variants_agree():
         torch.testing.assert_close(outs[0], o, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("k", [256, 4096])
 @pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11])
 @pytest.mark.parametrize("m", [1, 9, 16, 40, 64])
-def test_decode_linear_paths_all_modes(variant, m):
+def test_decode_linear_paths_all_modes(variant, m, k):
     """Both decode GEMM designs (and the GEMV's tile / ring-depth variants: at M > 16 the hand-counted
-    doubled rings 9/10/11), every epilogue, real-ish K (multi-split)."""
+    doubled rings 9/10/11), every epilogue, real-ish K (multi-split) and the whole-model tests' K = 256."""
     ops.GEMV_VARIANT = variant
     try:
-        k, n = 4096, 768
+        n = 768
         x = torch.randn(m, k)
         w, pg, pc = _mk_linear(n, k)
         y = ops.linear(x.to(DEV), pg, rms_eps=1e-5, out_dtype=torch.float32)
         _close(y, ref.linear(x, w, 1e-5, torch.float32), 1e-2, 1e-3)
         xb = x.to(BF16)
+        yb = ops.linear(xb.to(DEV), pg, rms_eps=1e-5, out_dtype=torch.float32)  # bf16 activations + fused norm
+        _close(yb, ref.linear(xb.float(), w, 1e-5, torch.float32), 1e-2, 1e-3)
         h = torch.randn(m, n)
         hg = h.to(DEV)
         ops.linear_residual(xb.to(DEV), pg, hg)

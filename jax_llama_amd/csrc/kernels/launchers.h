@@ -28,6 +28,31 @@ struct QKVArgs {
   bf16_t* res_bf16;           // MODE_RESIDUAL: optional bf16 mirror of the updated residual (next A operand)
 };
 
+// decode chain (chain.hip): wo -> w1|w3 -> w2 [-> next wqkv] as one launch at M <= 16 (bf16 activations)
+struct ChainStage {
+  const bf16_t* x;     // [M, K] row-major activations
+  const void* W;       // fragment-packed weights
+  void* out;           // residual stages: h (fp32 [M, N]); SwiGLU: [M, N/2] bf16; QKV: unused
+  bf16_t* mirror;      // residual stages: bf16 mirror of h
+  int N, K, mode;
+  float eps;           // >= 0: fused RMSNorm of x
+  QKVArgs qa;          // stage 3 only
+  // filled by decode_chain():
+  int wg_begin, wg_count, dep, publish;
+  int expect[8];       // producer (stage dep) arrivals per shard blockIdx % 8
+};
+struct ChainArgs {
+  ChainStage st[4];
+  int nstages, M;
+  unsigned* counters;        // [4][8][32] cumulative per-shard arrivals of this layer's stages, one 128-B line per
+                             // (stage, shard) word (zeroed once)
+  const unsigned* epoch;     // forwards since the counters were zeroed (>= 1 when the chain runs)
+  unsigned* error;           // set to 1 when a hand-off wait times out
+  long long timeout_ticks;   // wall-clock ticks (s_memrealtime, 100 MHz)
+  unsigned long long* stamps; // diagnostic: per workgroup [start, waited, streamed, done] wall clock (nullptr = off)
+};
+int decode_chain(ChainArgs a, hipStream_t s);
+int chain_epoch_bump(unsigned* epoch, hipStream_t s);
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
 // split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
@@ -94,7 +119,8 @@ unsigned jla_bounds_gemm(int reset);
 unsigned jla_bounds_gemv(int reset);
 unsigned jla_bounds_skinny(int reset);
 unsigned jla_bounds_attn_decode(int reset);
-unsigned jla_bounds_attn_prefill(int reset);  // DIAGNOSTIC: 1 = the streaming kernel skips its math (wrong results)  // 2 = streaming (default), 1 = v1 (A/B)
+unsigned jla_bounds_attn_prefill(int reset);
+unsigned jla_bounds_chain(int reset);  // DIAGNOSTIC: 1 = the streaming kernel skips its math (wrong results)  // 2 = streaming (default), 1 = v1 (A/B)
 int attn_decode_splits(int B, int Hkv, int T, int rep);
 // ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,

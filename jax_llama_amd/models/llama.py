@@ -327,6 +327,13 @@ class LLaMAForCausalLM:
                        self.head_dim, self.device)
 
     # ------------------------------------------------------------------ core forward
+    def chain_state(self) -> "ops.ChainState":
+        """Hand-off counters of the decode chain (ops.decode_chain), allocated on first use."""
+        st = getattr(self, "_chain_state", None)
+        if st is None:
+            st = self._chain_state = ops.ChainState(self.config.num_hidden_layers, self.device)
+        return st
+
     def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor, hb: torch.Tensor) -> None:
         """``h += x @ W^T`` where W is row-sharded. TP=1: the GEMM epilogue adds into the fp32 residual
         ``h`` and writes its bf16 mirror ``hb`` (the A operand of the next projection). TP>1: the GEMM

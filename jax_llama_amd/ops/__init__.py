@@ -391,6 +391,60 @@ def _slot_tensor(slot0, device):
 
 
 # ----------------------------------------------------------------------------------
+# Decode chain (csrc/kernels/chain.hip): wo -> w1|w3 -> w2 [-> next layer's wqkv] as one launch at M <= 16.
+# Opt-in (JLA_DECODE_CHAIN=1): correct and bit-identical, but measured SLOWER than the four launches it replaces on
+# MI355X (M = 1: 119 vs 84 us per layer; each in-launch hand-off waits 2-4 us for its producers' arrivals, more than
+# the launch boundary it removes, and the stages stream 15-30 % slower beside spinning consumers:
+# profiles/r2_decode_chain_timeline.jsonl).
+DECODE_CHAIN = os.environ.get("JLA_DECODE_CHAIN", "0") == "1"
+CHAIN_MAX_M = 16
+CHAIN_TIMEOUT_S = 0.25
+
+
+class ChainState:
+    """Per-model hand-off state of the decode chain: cumulative per-(layer, stage, XCD shard) arrival
+    counters, the forward counter (epoch) they are checked against, and the timeout error word. Zeroed
+    once at allocation (outside any graph capture); the counters stay consistent as long as every chained
+    forward bumps the epoch once and runs each layer's chain once."""
+
+    def __init__(self, n_layers: int, device):
+        self.counters = torch.zeros(n_layers, 4, 8, 32, dtype=torch.int32, device=device)  # a 128-B line per word
+        self.epoch = torch.zeros(4, dtype=torch.int32, device=device)
+        self.error = torch.zeros(4, dtype=torch.int32, device=device)
+
+    def check(self) -> None:
+        if int(self.error[0].item()) != 0:
+            raise RuntimeError("decode chain: a hand-off wait timed out (results of that step are invalid)")
+
+
+def chain_epoch_bump(state: ChainState) -> None:
+    ext().chain_epoch_bump(state.epoch)
+
+
+def decode_chain(a: torch.Tensor, w_o, w_gu, w_down, h: torch.Tensor, hb: torch.Tensor, act: torch.Tensor,
+                 rms_eps: float, state: ChainState, layer: int, qkv=None, stamps=None) -> Optional[torch.Tensor]:
+    """``h += a @ Wo^T`` (hb = bf16(h)); ``act = silu(g) * u`` of ``norm(hb) @ Wgu^T``; ``h += act @ Wd^T``
+    (hb = bf16(h)); and, with ``qkv = (w_qkv, table, positions, k_cache, v_cache, slot0, seq_len, H, Hkv, Dh)``
+    for the NEXT layer, its fused qkv + RoPE + KV-cache write -- one launch. Returns that layer's rotated q
+    ``[M, H, Dh]`` (or None)."""
+    e = ext()
+    m = a.shape[0]
+    q = None
+    if qkv is None:
+        e.decode_chain(a, w_o.weight, w_gu.weight, w_down.weight, h, hb, act, float(rms_eps), None, None, None, None,
+                       None, None, 1, 0, 0, 0, None, state.counters[layer], state.epoch, state.error, CHAIN_TIMEOUT_S,
+                       stamps)
+        return None
+    w_qkv, table, positions, kc, vc, slot0, seq_len, nh, nkv, dh = qkv
+    q = torch.empty(m, nh, dh, dtype=BF16, device=a.device)
+    e.decode_chain(a, w_o.weight, w_gu.weight, w_down.weight, h, hb, act, float(rms_eps), w_qkv.weight, table,
+                   positions.reshape(-1).to(torch.int32), kc, vc, _slot_tensor(slot0, a.device), int(seq_len),
+                   int(nh), int(nkv), int(dh), q, state.counters[layer], state.epoch, state.error, CHAIN_TIMEOUT_S,
+                   stamps)
+    return q
+
+
+# ----------------------------------------------------------------------------------
 def argmax(logits: torch.Tensor):
     """Row argmax (first max index, like ``jnp.argmax``). Returns (idx int32[B], val fp32[B])."""
     if not _is_gpu(logits):

@@ -101,15 +101,29 @@ void check_linear_out(const Tensor& out, int64_t m, int64_t n, int64_t mode) {
     check(out.scalar_type() == torch::kBFloat16 || out.scalar_type() == torch::kFloat32, "out must be bf16/fp32");
 }
 
+// packed-layout activation copy (common.h pack_off): bf16, >= ceil(M/16 -> 1, 2 or 4 m-tiles) * 16 rows of `cols`
+int64_t packed_rows(int64_t m) { return m <= 16 ? 16 : (m <= 32 ? 32 : 64); }
+jla::bf16_t* packed_ptr(const c10::optional<Tensor>& t, int64_t m, int64_t cols, const char* what) {
+  if (!t.has_value()) return nullptr;
+  check_gpu(*t, what);
+  check(t->scalar_type() == torch::kBFloat16 && t->numel() >= packed_rows(m) * cols && cols % 32 == 0,
+        "packed activation: bf16 [padded rows, cols], cols % 32 == 0");
+  return bf(*t);
+}
+
 // Decode linear dispatch. variant: 0 = auto (M == 1 -> K-split GEMV, else split-K skinny GEMM),
 // 1/2/3 = K-split GEMV (gemv.hip) with 4/8/16 waves, 4 = split-K skinny GEMM (skinny.hip), 5/6/8-11 = GEMV
 // tile / wave / ring-depth variants (gemv.hip dispatch_nt).
 void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* out, int64_t mode, double rms_eps,
                 bool accumulate, bool out_f32, const jla::QKVArgs* qa, int64_t variant, const Tensor& ws,
-                const Tensor& tickets) {
+                const Tensor& tickets, const jla::bf16_t* x_packed = nullptr) {
   const int64_t m = x.size(0);
   const bool f32 = x.scalar_type() == torch::kFloat32;
   if (variant == 0) variant = (m == 1) ? 1 : 4;
+  const bool xp_variant = variant >= 12 && variant <= 15;
+  check(xp_variant == (x_packed != nullptr), "packed-x variants (12-15) need x_packed, the others must not get it");
+  check(!xp_variant || !f32, "packed-x variants read bf16 activations");
+  check(!(xp_variant && mode == 2 && (variant == 12 || variant == 14)), "SwiGLU packed-x variants: 13 / 15");
   if (variant == 4) {
     check_gpu(ws, "ws");
     check_gpu(tickets, "tickets");
@@ -118,14 +132,15 @@ void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* ou
                           ptr<float>(ws), ws.numel(), ptr<int32_t>(tickets), tickets.numel(), stream()),
        "linear_splitk");
   } else {
-    rc(jla::linear_skinny(x.data_ptr(), f32, w.data_ptr(), out, m, n, k, mode, (float)rms_eps, accumulate, out_f32, qa,
-                          variant, stream()),
+    rc(jla::linear_skinny(x_packed ? (const void*)x_packed : x.data_ptr(), f32, w.data_ptr(), out, m, n, k, mode,
+                          (float)rms_eps, accumulate, out_f32, qa, variant, stream()),
        "linear_skinny");
   }
 }
 
 void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, double rms_eps,
-                   bool accumulate, int64_t variant, Tensor ws, Tensor tickets, c10::optional<Tensor> mirror) {
+                   bool accumulate, int64_t variant, Tensor ws, Tensor tickets, c10::optional<Tensor> mirror,
+                   c10::optional<Tensor> x_packed, c10::optional<Tensor> pack_out) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
@@ -136,8 +151,13 @@ void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t
   check_linear_out(out, m, n, mode);
   jla::QKVArgs qa{};
   qa.res_bf16 = mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr;
+  // packed copy of the bf16 output (the residual's mirror / the SwiGLU activation): GEMV variants only
+  qa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
+  check(!qa.pack || (mode == 1 || mode == 2), "pack_out: residual (mirror) or SwiGLU output only");
+  check(!qa.pack || (variant != 0 && variant != 4 && variant != 7), "pack_out: GEMV variants only");
+  check(!qa.pack || mode != 1 || qa.res_bf16, "pack_out of a residual needs the mirror");
   run_skinny(x, w, n, k, out.data_ptr(), mode, rms_eps, accumulate, out.scalar_type() == torch::kFloat32, &qa,
-             variant, ws, tickets);
+             variant, ws, tickets, packed_ptr(x_packed, m, k, "x_packed"));
 }
 
 // greedy lm_head at decode M (<= 64): GEMV with a first-max epilogue -> [M][N / 16] (value, index) partials in
@@ -200,13 +220,14 @@ jla::QKVArgs qkv_args(int64_t m, int64_t n, const Tensor& table, const Tensor& p
   qa.T = kc.size(2);
   qa.q = bf(q);
   qa.res_bf16 = nullptr;
+  qa.pack = nullptr;
   return qa;
 }
 
 // fused qkv projection + RoPE + KV-cache write (decode / small M)
 void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions, Tensor kc,
                 Tensor vc, Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q,
-                int64_t variant, Tensor ws, Tensor tickets) {
+                int64_t variant, Tensor ws, Tensor tickets, c10::optional<Tensor> x_packed) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k, "x must be [M, K]");
@@ -214,7 +235,8 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_qkv: M too large");
   jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
-  run_skinny(x, w, n, k, nullptr, MODE_QKV_ID, rms_eps, false, false, &qa, variant, ws, tickets);
+  run_skinny(x, w, n, k, nullptr, MODE_QKV_ID, rms_eps, false, false, &qa, variant, ws, tickets,
+             packed_ptr(x_packed, m, k, "x_packed"));
 }
 
 // decode chain (chain.hip): h += a @ Wo^T; act = SwiGLU(norm(hb) @ Wgu^T); h += act @ Wd^T; and, when the next
@@ -445,7 +467,7 @@ void check_attn(const Tensor& q, const Tensor& kc, const Tensor& vc, const Tenso
 }
 
 void attn_decode(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c10::optional<Tensor> key_mask,
-                 Tensor out, Tensor ws, Tensor tickets, int64_t t_cap, int64_t nsplit) {
+                 Tensor out, Tensor ws, Tensor tickets, int64_t t_cap, int64_t nsplit, c10::optional<Tensor> out_pack) {
   check_attn(q, kc, vc, slot, kv_start, key_mask, out);
   check(q.size(1) == 1, "attn_decode: one query per row");
   const int64_t b = q.size(0), h = q.size(2), dh = q.size(3), hkv = kc.size(1), T = kc.size(2);
@@ -457,7 +479,8 @@ void attn_decode(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c
   const uint8_t* km = key_mask.has_value() ? ptr<uint8_t>(*key_mask) : nullptr;
   const int ml = key_mask.has_value() ? key_mask->size(1) : 0;
   rc(jla::attn_decode(cbf(q), cbf(kc), cbf(vc), ptr<int32_t>(slot), ptr<int32_t>(kv_start), km, ml, bf(out),
-                      ptr<float>(ws), ptr<int32_t>(tickets), b, h, hkv, dh, T, t_cap, nsplit, stream()),
+                      ptr<float>(ws), ptr<int32_t>(tickets), b, h, hkv, dh, T, t_cap, nsplit, stream(),
+                      packed_ptr(out_pack, b, h * dh, "out_pack")),
      "attn_decode");
 }
 
@@ -668,7 +691,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("rmsnorm", &rmsnorm);
   m.def("linear_skinny", &linear_skinny, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"),
         py::arg("mode"), py::arg("rms_eps"), py::arg("accumulate"), py::arg("variant"), py::arg("ws"),
-        py::arg("tickets"), py::arg("mirror") = py::none());
+        py::arg("tickets"), py::arg("mirror") = py::none(), py::arg("x_packed") = py::none(),
+        py::arg("pack_out") = py::none());
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
         py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none());
@@ -704,7 +728,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("impl"), py::arg("waves_target") = 0);
   m.def("attn_decode_splits",
         [](int64_t b, int64_t hkv, int64_t t, int64_t rep) { return jla::attn_decode_splits(b, hkv, t, rep); });
-  m.def("linear_qkv", &linear_qkv);
+  m.def("linear_qkv", &linear_qkv, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("rms_eps"),
+        py::arg("table"), py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"),
+        py::arg("h"), py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("variant"), py::arg("ws"), py::arg("tickets"),
+        py::arg("x_packed") = py::none());
+  m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);
   m.def("decode_chain", &decode_chain, "wo -> w1|w3 -> w2 [-> next wqkv] decode chain (one launch, M <= 16)",
@@ -731,7 +759,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_set_v1_min_wgs", [](int64_t n) { jla::attn_set_v1_min_wgs((int)n); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
-        py::arg("nsplit"));
+        py::arg("nsplit"), py::arg("out_pack") = py::none());
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));
   m.def("attn_prefill_set_impl", [](int64_t impl) { jla::attn_prefill_set_impl((int)impl); });

@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
     attn_decode_v3_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                           const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int H,
-                          int Hkv, int T, int t_cap, float scale) {
+                          int Hkv, int T, int t_cap, float scale, bf16_t* __restrict__ out_pack) {
   constexpr int CH = AD3_WAVES * 4 * KPG;  // keys per chunk (8 waves x 4 groups x KPG rows)
   __shared__ float sm_m[AD3_WAVES][REP];
   __shared__ float sm_l[AD3_WAVES][REP];
@@ -407,7 +407,9 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
         den += f * sm_l[ww][h];
       }
     }
-    out[((size_t)b * H + h0 + h) * AD_DH + d] = f2bf(den > 0.f ? num / den : 0.f);
+    const bf16_t r = f2bf(den > 0.f ? num / den : 0.f);
+    out[((size_t)b * H + h0 + h) * AD_DH + d] = r;
+    if (out_pack) out_pack[pack_off(b, (h0 + h) * AD_DH + d, H * AD_DH)] = r;  // the o projection's packed x
   }
 }
 
@@ -858,6 +860,7 @@ static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_att
 static int g_attn_v3_max_pairs = 4096;  // up to the v2 threshold: faster than v1 at B = 1..256 (8 kv heads)
 void attn_set_v3_max_pairs(int n) { g_attn_v3_max_pairs = n; }
 static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv) && B * Hkv <= g_attn_v3_max_pairs; }
+int attn_decode_packs(int B, int Hkv, int rep) { return use_v3(B, Hkv, rep) ? 1 : 0; }
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
   if (use_v3(B, Hkv, rep)) return T;
@@ -879,8 +882,9 @@ int attn_decode_splits(int B, int Hkv, int T, int rep) {
 
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                 const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int32_t* tickets, int B, int H,
-                int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s) {
+                int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s, bf16_t* out_pack) {
   if (B <= 0) return 0;
+  if (out_pack && !use_v3(B, Hkv, H / Hkv)) return -3;  // only the small-batch kernel writes the packed copy
   if (Dh != AD_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   if (attn_decode_splits(B, Hkv, t_cap, rep) != nsplit) return -2;
@@ -890,7 +894,7 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
 #define JLA_AD3(R, K)                                                                                          \
   if (rep == R) {                                                                                              \
     attn_decode_v3_kernel<R, K><<<grid3, AD3_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, \
-                                                                 out, H, Hkv, T, t_cap, scale);                \
+                                                                 out, H, Hkv, T, t_cap, scale, out_pack);      \
     JLA_CHECK_LAUNCH();                                                                                        \
     return 0;                                                                                                  \
   }

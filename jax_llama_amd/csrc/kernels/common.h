@@ -98,6 +98,14 @@ JLA_DEV float dot8_bf16(const u32x4 a, const u32x4 b, float acc) {
   return acc;
 }
 
+// "Packed" activation layout: the MFMA A fragments of x [M, K] stored contiguously, [ceil(M/16)][K/32][64][8]
+// (one 1 KiB run per 16-row x 32-k fragment, like the packed weights). Element (m, k) lives at pack_off(m, k, K).
+// Written beside the row-major copy by the decode epilogues that produce the next projection's input, read by the
+// GEMV's packed-x variants (12-15): one contiguous 1 KiB load per fragment instead of 16 half-used 128-B lines.
+JLA_DEV size_t pack_off(int m, int k, int K) {
+  return ((size_t)((m >> 4) * (K >> 5) + (k >> 5)) * 64 + (m & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+}
+
 JLA_DEV f32x4 mfma16x16x32(const u32x4 a, const u32x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);

@@ -171,7 +171,9 @@ __global__ void __launch_bounds__(NW * 64)
       if (m < M && gtile < NTT) {
         const float sc = inv_rms[m];
         const float g = reduced(mt, 2 * p, ln, i) * sc, u = reduced(mt, 2 * p + 1, ln, i) * sc;
-        o[(size_t)m * F + (gtile >> 1) * 16 + c] = f2bf(silu(g) * u);
+        const bf16_t r = f2bf(silu(g) * u);
+        o[(size_t)m * F + (gtile >> 1) * 16 + c] = r;
+        if (qa.pack) qa.pack[pack_off(m, (gtile >> 1) * 16 + c, F)] = r;
       }
     }
   } else {
@@ -234,6 +236,7 @@ __global__ void __launch_bounds__(NW * 64)
           const float nv = accumulate ? o[idx] + v : v;
           o[idx] = nv;
           if (qa.res_bf16) qa.res_bf16[idx] = f2bf(nv);
+          if (qa.pack) qa.pack[pack_off(m, col, N)] = f2bf(nv);
         } else {
           if (out_f32)
             static_cast<float*>(out)[idx] = v;
@@ -321,18 +324,19 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       }
       if (variant == 10)
         return launch_skinny<XT, MT, 2, MODE, 4, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-      // diagnostic 12 / 13: variants 1 / 6 reading x as pre-packed fragments (TIMING ONLY: row-major input
-      // gives wrong results; M must fill its m-tiles so the packed reads stay in the buffer)
-      if (variant >= 12 && variant <= 15 && M == MT * 16) {
-        if (variant == 13)
-          return launch_skinny<XT, MT, 2, MODE, 4, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-        if (variant == 15)
-          return launch_skinny<XT, MT, 2, MODE, 4, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-        if constexpr (MODE != MODE_SWIGLU) {
-          if (variant == 14)
-            return launch_skinny<XT, MT, 1, MODE, 8, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    }
+    // packed-x variants (x is the packed copy, common.h pack_off, padded to MT * 16 rows): 12 = 1 tile x 8 waves,
+    // 13 = 2 tiles x 4 waves, 14 / 15 = the same with a doubled ring
+    if constexpr (sizeof(XT) == 2) {
+      if (variant == 13)
+        return launch_skinny<XT, MT, 2, MODE, 4, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      if (variant == 15)
+        return launch_skinny<XT, MT, 2, MODE, 4, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      if constexpr (MODE != MODE_SWIGLU) {
+        if (variant == 14)
+          return launch_skinny<XT, MT, 1, MODE, 8, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+        if (variant == 12)
           return launch_skinny<XT, MT, 1, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-        }
       }
     }
   }

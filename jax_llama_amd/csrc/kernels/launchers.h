@@ -26,6 +26,8 @@ struct QKVArgs {
   int S, H, Hkv, Dh, T;       // tokens per sequence in this call, heads, kv heads, head dim, cache len
   bf16_t* q;                  // [M, H, Dh] rotated queries
   bf16_t* res_bf16;           // MODE_RESIDUAL: optional bf16 mirror of the updated residual (next A operand)
+  bf16_t* pack;               // optional packed-layout copy (common.h pack_off) of the bf16 output: RESIDUAL -> the
+                              // mirror, SWIGLU -> the activation (GEMV only; the next projection's packed-x input)
 };
 
 // decode chain (chain.hip): wo -> w1|w3 -> w2 [-> next wqkv] as one launch at M <= 16 (bf16 activations)
@@ -125,7 +127,8 @@ int attn_decode_splits(int B, int Hkv, int T, int rep);
 // ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                 const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int32_t* tickets, int B, int H,
-                int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s);
+                int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s, bf16_t* out_pack = nullptr);
+int attn_decode_packs(int B, int Hkv, int rep);  // 1: attn_decode can also write the packed-layout output
 void attn_prefill_set_impl(int impl);  // 2 = GQA-shared MFMA 32x32 flash kernel (default), 1 = v1
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,

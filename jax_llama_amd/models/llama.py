@@ -334,14 +334,15 @@ class LLaMAForCausalLM:
             st = self._chain_state = ops.ChainState(self.config.num_hidden_layers, self.device)
         return st
 
-    def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor, hb: torch.Tensor) -> None:
+    def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor, hb: torch.Tensor,
+                      x_packed: Optional[torch.Tensor] = None, mirror_packed: Optional[torch.Tensor] = None) -> None:
         """``h += x @ W^T`` where W is row-sharded. TP=1: the GEMM epilogue adds into the fp32 residual
         ``h`` and writes its bf16 mirror ``hb`` (the A operand of the next projection). TP>1: the GEMM
         writes only this rank's partial (``comm.reduce_dtype``, bf16 by default) and one collective
         kernel sums the partials in rank order, adds them to ``h`` and rewrites ``hb``
         (``comm.all_reduce_residual_``; reference ``partition.py:67,70``)."""
         if self.comm.size == 1:
-            ops.linear_residual(x, w, h, mirror=hb)
+            ops.linear_residual(x, w, h, mirror=hb, x_packed=x_packed, mirror_packed=mirror_packed)
         else:
             part = ops.linear(x, w, out_dtype=self.comm.reduce_dtype)
             self.comm.all_reduce_residual_(part, h, hb)

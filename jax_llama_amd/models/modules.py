@@ -35,21 +35,25 @@ class LLaMAAttention:
         return self.model.layers[self.layer_idx]
 
     def __call__(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int,
-                 output_attentions: bool = False) -> Optional[torch.Tensor]:
+                 output_attentions: bool = False, pk: Optional["PackedActs"] = None) -> Optional[torch.Tensor]:
         m, lw = self.model, self.weights
         kc, vc = cache.layer(self.layer_idx)
         q = ops.linear_qkv_rope(hb, lw.qkv, m.eps, m.rope, positions, kc, vc, slot0, seq_len,
-                                m.n_heads, m.n_kv_heads, m.head_dim)
+                                m.n_heads, m.n_kv_heads, m.head_dim, x_packed=pk.hb_in() if pk else None)
         b = hb.shape[0] // seq_len
         q4 = q.reshape(b, seq_len, m.n_heads, m.head_dim)
         weights = None
+        att_p = None
         if output_attentions:  # debug path: materialised softmax weights (reference :277-286)
             s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
             a, weights = ref.attention(q4, kc, vc, s0, kv_start, key_mask, return_weights=True)
             a = a.reshape(b * seq_len, -1)
         else:
-            a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask)
-        m._row_parallel(a, lw.o, h, hb)
+            att_p = pk.att if pk is not None and ops.attention_packs(q4, kc) else None
+            a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask, out_packed=att_p)
+        m._row_parallel(a, lw.o, h, hb, x_packed=att_p, mirror_packed=pk.hb if pk else None)
+        if pk is not None:
+            pk.hb_ok = True
         return weights
 
 
@@ -58,10 +62,11 @@ class LLaMAMLP:
         self.model = model
         self.layer_idx = layer_idx
 
-    def __call__(self, h, hb) -> None:
+    def __call__(self, h, hb, pk: Optional["PackedActs"] = None) -> None:
         m, lw = self.model, self.model.layers[self.layer_idx]
-        g = ops.linear_swiglu(hb, lw.gu, rms_eps=m.eps)
-        m._row_parallel(g, lw.down, h, hb)
+        g = ops.linear_swiglu(hb, lw.gu, rms_eps=m.eps, x_packed=pk.hb_in() if pk else None,
+                              out_packed=pk.act if pk else None)
+        m._row_parallel(g, lw.down, h, hb, x_packed=pk.act if pk else None, mirror_packed=pk.hb if pk else None)
 
 
 class LLaMABlock:
@@ -72,10 +77,26 @@ class LLaMABlock:
         self.feed_forward = LLaMAMLP(model, layer_idx)
 
     def __call__(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int,
-                 output_attentions: bool = False):
-        w = self.attention(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len, output_attentions)
-        self.feed_forward(h, hb)
+                 output_attentions: bool = False, pk: Optional["PackedActs"] = None):
+        w = self.attention(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len, output_attentions, pk)
+        self.feed_forward(h, hb, pk)
         return w
+
+
+class PackedActs:
+    """Packed-layout copies (ops.packed_rows x cols, csrc/kernels/common.h pack_off) of the decode activations
+    that feed a projection: the residual mirror hb (written by the wo / w2 epilogues, read by wqkv and w1|w3),
+    the attention output (read by wo) and the SwiGLU output (read by w2). hb has no packed copy before the first
+    residual epilogue of the step (the embedding writes only the row-major mirror)."""
+
+    def __init__(self, rows: int, model, device):
+        self.hb = ops.packed_empty(rows, model.config.hidden_size, device)
+        self.att = ops.packed_empty(rows, model.n_heads * model.head_dim, device)
+        self.act = ops.packed_empty(rows, model.ffn, device)
+        self.hb_ok = False
+
+    def hb_in(self) -> Optional[torch.Tensor]:
+        return self.hb if self.hb_ok else None
 
 
 class LLaMABlockCollection:
@@ -125,10 +146,15 @@ class LLaMABlockCollection:
             self._chained(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len)
             return hidden, attns
         b = hb.shape[0] // seq_len
+        rows = hb.shape[0]
+        pk = None
+        if (ops.PACKED_X and hb.is_cuda and ops.PACKED_X_MIN_M <= rows <= ops.PACKED_X_MAX_M
+                and self.model.comm.size == 1):
+            pk = PackedActs(rows, self.model, hb.device)
         for blk in self.blocks:
             if output_hidden_states:
                 hidden.append(h.reshape(b, seq_len, -1).clone())
-            w = blk(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len, output_attentions)
+            w = blk(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len, output_attentions, pk)
             if output_attentions:
                 attns.append(w)
         return hidden, attns

@@ -150,35 +150,65 @@ def linear(x: torch.Tensor, w, rms_eps: Optional[float] = None, out_dtype=BF16,
 
 
 def linear_residual(x: torch.Tensor, w, residual: torch.Tensor, rms_eps: Optional[float] = None,
-                    accumulate: bool = True, mirror: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    accumulate: bool = True, mirror: Optional[torch.Tensor] = None,
+                    x_packed: Optional[torch.Tensor] = None, mirror_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``residual (fp32) += y`` (or ``= y`` when ``accumulate`` is False); ``mirror`` (bf16,
-    same shape) receives ``bf16(residual)`` from the same epilogue."""
+    same shape) receives ``bf16(residual)`` from the same epilogue. Decode (M <= 64): ``x_packed`` is an
+    optional packed-layout copy of ``x`` (``packed_rows``) the packed-x GEMV variants may read, and
+    ``mirror_packed`` receives a packed copy of the mirror (the next projection's packed x)."""
     if not _is_gpu(x):
         ref.linear_residual(x, w.dense(), residual, rms_eps, accumulate)
         if mirror is not None:
             mirror.copy_(residual.to(BF16))
         return residual
-    _gpu_linear(x, w, residual, MODE_RESIDUAL, rms_eps, accumulate, mirror)
+    _gpu_linear(x, w, residual, MODE_RESIDUAL, rms_eps, accumulate, mirror, x_packed, mirror_packed)
     return residual
 
 
-def linear_swiglu(x: torch.Tensor, w, rms_eps: Optional[float] = None) -> torch.Tensor:
-    """``silu(x W1^T) * (x W3^T)`` with W1/W3 packed as alternating 16-row tiles."""
+def linear_swiglu(x: torch.Tensor, w, rms_eps: Optional[float] = None, x_packed: Optional[torch.Tensor] = None,
+                  out_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``silu(x W1^T) * (x W3^T)`` with W1/W3 packed as alternating 16-row tiles (packed-x in/out as in
+    ``linear_residual``)."""
     if not _is_gpu(x):
         return ref.linear_swiglu(x, w.dense(), rms_eps)
     out = torch.empty(x.shape[0], w.n // 2, dtype=BF16, device=x.device)
-    _gpu_linear(x, w, out, MODE_SWIGLU, rms_eps, True)
+    _gpu_linear(x, w, out, MODE_SWIGLU, rms_eps, True, None, x_packed, out_packed)
     return out
 
 
-def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None):
+# ---- packed activations (csrc/kernels/common.h pack_off): the MFMA A fragments of a decode activation stored
+# contiguously, written beside the row-major copy by the producing GEMV epilogue (or decode attention) and read by
+# the packed-x GEMV variants 12-15 -- one 1 KiB load per 16 x 32 fragment instead of 16 half-used 128-B lines
+# (profiles/r2_decode_m32_asm_ring.jsonl: o 15.6 -> 10.5 us, down 36.6 -> 30.7 us at M = 32).
+PACKED_X = os.environ.get("JLA_PACKED_X", "1") != "0"
+PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
+PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "32"))
+XP_VARIANTS = (12, 13, 14, 15)
+
+
+def packed_rows(m: int) -> int:
+    """Rows of a packed activation buffer: the GEMV's m-tiles (1, 2 or 4) x 16."""
+    return 16 if m <= 16 else (32 if m <= 32 else 64)
+
+
+def packed_empty(m: int, cols: int, device) -> torch.Tensor:
+    return torch.empty(packed_rows(m), cols, dtype=BF16, device=device)
+
+
+def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None, x_packed=None, pack_out=None):
     assert x.is_contiguous() and out.is_contiguous()
     assert x.shape[1] == w.k, (x.shape, w.k)
     m = x.shape[0]
     e = ext()
-    v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, mode)
+    if m > e.SKINNY_MAX_M:
+        x_packed = pack_out = None
+    v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, mode, x_packed, pack_out)
     if v == TILED:
         _tiled(e, x, w.weight, w.n, w.k, out, mode, rms_eps, accumulate, mirror)
+    elif x_packed is not None or pack_out is not None:
+        ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
+        e.linear_skinny(x, w.weight, w.n, w.k, out, mode, -1.0 if rms_eps is None else float(rms_eps),
+                        bool(accumulate), v, ws, tk, mirror, x_packed if v in XP_VARIANTS else None, pack_out)
     else:
         ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode,
@@ -258,25 +288,38 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
     e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
 
 
-def _variant(e, x, w, mode) -> int:
+def _variant(e, x, w, mode, x_packed=None, pack_out=None) -> int:
     """Decode-kernel variant for this shape: pinned (JLA_GEMV_VARIANT / ops.GEMV_VARIANT) or
-    measured once per shape on the device (ops/autotune.py)."""
+    measured once per shape on the device (ops/autotune.py). With ``x_packed`` the packed-x variants are
+    candidates too; with ``pack_out`` only GEMV variants qualify (their epilogue writes the packed copy)."""
+    xp_in, p_out = x_packed is not None, pack_out is not None
     if GEMV_VARIANT:
-        return GEMV_VARIANT
+        v = GEMV_VARIANT
+        if (v in XP_VARIANTS and not xp_in) or (p_out and v in (4, TILED)):
+            v = 1
+        if v in (12, 14) and mode == MODE_SWIGLU:
+            v += 1
+        return v
     m = x.shape[0]
     pmode = MODE_STORE if mode == MODE_QKV else mode  # QKV epilogue has side effects: tune as STORE
     ws, tk = _skinny_ws(e, m, w.n, w.k, pmode, x.device)
     ncols = w.n // 2 if pmode == MODE_SWIGLU else w.n
     odt = torch.float32 if pmode == MODE_RESIDUAL else BF16
     scratch = workspace.get("tune_out", m * ncols, odt, x.device).view(m, ncols)
+    mirror = workspace.get("tune_mirror", m * ncols, BF16, x.device).view(m, ncols) if (
+        p_out and pmode == MODE_RESIDUAL) else None
+    pscratch = workspace.get("tune_pack", packed_rows(m) * ncols, BF16, x.device).view(-1, ncols) if p_out else None
 
     def run(v, xx, wt):
         if v == TILED:
             _tiled(e, xx, wt, w.n, w.k, scratch, pmode, 1e-5, True)
+        elif xp_in or p_out:
+            e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk, mirror,
+                            x_packed if v in XP_VARIANTS else None, pscratch)
         else:
             e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk)
 
-    return autotune.choose(e, x, w, pmode, run)
+    return autotune.choose(e, x, w, pmode, run, xp_in=xp_in, pack_out=p_out)
 
 
 _SK_SIZES = {}
@@ -314,7 +357,7 @@ def rope_kv_write(qkv: torch.Tensor, table: torch.Tensor, positions: torch.Tenso
 
 def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.Tensor, positions: torch.Tensor,
                     k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, seq_len: int, n_heads: int,
-                    n_kv_heads: int, head_dim: int) -> torch.Tensor:
+                    n_kv_heads: int, head_dim: int, x_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused ``qkv = [inv_rms(x) *] x @ Wqkv^T`` + interleaved RoPE on q/k + KV-cache write at slots
     ``slot0 + s``. Returns rotated q ``[M, H, Dh]`` bf16. Decode (M <= 64) is one kernel (the
     RoPE/cache write is the GEMV epilogue, rotating the fp32 accumulators); prefill runs the MFMA
@@ -325,7 +368,9 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
                                    n_heads, n_kv_heads, head_dim)
     m = x.shape[0]
     e = ext()
-    v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV)
+    if m > e.SKINNY_MAX_M:
+        x_packed = None
+    v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV, x_packed)
     if v == TILED:
         # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
         ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
@@ -349,12 +394,20 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)
     e.linear_qkv(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
                  positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, x.device),
-                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, v, ws, tk)
+                 int(seq_len), int(n_heads), int(n_kv_heads), int(head_dim), q, v, ws, tk,
+                 x_packed if v in XP_VARIANTS else None)
     return q
 
 
+def attention_packs(q: torch.Tensor, k_cache: torch.Tensor) -> bool:
+    """Whether ``attention(..., out_packed=...)`` can write the packed copy for this decode shape."""
+    bsz, s, h, _ = q.shape
+    return s == 1 and bool(ext().attn_decode_packs(bsz, k_cache.shape[1], h // k_cache.shape[1]))
+
+
 def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor,
-              key_mask: Optional[torch.Tensor] = None, max_kv: Optional[int] = None) -> torch.Tensor:
+              key_mask: Optional[torch.Tensor] = None, max_kv: Optional[int] = None,
+              out_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Causal/padded attention of ``q [B, S, H, Dh]`` (queries at cache slots slot0+s)
     against ``[B, Hkv, T, Dh]`` caches. Returns ``[B*S, H*Dh]`` bf16.
 
@@ -373,7 +426,7 @@ def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slo
         nsplit = e.attn_decode_splits(bsz, hkv, t_cap, h // hkv)
         ws = workspace.get("attn_decode", bsz * h * nsplit * (dh + 2), torch.float32, q.device)
         tickets = workspace.get_zeroed("attn_tickets", bsz * hkv, torch.int32, q.device)
-        e.attn_decode(q, k_cache, v_cache, slot_t, kv_start, key_mask, out, ws, tickets, t_cap, nsplit)
+        e.attn_decode(q, k_cache, v_cache, slot_t, kv_start, key_mask, out, ws, tickets, t_cap, nsplit, out_packed)
     else:
         e.attn_prefill(q, k_cache, v_cache, slot_t, kv_start, key_mask, out)
     return out

@@ -63,16 +63,27 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
 TILED_VARIANT = 7
 
 
-def choose(e, x: torch.Tensor, w, mode: int, run) -> int:
-    """``run(variant, x, weight_tensor)`` launches the op once."""
+XP_CANDIDATES = (12, 13, 14, 15)  # packed-x GEMV variants (gemv.hip dispatch_nt)
+
+
+def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False) -> int:
+    """``run(variant, x, weight_tensor)`` launches the op once. ``xp_in``: a packed copy of x exists, so the
+    packed-x variants compete too; ``pack_out``: the epilogue must also write a packed copy of its output,
+    which only the GEMV variants do (no split-K skinny 4, no tiled 7)."""
     m = x.shape[0]
-    key = (m_bucket(m), w.n, w.k, mode, x.dtype)
+    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out)
     v = _CACHE.get(key)
     if v is not None:
         return v
+    cands = list(candidates(m, w.n, swiglu=(mode == 2), bf16_x=(x.dtype == torch.bfloat16)))
+    if pack_out:
+        cands = [c for c in cands if c not in (4, TILED_VARIANT)]
+    if xp_in and x.dtype == torch.bfloat16:
+        cands += [c for c in XP_CANDIDATES if mode != 2 or c in (13, 15)]
     if not ENABLED or torch.cuda.is_current_stream_capturing():
-        return heuristic(m, w.n, w.k, mode)
-    v = _measure(x, w, run, candidates(m, w.n, swiglu=(mode == 2), bf16_x=(x.dtype == torch.bfloat16)))
+        h = heuristic(m, w.n, w.k, mode)
+        return h if h in cands else 1
+    v = _measure(x, w, run, tuple(cands))
     _CACHE[key] = v
     return v
 

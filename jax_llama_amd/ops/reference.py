@@ -38,6 +38,22 @@ def pack_frag16x32(w: torch.Tensor) -> torch.Tensor:
             .reshape(n // 16, k // 32, 64, 8))
 
 
+def pack_act(x: torch.Tensor, rows: int) -> torch.Tensor:
+    """Packed-layout copy of a decode activation ``x [M, K]`` (csrc/kernels/common.h pack_off): rows zero-padded to
+    ``rows`` (a multiple of 16), then the weights' fragment order; returned as ``[rows, K]`` (flat order
+    ``[rows/16][K/32][64][8]``)."""
+    m, k = x.shape
+    xp = torch.zeros(rows, k, dtype=x.dtype, device=x.device)
+    xp[:m] = x
+    return pack_frag16x32(xp).reshape(rows, k)
+
+
+def unpack_act(p: torch.Tensor, m: int) -> torch.Tensor:
+    """Inverse of ``pack_act`` (first ``m`` rows)."""
+    rows, k = p.shape
+    return unpack_frag16x32(p.reshape(rows // 16, k // 32, 64, 8), rows, k)[:m]
+
+
 def unpack_frag16x32(p: torch.Tensor, n: int, k: int) -> torch.Tensor:
     return (p.reshape(n // 16, k // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous()
             .reshape(n, k))

@@ -816,3 +816,48 @@ def _qkv_rope_stream_k(e, m, s):
     _close(qg, q, 2e-2, 2e-2)
     _close(kg, kc, 2e-2, 2e-2)
     _close(vg, vc, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("variant", [12, 13, 14, 15])
+@pytest.mark.parametrize("m", [1, 12, 16, 20, 32, 40])
+def test_packed_x_variants_and_packed_epilogues(m, variant):
+    """Packed-x GEMV variants read the packed copy (ref.pack_act) and match the fp32 reference; the residual /
+    SwiGLU epilogues write packed copies of their bf16 outputs that unpack to the row-major outputs exactly."""
+    k, n = 4096, 768
+    rows = ops.packed_rows(m)
+    x = torch.randn(m, k).to(BF16)
+    w, pg, _ = _mk_linear(n, k)
+    xp = ref.pack_act(x, rows).to(DEV)
+    ops.GEMV_VARIANT = variant
+    try:
+        y = torch.empty(m, n, dtype=torch.float32, device=DEV)
+        ops._gpu_linear(x.to(DEV), pg, y, ops.MODE_STORE, 1e-5, True, None, xp, None)
+        _close(y, ref.linear(x.float(), w, 1e-5, torch.float32), 1e-2, 1e-3)
+        h = torch.randn(m, n)
+        hg, mir, mp = h.to(DEV), torch.empty(m, n, dtype=BF16, device=DEV), ops.packed_empty(m, n, DEV)
+        ops.linear_residual(x.to(DEV), pg, hg, mirror=mir, x_packed=xp, mirror_packed=mp)
+        _close(hg, ref.linear_residual(x, w, h.clone()), 1e-2, 1e-3)
+        assert torch.equal(mir.cpu(), hg.cpu().to(BF16))
+        assert torch.equal(ref.unpack_act(mp.cpu(), m), mir.cpu())
+        gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+        ap = ops.packed_empty(m, n // 2, DEV)
+        y2 = ops.linear_swiglu(x.to(DEV), PackedLinear.from_dense(gu, DEV), rms_eps=1e-5, x_packed=xp, out_packed=ap)
+        _close(y2, ref.linear_swiglu(x.float(), gu, 1e-5), 3e-2, 3e-2)
+        assert torch.equal(ref.unpack_act(ap.cpu(), m), y2.cpu())
+    finally:
+        ops.GEMV_VARIANT = 0
+
+
+@pytest.mark.parametrize("b", [1, 12, 32])
+def test_attention_decode_packed_output(b):
+    h, hkv, dh, t = 32, 8, 128, 96
+    q = torch.randn(b, 1, h, dh).to(BF16)
+    kc = torch.randn(b, hkv, t, dh).to(BF16)
+    vc = torch.randn(b, hkv, t, dh).to(BF16)
+    kv_start = torch.zeros(b, dtype=torch.int32)
+    slot = torch.tensor([t - 1], dtype=torch.int32)
+    qg = q.to(DEV)
+    assert ops.attention_packs(qg, kc.to(DEV))
+    op = ops.packed_empty(b, h * dh, DEV)
+    out = ops.attention(qg, kc.to(DEV), vc.to(DEV), slot.to(DEV), kv_start.to(DEV), None, out_packed=op)
+    assert torch.equal(ref.unpack_act(op.cpu(), b), out.cpu())

@@ -160,3 +160,23 @@ def test_benchmark_helpers_at_max_sequence_length():
     assert t["ttft_ms"] > 0 and t["prompt_len"] == cfg.max_sequence_length
     d = decode_latency(m, 2, prompt_len=8, gen_len=16, steps=4)
     assert d["decode_ms_per_token"] > 0
+
+
+@pytest.mark.parametrize("rows", [12, 20, 32])
+def test_packed_activations_decode_rows(rows):
+    """Decode-shaped forward (one token per row) with the packed activation copies (ops.PACKED_X) vs without:
+    same logits up to the GEMV variants' summation order, and vs the CPU path."""
+    from jax_llama_amd import ops
+    cfg = gpu_config(num_attention_heads=2, num_key_value_heads=1)
+    cpu, gpu, _ = _pair(cfg, seed=9)
+    toks = torch.randint(0, cfg.vocab_size, (rows, 1), dtype=torch.int32)
+    saved = ops.PACKED_X
+    try:
+        ops.PACKED_X = True
+        a = gpu(toks).logits.cpu()
+        ops.PACKED_X = False
+        b = gpu(toks).logits.cpu()
+    finally:
+        ops.PACKED_X = saved
+    assert rel_err(a, b) < 1e-2
+    assert rel_err(a, cpu(toks).logits) < 2e-2

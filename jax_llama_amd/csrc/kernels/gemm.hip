@@ -1642,41 +1642,72 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
 }
 
 // ---- greedy lm_head: GEMM with the argmax in its epilogue (no fp32 logits round trip through HBM:
-// at M = 2048, V = 128256 that is 1 GB written + 1 GB read per decode step), then one wave per row
-// reduces the [M][P] partials. Ties go to the smaller index, so the result equals argmax_kernel's.
-__global__ void __launch_bounds__(256)
+// at M = 2048, V = 128256 that is 1 GB written + 1 GB read per decode step), then the [M][P] partials are
+// reduced per row. Ties go to the smaller index, so the result equals argmax_kernel's.
+JLA_DEV void amax_merge(float& bv, int& bi, float ov, int oi) {
+  if (ov > bv || (ov == bv && oi < bi)) {
+    bv = ov;
+    bi = oi;
+  }
+}
+
+// TPR threads per row (64: one wave per row, 4 rows per 256-thread block; 1024: one block per row for the
+// decode-sized M, where one wave walking ~8000 partials of a row with one dependent load per step took ~38 us).
+// Each thread keeps 4 independent (value, index) candidates so 4 loads are in flight per step.
+template <int TPR>
+__global__ void __launch_bounds__(TPR == 64 ? 256 : TPR)
     argmax_partials_kernel(const float2* __restrict__ part, int P, int M, int32_t* __restrict__ idx,
                            float* __restrict__ val) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  __shared__ float s_v[16];
+  __shared__ int s_i[16];
+  const int row = TPR == 64 ? blockIdx.x * 4 + (threadIdx.x >> 6) : blockIdx.x;
+  const int t = TPR == 64 ? (threadIdx.x & 63) : threadIdx.x;
   if (row >= M) return;
-  float bv = -INFINITY;
-  int bi = 0x7fffffff;
-  for (int k = lane; k < P; k += 64) {
-    const float2 e = part[(size_t)row * P + k];
-    const int ei = __float_as_int(e.y);
-    if (e.x > bv || (e.x == bv && ei < bi)) {
-      bv = e.x;
-      bi = ei;
+  const float2* pr = part + (size_t)row * P;
+  float bv[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int bi[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+  for (int k0 = t; k0 < P; k0 += 4 * TPR) {
+    float2 e[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * TPR;
+      e[u] = k < P ? pr[k] : make_float2(-INFINITY, __int_as_float(0x7fffffff));
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) amax_merge(bv[u], bi[u], e[u].x, __float_as_int(e[u].y));
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(bv, o, 64);
-    const int oi = __shfl_xor(bi, o, 64);
-    if (ov > bv || (ov == bv && oi < bi)) {
-      bv = ov;
-      bi = oi;
+  for (int u = 1; u < 4; ++u) amax_merge(bv[0], bi[0], bv[u], bi[u]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax_merge(bv[0], bi[0], __shfl_xor(bv[0], o, 64), __shfl_xor(bi[0], o, 64));
+  if constexpr (TPR > 64) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      s_v[w] = bv[0];
+      s_i[w] = bi[0];
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int ww = 1; ww < TPR / 64; ++ww) amax_merge(bv[0], bi[0], s_v[ww], s_i[ww]);
+      idx[row] = bi[0] == 0x7fffffff ? 0 : bi[0];
+      val[row] = bv[0];
+    }
+  } else if (t == 0) {
+    idx[row] = bi[0] == 0x7fffffff ? 0 : bi[0];
+    val[row] = bv[0];
   }
-  if (lane == 0) {
-    idx[row] = bi == 0x7fffffff ? 0 : bi;
-    val[row] = bv;
-  }
+}
+
+static void launch_argmax_partials(const float2* part, int P, int M, int32_t* idx, float* val, hipStream_t s) {
+  if (M <= 512)
+    argmax_partials_kernel<1024><<<M, 1024, 0, s>>>(part, P, M, idx, val);
+  else
+    argmax_partials_kernel<64><<<(M + 3) / 4, 256, 0, s>>>(part, P, M, idx, val);
 }
 
 int argmax_partials(const float* part, int P, int M, int32_t* idx, float* val, hipStream_t s) {
   if (M <= 0) return 0;
-  argmax_partials_kernel<<<(M + 3) / 4, 256, 0, s>>>(reinterpret_cast<const float2*>(part), P, M, idx, val);
+  launch_argmax_partials(reinterpret_cast<const float2*>(part), P, M, idx, val, s);
   JLA_CHECK_LAUNCH();
   return 0;
 }
@@ -1698,7 +1729,7 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, false, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
         x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{});
   JLA_CHECK_LAUNCH();
-  argmax_partials_kernel<<<(M + 3) / 4, 256, 0, s>>>(reinterpret_cast<const float2*>(ws), tn * 4, M, idx, val);
+  launch_argmax_partials(reinterpret_cast<const float2*>(ws), tn * 4, M, idx, val, s);
   JLA_CHECK_LAUNCH();
   return 0;
 }

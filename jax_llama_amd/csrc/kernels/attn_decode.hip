@@ -860,6 +860,13 @@ static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_att
 static int g_attn_v3_max_pairs = 4096;  // up to the v2 threshold: faster than v1 at B = 1..256 (8 kv heads)
 void attn_set_v3_max_pairs(int n) { g_attn_v3_max_pairs = n; }
 static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv) && B * Hkv <= g_attn_v3_max_pairs; }
+// v3 keys per lane-group row per chunk = base KPG (REP * KPG = 8) x this multiplier (1, 2, 4; capped at 8 rows):
+// fewer, larger chunks = fewer dependent load round trips on the latency-bound small-batch path
+// 0 = by size: x2 up to 128 (row, kv head) pairs (B <= 16 at 8 kv heads: B = 1 T = 384 12.4 -> 11.0 us, B = 8
+// 12.8 -> 11.3, B = 1 T = 1024 25.2 -> 22.1), x1 above (B = 32 / 64 slightly faster at x1;
+// profiles/r2_attn_decode_v3_kpg_ab.jsonl)
+static int g_v3_kpg_mult = 0;
+void attn_set_v3_kpg(int mult) { g_v3_kpg_mult = mult >= 4 ? 4 : (mult >= 2 ? 2 : (mult == 1 ? 1 : 0)); }
 int attn_decode_packs(int B, int Hkv, int rep) { return use_v3(B, Hkv, rep) ? 1 : 0; }
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
@@ -898,7 +905,14 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
     JLA_CHECK_LAUNCH();                                                                                        \
     return 0;                                                                                                  \
   }
-    JLA_AD3(1, 4) JLA_AD3(2, 4) JLA_AD3(4, 2) JLA_AD3(8, 1)
+    const int mult = g_v3_kpg_mult ? g_v3_kpg_mult : (B * Hkv <= 128 ? 2 : 1);
+    const int kpg3 = min(min(8, 16 / rep), (8 / rep) * mult);  // REP * KPG <= 16: no spills
+#define JLA_AD3K(R, K) \
+  if (kpg3 == K) {     \
+    JLA_AD3(R, K)      \
+  }
+    JLA_AD3K(1, 8) JLA_AD3K(2, 4) JLA_AD3K(2, 8) JLA_AD3K(4, 2) JLA_AD3K(4, 4) JLA_AD3K(8, 1) JLA_AD3K(8, 2)
+#undef JLA_AD3K
 #undef JLA_AD3
     return -1;
   }

@@ -113,6 +113,7 @@ void attn_set_v1_min_wgs(int n);
 void attn_set_v3_max_pairs(int n);  // single-workgroup-per-(row, kv head) decode kernel up to n pairs (0: off)  // v1 split sizing: smallest chunk giving >= n workgroups (default 256)
 void attn_set_impl(int impl, int waves_target);
 void attn_set_diag(int d);
+void attn_set_v3_kpg(int mult);  // small-batch decode attention: key rows per lane per chunk x mult (1, 2, 4)
 // bounds-checked debug build: per-translation-unit error words (JLA_BOUNDS_* bits; 0 in release builds)
 unsigned jla_bounds_norm_embed(int reset);
 unsigned jla_bounds_rope_kv(int reset);

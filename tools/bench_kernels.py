@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--sk-plans", nargs="*", default=None,
                     help="variant 4 (split-K skinny GEMM) plan overrides nt:ksplit, e.g. 1:16 2:8")
     ap.add_argument("--attn-shapes", nargs="*", default=None, help="BxT decode attention shapes (default: a sweep)")
+    ap.add_argument("--v3-kpg", type=int, nargs="*", default=[0],
+                    help="small-batch decode attention (v3) chunk-depth multipliers to sweep (0: by size, the default)")
     args = ap.parse_args()
     args.attn_impls = [tuple(int(v) for v in p.split(":")) for p in args.attn_impls.split(",")]
     cfg = get_preset(args.model)
@@ -120,19 +122,21 @@ def main():
         ks = torch.zeros(b, dtype=torch.int32, device=DEV)
         nbytes = 2 * kc.numel() * 2
         ref_out = None
-        for impl, target in args.attn_impls:
+        for (impl, target), kpg in [(it, kk) for it in args.attn_impls for kk in args.v3_kpg]:
             e.attn_set_diag(1 if impl >= 100 else 0)  # 100 + impl: diagnostic stream-only run of impl
             impl = impl % 100
             e.attn_set_impl(impl, target)
+            e.attn_set_v3_kpg(kpg)
             us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
             o = ops.attention(q, kc, vc, slot, ks).float()
             ref_out = o if ref_out is None else ref_out
-            print(json.dumps({"op": "attn_decode", "impl": impl, "waves_target": target, "b": b, "t": t,
+            print(json.dumps({"op": "attn_decode", "impl": impl, "waves_target": target, "v3_kpg": kpg, "b": b, "t": t,
                               "nsplit": e.attn_decode_splits(b, hkv, t, h // hkv), "us": round(us, 2),
                               "TBps": round(nbytes / us / 1e6, 3),
                               "max_diff_vs_first": round(float((o - ref_out).abs().max()), 5)}), flush=True)
         e.attn_set_diag(0)
         e.attn_set_impl(2, 4096)
+        e.attn_set_v3_kpg(0)
         del kc, vc
 
 

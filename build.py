@@ -125,7 +125,12 @@ def build_C(jobs: int, force: bool, debug_bounds: bool = False) -> Path:
         if did and src.stem in ("gemv", "skinny", "attn_decode", "chain"):  # (attn_decode: the v4 register ring)
             asm = odir / (src.stem + ".s")
             _run([HIPCC, *HIP_FLAGS, *extra, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
-            _run([sys.executable, str(ROOT / "tools" / "check_asm_ring.py"), str(asm)])
+            try:
+                _run([sys.executable, str(ROOT / "tools" / "check_asm_ring.py"), str(asm)])
+            except SystemExit:
+                # the object must not survive a failed check: it would look up to date to the next build
+                (odir / (src.stem + ".o")).unlink(missing_ok=True)
+                raise
     bsrc = CSRC / "bindings.cpp"
     bobj = odir / "bindings.o"
     if force or _stale(bobj, [bsrc, *headers]):

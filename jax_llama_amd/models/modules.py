@@ -52,7 +52,7 @@ class LLaMAAttention:
             att_p = pk.att if pk is not None and ops.attention_packs(q4, kc) else None
             a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask, out_packed=att_p)
         m._row_parallel(a, lw.o, h, hb, x_packed=att_p, mirror_packed=pk.hb if pk else None)
-        if pk is not None:
+        if pk is not None and pk.hb is not None:
             pk.hb_ok = True
         return weights
 
@@ -89,10 +89,12 @@ class PackedActs:
     the attention output (read by wo) and the SwiGLU output (read by w2). hb has no packed copy before the first
     residual epilogue of the step (the embedding writes only the row-major mirror)."""
 
-    def __init__(self, rows: int, model, device):
-        self.hb = ops.packed_empty(rows, model.config.hidden_size, device)
+    def __init__(self, rows: int, model, device, full: bool = True):
+        # full = False (33-64 rows): only the attention output is packed (wo reads it); hb / the SwiGLU output stay
+        # row-major so w1|w3 and w2 keep the tiled GEMM, which wins there (profiles/r2_packed_x_decode_ab.jsonl)
+        self.hb = ops.packed_empty(rows, model.config.hidden_size, device) if full else None
         self.att = ops.packed_empty(rows, model.n_heads * model.head_dim, device)
-        self.act = ops.packed_empty(rows, model.ffn, device)
+        self.act = ops.packed_empty(rows, model.ffn, device) if full else None
         self.hb_ok = False
 
     def hb_in(self) -> Optional[torch.Tensor]:
@@ -148,9 +150,9 @@ class LLaMABlockCollection:
         b = hb.shape[0] // seq_len
         rows = hb.shape[0]
         pk = None
-        if (ops.PACKED_X and hb.is_cuda and ops.PACKED_X_MIN_M <= rows <= ops.PACKED_X_MAX_M
+        if (ops.PACKED_X and hb.is_cuda and ops.PACKED_X_MIN_M <= rows <= ops.PACKED_ATT_MAX_M
                 and self.model.comm.size == 1):
-            pk = PackedActs(rows, self.model, hb.device)
+            pk = PackedActs(rows, self.model, hb.device, full=rows <= ops.PACKED_X_MAX_M)
         for blk in self.blocks:
             if output_hidden_states:
                 hidden.append(h.reshape(b, seq_len, -1).clone())

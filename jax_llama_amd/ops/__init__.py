@@ -183,6 +183,7 @@ def linear_swiglu(x: torch.Tensor, w, rms_eps: Optional[float] = None, x_packed:
 PACKED_X = os.environ.get("JLA_PACKED_X", "1") != "0"
 PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
 PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "32"))
+PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
 XP_VARIANTS = (12, 13, 14, 15)
 
 

@@ -19,6 +19,7 @@ import torch  # noqa: E402
 from jax_llama_amd import ops  # noqa: E402
 from jax_llama_amd.config import get_preset  # noqa: E402
 from jax_llama_amd.models.weights import PackedLinear  # noqa: E402
+from jax_llama_amd.ops import reference as ref  # noqa: E402
 
 DEV = "cuda"
 
@@ -79,6 +80,8 @@ def main():
                 runs += [(4, tuple(int(t) for t in p.split(":"))) for p in args.sk_plans]
             for var, plan in runs:
                 ops.GEMV_VARIANT = var
+                # packed-x variants (12-15) read a real packed copy of x (ref.pack_act), as in the model
+                xpk = ref.pack_act(x, ops.packed_rows(m)) if var in ops.XP_VARIANTS else None
                 e.skinny_set_plan(*(plan or (0, 0)))
                 ops._SK_SIZES.clear()
                 if mode == ops.MODE_QKV:
@@ -88,19 +91,22 @@ def main():
                     vc = torch.zeros_like(kc)
                     slot = torch.zeros(1, dtype=torch.int32, device=DEV)
 
-                    def fn(i, x=x, table=table, pos=pos, kc=kc, vc=vc, slot=slot):
-                        ops.linear_qkv_rope(x, ws[i % len(ws)], 1e-5, table, pos, kc, vc, slot, 1, h, hkv, hd)
+                    def fn(i, x=x, table=table, pos=pos, kc=kc, vc=vc, slot=slot, xpk=xpk):
+                        ops.linear_qkv_rope(x, ws[i % len(ws)], 1e-5, table, pos, kc, vc, slot, 1, h, hkv, hd,
+                                            x_packed=xpk)
                 elif mode == ops.MODE_RESIDUAL:
                     out = torch.zeros(m, n, device=DEV)
 
-                    def fn(i, x=x, out=out):
-                        ops.linear_residual(x, ws[i % len(ws)], out)
+                    def fn(i, x=x, out=out, xpk=xpk):
+                        ops.linear_residual(x, ws[i % len(ws)], out, x_packed=xpk)
                 elif mode == ops.MODE_SWIGLU:
-                    def fn(i, x=x):
-                        ops.linear_swiglu(x, ws[i % len(ws)], rms_eps=1e-5)
+                    def fn(i, x=x, xpk=xpk):
+                        ops.linear_swiglu(x, ws[i % len(ws)], rms_eps=1e-5, x_packed=xpk)
                 else:
-                    def fn(i, x=x):
-                        ops.linear(x, ws[i % len(ws)], rms_eps=1e-5, out_dtype=torch.float32)
+                    out32 = torch.empty(m, n, device=DEV)
+
+                    def fn(i, x=x, xpk=xpk, out32=out32):
+                        ops._gpu_linear(x, ws[i % len(ws)], out32, ops.MODE_STORE, 1e-5, True, None, xpk)
                 us = timeit(fn)
                 e.skinny_set_plan(0, 0)
                 ops._SK_SIZES.clear()

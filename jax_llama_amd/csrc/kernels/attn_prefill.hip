@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
     attn_prefill_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                            const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                            const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int S, int H,
-                           int Hkv, int T, float scale_log2, int npb, int hgroups, int n_qb) {
+                           int Hkv, int T, float scale_log2, int npb, int hgroups, int n_qb, int split) {
   constexpr int NT = NW * 64;
   constexpr int TILE_BYTES = FA_KT * AP_DH * 2;            // 16 KiB
   constexpr int CH_PER_T = FA_KT * 16 / NT;                 // 16-byte chunks per thread per tile (K or V)
@@ -229,8 +229,24 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
   char* Ks = lds;
   char* Vs = lds + TILE_BYTES;
 
-  const int kvh = blockIdx.y / hgroups, hg = blockIdx.y - kvh * hgroups;
-  const int b = blockIdx.z;
+  // split = 1 (small grids): the heavy and the light block of a pair are two workgroups of a 1-D grid, all heavy
+  // ones first -- ids g and g + items are the same pair, so when the second round of dispatch lands on the CUs in
+  // the order of the first, every CU again holds one (heavy, light) pair, now as two resident workgroups
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z, pass_lo = 0, pass_hi = 2;
+  if (split) {
+    const int P = (n_qb + 1) / 2, Y = Hkv * hgroups;  // 1-D grid of 2 x P x Y x B workgroups
+    const int items = (int)gridDim.x / 2;
+    int g = blockIdx.x;
+    const bool light = g >= items;
+    if (light) g -= items;
+    bx = g % P;
+    by = (g / P) % Y;
+    bz = g / (P * Y);
+    pass_lo = light ? 1 : 0;
+    pass_hi = light ? 2 : 1;
+  }
+  const int kvh = by / hgroups, hg = by - kvh * hgroups;
+  const int b = bz;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int hi = lane >> 5, col = lane & 31;
   const int rep = H / Hkv, hpw = NW / npb;
@@ -239,9 +255,9 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
   // causal balance: workgroup x runs query block n_qb-1-x (heavy) and then block x (light), so every
   // workgroup streams ~the same number of K/V tiles (with one block per workgroup, S = 2048 at B = 1 ran
   // the heaviest workgroup ~2x longer than the average one)
-  for (int pass = 0; pass < 2; ++pass) {
-  const int qb = pass == 0 ? n_qb - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  if (pass == 1 && qb >= n_qb - 1 - (int)blockIdx.x) break;  // odd n_qb: the middle block runs once
+  for (int pass = pass_lo; pass < pass_hi; ++pass) {
+  const int qb = pass == 0 ? n_qb - 1 - bx : bx;
+  if (pass == 1 && qb >= n_qb - 1 - bx) break;  // odd n_qb: the middle block runs once
   if (pass == 1) __syncthreads();  // every wave is done with the LDS images of the first block
   const int p0 = qb * QW * npb + QW * pb;   // first query position of this wave
   const int slot0 = slot_ptr[0];
@@ -423,7 +439,7 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   if (Dh != AP_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   constexpr int NW = 4;
-  if ((g_attn_prefill_impl == 2 || g_attn_prefill_impl == 3) && (rep % NW == 0 || NW % rep == 0)) {
+  if ((g_attn_prefill_impl >= 2 && g_attn_prefill_impl <= 4) && (rep % NW == 0 || NW % rep == 0)) {
     const int npb = rep >= NW ? 1 : NW / rep;    // position blocks per workgroup
     const int hpw = NW / npb;                    // q heads per workgroup
     const int hgroups = rep / hpw;
@@ -432,12 +448,21 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
       const int n_qb = (S + 64 * npb - 1) / (64 * npb);
       dim3 grid3((n_qb + 1) / 2, Hkv * hgroups, B);
       attn_prefill_v2_kernel<NW, 2><<<grid3, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S,
-                                                              H, Hkv, T, sl2, npb, hgroups, n_qb);
+                                                              H, Hkv, T, sl2, npb, hgroups, n_qb, 0);
     } else {
       const int n_qb = (S + 32 * npb - 1) / (32 * npb);
-      dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
-      attn_prefill_v2_kernel<NW, 1><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S,
-                                                              H, Hkv, T, sl2, npb, hgroups, n_qb);
+      const int pairs = (n_qb + 1) / 2 * Hkv * hgroups * B;
+      // fewer pairs than two workgroups per CU (B = 1 prefill): each half of a pair is its own workgroup, so a CU
+      // holds two resident workgroups (8 waves) instead of one; impl 4 = always paired (A/B)
+      const bool split = g_attn_prefill_impl == 2 && pairs < 2 * 256;
+      if (split) {
+        attn_prefill_v2_kernel<NW, 1><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
+            q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H, Hkv, T, sl2, npb, hgroups, n_qb, 1);
+      } else {
+        dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
+        attn_prefill_v2_kernel<NW, 1><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out,
+                                                                S, H, Hkv, T, sl2, npb, hgroups, n_qb, 0);
+      }
     }
     JLA_CHECK_LAUNCH();
     return 0;

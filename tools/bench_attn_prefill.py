@@ -38,7 +38,7 @@ def main():
         slot = torch.zeros(1, dtype=torch.int32, device="cuda")
         flops = 4.0 * b * h * 128 * s * (s + 1) / 2
         ref = None
-        for impl in (2, 3, 1):
+        for impl in (2, 4, 3, 1):
             if impl == 1 and s * s * b * h > 2048 * 2048 * 16 * 32:
                 continue
             if args.impl is not None and impl != args.impl:

@@ -452,7 +452,7 @@ def _slot_tensor(slot0, device):
 # profiles/r2_decode_chain_timeline.jsonl).
 DECODE_CHAIN = os.environ.get("JLA_DECODE_CHAIN", "0") == "1"
 CHAIN_MAX_M = 16
-CHAIN_TIMEOUT_S = 0.25
+CHAIN_TIMEOUT_S = 1.0
 
 
 class ChainState:

@@ -637,7 +637,8 @@ void car_allreduce(int64_t state, Tensor in, Tensor out, bool two_shot) {
 }
 
 // residual all-reduce of a row-parallel projection: h (fp32) += sum over ranks of partial; hb = bf16(h)
-void car_allreduce_residual(int64_t state, Tensor partial, Tensor h, Tensor hb, bool two_shot) {
+void car_allreduce_residual(int64_t state, Tensor partial, Tensor h, Tensor hb, bool two_shot,
+                            c10::optional<Tensor> hb_pack) {
   check_gpu(partial, "partial");
   check_gpu(h, "h");
   check_gpu(hb, "hb");
@@ -646,8 +647,10 @@ void car_allreduce_residual(int64_t state, Tensor partial, Tensor h, Tensor hb, 
   check(h.numel() == partial.numel() && hb.numel() == partial.numel(), "residual shapes");
   const int64_t nbytes = partial.numel() * partial.element_size();
   check(nbytes % 16 == 0, "car_allreduce_residual: bytes % 16");
+  const int64_t cols = h.size(-1);
+  jla::bf16_t* hp = packed_ptr(hb_pack, h.numel() / cols, cols, "hb_pack");
   rc(jla::car_reduce(reinterpret_cast<void*>(state), 1, partial.data_ptr(), nullptr, ptr<float>(h), bf(hb), nbytes,
-                     partial.scalar_type() == torch::kBFloat16, two_shot, stream()),
+                     partial.scalar_type() == torch::kBFloat16, two_shot, stream(), hp, hp ? (int)cols : 0),
      "car_allreduce_residual");
 }
 
@@ -770,7 +773,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("car_init", &car_init);
   m.def("car_allreduce", &car_allreduce, py::arg("state"), py::arg("inp"), py::arg("out"), py::arg("two_shot") = false);
   m.def("car_allreduce_residual", &car_allreduce_residual, py::arg("state"), py::arg("partial"), py::arg("h"),
-        py::arg("hb"), py::arg("two_shot") = false);
+        py::arg("hb"), py::arg("two_shot") = false, py::arg("hb_pack") = py::none());
   m.def("car_pairs", &car_pairs, py::arg("state"), py::arg("mode"), py::arg("vals"), py::arg("idx"),
         py::arg("idx_offset"), py::arg("k"), py::arg("out_v").none(true), py::arg("out_i"));
   m.def("car_error", [](int64_t st) { return jla::car_error(reinterpret_cast<void*>(st)); });

@@ -139,8 +139,11 @@ struct Piece {
 };
 
 // Apply the op to element range [e0, e0 + N) given the fp32 sum
+// hb_pack (optional, OP_RESID): packed-layout copy (common.h pack_off) of hb, rows of pack_cols elements -- the
+// next projection's packed-x input on the decode path
 template <int OP, bool BF16>
-JLA_DEV void car_epilogue(const float* sum, long long e0, void* out, float* h, bf16_t* hb) {
+JLA_DEV void car_epilogue(const float* sum, long long e0, void* out, float* h, bf16_t* hb, bf16_t* hb_pack,
+                          int pack_cols) {
   constexpr int N = BF16 ? 8 : 4;
   if constexpr (OP == OP_SUM) {
     if constexpr (BF16) {
@@ -168,13 +171,27 @@ JLA_DEV void car_epilogue(const float* sum, long long e0, void* out, float* h, b
       p[1] = pack2bf(r[2], r[3]);
       *reinterpret_cast<u32x2*>(hb + e0) = p;
     }
+    if (hb_pack) {
+      // N consecutive elements of one row (pack_cols % 32 == 0, e0 % N == 0): 8 (or 4) contiguous packed bf16
+      const int m = (int)(e0 / pack_cols), c = (int)(e0 - (long long)m * pack_cols);
+      bf16_t* dst = hb_pack + pack_off(m, c, pack_cols);
+      if constexpr (BF16) {
+        *reinterpret_cast<u32x4*>(dst) = pack8(r);
+      } else {
+        u32x2 p;
+        p[0] = pack2bf(r[0], r[1]);
+        p[1] = pack2bf(r[2], r[3]);
+        *reinterpret_cast<u32x2*>(dst) = p;
+      }
+    }
   }
 }
 
 template <int OP, bool BF16, bool TWO_SHOT>
 __global__ void __launch_bounds__(CAR_THREADS)
     car_reduce_kernel(const char* __restrict__ in, void* __restrict__ out, float* __restrict__ h,
-                      bf16_t* __restrict__ hb, long long nbytes, const CarDevice* __restrict__ dev) {
+                      bf16_t* __restrict__ hb, long long nbytes, const CarDevice* __restrict__ dev,
+                      bf16_t* __restrict__ hb_pack, int pack_cols) {
   const CarDevice& d = *dev;  // by reference: a by-value copy indexed with runtime p lives in scratch
   constexpr int ESZ = BF16 ? 2 : 4;
   constexpr int N = 16 / ESZ;
@@ -210,7 +227,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
       Piece<BF16> acc;
       acc.set(ld_sys16(mine, a_off + off));
       for (int p = 1; p < d.world; ++p) acc.add(ld_sys16(mine, a_off + (long long)p * slot + off));
-      car_epilogue<OP, BF16>(acc.v, off / ESZ, out, h, hb);
+      car_epilogue<OP, BF16>(acc.v, off / ESZ, out, h, hb, hb_pack, pack_cols);
     }
     return;
   }
@@ -243,7 +260,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[4 * q + i] = __uint_as_float(v[i]);
     }
-    car_epilogue<OP, BF16>(s, off / ESZ, out, h, hb);
+    car_epilogue<OP, BF16>(s, off / ESZ, out, h, hb, hb_pack, pack_cols);
   }
 }
 
@@ -370,29 +387,32 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
 
 template <int OP, bool BF16>
 static void launch_reduce(int two_shot, int grid, const void* in, void* out, float* h, bf16_t* hb, long long nbytes,
-                          const CarDevice* d, hipStream_t s) {
+                          const CarDevice* d, hipStream_t s, bf16_t* hb_pack, int pack_cols) {
   if (two_shot)
-    car_reduce_kernel<OP, BF16, true><<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), out, h, hb, nbytes, d);
+    car_reduce_kernel<OP, BF16, true><<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), out, h, hb, nbytes, d,
+                                                                   hb_pack, pack_cols);
   else
-    car_reduce_kernel<OP, BF16, false><<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), out, h, hb, nbytes, d);
+    car_reduce_kernel<OP, BF16, false><<<grid, CAR_THREADS, 0, s>>>(static_cast<const char*>(in), out, h, hb, nbytes, d,
+                                                                    hb_pack, pack_cols);
 }
 
 // op 0: out = sum(in) (same dtype); op 1: h += sum(in), hb = bf16(h) (h fp32, hb bf16, element count of in)
 int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t* hb, long long nbytes, int is_bf16,
-               int two_shot, hipStream_t s) {
+               int two_shot, hipStream_t s, bf16_t* hb_pack, int pack_cols) {
   CarHost* st = static_cast<CarHost*>(state);
   if (!st || nbytes <= 0) return nbytes == 0 ? 0 : -1;
   if (nbytes > st->h.max_bytes || (nbytes & 15)) return -2;
   if (op == OP_RESID && (!h || !hb)) return -1;
+  if (hb_pack && (op != OP_RESID || pack_cols <= 0 || (pack_cols & 31))) return -1;
   if (two_shot && st->h.world == 1) two_shot = 0;
   const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
   const int grid = (int)(nchunks < CAR_GRID ? nchunks : CAR_GRID);
   if (op == OP_SUM) {
-    if (is_bf16) launch_reduce<OP_SUM, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
-    else launch_reduce<OP_SUM, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
+    if (is_bf16) launch_reduce<OP_SUM, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s, nullptr, 0);
+    else launch_reduce<OP_SUM, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s, nullptr, 0);
   } else {
-    if (is_bf16) launch_reduce<OP_RESID, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
-    else launch_reduce<OP_RESID, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s);
+    if (is_bf16) launch_reduce<OP_RESID, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s, hb_pack, pack_cols);
+    else launch_reduce<OP_RESID, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s, hb_pack, pack_cols);
   }
   JLA_CHECK_LAUNCH();
   return 0;

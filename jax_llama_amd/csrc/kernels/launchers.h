@@ -149,7 +149,8 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
 // op 0: out = sum over ranks of in (bf16/fp32); op 1: h (fp32) += sum, hb (bf16) = h. two_shot: reduce-scatter +
 // all-gather instead of every rank reading every peer's copy
 int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t* hb, long long nbytes, int is_bf16,
-               int two_shot, hipStream_t s);
+               int two_shot, hipStream_t s,
+               bf16_t* hb_pack = nullptr, int pack_cols = 0);
 // all-gather of (fp32, int32 + idx_offset) pairs: mode 0 = first max over ranks per pair, mode 1 = [n/k][world*k]
 int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_offset, long long n, int k,
               float* out_a, int32_t* out_b, hipStream_t s);

@@ -344,8 +344,8 @@ class LLaMAForCausalLM:
         if self.comm.size == 1:
             ops.linear_residual(x, w, h, mirror=hb, x_packed=x_packed, mirror_packed=mirror_packed)
         else:
-            part = ops.linear(x, w, out_dtype=self.comm.reduce_dtype)
-            self.comm.all_reduce_residual_(part, h, hb)
+            part = ops.linear(x, w, out_dtype=self.comm.reduce_dtype, x_packed=x_packed)
+            self.comm.all_reduce_residual_(part, h, hb, hb_pack=mirror_packed)
 
     def forward_tokens(self, ids: torch.Tensor, positions: torch.Tensor, cache: KVCache, slot0,
                        kv_start: torch.Tensor, key_mask: Optional[torch.Tensor] = None,

@@ -134,8 +134,9 @@ def check_bounds(reset: bool = True):
 
 
 def linear(x: torch.Tensor, w, rms_eps: Optional[float] = None, out_dtype=BF16,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``y = [inv_rms(x) *] x @ W^T``; ``w`` is a ``models.weights.PackedLinear``."""
+           out: Optional[torch.Tensor] = None, x_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``y = [inv_rms(x) *] x @ W^T``; ``w`` is a ``models.weights.PackedLinear`` (``x_packed``: optional packed
+    copy of x for the packed-x decode variants)."""
     if not _is_gpu(x):
         r = ref.linear(x, w.dense(), rms_eps, out_dtype)
         if out is not None:
@@ -145,7 +146,7 @@ def linear(x: torch.Tensor, w, rms_eps: Optional[float] = None, out_dtype=BF16,
     m = x.shape[0]
     if out is None:
         out = torch.empty(m, w.n, dtype=out_dtype, device=x.device)
-    _gpu_linear(x, w, out, MODE_STORE, rms_eps, True)
+    _gpu_linear(x, w, out, MODE_STORE, rms_eps, True, None, x_packed)
     return out
 
 

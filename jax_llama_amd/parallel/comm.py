@@ -78,17 +78,25 @@ class TPComm:
         dist.all_reduce(t, group=self.group)
         return t
 
-    def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: Optional[torch.Tensor]):
-        """``h (fp32) += sum over ranks of partial``; ``hb = bf16(h)`` when given."""
+    def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: Optional[torch.Tensor],
+                             hb_pack: Optional[torch.Tensor] = None):
+        """``h (fp32) += sum over ranks of partial``; ``hb = bf16(h)`` when given; ``hb_pack``: a packed-layout
+        copy of hb too (custom path only -- callers ask ``packs_residual`` first)."""
         if self.size > 1 and self.custom is not None and hb is not None and self.custom.can_handle(partial):
-            self.custom.all_reduce_residual_(partial, h, hb)
+            self.custom.all_reduce_residual_(partial, h, hb, hb_pack=hb_pack)
             return h
+        if hb_pack is not None:
+            raise RuntimeError("all_reduce_residual_: the packed hb copy needs the custom all-reduce path")
         p = partial.float() if partial.dtype != torch.float32 else partial.clone()
         self.all_reduce_(p)
         h.add_(p.view_as(h))
         if hb is not None:
             hb.copy_(h)
         return h
+
+    def packs_residual(self, nbytes: int) -> bool:
+        """Whether ``all_reduce_residual_`` of an ``nbytes`` partial can also write a packed hb copy."""
+        return self.size == 1 or (self.custom is not None and 0 < nbytes <= self.custom.max_bytes and nbytes % 16 == 0)
 
     # ------------------------------------------------------------------ sampler gathers
     def argmax(self, val: torch.Tensor, idx: torch.Tensor, v_local: int) -> torch.Tensor:

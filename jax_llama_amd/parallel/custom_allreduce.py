@@ -120,10 +120,12 @@ class CustomAllReduce:
         ext().car_allreduce(self.state, t, out, ts)
         return out
 
-    def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: torch.Tensor, two_shot=None):
-        """``h += sum_ranks(partial)``; ``hb = bf16(h)`` (one kernel)."""
+    def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: torch.Tensor, two_shot=None,
+                             hb_pack=None):
+        """``h += sum_ranks(partial)``; ``hb = bf16(h)`` (one kernel); ``hb_pack``: also a packed-layout copy of hb
+        (``ops.packed_rows`` x D, the next projection's packed-x input)."""
         ts = self.use_two_shot(partial.numel() * partial.element_size()) if two_shot is None else bool(two_shot)
-        ext().car_allreduce_residual(self.state, partial, h, hb, ts)
+        ext().car_allreduce_residual(self.state, partial, h, hb, ts, hb_pack)
 
     def argmax_pairs(self, val: torch.Tensor, idx: torch.Tensor, idx_offset: int, out_val=None) -> torch.Tensor:
         """First max over ranks of each row's local ``(val, idx + idx_offset)``: int32 ``[B]``."""

@@ -72,7 +72,7 @@ def _gpu_params(cfg, seed):
     return meta_state_dict_to_params(sd, cfg.num_hidden_layers)
 
 
-def _worker(rank, world, port, kind, q):
+def _worker(rank, world, port, kind, q, rows=4):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world), LOCAL_RANK="0")
@@ -90,7 +90,10 @@ def _worker(rank, world, port, kind, q):
         cfg = _config(kind)
         params = _gpu_params(cfg, seed=21)
         tp_model = LLaMAForCausalLM(cfg, device="cuda", comm=comm, _do_init=False).load_params(params)
-        toks, mask = left_padded_batch([5, 9, 12, 12], 12, cfg.vocab_size, pad=2, seed=4)
+        # rows = 12: decode steps on the packed-activation path (ops.PACKED_X, 9-32 rows: the residual all-reduce
+        # also writes the packed hb copy, csrc/kernels/allreduce.hip)
+        lens = [5, 9, 12, 12] if rows == 4 else [5, 9, 12, 12, 7, 12, 3, 12, 10, 12, 8, 12][:rows]
+        toks, mask = left_padded_batch(lens, 12, cfg.vocab_size, pad=2, seed=4)
         pos = mask.cumsum(-1) - 1
         m = mask.bool()
         gen_len = 16
@@ -164,12 +167,12 @@ def _worker(rank, world, port, kind, q):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,kind", [(2, "small"), (4, "70b"), (8, "70b")])
-def test_tp_decode_matches_single_process(world, kind):
+@pytest.mark.parametrize("world,kind,rows", [(2, "small", 4), (4, "70b", 4), (8, "70b", 4), (2, "small", 12)])
+def test_tp_decode_matches_single_process(world, kind, rows):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, q, rows)) for r in range(world)]
     for p in procs:
         p.start()
     outs = []

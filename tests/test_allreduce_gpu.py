@@ -62,9 +62,17 @@ def _run(rank, world, q):
             for ts in (False, True):
                 h = h0.cuda()
                 hb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
-                car.all_reduce_residual_(x, h, hb, two_shot=ts)
+                # decode-shaped cases also get the packed hb copy (rows x 4096, common.h pack_off)
+                packed = n % 4096 == 0 and n // 4096 <= 64
+                hp = torch.empty(((n // 4096 + 15) // 16) * 16, 4096, dtype=torch.bfloat16,
+                                 device="cuda") if packed else None
+                car.all_reduce_residual_(x, h.view(-1, 4096) if packed else h, hb.view(-1, 4096) if packed else hb,
+                                         two_shot=ts, hb_pack=hp)
                 assert torch.equal(h.cpu(), h_want), ("residual", ts, n, dt)
                 assert torch.equal(hb.cpu(), h_want.to(torch.bfloat16)), ("mirror", ts, n, dt)
+                if packed:
+                    from jax_llama_amd.ops import reference as ref
+                    assert torch.equal(ref.unpack_act(hp.cpu(), n // 4096), hb.cpu().view(-1, 4096)), ("pack", ts, n)
     # (value, index) pairs: greedy argmax across ranks (ties -> lowest rank) and the top-k layout
     for b in (1, 7, 300):
         g = torch.Generator().manual_seed(5)

@@ -36,18 +36,22 @@ struct TkShared {
   uint32_t sel[2];
   uint32_t sk[64];  // merge: compacted survivors
   int32_t si[64];
+  uint32_t ck[TK_THREADS];  // chunk: prefiltered candidates (key, element index), in element order
+  int32_t cj[TK_THREADS];
+  uint32_t total;
 };
 
 // Block-wide radix select over TK_E keys per thread: T = the K-th largest key; need_eq = how many
 // keys equal to T are part of the top K (all keys > T are). Requires K <= number of keys.
-JLA_DEV void radix_select(const uint32_t (&key)[TK_E], int K, TkShared& sh, uint32_t& T, int& need_eq) {
+template <int E>
+JLA_DEV void radix_select(const uint32_t (&key)[E], int K, TkShared& sh, uint32_t& T, int& need_eq) {
   uint32_t prefix = 0, mask = 0;
   int kr = K;
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = threadIdx.x; i < 256; i += TK_THREADS) sh.hist[i] = 0;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < TK_E; ++j)
+    for (int j = 0; j < E; ++j)
       if ((key[j] & mask) == prefix) atomicAdd(&sh.hist[(key[j] >> shift) & 255u], 1u);
     __syncthreads();
     if (threadIdx.x < 64) {
@@ -104,11 +108,11 @@ JLA_DEV uint32_t block_excl_scan(uint32_t v, TkShared& sh) {
 }
 
 // Emit exactly K (key, index) pairs: keys > T in thread-major order, then the first need_eq keys == T.
-template <typename F>
-JLA_DEV void emit_topk(const uint32_t (&key)[TK_E], uint32_t T, int need_eq, int K, TkShared& sh, F&& put) {
+template <int E, typename F>
+JLA_DEV void emit_topk(const uint32_t (&key)[E], uint32_t T, int need_eq, int K, TkShared& sh, F&& put) {
   uint32_t ngt = 0, neq = 0;
 #pragma unroll
-  for (int j = 0; j < TK_E; ++j) {
+  for (int j = 0; j < E; ++j) {
     ngt += key[j] > T;
     neq += key[j] == T;
   }
@@ -116,7 +120,7 @@ JLA_DEV void emit_topk(const uint32_t (&key)[TK_E], uint32_t T, int need_eq, int
   int gpos = ex >> 16, epos = ex & 0xffff;
   const int count_gt = K - need_eq;
 #pragma unroll
-  for (int j = 0; j < TK_E; ++j) {
+  for (int j = 0; j < E; ++j) {
     if (key[j] > T) {
       put(gpos++, j);
     } else if (key[j] == T) {
@@ -147,11 +151,52 @@ __global__ void __launch_bounds__(TK_THREADS)
 #pragma unroll
     for (int j = 0; j < TK_E; ++j) key[j] = base + j < V ? fkey(x[base + j]) : 0u;  // 0 < key(-inf)
   }
-  uint32_t T;
-  int need_eq;
-  radix_select(key, K, sh, T, need_eq);
   float* ov = cv + ((size_t)b * nch + c) * K;
   int32_t* oi = ci + ((size_t)b * nch + c) * K;
+  // Prefilter: T0 = the K-th largest of the 256 per-thread maxima. At least K keys (those maxima) are >= T0, so the
+  // chunk's top K are all >= T0; on logits only ~K of the 4096 keys survive. The exact select then runs on the
+  // survivors, one per thread (256 LDS-histogram adds per radix pass instead of 4096 that pile onto the few hot
+  // exponent bins). More survivors than threads (flat or tied logits): the full 16-keys-per-thread select.
+  uint32_t tmax = 0;
+#pragma unroll
+  for (int j = 0; j < TK_E; ++j) tmax = max(tmax, key[j]);
+  uint32_t T0;
+  int ne0;
+  {
+    const uint32_t k1[1] = {tmax};
+    radix_select(k1, K, sh, T0, ne0);
+  }
+  uint32_t ns = 0;
+#pragma unroll
+  for (int j = 0; j < TK_E; ++j) ns += key[j] >= T0;
+  const uint32_t pos = block_excl_scan(ns, sh);
+  if (threadIdx.x == TK_THREADS - 1) sh.total = pos + ns;
+  __syncthreads();
+  const uint32_t S = sh.total;
+  uint32_t T;
+  int need_eq;
+  if (S <= (uint32_t)TK_THREADS) {
+    uint32_t r = pos;
+#pragma unroll
+    for (int j = 0; j < TK_E; ++j)
+      if (key[j] >= T0) {  // compacted in element order (thread-major, j ascending): ties keep index order
+        sh.ck[r] = key[j];
+        sh.cj[r] = base + j;
+        ++r;
+      }
+    __syncthreads();
+    const bool have = threadIdx.x < S;
+    const uint32_t k1[1] = {have ? sh.ck[threadIdx.x] : 0u};
+    const int e1 = have ? sh.cj[threadIdx.x] : V;
+    radix_select(k1, K, sh, T, need_eq);
+    emit_topk(k1, T, need_eq, K, sh, [&](int slot, int) {
+      const bool valid = e1 < V;
+      ov[slot] = valid ? kfloat(k1[0]) : -INFINITY;
+      oi[slot] = valid ? idx_offset + e1 : 0x7fffffff;
+    });
+    return;
+  }
+  radix_select(key, K, sh, T, need_eq);
   emit_topk(key, T, need_eq, K, sh, [&](int slot, int j) {
     const bool valid = base + j < V;
     ov[slot] = valid ? kfloat(key[j]) : -INFINITY;

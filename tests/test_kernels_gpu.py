@@ -503,6 +503,25 @@ def test_topk_candidates_exact(b, v, k):
     assert torch.equal(gv.cpu(), rv)
 
 
+@pytest.mark.parametrize("case", ["block", "flat", "ties"])
+def test_topk_candidates_prefilter_fallbacks(case):
+    """Chunks whose survivors of the per-thread-maximum prefilter exceed one per thread (a run of 300 large
+    logits in one chunk, all-equal logits) take the full select; many exact ties at the threshold keep the
+    lowest indices."""
+    b, v, k = 3, 128256, 50
+    logits = torch.randn(b, v) * 4
+    if case == "block":
+        logits[:, 8192:8492] = 50.0 + torch.randn(b, 300)
+    elif case == "flat":
+        logits[:] = 0.0
+    else:
+        logits[:, ::97] = 30.0  # ~1300 exact ties above everything else, spread over every chunk
+    gv, gi = ops.topk_candidates(logits.to(DEV), k)
+    rv, ri = ref.topk_sorted(logits, k)
+    assert torch.equal(gi.cpu(), ri)
+    assert torch.equal(gv.cpu(), rv)
+
+
 @pytest.mark.parametrize("b,v,k,temp,top_p", [(16, 128256, 50, 1.0, 1.0), (8, 32000, 50, 0.7, 0.9),
                                               (4, 1000, 64, 1.3, 0.5), (2, 50, 1, 1.0, 1.0)])
 def test_topk_sample_matches_reference(b, v, k, temp, top_p):

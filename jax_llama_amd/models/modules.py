@@ -150,7 +150,7 @@ class LLaMABlockCollection:
         b = hb.shape[0] // seq_len
         rows = hb.shape[0]
         pk = None
-        if (ops.PACKED_X and hb.is_cuda and ops.PACKED_X_MIN_M <= rows <= ops.PACKED_ATT_MAX_M
+        if (ops.PACKED_X and hb.is_cuda and ops.PACKED_X_MIN_M <= rows <= min(ops.PACKED_ATT_MAX_M, ops.SKINNY_M)
                 and self.model.comm.packs_residual(rows * self.model.config.hidden_size * 4)):
             # TP: the residual all-reduce writes the packed hb copy (csrc/kernels/allreduce.hip car_epilogue)
             pk = PackedActs(rows, self.model, hb.device, full=rows <= ops.PACKED_X_MAX_M)

@@ -185,6 +185,7 @@ PACKED_X = os.environ.get("JLA_PACKED_X", "1") != "0"
 PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
 PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "32"))
 PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
+SKINNY_M = 64  # decode GEMV rows (csrc: SKINNY_MAX_M): packed copies exist only on that path
 XP_VARIANTS = (12, 13, 14, 15)
 
 

@@ -22,7 +22,7 @@
 
 namespace jla {
 
-constexpr int TK_THREADS = 256, TK_E = 16, TK_CHUNK = TK_THREADS * TK_E;
+constexpr int TK_THREADS = 256, TK_E = 32, TK_CHUNK = TK_THREADS * TK_E;
 
 JLA_DEV uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -130,6 +130,53 @@ JLA_DEV void emit_topk(const uint32_t (&key)[E], uint32_t T, int need_eq, int K,
   }
 }
 
+// Exact top K of the block's TK_CHUNK keys (thread t holds elements base .. base + TK_E - 1; key 0 = padding past
+// n_valid), calling put(slot, key, element) once per slot 0..K-1 (ties at the threshold keep the lowest elements).
+// Prefilter: T0 = the K-th largest of the 256 per-thread maxima. At least K keys (those maxima) are >= T0, so the top
+// K are all >= T0; on logits only ~K keys survive, and the exact select runs on the survivors, one per thread (256
+// LDS-histogram adds per radix pass instead of TK_CHUNK that pile onto the few hot exponent bins). More survivors
+// than threads (flat, tied or clustered keys): the full TK_E-keys-per-thread select.
+template <int E, typename F>
+JLA_DEV void select_topk(const uint32_t (&key)[E], int base, int n_valid, int K, TkShared& sh, F&& put) {
+  uint32_t tmax = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) tmax = max(tmax, key[j]);
+  uint32_t T0;
+  int ne0;
+  {
+    const uint32_t k1[1] = {tmax};
+    radix_select(k1, K, sh, T0, ne0);
+  }
+  uint32_t ns = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) ns += key[j] >= T0;
+  const uint32_t pos = block_excl_scan(ns, sh);
+  if (threadIdx.x == TK_THREADS - 1) sh.total = pos + ns;
+  __syncthreads();
+  const uint32_t S = sh.total;
+  uint32_t T;
+  int need_eq;
+  if (S <= (uint32_t)TK_THREADS) {
+    uint32_t r = pos;
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (key[j] >= T0) {  // compacted in element order (thread-major, j ascending): ties keep index order
+        sh.ck[r] = key[j];
+        sh.cj[r] = base + j;
+        ++r;
+      }
+    __syncthreads();
+    const bool have = threadIdx.x < S;
+    const uint32_t k1[1] = {have ? sh.ck[threadIdx.x] : 0u};
+    const int e1 = have ? sh.cj[threadIdx.x] : n_valid;
+    radix_select(k1, K, sh, T, need_eq);
+    emit_topk(k1, T, need_eq, K, sh, [&](int slot, int) { put(slot, k1[0], e1); });
+    return;
+  }
+  radix_select(key, K, sh, T, need_eq);
+  emit_topk(key, T, need_eq, K, sh, [&](int slot, int j) { put(slot, key[j], base + j); });
+}
+
 __global__ void __launch_bounds__(TK_THREADS)
     topk_chunk_kernel(const float* __restrict__ logits, int V, int K, int idx_offset, float* __restrict__ cv,
                       int32_t* __restrict__ ci) {
@@ -153,54 +200,10 @@ __global__ void __launch_bounds__(TK_THREADS)
   }
   float* ov = cv + ((size_t)b * nch + c) * K;
   int32_t* oi = ci + ((size_t)b * nch + c) * K;
-  // Prefilter: T0 = the K-th largest of the 256 per-thread maxima. At least K keys (those maxima) are >= T0, so the
-  // chunk's top K are all >= T0; on logits only ~K of the 4096 keys survive. The exact select then runs on the
-  // survivors, one per thread (256 LDS-histogram adds per radix pass instead of 4096 that pile onto the few hot
-  // exponent bins). More survivors than threads (flat or tied logits): the full 16-keys-per-thread select.
-  uint32_t tmax = 0;
-#pragma unroll
-  for (int j = 0; j < TK_E; ++j) tmax = max(tmax, key[j]);
-  uint32_t T0;
-  int ne0;
-  {
-    const uint32_t k1[1] = {tmax};
-    radix_select(k1, K, sh, T0, ne0);
-  }
-  uint32_t ns = 0;
-#pragma unroll
-  for (int j = 0; j < TK_E; ++j) ns += key[j] >= T0;
-  const uint32_t pos = block_excl_scan(ns, sh);
-  if (threadIdx.x == TK_THREADS - 1) sh.total = pos + ns;
-  __syncthreads();
-  const uint32_t S = sh.total;
-  uint32_t T;
-  int need_eq;
-  if (S <= (uint32_t)TK_THREADS) {
-    uint32_t r = pos;
-#pragma unroll
-    for (int j = 0; j < TK_E; ++j)
-      if (key[j] >= T0) {  // compacted in element order (thread-major, j ascending): ties keep index order
-        sh.ck[r] = key[j];
-        sh.cj[r] = base + j;
-        ++r;
-      }
-    __syncthreads();
-    const bool have = threadIdx.x < S;
-    const uint32_t k1[1] = {have ? sh.ck[threadIdx.x] : 0u};
-    const int e1 = have ? sh.cj[threadIdx.x] : V;
-    radix_select(k1, K, sh, T, need_eq);
-    emit_topk(k1, T, need_eq, K, sh, [&](int slot, int) {
-      const bool valid = e1 < V;
-      ov[slot] = valid ? kfloat(k1[0]) : -INFINITY;
-      oi[slot] = valid ? idx_offset + e1 : 0x7fffffff;
-    });
-    return;
-  }
-  radix_select(key, K, sh, T, need_eq);
-  emit_topk(key, T, need_eq, K, sh, [&](int slot, int j) {
-    const bool valid = base + j < V;
-    ov[slot] = valid ? kfloat(key[j]) : -INFINITY;
-    oi[slot] = valid ? idx_offset + base + j : 0x7fffffff;
+  select_topk(key, base, V, K, sh, [&](int slot, uint32_t k, int e) {
+    const bool valid = e < V;
+    ov[slot] = valid ? kfloat(k) : -INFINITY;
+    oi[slot] = valid ? idx_offset + e : 0x7fffffff;
   });
 }
 
@@ -217,6 +220,10 @@ JLA_DEV uint4 philox4x32_10(uint4 ctr, uint2 k) {
 }
 
 // mode 0: write the sorted top-K (out_v/out_i [B, K]); mode 1: sample one token per row into nxt[B].
+// E candidates per thread: the smallest that covers C, so the candidates spread over most threads and the
+// per-thread-maximum prefilter of select_topk compacts them (with TK_E per thread, 16 chunks x 50 candidates sat
+// in 25 threads and every merge fell back to the full select)
+template <int E>
 __global__ void __launch_bounds__(TK_THREADS)
     topk_merge_kernel(const float* __restrict__ cv, const int32_t* __restrict__ ci, int C, int K, int mode,
                       float* __restrict__ out_v, int32_t* __restrict__ out_i, int32_t* __restrict__ nxt,
@@ -224,16 +231,13 @@ __global__ void __launch_bounds__(TK_THREADS)
                       const int32_t* __restrict__ step) {
   __shared__ TkShared sh;
   const int b = blockIdx.x;
-  const int base = threadIdx.x * TK_E;
-  uint32_t key[TK_E];
+  const int base = threadIdx.x * E;
+  uint32_t key[E];
 #pragma unroll
-  for (int j = 0; j < TK_E; ++j) key[j] = base + j < C ? fkey(cv[(size_t)b * C + base + j]) : 0u;
-  uint32_t T;
-  int need_eq;
-  radix_select(key, K, sh, T, need_eq);
-  emit_topk(key, T, need_eq, K, sh, [&](int slot, int j) {
-    sh.sk[slot] = key[j];
-    sh.si[slot] = ci[(size_t)b * C + base + j];
+  for (int j = 0; j < E; ++j) key[j] = base + j < C ? fkey(cv[(size_t)b * C + base + j]) : 0u;
+  select_topk(key, base, C, K, sh, [&](int slot, uint32_t k, int e) {
+    sh.sk[slot] = k;
+    sh.si[slot] = e < C ? ci[(size_t)b * C + e] : 0x7fffffff;
   });
   __syncthreads();
   if (threadIdx.x >= 64) return;
@@ -312,8 +316,18 @@ int topk_merge(const float* cv, const int32_t* ci, int B, int C, int K, int mode
   if (B <= 0) return 0;
   if (K < 1 || K > 64 || K > C || C > TK_CHUNK) return -1;
   if (mode == 1 && (!nxt || !step || !(temperature > 0.f))) return -2;
-  topk_merge_kernel<<<B, TK_THREADS, 0, s>>>(cv, ci, C, K, mode, out_v, out_i, nxt, 1.0f / temperature, top_p,
-                                             (uint32_t)seed, (uint32_t)(seed >> 32), step);
+#define JLA_TKM(E)                                                                                          \
+  topk_merge_kernel<E><<<B, TK_THREADS, 0, s>>>(cv, ci, C, K, mode, out_v, out_i, nxt, 1.0f / temperature, top_p, \
+                                                (uint32_t)seed, (uint32_t)(seed >> 32), step)
+  if (C <= 4 * TK_THREADS)
+    JLA_TKM(4);
+  else if (C <= 8 * TK_THREADS)
+    JLA_TKM(8);
+  else if (C <= 16 * TK_THREADS)
+    JLA_TKM(16);
+  else
+    JLA_TKM(TK_E);
+#undef JLA_TKM
   JLA_CHECK_LAUNCH();
   return 0;
 }

@@ -555,7 +555,7 @@ SAMPLER_MAX_K = 64
 
 def topk_candidates(logits: torch.Tensor, k: int, idx_offset: int = 0):
     """Sorted top-``k`` (values fp32 [B, k], global indices int32 [B, k]) of fp32 logits on the
-    device: per-4096-chunk radix select + one merge (csrc/kernels/topk_sample.hip)."""
+    device: per-8192-chunk prefiltered radix select + one merge (csrc/kernels/topk_sample.hip)."""
     if not _is_gpu(logits):
         v, i = ref.topk_sorted(logits, k)
         return v, i + idx_offset

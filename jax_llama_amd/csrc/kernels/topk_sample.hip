@@ -22,7 +22,7 @@
 
 namespace jla {
 
-constexpr int TK_THREADS = 256, TK_E = 32, TK_CHUNK = TK_THREADS * TK_E;
+constexpr int TK_THREADS = 256, TK_E = 64, TK_CHUNK = TK_THREADS * TK_E;
 
 JLA_DEV uint32_t fkey(float f) {
   const uint32_t u = __float_as_uint(f);

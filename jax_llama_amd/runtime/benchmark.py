@@ -20,7 +20,8 @@ def synthetic_prompts(vocab: int, batch: int, prompt_len: int, seed: int) -> tor
 
 def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256, steps: int = 64,
                    seed: int = 0, barrier=None, do_sample: bool = False) -> Dict[str, float]:
-    """Prefill ``batch`` prompts into a ``prompt_len + gen_len`` cache, then time ``steps`` replays of
+    """Prefill ``batch`` prompts into a ``prompt_len + gen_len`` cache (``prefill_ms``: the second, warm prefill; the
+    first autotunes), then time ``steps`` replays of
     the captured decode step (every layer, lm_head, sampler, state update). Every rank of a TP group
     must call this with the same arguments (the step contains the TP collectives)."""
     assert steps + 2 < gen_len, "replays must stay inside the cache"
@@ -31,11 +32,12 @@ def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256,
     eng.gc = gc
     prompts = synthetic_prompts(model.config.vocab_size, batch, prompt_len, seed)
     dev = model.device
+    eng.prefill(prompts, None)  # cold: autotunes new prefill shapes and grows the workspaces; not timed
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     ev0.record()
-    eng.prefill(prompts, None)
+    eng.prefill(prompts, None)  # warm prefill: ``prefill_ms``
     ev1.record()
     eng._decode_step()  # eager step: sizes the workspaces before capture
     eng._ensure_graph()

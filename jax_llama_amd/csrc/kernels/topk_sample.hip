@@ -43,11 +43,14 @@ struct TkShared {
 
 // Block-wide radix select over TK_E keys per thread: T = the K-th largest key; need_eq = how many
 // keys equal to T are part of the top K (all keys > T are). Requires K <= number of keys.
+// last_shift 16: two passes only, T = the K-th largest key with its low 16 bits cleared (a lower bound with at least K
+// keys >= T; need_eq is then meaningless).
 template <int E>
-JLA_DEV void radix_select(const uint32_t (&key)[E], int K, TkShared& sh, uint32_t& T, int& need_eq) {
+JLA_DEV void radix_select(const uint32_t (&key)[E], int K, TkShared& sh, uint32_t& T, int& need_eq,
+                          int last_shift = 0) {
   uint32_t prefix = 0, mask = 0;
   int kr = K;
-  for (int shift = 24; shift >= 0; shift -= 8) {
+  for (int shift = 24; shift >= last_shift; shift -= 8) {
     for (int i = threadIdx.x; i < 256; i += TK_THREADS) sh.hist[i] = 0;
     __syncthreads();
 #pragma unroll
@@ -132,12 +135,13 @@ JLA_DEV void emit_topk(const uint32_t (&key)[E], uint32_t T, int need_eq, int K,
 
 // Exact top K of the block's TK_CHUNK keys (thread t holds elements base .. base + TK_E - 1; key 0 = padding past
 // n_valid), calling put(slot, key, element) once per slot 0..K-1 (ties at the threshold keep the lowest elements).
-// Prefilter: T0 = the K-th largest of the 256 per-thread maxima. At least K keys (those maxima) are >= T0, so the top
+// Prefilter: T0 = the K-th largest of the 256 per-thread maxima (bound_shift 16: its top 16 bits). At least K keys are >= T0, so the top
 // K are all >= T0; on logits only ~K keys survive, and the exact select runs on the survivors, one per thread (256
 // LDS-histogram adds per radix pass instead of TK_CHUNK that pile onto the few hot exponent bins). More survivors
 // than threads (flat, tied or clustered keys): the full TK_E-keys-per-thread select.
 template <int E, typename F>
-JLA_DEV void select_topk(const uint32_t (&key)[E], int base, int n_valid, int K, TkShared& sh, F&& put) {
+JLA_DEV void select_topk(const uint32_t (&key)[E], int base, int n_valid, int K, TkShared& sh, F&& put,
+                         int bound_shift = 0) {
   uint32_t tmax = 0;
 #pragma unroll
   for (int j = 0; j < E; ++j) tmax = max(tmax, key[j]);
@@ -145,7 +149,7 @@ JLA_DEV void select_topk(const uint32_t (&key)[E], int base, int n_valid, int K,
   int ne0;
   {
     const uint32_t k1[1] = {tmax};
-    radix_select(k1, K, sh, T0, ne0);
+    radix_select(k1, K, sh, T0, ne0, bound_shift);  // a bound is enough
   }
   uint32_t ns = 0;
 #pragma unroll
@@ -200,11 +204,12 @@ __global__ void __launch_bounds__(TK_THREADS)
   }
   float* ov = cv + ((size_t)b * nch + c) * K;
   int32_t* oi = ci + ((size_t)b * nch + c) * K;
+  // logits: the top 16 bits (sign, exponent, 7 mantissa bits) of the bound admit ~K survivors; two radix passes saved
   select_topk(key, base, V, K, sh, [&](int slot, uint32_t k, int e) {
     const bool valid = e < V;
     ov[slot] = valid ? kfloat(k) : -INFINITY;
     oi[slot] = valid ? idx_offset + e : 0x7fffffff;
-  });
+  }, 16);
 }
 
 JLA_DEV uint4 philox4x32_10(uint4 ctr, uint2 k) {

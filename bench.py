@@ -18,9 +18,14 @@ Extra keys (outside the timed region, reported alongside the headline):
     the flash-prefill attention + last-position lm_head + greedy token);
   * ``sampled``: tokens/s of whole ``generate`` calls in the reference's default sampling mode
     (temperature 0.8, top-p 0.95, top-k 50: jax_example.py:33, generation.py:22,34) at the headline batch;
-  * ``tp_points`` (world > 1): the second half of the metric, Llama-3-70B tensor-parallel over every
-    GPU of the job (MP = world, README.md:52-53): decode ms/token at B = 1/32/256 through the custom
-    xGMI collectives, under a watchdog so a stuck collective can never cost the headline line.
+  * ``tp_points`` (world > 1): the second half of the metric, tensor-parallel over every GPU of the job
+    (MP = world): Llama-3-70B at MP 8 / 4 (README.md:52-53), Llama-2-13B at MP 2 (README.md:50); decode ms/token
+    at B = 1/32/256 through the custom xGMI collectives, under a watchdog so a stuck collective can never cost the
+    headline line;
+  * ``tp_rank_proxy`` (one GPU): ONE rank of Llama-3-70B at MP 8 -- rank 0's shards at the real per-rank shapes
+    (D 8192, 8 q / 1 kv heads, F 3584, V 16032, 80 layers, 17.6 GB), every per-token collective the same custom
+    kernel on a world-1 instance (parallel/comm.py TPRankProxyComm): the per-rank decode step time, launch
+    structure included, without the xGMI link's latency.
 
   python bench.py --gpus 1 --steps 3 --warmup 1
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 --model llama3-70b --tp 8
@@ -56,9 +61,13 @@ def main():
     ap.add_argument("--no-sampled", action="store_true", help="skip the sampling-mode throughput point")
     ap.add_argument("--ttft-len", type=int, default=2048, help="prompt length of the time-to-first-token point "
                     "(B = 1; 0 = skip)")
-    ap.add_argument("--tp-model", default="llama3-70b", help="model of the tensor-parallel points (world > 1)")
+    ap.add_argument("--tp-model", default="auto", help="model of the tensor-parallel points (world > 1); auto: "
+                    "the BASELINE model of that MP degree (2: llama2-13b, 4/8: llama3-70b)")
     ap.add_argument("--tp-batches", type=int, nargs="*", default=[1, 32, 256])
     ap.add_argument("--tp-timeout", type=float, default=420.0, help="watchdog (s) of the tensor-parallel points")
+    ap.add_argument("--proxy-model", default="llama3-70b", help="model of the one-GPU TP rank proxy ('' = skip)")
+    ap.add_argument("--proxy-tp", type=int, default=8)
+    ap.add_argument("--proxy-batches", type=int, nargs="*", default=[1, 32, 256])
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
 
@@ -152,15 +161,29 @@ def main():
     eng_mod._ENGINES.clear()  # free the headline batch's KV cache before the extra points
     torch.cuda.empty_cache()
 
-    # The extra points never cost the headline line: each one's failure is recorded in its key instead (every
-    # rank runs the same shapes, so a Python-level failure happens on all ranks alike).
+    # The extra points never cost the headline line: each one's failure is recorded in its key instead. A failure
+    # can be rank-local (OOM, one rank's comm.check()), so the ranks agree on every point's outcome before the next
+    # one: once any rank failed, the remaining collective points are skipped on every rank.
+    failed = {"any": False}
+
     def extra(key, fn):
+        ok = True
+        if failed["any"]:
+            res[key] = {"skipped": "an earlier extra point failed on some rank"}
+            return
         try:
             fn()
         except Exception as ex:  # noqa: BLE001
+            ok = False
             res[key] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
         eng_mod._ENGINES.clear()
         torch.cuda.empty_cache()
+        if world > 1:
+            oks = [None] * world
+            dist.all_gather_object(oks, ok)
+            ok = all(oks)
+        if not ok:
+            failed["any"] = True
 
     # ---- latency points (same model, BASELINE.md protocol)
     def latency_points():
@@ -197,11 +220,13 @@ def main():
         extra("ttft", ttft)
     if not args.no_sampled:
         extra("sampled", sampled)
+    if world == 1 and args.proxy_model and args.proxy_batches:
+        extra("tp_rank_proxy", lambda: res.__setitem__("tp_rank_proxy", _tp_rank_proxy(args)))
     res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}{'_rms' if k[4] else ''}": f"ks{v[0]}_tile{v[1]}"
                                for k, v in autotune.ksplit_table().items()}
 
-    # ---- tensor-parallel points: 70B over every GPU of the job (world > 1), under a watchdog
-    if world > 1 and args.tp == 1 and args.tp_model and args.tp_batches:
+    # ---- tensor-parallel points: the BASELINE model of MP = world over every GPU of the job, under a watchdog
+    if world > 1 and args.tp == 1 and args.tp_model and args.tp_batches and not failed["any"]:
         del model
         torch.cuda.empty_cache()
         res["tp_points"] = _tp_points(args, ctx, res)
@@ -221,9 +246,42 @@ def _emit(res, json_out):
             f.write(line + "\n")
 
 
+TP_MODEL_BY_MP = {2: "llama2-13b", 4: "llama3-70b", 8: "llama3-70b"}  # BASELINE.json configs 3 and 4
+
+
+def _tp_rank_proxy(args):
+    """One rank of ``--proxy-model`` at MP ``--proxy-tp`` on this GPU (``TPRankProxyComm``): decode ms/token at
+    ``--proxy-batches`` next to the per-rank HBM roofline."""
+    import torch
+
+    from jax_llama_amd.config import get_preset
+    from jax_llama_amd.models import LLaMAForCausalLM
+    from jax_llama_amd.parallel import TPRankProxyComm
+    from jax_llama_amd.runtime.benchmark import decode_latency
+
+    comm = TPRankProxyComm.create(args.proxy_tp)
+    cfg = get_preset(args.proxy_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+    model = LLaMAForCausalLM(cfg, device="cuda", comm=comm, _do_init=False).init_random(seed=4321)
+    out = {"model": args.proxy_model, "mp": args.proxy_tp, "rank": 0,
+           "note": "one rank's shards and launches; collectives on a world-1 instance of the custom kernels "
+                   "(no xGMI latency)",
+           "prompt_len": args.prompt_len, "cache_len": args.prompt_len + args.gen_len,
+           "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
+           "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
+           "launches_per_layer": 7}
+    try:
+        out["points"] = [decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=11)
+                         for b in args.proxy_batches]
+    finally:
+        del model
+        comm.close()
+        torch.cuda.empty_cache()
+    return out
+
+
 def _tp_points(args, ctx, res):
-    """Llama-3-70B at MP = world (one TP group over every GPU). A watchdog thread ends the process
-    with the headline line (and ``tp_points: timeout``) if the phase does not finish in time."""
+    """The BASELINE model of MP = world (one TP group over every GPU). A watchdog thread ends the process with the
+    headline line (and ``tp_points: timeout``) and a non-zero exit code if the phase does not finish in time."""
     import torch
 
     from jax_llama_amd.config import get_preset
@@ -239,17 +297,18 @@ def _tp_points(args, ctx, res):
                 res["tp_points"] = {"status": "timeout", "timeout_s": args.tp_timeout}
                 _emit(res, args.json_out)
             sys.stdout.flush()
-            os._exit(0)
+            os._exit(3)  # the headline line is out, but a stuck phase is not a clean run
 
     threading.Thread(target=watchdog, daemon=True).start()
     world = ctx.world
-    out = {"model": args.tp_model, "mp": world, "prompt_len": args.prompt_len, "cache_len":
+    tp_model = TP_MODEL_BY_MP.get(world, "llama3-70b") if args.tp_model == "auto" else args.tp_model
+    out = {"model": tp_model, "mp": world, "prompt_len": args.prompt_len, "cache_len":
            args.prompt_len + args.gen_len}
     try:
         ctx.setup_mesh(tp=world)
         comm = TPComm.from_context(ctx)
         out["custom_allreduce"] = comm.custom is not None
-        cfg = get_preset(args.tp_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+        cfg = get_preset(tp_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
         model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm, _do_init=False).init_random(seed=4321)
         out["weight_gb_per_gpu"] = round(model.weight_bytes() / 1e9, 3)
         out["hbm_roofline_ms_per_token"] = round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)

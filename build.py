@@ -88,11 +88,9 @@ def _scratch_users(remarks: str):
 # Kernels allowed to use scratch, by mangled-name substring -> max bytes/lane: rare shapes where a spill is
 # accepted, and epilogue-only spills (2-3 dwords AFTER the main loop; the loop itself is checked
 # spill-free at this bound: its 256 accumulators + two fragment sets use the whole 512-register file).
-SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20, "gemm4_kernelILi": 16,
+SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20,
               # gemm2 FA + fused RMS: a 3-dword spill in the split-K fixup tail (after the main loop)
-              "gemm2_kernelILi0ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16, "gemm2_kernelILi2ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16,
-              # prefill attention with 64 queries per wave (impl 3, A/B): 512 registers, a few spilled dwords
-              "attn_prefill_v2_kernelILi4ELi2E": 64}
+              "gemm2_kernelILi0ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16, "gemm2_kernelILi2ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16}
 
 
 def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):
@@ -122,7 +120,7 @@ def build_C(jobs: int, force: bool, debug_bounds: bool = False) -> Path:
         rebuilt = list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force, extra), zip(srcs, objs)))
     # the hand-counted load rings must never be read before their waits: check the assembly
     for src, did in zip(srcs, rebuilt):
-        if did and src.stem in ("gemv", "skinny", "attn_decode", "chain"):  # (attn_decode: the v4 register ring)
+        if did and src.stem in ("gemv", "skinny", "attn_decode"):  # (attn_decode: the v4 register ring)
             asm = odir / (src.stem + ".s")
             _run([HIPCC, *HIP_FLAGS, *extra, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
             try:

@@ -84,6 +84,32 @@ void rmsnorm(Tensor x, Tensor w, Tensor out, double eps) {
   rc(jla::rmsnorm(ptr<float>(x), ptr<float>(w), ptr<float>(out), M, D, (float)eps, stream()), "rmsnorm");
 }
 
+// h (fp32) += p (bf16 / fp32, same element count); hb = bf16(h)
+void residual_add(Tensor h, Tensor p, Tensor hb) {
+  check_gpu(h, "h");
+  check_gpu(p, "p");
+  check_gpu(hb, "hb");
+  check(h.scalar_type() == torch::kFloat32 && hb.scalar_type() == torch::kBFloat16 &&
+            (p.scalar_type() == torch::kBFloat16 || p.scalar_type() == torch::kFloat32),
+        "residual_add dtypes");
+  check(p.numel() == h.numel() && hb.numel() == h.numel() && h.numel() % 8 == 0, "residual_add shapes");
+  rc(jla::residual_add(ptr<float>(h), p.data_ptr(), p.scalar_type() == torch::kBFloat16, bf(hb), h.numel(), stream()),
+     "residual_add");
+}
+
+// y [M, N] = x [M, K] @ w [N, K]^T, all fp32 (precision='highest' lm_head)
+void gemm_f32(Tensor x, Tensor w, Tensor y) {
+  check_gpu(x, "x");
+  check_gpu(w, "w");
+  check_gpu(y, "y");
+  check(x.scalar_type() == torch::kFloat32 && w.scalar_type() == torch::kFloat32 && y.scalar_type() == torch::kFloat32,
+        "gemm_f32 dtypes");
+  check(x.dim() == 2 && w.dim() == 2 && y.dim() == 2 && x.size(1) == w.size(1) && y.size(0) == x.size(0) &&
+            y.size(1) == w.size(0),
+        "gemm_f32 shapes");
+  rc(jla::gemm_f32(ptr<float>(x), ptr<float>(w), ptr<float>(y), x.size(0), w.size(0), x.size(1), stream()), "gemm_f32");
+}
+
 void check_packed(const Tensor& w, int64_t n, int64_t k) {
   check_gpu(w, "weight");
   check(w.scalar_type() == torch::kBFloat16, "weight must be bf16");
@@ -239,74 +265,6 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
              packed_ptr(x_packed, m, k, "x_packed"));
 }
 
-// decode chain (chain.hip): h += a @ Wo^T; act = SwiGLU(norm(hb) @ Wgu^T); h += act @ Wd^T; and, when the next
-// layer's qkv weight is given, its fused qkv + RoPE + KV write -- one launch, M <= 16, TP = 1
-void decode_chain(Tensor a, Tensor w_o, Tensor w_gu, Tensor w_down, Tensor h, Tensor hb, Tensor act, double eps,
-                  c10::optional<Tensor> w_qkv, c10::optional<Tensor> table, c10::optional<Tensor> positions,
-                  c10::optional<Tensor> kc, c10::optional<Tensor> vc, c10::optional<Tensor> slot, int64_t seq_len,
-                  int64_t nh, int64_t nkv, int64_t dh, c10::optional<Tensor> q, Tensor counters, Tensor epoch,
-                  Tensor error, double timeout_s, c10::optional<Tensor> stamps) {
-  for (auto* t : {&a, &h, &hb, &act, &counters, &epoch, &error}) check_gpu(*t, "decode_chain arg");
-  const int64_t m = a.size(0), d = h.size(1), f = act.size(1);
-  check(m >= 1 && m <= 16, "decode_chain: M must be 1..16");
-  check(a.scalar_type() == torch::kBFloat16 && hb.scalar_type() == torch::kBFloat16 &&
-            act.scalar_type() == torch::kBFloat16 && h.scalar_type() == torch::kFloat32,
-        "decode_chain dtypes");
-  check(h.dim() == 2 && h.size(0) == m && hb.sizes() == h.sizes() && act.size(0) == m, "decode_chain shapes");
-  const int64_t ka = a.size(1);
-  check_packed(w_o, d, ka);
-  check_packed(w_gu, 2 * f, d);
-  check_packed(w_down, d, f);
-  check(counters.scalar_type() == torch::kInt32 && counters.numel() >= 4 * 8 * 32 && epoch.scalar_type() == torch::kInt32 &&
-            epoch.numel() >= 1 && error.scalar_type() == torch::kInt32 && error.numel() >= 1,
-        "decode_chain counters / epoch / error (int32)");
-  jla::ChainArgs c{};
-  c.M = (int)m;
-  c.counters = reinterpret_cast<unsigned*>(counters.data_ptr());
-  c.epoch = reinterpret_cast<const unsigned*>(epoch.data_ptr());
-  c.error = reinterpret_cast<unsigned*>(error.data_ptr());
-  int dev = 0, rate_khz = 0;
-  (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0)
-    rate_khz = 100000;
-  c.timeout_ticks = (long long)(timeout_s * 1000.0 * rate_khz);
-  auto stage = [&](int i, const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* out, jla::bf16_t* mirror,
-                   int mode, double e) {
-    jla::ChainStage& st = c.st[i];
-    st.x = cbf(x);
-    st.W = w.data_ptr();
-    st.out = out;
-    st.mirror = mirror;
-    st.N = (int)n;
-    st.K = (int)k;
-    st.mode = mode;
-    st.eps = (float)e;
-  };
-  stage(0, a, w_o, d, ka, h.data_ptr(), bf(hb), 1, -1.0);
-  stage(1, hb, w_gu, 2 * f, d, act.data_ptr(), nullptr, 2, eps);
-  stage(2, act, w_down, d, f, h.data_ptr(), bf(hb), 1, -1.0);
-  c.nstages = 3;
-  if (w_qkv.has_value()) {
-    check(table && positions && kc && vc && slot && q, "decode_chain: qkv stage arguments");
-    const int64_t n = (nh + 2 * nkv) * dh;
-    check_packed(*w_qkv, n, d);
-    c.st[3].qa = qkv_args(m, n, *table, *positions, *kc, *vc, *slot, seq_len, nh, nkv, dh, *q);
-    stage(3, hb, *w_qkv, n, d, nullptr, nullptr, MODE_QKV_ID, eps);
-    c.nstages = 4;
-  }
-  if (stamps.has_value()) {  // diagnostic timeline: int64 [>= total workgroups * 4]
-    check_gpu(*stamps, "stamps");
-    check(stamps->scalar_type() == torch::kInt64 && stamps->numel() >= 4 * 4096, "stamps: int64 [>= 16384]");
-    c.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr());
-  }
-  rc(jla::decode_chain(c, stream()), "decode_chain");
-}
-
-void chain_epoch_bump(Tensor epoch) {
-  check_gpu(epoch, "epoch");
-  check(epoch.scalar_type() == torch::kInt32, "epoch int32");
-  rc(jla::chain_epoch_bump(reinterpret_cast<unsigned*>(epoch.data_ptr()), stream()), "chain_epoch_bump");
-}
 
 void check_gemm_ws(const c10::optional<Tensor>& ws, int64_t ksplit, int64_t m, int64_t n, bool rms = false) {
   if (ksplit <= 1) return;
@@ -692,6 +650,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("mirror") = py::none());
   m.def("rms_scale", &rms_scale);
   m.def("rmsnorm", &rmsnorm);
+  m.def("residual_add", &residual_add);
+  m.def("gemm_f32", &gemm_f32);
   m.def("linear_skinny", &linear_skinny, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"),
         py::arg("mode"), py::arg("rms_eps"), py::arg("accumulate"), py::arg("variant"), py::arg("ws"),
         py::arg("tickets"), py::arg("mirror") = py::none(), py::arg("x_packed") = py::none(),
@@ -724,7 +684,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
   m.def("skinny_set_plan", [](int64_t nt, int64_t ks) { jla::skinny_set_plan((int)nt, (int)ks); });
-  m.def("gemm4_set_variant", [](int64_t v) { jla::gemm4_set_variant((int)v); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_set_impl", [](int64_t impl, int64_t waves_target) { jla::attn_set_impl(impl, waves_target); },
@@ -738,18 +697,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);
-  m.def("decode_chain", &decode_chain, "wo -> w1|w3 -> w2 [-> next wqkv] decode chain (one launch, M <= 16)",
-        py::arg("a"), py::arg("w_o"), py::arg("w_gu"), py::arg("w_down"), py::arg("h"), py::arg("hb"), py::arg("act"),
-        py::arg("eps"), py::arg("w_qkv"), py::arg("table"), py::arg("positions"), py::arg("kc"), py::arg("vc"),
-        py::arg("slot"), py::arg("seq_len"), py::arg("nh"), py::arg("nkv"), py::arg("dh"), py::arg("q"),
-        py::arg("counters"), py::arg("epoch"), py::arg("error"), py::arg("timeout_s"), py::arg("stamps") = py::none());
-  m.def("chain_epoch_bump", &chain_epoch_bump);
   m.def("bounds_error", [](bool reset) {
     const int r = reset ? 1 : 0;
     return (int64_t)(jla::jla_bounds_norm_embed(r) | jla::jla_bounds_rope_kv(r) | jla::jla_bounds_sample(r) |
                      jla::jla_bounds_gemm(r) | jla::jla_bounds_gemv(r) | jla::jla_bounds_skinny(r) |
-                     jla::jla_bounds_attn_decode(r) | jla::jla_bounds_attn_prefill(r) |
-                     jla::jla_bounds_chain(r));
+                     jla::jla_bounds_attn_decode(r) | jla::jla_bounds_attn_prefill(r));
   }, "OR of the bounds-checked debug build's error words (JLA_BOUNDS_* bits); always 0 in a release build",
         py::arg("reset") = false);
 #ifdef JLA_DEBUG_BOUNDS
@@ -778,6 +730,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("idx_offset"), py::arg("k"), py::arg("out_v").none(true), py::arg("out_i"));
   m.def("car_error", [](int64_t st) { return jla::car_error(reinterpret_cast<void*>(st)); });
   m.def("car_destroy", [](int64_t st) { jla::car_destroy(reinterpret_cast<void*>(st)); });
+  m.def("car_free", [](int64_t buf, int64_t sig) {
+    jla::car_free(reinterpret_cast<void*>(buf), reinterpret_cast<void*>(sig));
+  }, "free car_alloc's buffers (a failed rendezvous)");
   m.def("topk_chunk", &topk_chunk);
   m.def("topk_merge", &topk_merge, py::arg("cv"), py::arg("ci"), py::arg("k"), py::arg("mode"),
         py::arg("out_v") = py::none(), py::arg("out_i") = py::none(), py::arg("nxt") = py::none(),

@@ -19,9 +19,16 @@
 //   to a known compiler hazard (the vmcnt wait after buffer_wbl2 can be dropped).
 //
 // Block b of every rank handles chunks c == b (mod CAR_GRID) of every message, so block b only ever
-// pairs with block b of its peers; barriers count per block and flags are monotonic. The parity
-// buffers make one barrier per round enough: a parity slot is overwritten two calls later, and by then
-// the writer has passed a barrier that every peer reached after finishing its reads of that slot.
+// pairs with block b of its peers; barriers count per block and flags are monotonic. Every kernel maps
+// chunk c to the SAME bytes of a slot -- [c * CAR_CHUNK, (c + 1) * CAR_CHUNK) of A, and
+// [c * 2 * CAR_CHUNK, (c + 1) * 2 * CAR_CHUNK) of R whatever the element type -- so a block's slot bytes are
+// only ever touched by that block (and the same block of the peers), whichever kernel runs. The parity
+// buffers make one barrier per round enough: block b's parity slot is overwritten two of ITS calls
+// later, and by then the writer has passed a block-b barrier that every peer's block b reached after
+// finishing its reads of that slot. (Blocks past a message's chunk count skip the call entirely, so
+// block b's parity counts block b's calls only; with the byte mapping above that is all it needs.)
+// Failure: a wait that times out sets the error word; every later wait sees it and gives up at once (no
+// hang, results invalid), and the host refuses further calls once it has read the error.
 // Graph-capturable: all state (pointers, counters) lives in device memory.
 //
 // Kernels
@@ -46,7 +53,8 @@ constexpr int CAR_BLOCKS = 64;   // signal rows (one per block)
 constexpr int CAR_GRID = 63;     // chunk c -> block c % CAR_GRID on every call (fixed mapping)
 constexpr int CAR_THREADS = 256;
 constexpr int CAR_CHUNK = CAR_THREADS * 16;  // input bytes per block iteration
-constexpr int CAR_PAIR_CHUNK = CAR_THREADS;  // pairs per block iteration
+constexpr int CAR_PAIR_CHUNK = CAR_CHUNK / 8;  // pairs per block iteration: the same slot bytes as a reduce chunk
+constexpr int CAR_PAIRS_PER_THREAD = CAR_PAIR_CHUNK / CAR_THREADS;
 
 enum { OP_SUM = 0, OP_RESID = 1 };
 enum { PAIRS_ARGMAX = 0, PAIRS_TOPK = 1 };
@@ -106,6 +114,8 @@ JLA_DEV void car_barrier(const CarDevice& d, int b, int* s_word) {
     const int* f = d.sig[d.rank] + b * CAR_MAX_WORLD + threadIdx.x;
     const long long t0 = (long long)wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      // an earlier wait already gave up: the protocol state is out of step, do not wait again
+      if (__hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
       if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
         __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -239,7 +249,8 @@ __global__ void __launch_bounds__(CAR_THREADS)
     Piece<BF16> acc;
     acc.set(ld_sys16(mine, a_off + off));
     for (int p = 1; p < d.world; ++p) acc.add(ld_sys16(mine, a_off + (long long)p * slot + off));
-    const long long roff = r_off + (off / ESZ) * 4;  // fp32 result of element off / ESZ
+    // fp32 result of element off / ESZ, in chunk c's own 2 * CAR_CHUNK bytes of R
+    const long long roff = r_off + c * 2 * CAR_CHUNK + ((off - c * CAR_CHUNK) / ESZ) * 4;
 #pragma unroll
     for (int q = 0; q < N / 4; ++q) {
       const u32x4 v = {__float_as_uint(acc.v[4 * q]), __float_as_uint(acc.v[4 * q + 1]),
@@ -252,7 +263,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
   for (long long c = b; c < nchunks; c += CAR_GRID) {
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
-    const long long roff = r_off + (off / ESZ) * 4;
+    const long long roff = r_off + c * 2 * CAR_CHUNK + ((off - c * CAR_CHUNK) / ESZ) * 4;
     float s[N];
 #pragma unroll
     for (int q = 0; q < N / 4; ++q) {
@@ -279,14 +290,18 @@ __global__ void __launch_bounds__(CAR_THREADS)
   const long long a_off = (long long)parity * d.world * slot;
   const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
   for (long long c = blk; c < nchunks; c += CAR_GRID) {
-    const long long i = c * CAR_PAIR_CHUNK + threadIdx.x;
-    if (i >= n) continue;
-    const u32x2 v = {__float_as_uint(a[i]), (unsigned)(bi[i] + idx_offset)};
-    for (int p = 0; p < d.world; ++p) st_sys8(rsrc(d.buf[p]), a_off + (long long)d.rank * slot + i * 8, v);
+#pragma unroll
+    for (int t = 0; t < CAR_PAIRS_PER_THREAD; ++t) {
+      const long long i = c * CAR_PAIR_CHUNK + t * CAR_THREADS + threadIdx.x;
+      if (i >= n) continue;
+      const u32x2 v = {__float_as_uint(a[i]), (unsigned)(bi[i] + idx_offset)};
+      for (int p = 0; p < d.world; ++p) st_sys8(rsrc(d.buf[p]), a_off + (long long)d.rank * slot + i * 8, v);
+    }
   }
   car_barrier(d, blk, &s_word);
   for (long long c = blk; c < nchunks; c += CAR_GRID) {
-    const long long i = c * CAR_PAIR_CHUNK + threadIdx.x;
+   for (int t = 0; t < CAR_PAIRS_PER_THREAD; ++t) {
+    const long long i = c * CAR_PAIR_CHUNK + t * CAR_THREADS + threadIdx.x;
     if (i >= n) continue;
     if (MODE == PAIRS_ARGMAX) {
       u32x2 best = ld_sys8(mine, a_off + i * 8);
@@ -305,6 +320,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
         out_b[o] = (int32_t)v[1];
       }
     }
+   }
   }
 }
 
@@ -318,6 +334,8 @@ struct CarHost {
   int n_opened;
 };
 
+// A: 2 parities x world slots x max_bytes; R: 2 parities x 2 * max_bytes (max_bytes % CAR_CHUNK == 0, so chunk c's
+// 2 * CAR_CHUNK bytes of R fit for every chunk of a max_bytes message)
 size_t car_buffer_bytes(long long max_bytes, int world) {
   return (size_t)2 * world * max_bytes + (size_t)2 * 2 * max_bytes;
 }
@@ -325,18 +343,30 @@ size_t car_signal_bytes() { return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(i
 
 int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemHandle_t* hbuf,
               hipIpcMemHandle_t* hsig) {
-  if (world < 1 || world > CAR_MAX_WORLD || max_bytes <= 0 || (max_bytes & 15)) return -1;
+  if (world < 1 || world > CAR_MAX_WORLD || max_bytes <= 0 || (max_bytes % CAR_CHUNK)) return -1;
   if (car_buffer_bytes(max_bytes, world) >= 0x7fffffffull) return -3;  // buffer-resource offsets are 31-bit
+  *buf = *sig = nullptr;
   hipError_t e = hipExtMallocWithFlags(buf, car_buffer_bytes(max_bytes, world), hipDeviceMallocUncached);
-  if (e != hipSuccess) return (int)e;
-  e = hipExtMallocWithFlags(sig, car_signal_bytes(), hipDeviceMallocUncached);
-  if (e != hipSuccess) return (int)e;
-  e = hipMemset(*sig, 0, car_signal_bytes());
-  if (e != hipSuccess) return (int)e;
-  e = hipIpcGetMemHandle(hbuf, *buf);
-  if (e != hipSuccess) return (int)e;
-  e = hipIpcGetMemHandle(hsig, *sig);
+  if (e == hipSuccess) e = hipExtMallocWithFlags(sig, car_signal_bytes(), hipDeviceMallocUncached);
+  if (e == hipSuccess) e = hipMemset(*sig, 0, car_signal_bytes());
+  if (e == hipSuccess) e = hipIpcGetMemHandle(hbuf, *buf);
+  if (e == hipSuccess) e = hipIpcGetMemHandle(hsig, *sig);
+  if (e != hipSuccess) {
+    car_free(*buf, *sig);
+    *buf = *sig = nullptr;
+  }
   return (int)e;
+}
+
+// frees car_alloc's buffers (a rank whose car_init failed, or every rank after a failed rendezvous)
+void car_free(void* buf, void* sig) {
+  if (buf) (void)hipFree(buf);
+  if (sig) (void)hipFree(sig);
+}
+
+static void car_close_opened(CarHost* st) {
+  for (int i = 0; i < st->n_opened; ++i) (void)hipIpcCloseMemHandle(st->opened[i]);
+  st->n_opened = 0;
 }
 
 // handles[p] for p != rank are opened; own pointers are used for p == rank
@@ -364,11 +394,16 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
     void* pb = nullptr;
     void* ps = nullptr;
     hipError_t e = hipIpcOpenMemHandle(&pb, hbufs[p], hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return (int)e;
-    e = hipIpcOpenMemHandle(&ps, hsigs[p], hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return (int)e;
-    st->opened[st->n_opened++] = pb;
-    st->opened[st->n_opened++] = ps;
+    if (e == hipSuccess) {
+      st->opened[st->n_opened++] = pb;
+      e = hipIpcOpenMemHandle(&ps, hsigs[p], hipIpcMemLazyEnablePeerAccess);
+      if (e == hipSuccess) st->opened[st->n_opened++] = ps;
+    }
+    if (e != hipSuccess) {  // undo this rank's mappings; the caller still owns (and frees) its own buffers
+      car_close_opened(st);
+      delete st;
+      return (int)e;
+    }
     st->h.buf[p] = static_cast<char*>(pb);
     st->h.sig[p] = static_cast<int*>(ps);
   }
@@ -377,10 +412,15 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   st->h.barrier_count = tail;
   st->h.call_count = tail + CAR_BLOCKS;
   st->h.error = tail + 2 * CAR_BLOCKS;
+  st->d = nullptr;
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&st->d), sizeof(CarDevice));
-  if (e != hipSuccess) return (int)e;
-  e = hipMemcpy(st->d, &st->h, sizeof(CarDevice), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return (int)e;
+  if (e == hipSuccess) e = hipMemcpy(st->d, &st->h, sizeof(CarDevice), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    if (st->d) (void)hipFree(st->d);
+    car_close_opened(st);
+    delete st;
+    return (int)e;
+  }
   *state = st;
   return 0;
 }
@@ -448,7 +488,7 @@ int car_error(void* state) {
 void car_destroy(void* state) {
   CarHost* st = static_cast<CarHost*>(state);
   if (!st) return;
-  for (int i = 0; i < st->n_opened; ++i) (void)hipIpcCloseMemHandle(st->opened[i]);
+  car_close_opened(st);
   (void)hipFree(st->d);
   (void)hipFree(st->own_buf);
   (void)hipFree(st->own_sig);

@@ -439,17 +439,12 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   if (Dh != AP_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   constexpr int NW = 4;
-  if ((g_attn_prefill_impl >= 2 && g_attn_prefill_impl <= 4) && (rep % NW == 0 || NW % rep == 0)) {
+  if ((g_attn_prefill_impl == 2 || g_attn_prefill_impl == 4) && (rep % NW == 0 || NW % rep == 0)) {
     const int npb = rep >= NW ? 1 : NW / rep;    // position blocks per workgroup
     const int hpw = NW / npb;                    // q heads per workgroup
     const int hgroups = rep / hpw;
     const float sl2 = 1.4426950408889634f / sqrtf((float)Dh);
-    if (g_attn_prefill_impl == 3) {  // 64 queries per wave
-      const int n_qb = (S + 64 * npb - 1) / (64 * npb);
-      dim3 grid3((n_qb + 1) / 2, Hkv * hgroups, B);
-      attn_prefill_v2_kernel<NW, 2><<<grid3, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S,
-                                                              H, Hkv, T, sl2, npb, hgroups, n_qb, 0);
-    } else {
+    {
       const int n_qb = (S + 32 * npb - 1) / (32 * npb);
       const int pairs = (n_qb + 1) / 2 * Hkv * hgroups * B;
       // fewer pairs than two workgroups per CU (B = 1 prefill): each half of a pair is its own workgroup, so a CU

@@ -1414,10 +1414,7 @@ template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
                          int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile,
                          hipStream_t s) {
-  if (tile == 5 && MODE != MODE_PARTIAL && ksplit == 1 && (K & 63) == 0) {  // gemm4 (gemm4.hip)
-    gemm4_launch(MODE, x, w, out, M, N, K, accumulate, out_f32, mirror, kc, 1, rms_eps, ssq, s);
-    return;
-  }
+
   if (g_gemm_impl == 2) {
     launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s);
   } else {

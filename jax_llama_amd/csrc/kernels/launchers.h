@@ -13,6 +13,8 @@ int embedding(const int32_t* ids, const bf16_t* table, float* out, bf16_t* mirro
               hipStream_t s);
 int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
+int residual_add(float* h, const void* p, int p_bf16, bf16_t* hb, long long n, hipStream_t s);
+int gemm_f32(const float* x, const float* w, float* y, int M, int N, int K, hipStream_t s);
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
 
 // Epilogue arguments of the fused qkv projection (MODE_QKV): RoPE + KV-cache write.
@@ -30,31 +32,6 @@ struct QKVArgs {
                               // mirror, SWIGLU -> the activation (GEMV only; the next projection's packed-x input)
 };
 
-// decode chain (chain.hip): wo -> w1|w3 -> w2 [-> next wqkv] as one launch at M <= 16 (bf16 activations)
-struct ChainStage {
-  const bf16_t* x;     // [M, K] row-major activations
-  const void* W;       // fragment-packed weights
-  void* out;           // residual stages: h (fp32 [M, N]); SwiGLU: [M, N/2] bf16; QKV: unused
-  bf16_t* mirror;      // residual stages: bf16 mirror of h
-  int N, K, mode;
-  float eps;           // >= 0: fused RMSNorm of x
-  QKVArgs qa;          // stage 3 only
-  // filled by decode_chain():
-  int wg_begin, wg_count, dep, publish;
-  int expect[8];       // producer (stage dep) arrivals per shard blockIdx % 8
-};
-struct ChainArgs {
-  ChainStage st[4];
-  int nstages, M;
-  unsigned* counters;        // [4][8][32] cumulative per-shard arrivals of this layer's stages, one 128-B line per
-                             // (stage, shard) word (zeroed once)
-  const unsigned* epoch;     // forwards since the counters were zeroed (>= 1 when the chain runs)
-  unsigned* error;           // set to 1 when a hand-off wait times out
-  long long timeout_ticks;   // wall-clock ticks (s_memrealtime, 100 MHz)
-  unsigned long long* stamps; // diagnostic: per workgroup [start, waited, streamed, done] wall clock (nullptr = off)
-};
-int decode_chain(ChainArgs a, hipStream_t s);
-int chain_epoch_bump(unsigned* epoch, hipStream_t s);
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
 // split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
@@ -88,10 +65,6 @@ int gemm_fix_tiles(int M, int N);
 size_t gemm_hybrid_workspace_floats(int M, int N);
 void gemm_set_fixup(int on);  // A/B: 0 = partial slabs + reduce kernel even when tickets are given
 int gemm_fixup_enabled();
-// gemm4 (gemm4.hip): 256x256 tile on 4 waves of 128x128 (K multiple of 64, no K split); gemm() tile config 5
-int gemm4_launch(int mode, const bf16_t* x, const void* w, void* out, int M, int N, int K, int accumulate,
-                 int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, hipStream_t s);
-void gemm4_set_variant(int v);
 // greedy lm_head: GEMM + first-max argmax epilogue (ws >= gemm_argmax_workspace_floats(M, N) floats)
 int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
                 int32_t* idx, float* val, hipStream_t s);
@@ -123,7 +96,6 @@ unsigned jla_bounds_gemv(int reset);
 unsigned jla_bounds_skinny(int reset);
 unsigned jla_bounds_attn_decode(int reset);
 unsigned jla_bounds_attn_prefill(int reset);
-unsigned jla_bounds_chain(int reset);  // DIAGNOSTIC: 1 = the streaming kernel skips its math (wrong results)  // 2 = streaming (default), 1 = v1 (A/B)
 int attn_decode_splits(int B, int Hkv, int T, int rep);
 // ws: >= B*H*nsplit*(Dh+2) floats; tickets: B*Hkv int32, zero-initialised once (self-resetting)
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
@@ -144,6 +116,7 @@ int topk_merge(const float* cv, const int32_t* ci, int B, int C, int K, int mode
 // custom xGMI collectives over IPC-mapped uncached buffers (allreduce.hip)
 size_t car_buffer_bytes(long long max_bytes, int world);
 int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemHandle_t* hbuf, hipIpcMemHandle_t* hsig);
+void car_free(void* buf, void* sig);
 int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_sig, const hipIpcMemHandle_t* hbufs,
              const hipIpcMemHandle_t* hsigs, double timeout_s, void** state);
 // op 0: out = sum over ranks of in (bf16/fp32); op 1: h (fp32) += sum, hb (bf16) = h. two_shot: reduce-scatter +

@@ -119,6 +119,42 @@ int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps,
   return 0;
 }
 
+// h (fp32) += p (bf16 or fp32); hb = bf16(h) -- the residual epilogue of a row-parallel projection whose
+// partial sums came back from RCCL (tensor-parallel prefill-sized messages): one pass instead of add_ + copy_.
+template <bool BF16>
+__global__ void __launch_bounds__(256) residual_add_kernel(float* __restrict__ h, const void* __restrict__ p,
+                                                           bf16_t* __restrict__ hb, long long n8) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float a[8];
+    if constexpr (BF16) {
+      unpack8(reinterpret_cast<const u32x4*>(p)[i], a);
+    } else {
+      const float4 v0 = reinterpret_cast<const float4*>(p)[2 * i], v1 = reinterpret_cast<const float4*>(p)[2 * i + 1];
+      a[0] = v0.x; a[1] = v0.y; a[2] = v0.z; a[3] = v0.w; a[4] = v1.x; a[5] = v1.y; a[6] = v1.z; a[7] = v1.w;
+    }
+    float4* hv = reinterpret_cast<float4*>(h) + 2 * i;
+    float4 x0 = hv[0], x1 = hv[1];
+    x0.x += a[0]; x0.y += a[1]; x0.z += a[2]; x0.w += a[3];
+    x1.x += a[4]; x1.y += a[5]; x1.z += a[6]; x1.w += a[7];
+    hv[0] = x0;
+    hv[1] = x1;
+    const float r[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    reinterpret_cast<u32x4*>(hb)[i] = pack8(r);
+  }
+}
+
+int residual_add(float* h, const void* p, int p_bf16, bf16_t* hb, long long n, hipStream_t s) {
+  if (n % 8) return -1;
+  if (n == 0) return 0;
+  const long long n8 = n / 8;
+  const long long want = (n8 + 255) / 256;
+  const int grid = (int)(want < 4096 ? want : 4096);
+  if (p_bf16) residual_add_kernel<true><<<grid, 256, 0, s>>>(h, p, hb, n8);
+  else residual_add_kernel<false><<<grid, 256, 0, s>>>(h, p, hb, n8);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 JLA_BOUNDS_ACCESSOR(norm_embed)
 
 }  // namespace jla

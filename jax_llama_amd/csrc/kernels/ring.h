@@ -1,4 +1,4 @@
-// Register load ring helpers shared by the decode GEMV (gemv.hip) and the decode chain (chain.hip).
+// Register load ring helpers of the decode GEMV (gemv.hip).
 #pragma once
 #include "common.h"
 
@@ -37,7 +37,7 @@ JLA_DEV void asm_load16(u32x4& r, const void* p) {
     r = reinterpret_cast<const u32x4*>(p)[1];
 }
 // agent-coherent (sc1) load: bypasses the caches that can hold a stale copy of a line another
-// workgroup of the same launch wrote write-through (decode chain hand-offs, Guideline 16 R1)
+// workgroup of the same launch wrote write-through (in-launch hand-offs, Guideline 16 R1)
 JLA_DEV void asm_load_sc1(u32x4& r, const void* p) {
   asm volatile("global_load_dwordx4 %0, %1, off sc1" : "+v"(r) : "v"(p) : "memory");
 }

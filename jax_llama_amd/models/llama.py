@@ -327,13 +327,6 @@ class LLaMAForCausalLM:
                        self.head_dim, self.device)
 
     # ------------------------------------------------------------------ core forward
-    def chain_state(self) -> "ops.ChainState":
-        """Hand-off counters of the decode chain (ops.decode_chain), allocated on first use."""
-        st = getattr(self, "_chain_state", None)
-        if st is None:
-            st = self._chain_state = ops.ChainState(self.config.num_hidden_layers, self.device)
-        return st
-
     def _row_parallel(self, x: torch.Tensor, w: PackedLinear, h: torch.Tensor, hb: torch.Tensor,
                       x_packed: Optional[torch.Tensor] = None, mirror_packed: Optional[torch.Tensor] = None) -> None:
         """``h += x @ W^T`` where W is row-sharded. TP=1: the GEMM epilogue adds into the fp32 residual
@@ -369,7 +362,7 @@ class LLaMAForCausalLM:
             logits = None
         elif self.precision == "highest":  # fp32 lm_head weights + fp32 GEMM (reference model.py:698-736)
             hl = h if logits_mode == "all" else h.reshape(b, s, d)[:, -1].contiguous()
-            logits = self.final_norm(hl) @ self.lm_head_f32.t()
+            logits = ops.linear_f32(self.final_norm(hl), self.lm_head_f32)
             if logits_mode == "argmax":
                 logits = ops.argmax(logits.contiguous())
         elif logits_mode == "argmax":  # greedy: (idx, val) of this rank's vocab shard, argmax fused in the GEMM

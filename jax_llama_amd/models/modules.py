@@ -112,41 +112,9 @@ class LLaMABlockCollection:
     def __len__(self):
         return len(self.blocks)
 
-    def _chain_ok(self, hb, collect: bool) -> bool:
-        m = self.model
-        return (ops.DECODE_CHAIN and not collect and hb.is_cuda and hb.shape[0] <= ops.CHAIN_MAX_M
-                and m.comm.size == 1 and len(self.blocks) > 0)
-
-    def _chained(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int):
-        """M <= 16, TP = 1: per layer two launches -- attention, then the decode chain (wo, w1|w3, w2 and the
-        next layer's qkv + RoPE + KV write in one kernel, csrc/kernels/chain.hip) -- instead of five."""
-        m = self.model
-        st = m.chain_state()
-        ops.chain_epoch_bump(st)
-        rows = hb.shape[0]
-        b = rows // seq_len
-        act = torch.empty(rows, m.layers[0].gu.n // 2, dtype=hb.dtype, device=hb.device)
-        kc, vc = cache.layer(0)
-        q = ops.linear_qkv_rope(hb, m.layers[0].qkv, m.eps, m.rope, positions, kc, vc, slot0, seq_len,
-                                m.n_heads, m.n_kv_heads, m.head_dim)
-        n_layers = len(self.blocks)
-        for i in range(n_layers):
-            lw = m.layers[i]
-            kc, vc = cache.layer(i)
-            a = ops.attention(q.reshape(b, seq_len, m.n_heads, m.head_dim), kc, vc, slot0, kv_start, key_mask)
-            nxt = None
-            if i + 1 < n_layers:
-                kn, vn = cache.layer(i + 1)
-                nxt = (m.layers[i + 1].qkv, m.rope, positions, kn, vn, slot0, seq_len, m.n_heads, m.n_kv_heads,
-                       m.head_dim)
-            q = ops.decode_chain(a, lw.o, lw.gu, lw.down, h, hb, act, m.eps, st, i, nxt)
-
     def __call__(self, h, hb, positions, cache, slot0, kv_start, key_mask, seq_len: int,
                  output_hidden_states: bool = False, output_attentions: bool = False):
         hidden, attns = [], []
-        if self._chain_ok(hb, output_hidden_states or output_attentions):
-            self._chained(h, hb, positions, cache, slot0, kv_start, key_mask, seq_len)
-            return hidden, attns
         b = hb.shape[0] // seq_len
         rows = hb.shape[0]
         pk = None

@@ -95,6 +95,33 @@ def rms_scale(x: torch.Tensor, eps: float) -> torch.Tensor:
     return out
 
 
+def residual_add_(h: torch.Tensor, p: torch.Tensor, mirror: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``h (fp32) += p`` (bf16 or fp32, same shape) and ``mirror = bf16(h)`` in one pass (GPU: one kernel)."""
+    if not _is_gpu(h):
+        h.add_(p.float().view_as(h))
+        if mirror is not None:
+            mirror.copy_(h.to(BF16))
+        return h
+    assert h.is_contiguous() and h.dtype == torch.float32
+    if mirror is None or h.numel() % 8:
+        h.add_(p.view_as(h))
+        if mirror is not None:
+            mirror.copy_(h)
+        return h
+    ext().residual_add(h, p.contiguous(), mirror)
+    return h
+
+
+def linear_f32(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``x [M, K] @ w [N, K]^T`` with fp32 inputs, accumulation and output (precision='highest' lm_head; GPU: the
+    exact-f32 MFMA kernel, csrc/kernels/gemm_f32.hip)."""
+    if not _is_gpu(x):
+        return x.float() @ w.float().t()
+    y = torch.empty(x.shape[0], w.shape[0], dtype=torch.float32, device=x.device)
+    ext().gemm_f32(x.float().contiguous(), w.float().contiguous(), y)
+    return y
+
+
 def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
     """Stand-alone RMSNorm (fp32 out); the model folds norm weights into GEMMs instead."""
     if not _is_gpu(x):
@@ -444,60 +471,6 @@ def _slot_tensor(slot0, device):
     # Host int -> small device tensor (not graph-capturable; the engine passes tensors).
     t = torch.tensor([int(slot0)], dtype=torch.int32, device=device)
     return t
-
-
-# ----------------------------------------------------------------------------------
-# Decode chain (csrc/kernels/chain.hip): wo -> w1|w3 -> w2 [-> next layer's wqkv] as one launch at M <= 16.
-# Opt-in (JLA_DECODE_CHAIN=1): correct and bit-identical, but measured SLOWER than the four launches it replaces on
-# MI355X (M = 1: 119 vs 84 us per layer; each in-launch hand-off waits 2-4 us for its producers' arrivals, more than
-# the launch boundary it removes, and the stages stream 15-30 % slower beside spinning consumers:
-# profiles/r2_decode_chain_timeline.jsonl).
-DECODE_CHAIN = os.environ.get("JLA_DECODE_CHAIN", "0") == "1"
-CHAIN_MAX_M = 16
-CHAIN_TIMEOUT_S = 1.0
-
-
-class ChainState:
-    """Per-model hand-off state of the decode chain: cumulative per-(layer, stage, XCD shard) arrival
-    counters, the forward counter (epoch) they are checked against, and the timeout error word. Zeroed
-    once at allocation (outside any graph capture); the counters stay consistent as long as every chained
-    forward bumps the epoch once and runs each layer's chain once."""
-
-    def __init__(self, n_layers: int, device):
-        self.counters = torch.zeros(n_layers, 4, 8, 32, dtype=torch.int32, device=device)  # a 128-B line per word
-        self.epoch = torch.zeros(4, dtype=torch.int32, device=device)
-        self.error = torch.zeros(4, dtype=torch.int32, device=device)
-
-    def check(self) -> None:
-        if int(self.error[0].item()) != 0:
-            raise RuntimeError("decode chain: a hand-off wait timed out (results of that step are invalid)")
-
-
-def chain_epoch_bump(state: ChainState) -> None:
-    ext().chain_epoch_bump(state.epoch)
-
-
-def decode_chain(a: torch.Tensor, w_o, w_gu, w_down, h: torch.Tensor, hb: torch.Tensor, act: torch.Tensor,
-                 rms_eps: float, state: ChainState, layer: int, qkv=None, stamps=None) -> Optional[torch.Tensor]:
-    """``h += a @ Wo^T`` (hb = bf16(h)); ``act = silu(g) * u`` of ``norm(hb) @ Wgu^T``; ``h += act @ Wd^T``
-    (hb = bf16(h)); and, with ``qkv = (w_qkv, table, positions, k_cache, v_cache, slot0, seq_len, H, Hkv, Dh)``
-    for the NEXT layer, its fused qkv + RoPE + KV-cache write -- one launch. Returns that layer's rotated q
-    ``[M, H, Dh]`` (or None)."""
-    e = ext()
-    m = a.shape[0]
-    q = None
-    if qkv is None:
-        e.decode_chain(a, w_o.weight, w_gu.weight, w_down.weight, h, hb, act, float(rms_eps), None, None, None, None,
-                       None, None, 1, 0, 0, 0, None, state.counters[layer], state.epoch, state.error, CHAIN_TIMEOUT_S,
-                       stamps)
-        return None
-    w_qkv, table, positions, kc, vc, slot0, seq_len, nh, nkv, dh = qkv
-    q = torch.empty(m, nh, dh, dtype=BF16, device=a.device)
-    e.decode_chain(a, w_o.weight, w_gu.weight, w_down.weight, h, hb, act, float(rms_eps), w_qkv.weight, table,
-                   positions.reshape(-1).to(torch.int32), kc, vc, _slot_tensor(slot0, a.device), int(seq_len),
-                   int(nh), int(nkv), int(dh), q, state.counters[layer], state.epoch, state.error, CHAIN_TIMEOUT_S,
-                   stamps)
-    return q
 
 
 # ----------------------------------------------------------------------------------

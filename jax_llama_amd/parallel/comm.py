@@ -40,7 +40,7 @@ class TPComm:
 
     @classmethod
     def from_context(cls, ctx, use_custom: bool = True, max_bytes: int = 16 << 20,
-                     reduce_dtype: Optional[torch.dtype] = None) -> "TPComm":
+                     reduce_dtype: Optional[torch.dtype] = None, timeout_s: float = 10.0) -> "TPComm":
         custom = None
         if ctx.tp_size > 1 and ctx.device.type == "cuda" and use_custom:
             try:
@@ -50,7 +50,7 @@ class TPComm:
             if CustomAllReduce is not None:
                 from .custom_allreduce import CustomAllReduceError
                 try:
-                    custom = CustomAllReduce.create(ctx, max_bytes=max_bytes)
+                    custom = CustomAllReduce.create(ctx, max_bytes=max_bytes, timeout_s=timeout_s)
                 except CustomAllReduceError as ex:  # same verdict on every rank: all fall back to RCCL
                     import logging
                     logging.getLogger(__name__).warning("custom all-reduce disabled: %s", ex)
@@ -87,11 +87,19 @@ class TPComm:
             return h
         if hb_pack is not None:
             raise RuntimeError("all_reduce_residual_: the packed hb copy needs the custom all-reduce path")
-        p = partial.float() if partial.dtype != torch.float32 else partial.clone()
-        self.all_reduce_(p)
-        h.add_(p.view_as(h))
-        if hb is not None:
-            hb.copy_(h)
+        # prefill-sized messages: the partials go over RCCL in reduce_dtype as they are (bf16 by default: half the
+        # bytes of fp32), then ONE kernel adds the sum into h and rewrites the mirror (ops.residual_add_)
+        if self.size > 1:
+            p = partial if partial.is_contiguous() else partial.contiguous()
+            if p.dtype == torch.bfloat16 and (not p.is_cuda or self._host_staged(p)):
+                p = p.float()  # gloo: sum in fp32
+            elif p.data_ptr() == partial.data_ptr():
+                p = p.clone()  # never reduce the caller's buffer in place
+            self.all_reduce_(p)
+        else:
+            p = partial
+        from .. import ops
+        ops.residual_add_(h, p.view_as(h), hb)
         return h
 
     def packs_residual(self, nbytes: int) -> bool:
@@ -145,3 +153,48 @@ class TPComm:
 
 
 NO_COMM = TPComm()
+
+
+class TPRankProxyComm(TPComm):
+    """One rank of a ``size``-way tensor-parallel group, alone on one GPU (``bench.py`` ``tp_rank_proxy``).
+
+    The model built on it holds exactly rank 0's shards (column / row / vocab slices at the real per-rank shapes)
+    and issues exactly the launches a TP rank issues: every per-token collective runs the same custom kernel
+    (``csrc/kernels/allreduce.hip``) on a world-1 instance -- same push / flag barrier / rank-order sum / fused
+    residual + mirror epilogue -- so the step's launch structure and the kernels' local cost are the real ones.
+    What it leaves out is the xGMI link: peer writes and peer flags land in local memory. Larger messages (prefill)
+    are the identity sum (the RCCL call is skipped). Not a correctness path: the numbers are one shard's."""
+
+    def __init__(self, size: int, custom=None, reduce_dtype: Optional[torch.dtype] = None):
+        super().__init__(size=size, rank=0, group=None, custom=custom, reduce_dtype=reduce_dtype)
+
+    @classmethod
+    def create(cls, size: int, max_bytes: int = 16 << 20) -> "TPRankProxyComm":
+        from .custom_allreduce import CustomAllReduce
+        return cls(size, CustomAllReduce.local(max_bytes=max_bytes))
+
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        return False
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.custom is not None and self.custom.can_handle(t):
+            self.custom.all_reduce_(t)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return t.unsqueeze(0).expand((self.size,) + tuple(t.shape)).contiguous()
+
+    def argmax(self, val: torch.Tensor, idx: torch.Tensor, v_local: int) -> torch.Tensor:
+        if self.custom is not None and val.is_cuda and self.custom.can_handle_pairs(val.numel()):
+            return self.custom.argmax_pairs(val.float(), idx.to(torch.int32), 0)
+        return idx.to(torch.int32)
+
+    def gather_topk(self, vals: torch.Tensor, idx: torch.Tensor):
+        if self.custom is not None and vals.is_cuda and self.custom.can_handle_pairs(vals.numel()):
+            return self.custom.topk_pairs(vals, idx, 0)
+        return vals, idx
+
+    def close(self):
+        if self.custom is not None:
+            self.custom.close()
+            self.custom = None

@@ -18,7 +18,8 @@ per link. Both sum in rank order in fp32, so they are bit-identical to each othe
 
 Rendezvous: each rank allocates its buffers, the IPC handles are exchanged with
 ``all_gather_object`` on the TP group, then every rank maps its peers'. A peer that never arrives
-makes the kernel give up after ``timeout_s`` and set an error word; ``check()`` raises on it.
+makes the kernel give up after ``timeout_s`` and set an error word (every later wait then gives up at
+once, so nothing hangs); ``check()`` raises on it and the object refuses every later call.
 """
 from __future__ import annotations
 
@@ -33,6 +34,7 @@ from ..ops import ext
 # world-1 links (bytes per link); two-shot moves 3 x bytes / world per link (bf16 partial scatter + fp32 sum
 # gather) at the price of a second barrier.
 TWO_SHOT_MIN_BYTES = int(os.environ.get("JLA_CAR_TWO_SHOT_BYTES", str(512 << 10)))
+CHUNK_BYTES = 4096  # allreduce.hip CAR_CHUNK: buffers hold whole chunks
 
 
 class CustomAllReduceError(RuntimeError):
@@ -47,6 +49,14 @@ class CustomAllReduce:
         self.rank = rank
         self.world = world
         self.max_bytes = max_bytes
+        self.failed = False  # set once a timeout was seen: the per-block counters are out of step for good
+
+    def _live(self) -> int:
+        if self.failed:
+            raise CustomAllReduceError("custom all-reduce timed out earlier; re-create it (every rank) before reuse")
+        if not self.state:
+            raise CustomAllReduceError("custom all-reduce is closed")
+        return self.state
 
     @classmethod
     def create(cls, ctx, max_bytes: int = 16 << 20, group=None, timeout_s: float = 10.0) -> "CustomAllReduce":
@@ -58,22 +68,34 @@ class CustomAllReduce:
                    timeout_s: float = 10.0) -> "CustomAllReduce":
         if world > 8:
             raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI hop)")
-        max_bytes = (max_bytes + 15) // 16 * 16
+        max_bytes = (max_bytes + CHUNK_BYTES - 1) // CHUNK_BYTES * CHUNK_BYTES  # whole kernel chunks
         e = ext()
-        buf, sig, hbuf, hsig = e.car_alloc(max_bytes, world)
-        handles = [None] * world
-        dist.all_gather_object(handles, (bytes(hbuf), bytes(hsig)), group=group)
-        err = None
+        buf = sig = 0
+        state, err = 0, None
         try:
-            state = e.car_init(rank, world, max_bytes, buf, sig, [h[0] for h in handles], [h[1] for h in handles],
-                               float(timeout_s))
-        except RuntimeError as ex:  # e.g. the IPC import failed on this rank
-            state, err = 0, str(ex)
+            buf, sig, hbuf, hsig = e.car_alloc(max_bytes, world)
+            mine = (bytes(hbuf), bytes(hsig))
+        except RuntimeError as ex:  # allocation / IPC export failed here: still join the rendezvous
+            mine, err = None, f"car_alloc: {ex}"
+        handles = [None] * world
+        dist.all_gather_object(handles, mine, group=group)
+        if err is None and all(h is not None for h in handles):
+            try:
+                state = e.car_init(rank, world, max_bytes, buf, sig, [h[0] for h in handles], [h[1] for h in handles],
+                                   float(timeout_s))
+            except RuntimeError as ex:  # e.g. the IPC import failed on this rank
+                state, err = 0, str(ex)
+        elif err is None:
+            err = "a peer failed to allocate its buffers"
         # every rank learns whether every rank mapped its peers: one rank failing must not leave the
-        # others spinning in a collective it will never join
+        # others spinning in a collective it will never join -- and none may keep its mappings or buffers
         oks = [None] * world
         dist.all_gather_object(oks, err is None, group=group)
         if not all(oks):
+            if state:
+                e.car_destroy(state)  # unmaps the peers and frees this rank's buffers
+            else:
+                e.car_free(buf, sig)
             raise CustomAllReduceError(f"custom all-reduce setup failed on ranks "
                                        f"{[r for r, ok in enumerate(oks) if not ok]}: {err}")
         car = cls(state, rank, world, max_bytes)
@@ -84,6 +106,20 @@ class CustomAllReduce:
             car.close()
             raise CustomAllReduceError("custom all-reduce self-test failed (wrong sums or a timeout)")
         return car
+
+    @classmethod
+    def local(cls, max_bytes: int = 16 << 20, timeout_s: float = 10.0) -> "CustomAllReduce":
+        """A world-1 instance (no rendezvous): the same kernels, launch structure and hand-off protocol with this
+        rank as its only peer -- the collective of the one-GPU tensor-parallel rank proxy (``TPRankProxyComm``)."""
+        max_bytes = (max_bytes + CHUNK_BYTES - 1) // CHUNK_BYTES * CHUNK_BYTES
+        e = ext()
+        buf, sig, hbuf, hsig = e.car_alloc(max_bytes, 1)
+        try:
+            state = e.car_init(0, 1, max_bytes, buf, sig, [bytes(hbuf)], [bytes(hsig)], float(timeout_s))
+        except RuntimeError:
+            e.car_free(buf, sig)
+            raise
+        return cls(state, 0, 1, max_bytes)
 
     def self_test(self) -> bool:
         """One-shot and two-shot sums of rank-dependent data (bit-exact integers in fp32)."""
@@ -111,13 +147,13 @@ class CustomAllReduce:
     # ------------------------------------------------------------------ collectives
     def all_reduce_(self, t: torch.Tensor, two_shot=None) -> torch.Tensor:
         ts = self.use_two_shot(t.numel() * t.element_size()) if two_shot is None else bool(two_shot)
-        ext().car_allreduce(self.state, t, t, ts)
+        ext().car_allreduce(self._live(), t, t, ts)
         return t
 
     def all_reduce(self, t: torch.Tensor, two_shot=None) -> torch.Tensor:
         out = torch.empty_like(t)
         ts = self.use_two_shot(t.numel() * t.element_size()) if two_shot is None else bool(two_shot)
-        ext().car_allreduce(self.state, t, out, ts)
+        ext().car_allreduce(self._live(), t, out, ts)
         return out
 
     def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: torch.Tensor, two_shot=None,
@@ -125,12 +161,12 @@ class CustomAllReduce:
         """``h += sum_ranks(partial)``; ``hb = bf16(h)`` (one kernel); ``hb_pack``: also a packed-layout copy of hb
         (``ops.packed_rows`` x D, the next projection's packed-x input)."""
         ts = self.use_two_shot(partial.numel() * partial.element_size()) if two_shot is None else bool(two_shot)
-        ext().car_allreduce_residual(self.state, partial, h, hb, ts, hb_pack)
+        ext().car_allreduce_residual(self._live(), partial, h, hb, ts, hb_pack)
 
     def argmax_pairs(self, val: torch.Tensor, idx: torch.Tensor, idx_offset: int, out_val=None) -> torch.Tensor:
         """First max over ranks of each row's local ``(val, idx + idx_offset)``: int32 ``[B]``."""
         out = torch.empty(idx.numel(), dtype=torch.int32, device=idx.device)
-        ext().car_pairs(self.state, 0, val.contiguous(), idx.contiguous(), int(idx_offset), 1, out_val, out)
+        ext().car_pairs(self._live(), 0, val.contiguous(), idx.contiguous(), int(idx_offset), 1, out_val, out)
         return out
 
     def topk_pairs(self, vals: torch.Tensor, idx: torch.Tensor, idx_offset: int):
@@ -138,7 +174,7 @@ class CustomAllReduce:
         b, k = vals.shape
         ov = torch.empty(b, self.world * k, dtype=torch.float32, device=vals.device)
         oi = torch.empty(b, self.world * k, dtype=torch.int32, device=vals.device)
-        ext().car_pairs(self.state, 1, vals.contiguous(), idx.contiguous(), int(idx_offset), int(k), ov, oi)
+        ext().car_pairs(self._live(), 1, vals.contiguous(), idx.contiguous(), int(idx_offset), int(k), ov, oi)
         return ov, oi
 
     # ------------------------------------------------------------------ failure detection
@@ -147,7 +183,11 @@ class CustomAllReduce:
         return int(ext().car_error(self.state))
 
     def check(self):
-        if self.state and self.error():
+        """Raise if a kernel gave up waiting (the host's periodic poll). From then on every call raises too:
+        the per-block call / barrier counters are out of step with the peers', so the object must be
+        re-created on every rank."""
+        if self.failed or (self.state and self.error()):
+            self.failed = True
             raise CustomAllReduceError(
                 "custom all-reduce: a peer did not arrive within the timeout; results since then are invalid")
 

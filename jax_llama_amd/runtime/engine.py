@@ -255,13 +255,26 @@ class DecodeEngine:
 
     def run(self, input_ids, attention_mask, gc: GenerationConfig) -> torch.Tensor:
         self.gc = gc
+        rng_saved = None
         if gc.do_sample:
             self._gen = torch.Generator(device=self.device)
             self._gen.manual_seed(int(gc.seed))
             if self.use_graph:
-                # graph-safe RNG: default generator (philox offsets advance per replay)
+                # The on-device sampler (ops.topk_sample, top_k <= 64) draws from its own Philox stream keyed by
+                # (seed, step) and touches no torch RNG. The torch fallback (top_k = 0 or > 64) under graph capture
+                # needs the device's default generator (graph-safe philox offsets): seed it for this call and give
+                # the caller's RNG state back afterwards.
                 self._gen = None
-                torch.manual_seed(int(gc.seed))
+                if self.device.type == "cuda":
+                    rng_saved = torch.cuda.get_rng_state(self.device)
+                    torch.cuda.manual_seed(int(gc.seed))
+        try:
+            return self._run(input_ids, attention_mask)
+        finally:
+            if rng_saved is not None:
+                torch.cuda.set_rng_state(rng_saved, self.device)
+
+    def _run(self, input_ids, attention_mask) -> torch.Tensor:
         cur = self.prefill(input_ids, attention_mask)
         steps_left = self.max_length - cur
         done = steps_left <= 0

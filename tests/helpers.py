@@ -48,3 +48,44 @@ def left_padded_batch(lengths, s, vocab, pad, seed=0):
         toks[i, s - n:] = torch.randint(3, vocab, (n,), generator=g, dtype=torch.int32)
         mask[i, s - n:] = 1
     return toks, mask
+
+
+def gpu_meta_state_dict(cfg: LLaMAConfig, seed: int, emb_std: float = 1.0, std: float = 0.02,
+                        device: str = "cuda") -> dict:
+    """Random Meta-layout state dict generated on the GPU (fast at real model dims), bf16 values. Norm weights
+    1 + 0.1 noise so the folded norms are exercised."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    d, hd, f, v = cfg.hidden_size, cfg.head_dim, cfg.intermediate_size, cfg.vocab_size
+    hq, hkv = cfg.num_attention_heads * hd, cfg.num_key_value_heads * hd
+
+    def rnd(*shape, s=std):
+        return (torch.randn(*shape, generator=g, device=device) * s).to(torch.bfloat16)
+
+    def norm():
+        return (1.0 + 0.1 * torch.randn(d, generator=g, device=device)).to(torch.bfloat16)
+
+    sd = {"tok_embeddings.weight": rnd(v, d, s=emb_std), "norm.weight": norm(), "output.weight": rnd(v, d)}
+    for i in range(cfg.num_hidden_layers):
+        p = f"layers.{i}."
+        sd[p + "attention.wq.weight"] = rnd(hq, d)
+        sd[p + "attention.wk.weight"] = rnd(hkv, d)
+        sd[p + "attention.wv.weight"] = rnd(hkv, d)
+        sd[p + "attention.wo.weight"] = rnd(d, hq)
+        sd[p + "feed_forward.w1.weight"] = rnd(f, d)
+        sd[p + "feed_forward.w2.weight"] = rnd(d, f, s=std / 2)
+        sd[p + "feed_forward.w3.weight"] = rnd(f, d)
+        sd[p + "attention_norm.weight"] = norm()
+        sd[p + "ffn_norm.weight"] = norm()
+    return sd
+
+
+def argmax_gap(oracle, seq: torch.Tensor, mask: torch.Tensor, start: int) -> float:
+    """Teacher-forced oracle logits over ``seq``: for every token from ``start`` on, (max logit - its logit) relative
+    to the row's logit scale. 0 wherever the token is the oracle's argmax; a near-tie broken the other way costs at
+    most the rounding error of the logits."""
+    full_mask = torch.cat([mask, torch.ones(mask.shape[0], seq.shape[1] - mask.shape[1], dtype=mask.dtype)], 1)
+    full_pos = full_mask.cumsum(-1) - 1
+    lf = oracle.forward(seq, full_mask, full_pos).float()
+    prev = lf[:, start - 1:-1]
+    chosen = prev.gather(-1, seq[:, start:].long().to(prev.device).unsqueeze(-1)).squeeze(-1)
+    return float(((prev.max(-1).values - chosen) / prev.abs().amax(-1)).max())

@@ -44,14 +44,18 @@ class OracleLLaMA:
                 position_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Full-sequence forward (no cache). Returns fp32 logits (B, S, V)."""
         sd = self.sd
+        dev = sd["tok_embeddings.weight"].device  # runs where its weights are (CPU, or fp32 on the GPU)
         b, s = tokens.shape
         if attention_mask is None:
             attention_mask = torch.ones(b, s, dtype=torch.int64)
         if position_ids is None:
             position_ids = torch.arange(s).expand(b, s)
+        tokens, attention_mask, position_ids = tokens.to(dev), attention_mask.to(dev), position_ids.to(dev)
+        if self.freqs.device != dev:
+            self.freqs = self.freqs.to(dev)
         h = sd["tok_embeddings.weight"][tokens.long()]
         fc = self.freqs[position_ids.long().clamp(min=0)]
-        causal = torch.tril(torch.ones(s, s, dtype=torch.bool))
+        causal = torch.tril(torch.ones(s, s, dtype=torch.bool, device=dev))
         mask = causal[None, None] & attention_mask.bool()[:, None, None, :]
         bias = torch.where(mask, 0.0, torch.finfo(torch.float32).min)
         rep = self.H // self.Hkv

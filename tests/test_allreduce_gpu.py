@@ -89,6 +89,29 @@ def _run(rank, world, q):
         ov, oi = car.topk_pairs(tv[rank].cuda(), ti[rank].cuda(), 0)
         assert torch.equal(ov.cpu(), tv.permute(1, 0, 2).reshape(b, world * k))
         assert torch.equal(oi.cpu(), ti.permute(1, 0, 2).reshape(b, world * k))
+    # the decode step's mix on ONE object: a one-chunk argmax (only block 0 runs), multi-chunk residual reduces, then a
+    # top-k gather with B*k > 512 pairs (several pair chunks): every kernel maps chunk c to the same slot bytes, so
+    # block b's parity stays consistent whichever kernels skipped it (the pairs chunks used to straddle
+    # the reduce chunks' bytes)
+    for it in range(6):
+        g = torch.Generator().manual_seed(40 + it)
+        vals = torch.randn(world, 3, generator=g)
+        idx = torch.randint(0, 1000, (world, 3), generator=g, dtype=torch.int32)
+        out = car.argmax_pairs(vals[rank].cuda(), idx[rank].cuda(), idx_offset=0).cpu()
+        assert torch.equal(out, idx.gather(0, vals.argmax(0)[None])[0]), ("mix argmax", it)
+        n = 3 * 4096 * 4 + 8
+        for rep in range(2):
+            x = _inputs(rank, n, torch.bfloat16, 60 + it + rep).cuda()
+            h0 = _inputs(79, n, torch.float32, it)
+            h, hb = h0.cuda(), torch.empty(n, dtype=torch.bfloat16, device="cuda")
+            car.all_reduce_residual_(x, h, hb, two_shot=bool(rep))
+            assert torch.equal(h.cpu(), h0 + _exact_sum(n, torch.bfloat16, 60 + it + rep, world)), ("mix resid", it)
+        b, k = 64, 50
+        tv = torch.randn(world, b, k, generator=g)
+        ti = torch.randint(0, 1 << 20, (world, b, k), generator=g, dtype=torch.int32)
+        ov, oi = car.topk_pairs(tv[rank].cuda(), ti[rank].cuda(), 0)
+        assert torch.equal(ov.cpu(), tv.permute(1, 0, 2).reshape(b, world * k)), ("mix topk", it)
+        assert torch.equal(oi.cpu(), ti.permute(1, 0, 2).reshape(b, world * k)), ("mix topk idx", it)
     # hipGraph capture + replay (fused residual, both variants)
     n = 4096 * 4
     x = _inputs(rank, n, torch.bfloat16, 99).cuda()

@@ -1,0 +1,218 @@
+"""Failure detection of the custom xGMI collectives (bounded spins -> error; reference has none).
+
+World-2 process groups on the test box's one GPU (IPC mapping between processes works the same on one device as
+across xGMI peers). Three behaviours:
+  * a peer that skips a collective: the waiting rank's kernel returns after ``timeout_s`` (no hang), the error word
+    is 1, ``check()`` raises ``CustomAllReduceError``, later kernels give up at once, and the object refuses every
+    later call until it is re-created;
+  * the same inside ``DecodeEngine.run`` (prefill + hipGraph-replayed decode): the engine's periodic poll raises;
+  * a setup failure on ONE rank (its IPC import raises) moves EVERY rank to the RCCL/gloo fallback, and no rank
+    keeps its buffers."""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import socket
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TIMEOUT_S = 0.5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _missing_peer(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from jax_llama_amd.ops import ext
+        from jax_llama_amd.parallel.custom_allreduce import CustomAllReduce, CustomAllReduceError
+        car = CustomAllReduce.create_for(rank, world, None, max_bytes=1 << 20, timeout_s=TIMEOUT_S)
+        n = 4 * 4096
+        x = torch.full((n,), float(rank + 1), dtype=torch.bfloat16, device="cuda")
+        h = torch.zeros(n, dtype=torch.float32, device="cuda")
+        hb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        res = {}
+        car.all_reduce_residual_(x, h, hb)  # both ranks: a good round
+        torch.cuda.synchronize()
+        res["first_ok"] = bool((h == 3.0).all()) and car.error() == 0
+        dist.barrier()
+        if rank == 0:  # rank 1 skips this one
+            t0 = time.perf_counter()
+            car.all_reduce_residual_(x, h, hb)
+            torch.cuda.synchronize()
+            res["timeout_wait_s"] = time.perf_counter() - t0
+            res["error_word"] = car.error()
+            # a later kernel on the same state gives up at once instead of waiting another timeout
+            t0 = time.perf_counter()
+            ext().car_allreduce(car.state, x, torch.empty_like(x), False)
+            torch.cuda.synchronize()
+            res["after_error_wait_s"] = time.perf_counter() - t0
+            try:
+                car.check()
+                res["check_raised"] = False
+            except CustomAllReduceError:
+                res["check_raised"] = True
+            try:
+                car.all_reduce_residual_(x, h, hb)
+                res["refuses_after"] = False
+            except CustomAllReduceError:
+                res["refuses_after"] = True
+        dist.barrier()  # rank 0's kernels are done before rank 1 unmaps its buffers
+        car.close()
+        dist.destroy_process_group()
+        q.put(("ok", rank, res))
+    except Exception:  # pragma: no cover - surfaced in the parent
+        import traceback
+        q.put(("err", rank, traceback.format_exc()))
+
+
+def _engine_missing_peer(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from helpers import gpu_config
+        from jax_llama_amd.models import LLaMAForCausalLM
+        from jax_llama_amd.parallel import TPComm, init_distributed
+        from jax_llama_amd.parallel.custom_allreduce import CustomAllReduceError
+        from jax_llama_amd.runtime.engine import DecodeEngine, GenerationConfig
+        ctx = init_distributed(backend="gloo", device_type="cuda")  # joins the group _init created
+        ctx.setup_mesh(tp=world)
+        comm = TPComm.from_context(ctx, timeout_s=TIMEOUT_S)
+        assert comm.custom is not None
+        cfg = gpu_config(num_attention_heads=4, num_key_value_heads=2, hidden_size=512, intermediate_size=1024)
+        model = LLaMAForCausalLM(cfg, device="cuda", comm=comm, _do_init=False).init_random(seed=3)
+        res = {}
+        dist.barrier()
+        if rank == 0:  # rank 1 never runs the step: every collective of rank 0 misses its peer
+            toks = torch.randint(3, cfg.vocab_size, (2, 8), dtype=torch.int32)
+            gc = GenerationConfig(max_length=8 + 40, do_sample=False, pad_token_id=0, eos_token_id=-1)
+            eng = DecodeEngine(model, 2, gc.max_length, use_graph=True)
+            t0 = time.perf_counter()
+            try:
+                eng.run(toks, None, gc)
+                res["raised"] = False
+            except CustomAllReduceError:
+                res["raised"] = True
+            torch.cuda.synchronize()
+            res["elapsed_s"] = time.perf_counter() - t0
+            del eng
+        dist.barrier()
+        comm.custom.close()
+        dist.destroy_process_group()
+        q.put(("ok", rank, res))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", rank, traceback.format_exc()))
+
+
+def _setup_failure(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from jax_llama_amd.ops import ext
+        from jax_llama_amd.parallel import TPComm, init_distributed
+        ctx = init_distributed(backend="gloo", device_type="cuda")  # joins the group _init created
+        ctx.setup_mesh(tp=world)
+        e = ext()
+        calls = {"destroy": 0, "free": 0}
+        real_destroy, real_free = e.car_destroy, e.car_free
+
+        def destroy(st):
+            calls["destroy"] += 1
+            real_destroy(st)
+
+        def free(b, s):
+            calls["free"] += 1
+            real_free(b, s)
+
+        e.car_destroy, e.car_free = destroy, free
+        if rank == 1:
+            def broken_init(*a, **k):
+                raise RuntimeError("injected IPC import failure")
+            e.car_init = broken_init
+        torch.cuda.synchronize()
+        dist.barrier()
+        free0 = torch.cuda.mem_get_info()[0]
+        dist.barrier()
+        comm = TPComm.from_context(ctx)
+        torch.cuda.synchronize()
+        dist.barrier()
+        free1 = torch.cuda.mem_get_info()[0]
+        # (device free memory is informative only: the runtime may keep IPC-exported allocations mapped)
+        res = {"custom_none": comm.custom is None, "leak_mb": (free0 - free1) / 2**20, "calls": calls}
+        # the fallback still sums (host-staged gloo here; RCCL on a real node)
+        t = torch.full((1024,), float(rank + 1), device="cuda")
+        comm.all_reduce_(t)
+        res["fallback_sum_ok"] = bool((t == 3.0).all())
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put(("ok", rank, res))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", rank, traceback.format_exc()))
+
+
+def _spawn(target, world=2, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = []
+    try:
+        for _ in range(world):
+            outs.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for status, rank, payload in outs:
+        assert status == "ok", payload
+    return {rank: payload for _, rank, payload in outs}
+
+
+@pytest.mark.timeout(300)
+def test_missing_peer_times_out_and_poisons():
+    res = _spawn(_missing_peer)
+    assert res[0]["first_ok"] and res[1]["first_ok"]
+    r0 = res[0]
+    assert r0["error_word"] == 1
+    assert 0.8 * TIMEOUT_S <= r0["timeout_wait_s"] < 10 * TIMEOUT_S, r0["timeout_wait_s"]
+    assert r0["after_error_wait_s"] < 0.5 * TIMEOUT_S, r0["after_error_wait_s"]
+    assert r0["check_raised"] and r0["refuses_after"]
+
+
+@pytest.mark.timeout(300)
+def test_decode_engine_raises_on_missing_peer():
+    res = _spawn(_engine_missing_peer)
+    assert res[0]["raised"], res[0]
+    # one timeout, then every later wait gives up at once: the run ends in about one timeout, not one per call
+    assert res[0]["elapsed_s"] < 20 * TIMEOUT_S + 10.0, res[0]
+
+
+@pytest.mark.timeout(300)
+def test_setup_failure_on_one_rank_falls_back_everywhere():
+    res = _spawn(_setup_failure)
+    for r in (0, 1):
+        assert res[r]["custom_none"], res[r]
+        assert res[r]["fallback_sum_ok"], res[r]
+    # rank 0 mapped its peer before the verdict: it unmaps and frees through car_destroy; rank 1 never got a state
+    assert res[0]["calls"] == {"destroy": 1, "free": 0}, res[0]
+    assert res[1]["calls"] == {"destroy": 0, "free": 1}, res[1]

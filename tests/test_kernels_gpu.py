@@ -255,7 +255,7 @@ def _attn_ref_gpu(q, kc, vc, slot0, kv_start, key_mask=None, chunk=512):
     return out.reshape(b * s, h * dh)
 
 
-@pytest.mark.parametrize("impl", [3, 2, 1])
+@pytest.mark.parametrize("impl", [4, 2, 1])
 @pytest.mark.parametrize("rep", [1, 4, 8])
 @pytest.mark.parametrize("s,slot0,masked", [(7, 0, False), (130, 10, False), (512, 0, False), (300, 0, True),
                                             (2048, 0, False)])
@@ -880,3 +880,29 @@ def test_attention_decode_packed_output(b):
     op = ops.packed_empty(b, h * dh, DEV)
     out = ops.attention(qg, kc.to(DEV), vc.to(DEV), slot.to(DEV), kv_start.to(DEV), None, out_packed=op)
     assert torch.equal(ref.unpack_act(op.cpu(), b), out.cpu())
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 512, 256), (5, 1000, 4096), (130, 257, 96), (256, 128256, 128)])
+def test_gemm_f32_exact_mfma(m, n, k):
+    """precision='highest' lm_head kernel (gemm_f32.hip, v_mfma_f32_32x32x2_f32) against an fp64 reference: an fp32
+    fmaf chain, so the error is a few ulps of sum |a b|; ragged M / N / K exercise the tile guards."""
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    x = torch.randn(m, k, device=DEV, generator=g)
+    w = torch.randn(n, k, device=DEV, generator=g)
+    got = ops.linear_f32(x, w)
+    want = x.double() @ w.double().t()
+    scale = (x.double().abs() @ w.double().abs().t())
+    assert float(((got.double() - want).abs() / scale).max()) < 5e-6
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_residual_add_kernel(dt):
+    """TP prefill residual epilogue (norm_embed.hip residual_add): h += p; mirror = bf16(h), exact."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    h = torch.randn(37, 4096, device=DEV, generator=g)
+    p = torch.randn(37, 4096, device=DEV, generator=g).to(dt)
+    want = h + p.float()
+    mirror = torch.empty(37, 4096, dtype=BF16, device=DEV)
+    ops.residual_add_(h, p, mirror)
+    assert torch.equal(h, want)
+    assert torch.equal(mirror, want.to(BF16))

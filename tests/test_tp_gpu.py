@@ -12,6 +12,8 @@ Checks, per rank:
   * hipGraph replay == eager (bit-identical sequences), fused-argmax lm_head == logits + argmax;
   * sampling: every rank draws the same tokens;
   * the custom collectives never timed out (``error() == 0``).
+The MHA configs of BASELINE.json run at their real per-rank dims too: Llama-2-13B at MP 2 (README.md:50) and
+LLaMA-1-65B at MP 8 (README.md:52; 8 kv heads per rank, rep 1, F 2752, V 4000 per rank).
 Reference: partition.py:62-78 (Megatron column/row split, vocab-parallel lm_head), README.md:52-53
 (65B/70B need MP=8)."""
 from __future__ import annotations
@@ -39,6 +41,12 @@ def _config(kind):
     if kind == "small":
         return gpu_config(num_attention_heads=4, num_key_value_heads=2, hidden_size=512, intermediate_size=1024,
                           vocab_size=512)
+    if kind == "13b":  # Llama-2-13B dims (MHA): 20 q / 20 kv heads per rank at MP 2, F 6912, V 16000 per rank
+        return gpu_config(vocab_size=32000, hidden_size=5120, intermediate_size=13824, num_hidden_layers=2,
+                          num_attention_heads=40, num_key_value_heads=40, max_sequence_length=256)
+    if kind == "65b":  # LLaMA-1-65B dims (MHA): 8 q / 8 kv heads per rank at MP 8, F 2752, V 4000 per rank
+        return gpu_config(vocab_size=32000, hidden_size=8192, intermediate_size=22016, num_hidden_layers=2,
+                          num_attention_heads=64, num_key_value_heads=64, max_sequence_length=256)
     # Llama-3-70B dims, 2 layers
     return gpu_config(vocab_size=128256, hidden_size=8192, intermediate_size=28672, num_hidden_layers=2,
                       num_attention_heads=64, num_key_value_heads=8, max_sequence_length=256, rope_theta=500000.0)
@@ -46,30 +54,9 @@ def _config(kind):
 
 def _gpu_params(cfg, seed):
     """Reference-named random tree generated on the GPU (fast at 70B dims), bf16."""
+    from helpers import gpu_meta_state_dict
     from jax_llama_amd.utils.checkpoint import meta_state_dict_to_params
-    g = torch.Generator(device="cuda").manual_seed(seed)
-    d, hd, f, v = cfg.hidden_size, cfg.head_dim, cfg.intermediate_size, cfg.vocab_size
-    hq, hkv = cfg.num_attention_heads * hd, cfg.num_key_value_heads * hd
-
-    def rnd(*shape, s=0.02):
-        return (torch.randn(*shape, generator=g, device="cuda") * s).to(torch.bfloat16)
-
-    def norm():
-        return (1.0 + 0.1 * torch.randn(d, generator=g, device="cuda")).to(torch.bfloat16)
-
-    sd = {"tok_embeddings.weight": rnd(v, d, s=1.0), "norm.weight": norm(), "output.weight": rnd(v, d)}
-    for i in range(cfg.num_hidden_layers):
-        p = f"layers.{i}."
-        sd[p + "attention.wq.weight"] = rnd(hq, d)
-        sd[p + "attention.wk.weight"] = rnd(hkv, d)
-        sd[p + "attention.wv.weight"] = rnd(hkv, d)
-        sd[p + "attention.wo.weight"] = rnd(d, hq)
-        sd[p + "feed_forward.w1.weight"] = rnd(f, d)
-        sd[p + "feed_forward.w2.weight"] = rnd(d, f, s=0.01)
-        sd[p + "feed_forward.w3.weight"] = rnd(f, d)
-        sd[p + "attention_norm.weight"] = norm()
-        sd[p + "ffn_norm.weight"] = norm()
-    return meta_state_dict_to_params(sd, cfg.num_hidden_layers)
+    return meta_state_dict_to_params(gpu_meta_state_dict(cfg, seed), cfg.num_hidden_layers)
 
 
 def _worker(rank, world, port, kind, q, rows=4):
@@ -167,7 +154,8 @@ def _worker(rank, world, port, kind, q, rows=4):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,kind,rows", [(2, "small", 4), (4, "70b", 4), (8, "70b", 4), (2, "small", 12)])
+@pytest.mark.parametrize("world,kind,rows", [(2, "small", 4), (4, "70b", 4), (8, "70b", 4), (2, "small", 12),
+                                             (2, "13b", 4), (8, "65b", 4)])
 def test_tp_decode_matches_single_process(world, kind, rows):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

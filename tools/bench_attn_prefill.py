@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Prefill attention throughput (causal, GQA) at real model shapes: TFLOP/s of impl 2 (GQA-shared
-32x32x16 MFMA flash kernel, 32 queries per wave), impl 3 (same, 64 queries per wave) and impl 1 (v1). FLOPs counted for the causal triangle only:
+32x32x16 MFMA flash kernel, 32 queries per wave), impl 4 (always paired launch) and impl 1 (v1). FLOPs counted for the causal triangle only:
 4 * B * H * Dh * S (S + 1) / 2. Prints one JSON line per (shape, impl)."""
 from __future__ import annotations
 

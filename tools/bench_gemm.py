@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--fixup", type=int, nargs="+", default=[0], help="split-K: 0 partial slabs + reduce kernel, "
                     "1 in-kernel fixup (tickets); tile 6 always uses the fixup")
     ap.add_argument("--tile", type=int, nargs="+", default=[0], help="gemm2 tile config(s): 0 auto, 1 256x256, "
-                    "2 128x256, 3 128x128, 5 gemm4; 50 + v: gemm4 variant v")
+                    "2 128x256, 3 128x128")
     args = ap.parse_args()
     cfg = get_preset(args.model)
     d, f, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
@@ -100,9 +100,6 @@ def main():
                           ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
 
                       tcfg = tile
-                      if tile >= 50:
-                          e.gemm4_set_variant(tile - 50)
-                          tcfg = 5
 
                       def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk):
                           e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk,

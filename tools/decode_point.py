@@ -22,16 +22,23 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--sample", action="store_true")
+    ap.add_argument("--tp-proxy", type=int, default=1, help="> 1: ONE rank of that MP degree on this GPU "
+                    "(parallel/comm.py TPRankProxyComm; bench.py tp_rank_proxy)")
     args = ap.parse_args()
     import torch
     from jax_llama_amd.config import get_preset
     from jax_llama_amd.models import LLaMAForCausalLM
     from jax_llama_amd.runtime.benchmark import decode_latency
     cfg = get_preset(args.model, max_seq_len=2048)
-    m = LLaMAForCausalLM(cfg, device="cuda", _do_init=False).init_random(seed=1)
+    comm = None
+    if args.tp_proxy > 1:
+        from jax_llama_amd.parallel import TPRankProxyComm
+        comm = TPRankProxyComm.create(args.tp_proxy)
+    m = LLaMAForCausalLM(cfg, device="cuda", comm=comm, _do_init=False).init_random(seed=1)
     for b in args.batch:
         r = decode_latency(m, b, args.prompt_len, args.gen_len, steps=args.steps, do_sample=args.sample)
         r["model"] = args.model
+        r["mp"] = args.tp_proxy
         r["hbm_roofline_ms"] = round(m.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()

@@ -62,8 +62,8 @@ enum { PAIRS_ARGMAX = 0, PAIRS_TOPK = 1 };
 struct CarDevice {
   char* buf[CAR_MAX_WORLD];     // every rank's buffer (A then R), mapped here
   int* sig[CAR_MAX_WORLD];      // every rank's flags [CAR_BLOCKS][CAR_MAX_WORLD]
-  int* barrier_count;           // [CAR_BLOCKS] barriers passed by block b (local)
-  int* call_count;              // [CAR_BLOCKS] calls made by block b (local; parity)
+  int2* ctr;                    // [CAR_BLOCKS] {calls made, barriers passed} by block b (local): ONE 8-byte load
+                                // at the start of a call gives both the parity and the flag epoch
   int* error;                   // 1 once a wait timed out
   long long max_bytes;          // A slot size; R holds 2 * max_bytes per parity
   long long timeout_ticks;      // wall-clock ticks (s_memrealtime, 100 MHz) before giving up
@@ -89,25 +89,32 @@ JLA_DEV u32x2 ld_sys8(__amdgpu_buffer_rsrc_t r, long long off) {
   return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, SYS);
 }
 
-// Start of a call for block b: bump the call counter (parity) once per call.
-JLA_DEV int car_begin(const CarDevice& d, int b, int* s_word) {
+// Per-call state of block b, in LDS: the call and barrier counters are read once at the start (uncached memory:
+// every access is a memory round trip) and written back once at the end.
+struct CarCalls {
+  int calls, bars;
+};
+
+// Start of a call for block b: read the counters, bump the call counter (parity).
+JLA_DEV int car_begin(const CarDevice& d, int b, CarCalls* st) {
   if (threadIdx.x == 0) {
-    const int c = d.call_count[b] + 1;
-    d.call_count[b] = c;
-    *s_word = c;
+    const int2 c = d.ctr[b];
+    st->calls = c.x + 1;
+    st->bars = c.y;
   }
   __syncthreads();
-  return *s_word & 1;
+  return st->calls & 1;
+}
+JLA_DEV void car_end(const CarDevice& d, int b, const CarCalls* st) {
+  if (threadIdx.x == 0) d.ctr[b] = make_int2(st->calls, st->bars);
 }
 
 // Barrier of block b with block b of every peer. Every wave of the block must have issued its
 // hand-off stores before calling.
-JLA_DEV void car_barrier(const CarDevice& d, int b, int* s_word) {
+JLA_DEV void car_barrier(const CarDevice& d, int b, CarCalls* st) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) *s_word = d.barrier_count[b] + 1;
-  __syncthreads();
-  const int e = *s_word;
+  const int e = st->bars + 1;
   if (threadIdx.x < d.world) {
     __hip_atomic_store(d.sig[threadIdx.x] + b * CAR_MAX_WORLD + d.rank, e, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -124,7 +131,7 @@ JLA_DEV void car_barrier(const CarDevice& d, int b, int* s_word) {
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) d.barrier_count[b] = e;
+  if (threadIdx.x == 0) st->bars = e;
 }
 
 // fp32 values of one 16-byte input piece (8 bf16 or 4 fp32)
@@ -153,7 +160,7 @@ struct Piece {
 // next projection's packed-x input on the decode path
 template <int OP, bool BF16>
 JLA_DEV void car_epilogue(const float* sum, long long e0, void* out, float* h, bf16_t* hb, bf16_t* hb_pack,
-                          int pack_cols) {
+                          int pack_cols, bool pre, f32x4 pre0, f32x4 pre1) {
   constexpr int N = BF16 ? 8 : 4;
   if constexpr (OP == OP_SUM) {
     if constexpr (BF16) {
@@ -165,7 +172,7 @@ JLA_DEV void car_epilogue(const float* sum, long long e0, void* out, float* h, b
     float r[N];
 #pragma unroll
     for (int q = 0; q < N / 4; ++q) {
-      f32x4 hv = *reinterpret_cast<const f32x4*>(h + e0 + 4 * q);
+      f32x4 hv = pre ? (q == 0 ? pre0 : pre1) : *reinterpret_cast<const f32x4*>(h + e0 + 4 * q);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         r[4 * q + i] = hv[i] + sum[4 * q + i];
@@ -208,8 +215,21 @@ __global__ void __launch_bounds__(CAR_THREADS)
   const int b = blockIdx.x;
   const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
   if (b >= nchunks) return;
-  __shared__ int s_word;
-  const int parity = car_begin(d, b, &s_word);
+  __shared__ CarCalls st;
+  // the first chunk's input (and, one-shot OP_RESID, its residual rows) are loaded before the counters come back:
+  // independent of the hand-off, so their latency hides behind the counter read
+  const long long off0 = (long long)b * CAR_CHUNK + (long long)threadIdx.x * 16;
+  const bool have0 = off0 < nbytes;
+  u32x4 in0 = {0u, 0u, 0u, 0u};
+  f32x4 h0a = {0.f, 0.f, 0.f, 0.f}, h0b = {0.f, 0.f, 0.f, 0.f};
+  if (have0) in0 = *reinterpret_cast<const u32x4*>(in + off0);
+  if constexpr (OP == OP_RESID && !TWO_SHOT) {
+    if (have0) {
+      h0a = *reinterpret_cast<const f32x4*>(h + off0 / ESZ);
+      if constexpr (N == 8) h0b = *reinterpret_cast<const f32x4*>(h + off0 / ESZ + 4);
+    }
+  }
+  const int parity = car_begin(d, b, &st);
   const long long slot = d.max_bytes;
   const long long a_off = (long long)parity * d.world * slot;
   const long long r_off = 2 * (long long)d.world * slot + (long long)parity * 2 * slot;
@@ -219,7 +239,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
   for (long long c = b; c < nchunks; c += CAR_GRID) {
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
-    const u32x4 v = *reinterpret_cast<const u32x4*>(in + off);
+    const u32x4 v = c == b ? in0 : *reinterpret_cast<const u32x4*>(in + off);
     if (TWO_SHOT) {
       const int o = (int)(c % d.world);
       st_sys16(rsrc(d.buf[o]), a_off + (long long)d.rank * slot + off, v);
@@ -227,7 +247,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
       for (int p = 0; p < d.world; ++p) st_sys16(rsrc(d.buf[p]), a_off + (long long)d.rank * slot + off, v);
     }
   }
-  car_barrier(d, b, &s_word);
+  car_barrier(d, b, &st);
 
   if (!TWO_SHOT) {
     // 2. sum the slots in rank order, apply the op
@@ -237,8 +257,9 @@ __global__ void __launch_bounds__(CAR_THREADS)
       Piece<BF16> acc;
       acc.set(ld_sys16(mine, a_off + off));
       for (int p = 1; p < d.world; ++p) acc.add(ld_sys16(mine, a_off + (long long)p * slot + off));
-      car_epilogue<OP, BF16>(acc.v, off / ESZ, out, h, hb, hb_pack, pack_cols);
+      car_epilogue<OP, BF16>(acc.v, off / ESZ, out, h, hb, hb_pack, pack_cols, OP == OP_RESID && c == b, h0a, h0b);
     }
+    car_end(d, b, &st);
     return;
   }
   // 2. owner: sum its chunks in rank order, push the fp32 sum to every rank's R region
@@ -258,7 +279,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
       for (int p = 0; p < d.world; ++p) st_sys16(rsrc(d.buf[p]), roff + 16 * q, v);
     }
   }
-  car_barrier(d, b, &s_word);
+  car_barrier(d, b, &st);
   // 3. every rank: apply the op to every chunk from the gathered sums
   for (long long c = b; c < nchunks; c += CAR_GRID) {
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
@@ -271,8 +292,9 @@ __global__ void __launch_bounds__(CAR_THREADS)
 #pragma unroll
       for (int i = 0; i < 4; ++i) s[4 * q + i] = __uint_as_float(v[i]);
     }
-    car_epilogue<OP, BF16>(s, off / ESZ, out, h, hb, hb_pack, pack_cols);
+    car_epilogue<OP, BF16>(s, off / ESZ, out, h, hb, hb_pack, pack_cols, false, f32x4{}, f32x4{});
   }
+  car_end(d, b, &st);
 }
 
 // (value, index) pairs: granule i = (a[i], b[i] + idx_offset)
@@ -284,8 +306,8 @@ __global__ void __launch_bounds__(CAR_THREADS)
   const int blk = blockIdx.x;
   const long long nchunks = (n + CAR_PAIR_CHUNK - 1) / CAR_PAIR_CHUNK;
   if (blk >= nchunks) return;
-  __shared__ int s_word;
-  const int parity = car_begin(d, blk, &s_word);
+  __shared__ CarCalls st;
+  const int parity = car_begin(d, blk, &st);
   const long long slot = d.max_bytes;
   const long long a_off = (long long)parity * d.world * slot;
   const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
@@ -298,7 +320,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
       for (int p = 0; p < d.world; ++p) st_sys8(rsrc(d.buf[p]), a_off + (long long)d.rank * slot + i * 8, v);
     }
   }
-  car_barrier(d, blk, &s_word);
+  car_barrier(d, blk, &st);
   for (long long c = blk; c < nchunks; c += CAR_GRID) {
    for (int t = 0; t < CAR_PAIRS_PER_THREAD; ++t) {
     const long long i = c * CAR_PAIR_CHUNK + t * CAR_THREADS + threadIdx.x;
@@ -322,6 +344,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
     }
    }
   }
+  car_end(d, blk, &st);
 }
 
 // ---- host side -------------------------------------------------------------------------------
@@ -409,8 +432,7 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   }
   // barrier / call counters and the error word live after the flags in the local signal allocation
   int* tail = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int));
-  st->h.barrier_count = tail;
-  st->h.call_count = tail + CAR_BLOCKS;
+  st->h.ctr = reinterpret_cast<int2*>(tail);  // [CAR_BLOCKS] {calls, barriers}
   st->h.error = tail + 2 * CAR_BLOCKS;
   st->d = nullptr;
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&st->d), sizeof(CarDevice));

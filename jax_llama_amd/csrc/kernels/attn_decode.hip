@@ -414,6 +414,220 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
 }
 
 // ---------------------------------------------------------------------------------------------
+// v5 (small batch, split over keys): v3 runs a whole (row, kv head) pair on ONE workgroup, so at B x Hkv << CUs the
+// pair's scoring is compute-bound on one CU (Llama-3-70B at MP 8, B = 1: 8 q heads x ~200 keys on a single CU,
+// 13 us per layer in the decode trace). Here the valid keys [kv_start, slot] are cut into CH-key splits, one
+// 4-wave workgroup each (every K / V row of the split issued at once: one memory round trip), scores by v_dot2,
+// a per-wave online softmax, one LDS merge of the 4 waves; a split publishes its (m, l, o) with write-through (sc1)
+// 16-B stores and takes the pair's agent-scope ticket, and the last arriver merges the splits in split order
+// (sc1 loads; cdna_hip_programming.md Guideline 16 R1 form) and writes the output (+ the packed copy for the o
+// projection). Splits outside the valid key range exit at once (the grid covers the whole cache, the valid range is
+// device state), so the ticket counts only the active splits; a pair with one active split writes directly.
+constexpr int AD5_WAVES = 4;
+static int g_attn_v5_max_pairs = 64;  // v5 up to this many (row, kv head) pairs (0: off)
+void attn_set_v5_max_pairs(int n) { g_attn_v5_max_pairs = n < 0 ? 64 : n; }
+static int kpg5(int rep) { return rep >= 16 ? 1 : (rep == 8 ? 2 : (rep == 4 ? 4 : 8)); }
+
+template <int REP, int KPG>
+__global__ void __launch_bounds__(AD5_WAVES * 64)
+    attn_decode_v5_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+                          const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
+                          const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out,
+                          float* __restrict__ ws, int32_t* __restrict__ tickets, int H, int Hkv, int T, int t_cap,
+                          int nsplit, float scale, bf16_t* __restrict__ out_pack) {
+  constexpr int CH = AD5_WAVES * 4 * KPG;     // keys per split
+  constexpr int HS = AD_DH + 4;               // floats per head of a partial: [m, l, 0, 0, o[128]]
+  constexpr int PS = REP * HS;                // floats per split partial
+  __shared__ float sm_m[AD5_WAVES][REP];
+  __shared__ float sm_l[AD5_WAVES][REP];
+  __shared__ float sm_o[AD5_WAVES][REP][AD_DH];
+  __shared__ int last_flag;
+
+  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int slot = slot_ptr[0];
+  if (slot >= T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);  // keys past the cache are never read
+  const int lo = kv_start[b];
+  const int hi = min(slot + 1, t_cap);  // valid keys [lo, hi)
+  const int s_lo = lo / CH, s_hi = hi > lo ? (hi + CH - 1) / CH : s_lo;
+  const int n_act = s_hi - s_lo;
+  const int h0 = kvh * REP;
+  const int HD = H * AD_DH;
+  auto store_out = [&](int h, int d, const float* v) {  // 4 consecutive dims of head h
+    bf16_t* o = out + ((size_t)b * H + h0 + h) * AD_DH + d;
+    u32x2 pk;
+    pk[0] = pack2bf(v[0], v[1]);
+    pk[1] = pack2bf(v[2], v[3]);
+    *reinterpret_cast<u32x2*>(o) = pk;
+    if (out_pack) *reinterpret_cast<u32x2*>(out_pack + pack_off(b, (h0 + h) * AD_DH + d, HD)) = pk;
+  };
+  if (n_act <= 0) {  // no valid key for this row: 0 (never NaN), written once
+    if (split == 0)
+      for (int it = threadIdx.x; it < REP * 32; it += AD5_WAVES * 64) {
+        const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        store_out(it >> 5, 4 * (it & 31), z);
+      }
+    return;
+  }
+  if (split < s_lo || split >= s_hi) return;
+
+  // ---- every K and V row of the split, then q (rows past the valid range re-read a valid one: masked)
+  const int c0 = split * CH;
+  const size_t head_off = ((size_t)b * Hkv + kvh) * T * AD_DH + 8 * li;
+  u32x4 kr[KPG], vr[KPG], qv[REP];
+#pragma unroll
+  for (int r = 0; r < KPG; ++r) {
+    const int jc = min(max(c0 + 16 * r + 4 * w + g, lo), hi - 1);
+    kr[r] = *reinterpret_cast<const u32x4*>(kc + head_off + (size_t)jc * AD_DH);
+  }
+#pragma unroll
+  for (int r = 0; r < KPG; ++r) {
+    const int jc = min(max(c0 + 16 * r + 4 * w + g, lo), hi - 1);
+    vr[r] = *reinterpret_cast<const u32x4*>(vc + head_off + (size_t)jc * AD_DH);
+  }
+#pragma unroll
+  for (int h = 0; h < REP; ++h) qv[h] = *reinterpret_cast<const u32x4*>(q + ((size_t)b * H + h0 + h) * AD_DH + 8 * li);
+  const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
+
+  // ---- scores (v_dot2 over the lane's 8 dims, 16-lane DPP sum: every lane of the group gets the score)
+  float sc[REP][KPG];
+#pragma unroll
+  for (int r = 0; r < KPG; ++r) {
+    const int j = c0 + 16 * r + 4 * w + g;
+    bool valid = j >= lo && j < hi;
+    if (mrow) valid = valid && j < mask_len && mrow[j] != 0;
+#pragma unroll
+    for (int h = 0; h < REP; ++h) {
+      const float d = row16_sum(dot8_bf16(qv[h], kr[r], 0.f)) * scale;
+      sc[h][r] = valid ? d : -INFINITY;
+    }
+  }
+  // ---- per wave: max, p = exp(s - m), l, o = P.V over the lane's 8 dims; the 4 groups summed by shuffles
+#pragma unroll
+  for (int h = 0; h < REP; ++h) {
+    float mx = sc[h][0];
+#pragma unroll
+    for (int r = 1; r < KPG; ++r) mx = fmaxf(mx, sc[h][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (mx != -INFINITY) {  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < KPG; ++r) {
+        const float p = sc[h][r] == -INFINITY ? 0.f : __expf(sc[h][r] - mx);
+        l += p;  // the 16 lanes of a group hold the same p
+        float vf[8];
+        unpack8(vr[r], vf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += p * vf[e];
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] += __shfl_xor(o[e], 16, 64);
+      o[e] += __shfl_xor(o[e], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm_o[w][h][8 * li + e] = o[e];
+      if (li == 0) {
+        sm_m[w][h] = mx;
+        sm_l[w][h] = l;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- the workgroup's (m, l, o) per head: thread -> (head, 4 dims)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(ws + ((size_t)b * Hkv + kvh) * nsplit * PS, 0, nsplit * PS * 4, 0x00020000);
+  for (int it = threadIdx.x; it < REP * 32; it += AD5_WAVES * 64) {
+    const int h = it >> 5, d = 4 * (it & 31);
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < AD5_WAVES; ++ww) M = fmaxf(M, sm_m[ww][h]);
+    float num[4] = {0.f, 0.f, 0.f, 0.f}, den = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < AD5_WAVES; ++ww) {
+        const float mw = sm_m[ww][h];
+        const float f = mw == -INFINITY ? 0.f : __expf(mw - M);
+        den += f * sm_l[ww][h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) num[e] += f * sm_o[ww][h][d + e];
+      }
+    }
+    if (n_act == 1) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = den > 0.f ? num[e] / den : 0.f;
+      store_out(h, d, v);
+    } else {
+      const int off = (split * PS + h * HS) * 4;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          u32x4{__float_as_uint(num[0]), __float_as_uint(num[1]), __float_as_uint(num[2]), __float_as_uint(num[3])},
+          rs, off + (4 + d) * 4, 0, 16);
+      if (d == 0)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(M), __float_as_uint(den), 0u, 0u}, rs, off, 0, 16);
+    }
+  }
+  if (n_act == 1) return;
+
+  // ---- publish: every storing wave drains its write-through stores, then one ticket add per workgroup
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t* tk = tickets + (size_t)b * Hkv + kvh;
+    const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == n_act - 1;
+    if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for the next call
+    last_flag = last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+
+  // ---- last arriver: online merge of the active splits in split order (sc1 loads, 4 splits in flight)
+  for (int it = threadIdx.x; it < REP * 32; it += AD5_WAVES * 64) {
+    const int h = it >> 5, d = 4 * (it & 31);
+    float Mr = -INFINITY, Lr = 0.f, Or[4] = {0.f, 0.f, 0.f, 0.f};
+    auto fold = [&](const u32x4 ml, const u32x4 ov) {
+      const float ms = __uint_as_float(ml[0]);
+      if (ms == -INFINITY) return;
+      const float mn = fmaxf(Mr, ms);
+      const float a = Mr == -INFINITY ? 0.f : __expf(Mr - mn), f = __expf(ms - mn);
+      Lr = Lr * a + f * __uint_as_float(ml[1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Or[e] = Or[e] * a + f * __uint_as_float(ov[e]);
+      Mr = mn;
+    };
+    int s = s_lo;
+    for (; s + 4 <= s_hi; s += 4) {
+      u32x4 ml[4], ov[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int off = ((s + u) * PS + h * HS) * 4;
+        ml[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+        ov[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + (4 + d) * 4, 0, 16);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) fold(ml[u], ov[u]);
+    }
+    for (; s < s_hi; ++s) {
+      const int off = (s * PS + h * HS) * 4;
+      fold(__builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16),
+           __builtin_amdgcn_raw_buffer_load_b128(rs, off + (4 + d) * 4, 0, 16));
+    }
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = Lr > 0.f ? Or[e] / Lr : 0.f;
+    store_out(h, d, v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // v2 (default): streaming decode attention, one WAVE per work item (batch row, kv head, key split).
 //
 // v1 above gives every 128-key chunk its own workgroup (load everything, compute, merge), so a CU's
@@ -867,14 +1081,20 @@ static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv)
 // profiles/r2_attn_decode_v3_kpg_ab.jsonl)
 static int g_v3_kpg_mult = 0;
 void attn_set_v3_kpg(int mult) { g_v3_kpg_mult = mult >= 4 ? 4 : (mult >= 2 ? 2 : (mult == 1 ? 1 : 0)); }
-int attn_decode_packs(int B, int Hkv, int rep) { return use_v3(B, Hkv, rep) ? 1 : 0; }
+// v5 (split small-batch kernel) below g_attn_v5_max_pairs (row, kv head) pairs, ahead of v3
+static bool use_v5(int B, int Hkv, int rep) {
+  return g_attn_impl == 2 && rep <= 16 && (rep & (rep - 1)) == 0 && B * Hkv <= g_attn_v5_max_pairs;
+}
+int attn_decode_packs(int B, int Hkv, int rep) { return (use_v5(B, Hkv, rep) || use_v3(B, Hkv, rep)) ? 1 : 0; }
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
+  if (use_v5(B, Hkv, rep)) return 16 * kpg5(rep);
   if (use_v3(B, Hkv, rep)) return T;
   return use_v2(B, Hkv) ? 4 * kpg_v2(rep, B * Hkv) : 16 * kpg_v1(rep, B, Hkv, T);
 }
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
+  if (use_v5(B, Hkv, rep)) return (T + 16 * kpg5(rep) - 1) / (16 * kpg5(rep));
   if (use_v3(B, Hkv, rep)) return 1;
   if (!use_v2(B, Hkv)) {
     const int ch = 16 * kpg_v1(rep, B, Hkv, T);
@@ -891,11 +1111,25 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
                 const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int32_t* tickets, int B, int H,
                 int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s, bf16_t* out_pack) {
   if (B <= 0) return 0;
-  if (out_pack && !use_v3(B, Hkv, H / Hkv)) return -3;  // only the small-batch kernel writes the packed copy
+  if (out_pack && !attn_decode_packs(B, Hkv, H / Hkv)) return -3;  // only the small-batch kernels write the packed copy
   if (Dh != AD_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   if (attn_decode_splits(B, Hkv, t_cap, rep) != nsplit) return -2;
   const float scale = 1.f / sqrtf((float)Dh);
+  if (use_v5(B, Hkv, rep)) {
+    dim3 grid5(nsplit, Hkv, B);
+#define JLA_AD5(R, K)                                                                                          \
+  if (rep == R) {                                                                                              \
+    attn_decode_v5_kernel<R, K><<<grid5, AD5_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, \
+                                                                 out, ws, tickets, H, Hkv, T, t_cap, nsplit,   \
+                                                                 scale, out_pack);                             \
+    JLA_CHECK_LAUNCH();                                                                                        \
+    return 0;                                                                                                  \
+  }
+    JLA_AD5(1, 8) JLA_AD5(2, 8) JLA_AD5(4, 4) JLA_AD5(8, 2) JLA_AD5(16, 1)
+#undef JLA_AD5
+    return -1;
+  }
   if (use_v3(B, Hkv, rep)) {
     dim3 grid3(Hkv, B);
 #define JLA_AD3(R, K)                                                                                          \

@@ -350,6 +350,12 @@ class LLaMAForCausalLM:
         ``(logits_local, h, hidden_states, attentions)`` where logits are this rank's
         vocab shard: ``[B, V/tp]`` ("last"), ``[B*S, V/tp]`` ("all"), None ("none"), or the
         shard's greedy ``(idx int32[B], val fp32[B])`` of the last position ("argmax")."""
+        with ops.autotune.tp_scope(self.comm):  # TP: rank 0 picks the kernel plans for every rank
+            return self._forward_tokens(ids, positions, cache, slot0, kv_start, key_mask, logits_mode,
+                                        collect_hidden, collect_attn)
+
+    def _forward_tokens(self, ids, positions, cache, slot0, kv_start, key_mask, logits_mode, collect_hidden,
+                        collect_attn):
         b, s = ids.shape
         d = self.config.hidden_size
         # residual stream: fp32 h plus its bf16 mirror hb (the A operand of every projection

@@ -454,7 +454,7 @@ def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slo
     if s == 1:
         hkv = k_cache.shape[1]
         nsplit = e.attn_decode_splits(bsz, hkv, t_cap, h // hkv)
-        ws = workspace.get("attn_decode", bsz * h * nsplit * (dh + 2), torch.float32, q.device)
+        ws = workspace.get("attn_decode", bsz * h * nsplit * (dh + 4), torch.float32, q.device)
         tickets = workspace.get_zeroed("attn_tickets", bsz * hkv, torch.int32, q.device)
         e.attn_decode(q, k_cache, v_cache, slot_t, kv_start, key_mask, out, ws, tickets, t_cap, nsplit, out_packed)
     else:

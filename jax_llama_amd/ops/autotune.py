@@ -12,16 +12,112 @@ Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 ti
 with 16 waves / a doubled register ring (M > 16, bf16 activations),
 4 = split-K skinny GEMM, 7 = tiled MFMA GEMM with split-K (gemm.hip; a candidate for M > 16, always used
 for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
+
+Tensor parallelism: inside ``tp_scope(comm)`` (the model's forward under TP) a decision is collective -- rank 0
+of the TP group measures and broadcasts its choice, so every rank runs the same plans (a rank on a slower plan
+would set the pace of every collective). Persistence: decisions are kept per (arch, shape) in a JSON table
+(``JLA_TUNE_FILE``, default ``$XDG_CACHE_HOME/jax_llama_amd/tune_<arch>.json``), loaded at first use and
+rewritten after every new measurement, so a later process skips the measurement (a cold B = 8 prefill
+autotunes for ~1 s).
 """
 from __future__ import annotations
 
+import contextlib
+import json
 import os
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
 _CACHE: Dict[Tuple, int] = {}
 ENABLED = os.environ.get("JLA_AUTOTUNE", "1") != "0"
+ARCH = "gfx950"
+
+# ---- TP scope: the comm whose rank 0 decides (None: every process decides for itself)
+_SCOPE = {"comm": None}
+
+
+@contextlib.contextmanager
+def tp_scope(comm):
+    """Decisions taken inside are made by rank 0 of ``comm`` (when it spans > 1 rank) and broadcast."""
+    prev = _SCOPE["comm"]
+    _SCOPE["comm"] = comm if comm is not None and getattr(comm, "size", 1) > 1 else None
+    try:
+        yield
+    finally:
+        _SCOPE["comm"] = prev
+
+
+def _collective(decide):
+    """Run ``decide()`` on rank 0 of the current TP scope and broadcast its (JSON-able) result."""
+    comm = _SCOPE["comm"]
+    if comm is None or comm.group is None and not _dist_ready():
+        return decide()
+    import torch.distributed as dist
+    obj = [decide() if comm.rank == 0 else None]
+    src = dist.get_global_rank(comm.group, 0) if comm.group is not None else 0
+    dist.broadcast_object_list(obj, src=src, group=comm.group)
+    v = obj[0]
+    return tuple(v) if isinstance(v, list) else v
+
+
+def _dist_ready() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+# ---- persistence
+_LOADED = {"done": False}
+
+
+def tune_file() -> str:
+    env = os.environ.get("JLA_TUNE_FILE")
+    if env:
+        return env
+    base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+    return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
+
+
+def _key_str(kind: str, key: Tuple) -> str:
+    return kind + ":" + ",".join(str(k).replace("torch.", "") for k in key)
+
+
+def _load():
+    if _LOADED["done"]:
+        return
+    _LOADED["done"] = True
+    if os.environ.get("JLA_TUNE_PERSIST", "1") == "0":
+        return
+    try:
+        with open(tune_file()) as f:
+            data = json.load(f)
+    except (OSError, ValueError):
+        return
+    _PERSISTED.update(data if isinstance(data, dict) else {})
+
+
+_PERSISTED: Dict[str, object] = {}
+
+
+def _save(kind: str, key: Tuple, value):
+    if os.environ.get("JLA_TUNE_PERSIST", "1") == "0":
+        return
+    _PERSISTED[_key_str(kind, key)] = list(value) if isinstance(value, tuple) else value
+    path = tune_file()
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            json.dump(_PERSISTED, f, indent=0, sort_keys=True)
+        os.replace(tmp, path)
+    except OSError:
+        pass
+
+
+def _persisted(kind: str, key: Tuple) -> Optional[object]:
+    _load()
+    v = _PERSISTED.get(_key_str(kind, key))
+    return tuple(v) if isinstance(v, list) else v
 
 
 def m_bucket(m: int) -> int:
@@ -49,6 +145,10 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
     c = [1, 6, 4]
     if n % 64 == 0:
         c.insert(1, 5)
+    if n // 16 < 512:
+        # few n-tiles (tensor-parallel qkv / o shards, e.g. Llama-3-70B at MP 8: qkv N = 1280 -> 80 workgroups): 8 or
+        # 16 waves per workgroup keep more weight bytes in flight per CU (gemv.hip pick_nw variants 2 / 3)
+        c.extend([2, 3])
     if m > 16:
         c.append(TILED_VARIANT)
         if bf16_x:
@@ -71,7 +171,8 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     packed-x variants compete too; ``pack_out``: the epilogue must also write a packed copy of its output,
     which only the GEMV variants do (no split-K skinny 4, no tiled 7)."""
     m = x.shape[0]
-    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out)
+    # (TP-scoped decisions are cached apart: every rank of the group must take the same collective path)
+    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out, _SCOPE["comm"] is not None)
     v = _CACHE.get(key)
     if v is not None:
         return v
@@ -83,7 +184,15 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     if not ENABLED or torch.cuda.is_current_stream_capturing():
         h = heuristic(m, w.n, w.k, mode)
         return h if h in cands else 1
-    v = _measure(x, w, run, tuple(cands))
+    def decide():
+        pv = _persisted("gemv", key[:-1])
+        if pv in cands:
+            return pv
+        mv = _measure(x, w, run, tuple(cands))
+        _save("gemv", key[:-1], mv)
+        return mv
+
+    v = _collective(decide)
     _CACHE[key] = v
     return v
 
@@ -133,7 +242,7 @@ def choose_gemm_plan(e, m: int, n: int, k: int, device, mode: int = 0, rms: bool
     in the reduce kernel, and the residual epilogue (fp32 read-modify-write + bf16 mirror) costs the reduce
     ~2x the bf16 store's, which moves the best split factor of wo / w2."""
     mode = 0 if mode == 3 else mode  # QKV (RoPE + cache write, side effects) is tuned as a plain store
-    key = (m, n, k, mode, bool(rms))
+    key = (m, n, k, mode, bool(rms), _SCOPE["comm"] is not None)
     plan = _KS_CACHE.get(key)
     if plan is not None:
         return plan
@@ -142,7 +251,15 @@ def choose_gemm_plan(e, m: int, n: int, k: int, device, mode: int = 0, rms: bool
     # multi-GB scratch outputs)
     if m <= 128 or m > TUNE_MAX_M or not ENABLED or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
         return heur, 0
-    plan = _measure_plan(e, m, n, k, device, heur, mode, rms)
+    def decide():
+        pv = _persisted("gemm", key[:-1])
+        if isinstance(pv, tuple) and len(pv) == 2:
+            return pv
+        mv = _measure_plan(e, m, n, k, device, heur, mode, rms)
+        _save("gemm", key[:-1], mv)
+        return mv
+
+    plan = tuple(_collective(decide))
     _KS_CACHE[key] = plan
     return plan
 

@@ -92,7 +92,9 @@ def _engine_missing_peer(rank, world, port, q):
         from jax_llama_amd.models import LLaMAForCausalLM
         from jax_llama_amd.parallel import TPComm, init_distributed
         from jax_llama_amd.parallel.custom_allreduce import CustomAllReduceError
+        from jax_llama_amd.ops import autotune
         from jax_llama_amd.runtime.engine import DecodeEngine, GenerationConfig
+        autotune.ENABLED = False  # rank 1 never runs a forward: no collective plan decisions (ops/autotune.py)
         ctx = init_distributed(backend="gloo", device_type="cuda")  # joins the group _init created
         ctx.setup_mesh(tp=world)
         comm = TPComm.from_context(ctx, timeout_s=TIMEOUT_S)

@@ -82,3 +82,58 @@ def test_tensor_parallel_matches_single_process(world, kv):
     assert (logits[m] - want[m]).abs().max() < 2e-2
     assert torch.equal(seq.long(), want_seq.long())
     assert sseq.shape == seq.shape and int(sseq.min()) >= 0 and int(sseq.max()) < cfg.vocab_size
+
+
+def _tune_worker(rank, world, port, path, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank), JLA_TUNE_FILE=path)
+        from jax_llama_amd.ops import autotune
+        from jax_llama_amd.parallel import TPComm, init_distributed
+        ctx = init_distributed(backend="gloo", device_type="cpu")
+        ctx.setup_mesh(tp=world)
+        comm = TPComm.from_context(ctx)
+        with autotune.tp_scope(comm):
+            got = autotune._collective(lambda: (rank + 1, 10 * (rank + 1)))  # each rank would "measure" differently
+        local = autotune._collective(lambda: rank)  # outside a TP scope: every process decides for itself
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put(("ok", rank, (got, local)))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put(("err", rank, traceback.format_exc()))
+
+
+def test_autotune_decisions_are_collective_under_tp(tmp_path):
+    """Under TP every rank must run the same kernel plans: rank 0 decides and broadcasts (ops/autotune.py)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, str(tmp_path / "t.json"), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for status, rank, payload in outs:
+        assert status == "ok", payload
+    res = {rank: payload for _, rank, payload in outs}
+    for r in range(world):
+        assert res[r][0] == (1, 10), res[r]  # rank 0's decision everywhere
+        assert res[r][1] == r
+
+
+def test_autotune_table_persists(tmp_path, monkeypatch):
+    from jax_llama_amd.ops import autotune
+    path = tmp_path / "tune.json"
+    monkeypatch.setenv("JLA_TUNE_FILE", str(path))
+    monkeypatch.setattr(autotune, "_PERSISTED", {})
+    monkeypatch.setitem(autotune._LOADED, "done", False)
+    key = (16, 6144, 4096, 3, torch.bfloat16, False, False)
+    autotune._save("gemv", key, 9)
+    autotune._save("gemm", (2048, 4096, 4096, 1, False), (2, 1))
+    monkeypatch.setattr(autotune, "_PERSISTED", {})
+    monkeypatch.setitem(autotune._LOADED, "done", False)
+    assert autotune._persisted("gemv", key) == 9
+    assert autotune._persisted("gemm", (2048, 4096, 4096, 1, False)) == (2, 1)
+    assert autotune._persisted("gemm", (1, 2, 3, 0, False)) is None

@@ -906,3 +906,45 @@ def test_residual_add_kernel(dt):
     ops.residual_add_(h, p, mirror)
     assert torch.equal(h, want)
     assert torch.equal(mirror, want.to(BF16))
+
+
+@pytest.mark.parametrize("kernel", ["v3", "v5"])
+@pytest.mark.parametrize("rep", [1, 4, 8, 16])
+@pytest.mark.parametrize("t,slot", [(40, 17), (384, 200), (1030, 1029)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_decode_small_batch_kernels(kernel, rep, t, slot, masked):
+    """The two small-batch decode kernels against the fp32 reference: v3 (one workgroup per (row, kv head)) and v5
+    (keys split over workgroups, last-arriver merge): left padding that starts inside a split, a row with no valid
+    key (zeros), the general key mask, rep up to 16; the packed output copy equals the row-major one."""
+    if kernel == "v3" and rep == 16:
+        pytest.skip("v3 serves rep <= 8")
+    e = ops.ext()
+    b, hkv, dh = 3, 2, 128
+    h = hkv * rep
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, 1, h, dh).to(BF16)
+    kv_start = torch.tensor([0, 37, slot + 1], dtype=torch.int32)
+    mask = None
+    if masked:
+        mask = (torch.rand(b, t) > 0.3).to(torch.uint8)
+        mask[:, slot] = 1
+        kv_start[1] = 0
+    expect = ref.attention(q, kc, vc, slot, kv_start, mask).reshape(b, h * dh)
+    try:
+        e.attn_set_v5_max_pairs(4096 if kernel == "v5" else 0)
+        qd = q.to(DEV)
+        kd, vd = kc.to(DEV), vc.to(DEV)
+        assert ops.attention_packs(qd, kd)
+        packed = ops.packed_empty(b, h * dh, DEV)
+        got = ops.attention(qd, kd, vd, torch.tensor([slot], dtype=torch.int32, device=DEV), kv_start.to(DEV),
+                            None if mask is None else mask.to(DEV), out_packed=packed)
+        again = ops.attention(qd, kd, vd, torch.tensor([slot], dtype=torch.int32, device=DEV), kv_start.to(DEV),
+                              None if mask is None else mask.to(DEV))
+        torch.cuda.synchronize()
+    finally:
+        e.attn_set_v5_max_pairs(-1)
+    _close(got, expect, 2e-2, 2e-2)
+    assert torch.equal(got, again)  # tickets reset themselves: a second call merges the same way
+    if not masked:
+        assert got[2].float().abs().max().item() == 0.0
+    assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Decode attention latency as a decode step sees it: hipGraph-replayed, K/V cold (a 512 MiB fill between calls
+evicts L2 and the Infinity Cache, as the weight stream of a real step does). Time per call = (graph of R x
+[fill, attention]) - (graph of R x [fill]) over R, min over rounds; impls interleaved in one process.
+
+  python tools/bench_attn_decode.py --model llama3-70b --tp 8 --shapes 1x192 1x384 32x384 --impls 2 5
+
+impl (ext.attn_set_impl / attn_set_v3_max_pairs): 2 = default dispatch; 1 = the split v1 kernel (v3 off);
+5 = split small-batch kernel (v5) where it applies. Prints one JSON line per (shape, impl).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from jax_llama_amd import ops  # noqa: E402
+from jax_llama_amd.config import get_preset  # noqa: E402
+
+
+def set_impl(e, impl):
+    e.attn_set_impl(2, 4096)
+    e.attn_set_v3_max_pairs(0 if impl == 1 else 4096)
+    if hasattr(e, "attn_set_v5_max_pairs"):
+        e.attn_set_v5_max_pairs(4096 if impl == 5 else (0 if impl in (1, 3) else -1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--shapes", nargs="+", default=["1x192", "1x384", "8x384", "32x384"], help="BxT (T = valid keys)")
+    ap.add_argument("--cache-len", type=int, default=0, help="cache length (default: T)")
+    ap.add_argument("--impls", type=int, nargs="+", default=[2, 1])
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    e = ops.ext()
+    cfg = get_preset(args.model)
+    h, hkv, hd = cfg.num_attention_heads // args.tp, cfg.num_key_value_heads // args.tp, cfg.head_dim
+    flush = torch.empty(512 << 18, dtype=torch.int32, device="cuda")  # 512 MiB
+    for shape in args.shapes:
+        b, t = (int(v) for v in shape.split("x"))
+        tc = max(args.cache_len, t)
+        g = torch.Generator(device="cuda").manual_seed(b * 7 + t)
+        kc = torch.randn(b, hkv, tc, hd, device="cuda", generator=g).to(torch.bfloat16)
+        vc = torch.randn(b, hkv, tc, hd, device="cuda", generator=g).to(torch.bfloat16)
+        q = torch.randn(b, 1, h, hd, device="cuda", generator=g).to(torch.bfloat16)
+        slot = torch.tensor([t - 1], dtype=torch.int32, device="cuda")
+        ks = torch.zeros(b, dtype=torch.int32, device="cuda")
+        res, first = {}, None
+        graphs = {}
+        for impl in args.impls:
+            set_impl(e, impl)
+            out = ops.attention(q, kc, vc, slot, ks)  # sizes the workspaces before capture
+            torch.cuda.synchronize()
+            first = out.float() if first is None else first
+            diff = float((out.float() - first).abs().max())
+            ga, gf = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                for _ in range(args.reps):
+                    flush.fill_(1)
+                    ops.attention(q, kc, vc, slot, ks)
+            with torch.cuda.graph(gf):
+                for _ in range(args.reps):
+                    flush.fill_(1)
+            graphs[impl] = (ga, gf, diff)
+        set_impl(e, 2)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best = {impl: float("inf") for impl in args.impls}
+        for _ in range(args.rounds):
+            for impl in args.impls:
+                ga, gf, _ = graphs[impl]
+                tt = []
+                for gr in (ga, gf):
+                    gr.replay()
+                    ev0.record()
+                    gr.replay()
+                    ev1.record()
+                    ev1.synchronize()
+                    tt.append(ev0.elapsed_time(ev1))
+                best[impl] = min(best[impl], (tt[0] - tt[1]) * 1000.0 / args.reps)
+        for impl in args.impls:
+            res = {"op": "attn_decode_graph", "model": args.model, "tp": args.tp, "b": b, "t": t, "cache_len": tc,
+                   "impl": impl, "us": round(best[impl], 2), "max_diff_vs_first": round(graphs[impl][2], 5)}
+            print(json.dumps(res), flush=True)
+        del graphs, kc, vc
+
+
+if __name__ == "__main__":
+    main()

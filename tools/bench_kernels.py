@@ -133,6 +133,7 @@ def main():
             impl = impl % 100
             e.attn_set_impl(impl, target)
             e.attn_set_v3_kpg(kpg)
+            e.attn_set_v3_max_pairs(0 if impl == 1 else 4096)  # impl 1: the split v1 kernel even at small batch
             us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
             o = ops.attention(q, kc, vc, slot, ks).float()
             ref_out = o if ref_out is None else ref_out
@@ -143,6 +144,7 @@ def main():
         e.attn_set_diag(0)
         e.attn_set_impl(2, 4096)
         e.attn_set_v3_kpg(0)
+        e.attn_set_v3_max_pairs(4096)
         del kc, vc
 
 

@@ -97,6 +97,20 @@ void residual_add(Tensor h, Tensor p, Tensor hb) {
      "residual_add");
 }
 
+// load every byte of t with the default cache policy (Infinity Cache warm-up of the next projection's weights)
+void prefetch(Tensor t, int64_t grid) {
+  check(t.is_cuda() && t.is_contiguous(), "prefetch: contiguous GPU tensor");
+  static unsigned* sink = nullptr;  // allocated at the first (eager) call: never inside a graph capture
+  if (!sink) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(stream(), &st);
+    check(st == hipStreamCaptureStatusNone, "prefetch: first call under graph capture");
+    rc((int)hipMalloc(reinterpret_cast<void**>(&sink), 64), "prefetch sink");
+  }
+  const int64_t nbytes = t.numel() * t.element_size() / 16 * 16;
+  rc(jla::prefetch(t.data_ptr(), nbytes, (int)grid, sink, stream()), "prefetch");
+}
+
 // y [M, N] = x [M, K] @ w [N, K]^T, all fp32 (precision='highest' lm_head)
 void gemm_f32(Tensor x, Tensor w, Tensor y) {
   check_gpu(x, "x");
@@ -652,6 +666,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("rmsnorm", &rmsnorm);
   m.def("residual_add", &residual_add);
   m.def("gemm_f32", &gemm_f32);
+  m.def("prefetch", &prefetch, py::arg("t"), py::arg("grid") = 128);
   m.def("linear_skinny", &linear_skinny, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"),
         py::arg("mode"), py::arg("rms_eps"), py::arg("accumulate"), py::arg("variant"), py::arg("ws"),
         py::arg("tickets"), py::arg("mirror") = py::none(), py::arg("x_packed") = py::none(),
@@ -729,6 +744,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("hb"), py::arg("two_shot") = false, py::arg("hb_pack") = py::none());
   m.def("car_pairs", &car_pairs, py::arg("state"), py::arg("mode"), py::arg("vals"), py::arg("idx"),
         py::arg("idx_offset"), py::arg("k"), py::arg("out_v").none(true), py::arg("out_i"));
+  m.def("car_set_gran_max", [](int64_t n) { jla::car_set_gran_max(n); });
   m.def("car_error", [](int64_t st) { return jla::car_error(reinterpret_cast<void*>(st)); });
   m.def("car_destroy", [](int64_t st) { jla::car_destroy(reinterpret_cast<void*>(st)); });
   m.def("car_free", [](int64_t buf, int64_t sig) {

@@ -297,6 +297,88 @@ __global__ void __launch_bounds__(CAR_THREADS)
   car_end(d, b, &st);
 }
 
+// ---- granule one-shot (decode-sized messages): no flag, no barrier -------------------------------------
+// Every 4 payload bytes travel as one 8-byte granule {data, tag} written by ONE store (16-B sc0 sc1 stores = two
+// granules, each observed untorn on gfx950; MI355X_MICROARCH.md handoff-1to1 vs handoff-flag), tag = the call's epoch
+// (a quiet-NaN pattern, never a payload of a working model), so the consumer polls the data itself: one memory round
+// trip instead of payload -> vmcnt(0) drain -> flag store -> flag poll -> payload load. The granules of payload chunk c
+// (2 KiB of payload, 4 KiB of granules) occupy exactly the A-slot bytes of chunk c, so the block ownership and parity
+// rules of the flag protocol hold unchanged (the kernels mix freely on one state).
+constexpr int GRAN_THREADS = 128;
+constexpr int GRAN_PAYLOAD = GRAN_THREADS * 16;  // payload bytes per chunk (4 KiB of granules)
+static_assert(2 * GRAN_PAYLOAD == CAR_CHUNK, "a granule chunk covers one reduce chunk's bytes");
+
+JLA_DEV unsigned gran_tag(int calls) { return 0x7FC00000u | ((unsigned)calls & 0x003FFFFFu); }
+
+template <int OP, bool BF16>
+__global__ void __launch_bounds__(GRAN_THREADS)
+    car_gran_kernel(const char* __restrict__ in, void* __restrict__ out, float* __restrict__ h,
+                    bf16_t* __restrict__ hb, long long nbytes, const CarDevice* __restrict__ dev,
+                    bf16_t* __restrict__ hb_pack, int pack_cols) {
+  const CarDevice& d = *dev;
+  constexpr int ESZ = BF16 ? 2 : 4;
+  constexpr int N = 16 / ESZ;
+  const int b = blockIdx.x;
+  const long long nchunks = (nbytes + GRAN_PAYLOAD - 1) / GRAN_PAYLOAD;
+  if (b >= nchunks) return;
+  __shared__ CarCalls st;
+  const long long off0 = (long long)b * GRAN_PAYLOAD + (long long)threadIdx.x * 16;
+  const bool have0 = off0 < nbytes;
+  u32x4 in0 = {0u, 0u, 0u, 0u};
+  f32x4 h0a = {0.f, 0.f, 0.f, 0.f}, h0b = {0.f, 0.f, 0.f, 0.f};
+  if (have0) {
+    in0 = *reinterpret_cast<const u32x4*>(in + off0);
+    if constexpr (OP == OP_RESID) {
+      h0a = *reinterpret_cast<const f32x4*>(h + off0 / ESZ);
+      if constexpr (N == 8) h0b = *reinterpret_cast<const f32x4*>(h + off0 / ESZ + 4);
+    }
+  }
+  const int parity = car_begin(d, b, &st);
+  const unsigned tag = gran_tag(st.calls);
+  const long long slot = d.max_bytes;
+  const long long a_off = (long long)parity * d.world * slot;
+  const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
+  // 1. push: granules of this rank's payload into slot `rank` of every peer
+  for (long long c = b; c < nchunks; c += CAR_GRID) {
+    const long long off = c * GRAN_PAYLOAD + (long long)threadIdx.x * 16;
+    if (off >= nbytes) continue;
+    const u32x4 v = c == b ? in0 : *reinterpret_cast<const u32x4*>(in + off);
+    const long long g = a_off + (long long)d.rank * slot + 2 * off;  // granule bytes: 2 x payload offset
+    const u32x4 g0 = {v[0], tag, v[1], tag}, g1 = {v[2], tag, v[3], tag};
+    for (int p = 0; p < d.world; ++p) {
+      st_sys16(rsrc(d.buf[p]), g, g0);
+      st_sys16(rsrc(d.buf[p]), g + 16, g1);
+    }
+  }
+  // 2. per 16 payload bytes: poll every rank's two granule pairs until they carry this call's tag, sum in rank order
+  const bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  for (long long c = b; c < nchunks; c += CAR_GRID) {
+    const long long off = c * GRAN_PAYLOAD + (long long)threadIdx.x * 16;
+    if (off >= nbytes) continue;
+    Piece<BF16> acc;
+    for (int p = 0; p < d.world; ++p) {
+      const long long g = a_off + (long long)p * slot + 2 * off;
+      u32x4 g0 = ld_sys16(mine, g), g1 = ld_sys16(mine, g + 16);
+      if (!give_up && (g0[1] != tag || g0[3] != tag || g1[1] != tag || g1[3] != tag)) {
+        const long long t0 = (long long)wall_clock64();
+        while (g0[1] != tag || g0[3] != tag || g1[1] != tag || g1[3] != tag) {
+          if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
+            __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          g0 = ld_sys16(mine, g);
+          g1 = ld_sys16(mine, g + 16);
+        }
+      }
+      const u32x4 v = {g0[0], g0[2], g1[0], g1[2]};
+      if (p == 0) acc.set(v); else acc.add(v);
+    }
+    car_epilogue<OP, BF16>(acc.v, off / ESZ, out, h, hb, hb_pack, pack_cols, OP == OP_RESID && c == b, h0a, h0b);
+  }
+  car_end(d, b, &st);
+}
+
 // (value, index) pairs: granule i = (a[i], b[i] + idx_offset)
 template <int MODE>
 __global__ void __launch_bounds__(CAR_THREADS)
@@ -458,6 +540,10 @@ static void launch_reduce(int two_shot, int grid, const void* in, void* out, flo
                                                                     hb_pack, pack_cols);
 }
 
+// granule one-shot up to this many payload bytes per rank (the granules take 2x the bytes of the A slot)
+static long long g_car_gran_max = 256 << 10;
+void car_set_gran_max(long long n) { g_car_gran_max = n; }
+
 // op 0: out = sum(in) (same dtype); op 1: h += sum(in), hb = bf16(h) (h fp32, hb bf16, element count of in)
 int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t* hb, long long nbytes, int is_bf16,
                int two_shot, hipStream_t s, bf16_t* hb_pack, int pack_cols) {
@@ -467,6 +553,22 @@ int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t*
   if (op == OP_RESID && (!h || !hb)) return -1;
   if (hb_pack && (op != OP_RESID || pack_cols <= 0 || (pack_cols & 31))) return -1;
   if (two_shot && st->h.world == 1) two_shot = 0;
+  if (!two_shot && nbytes <= g_car_gran_max && 2 * nbytes <= st->h.max_bytes) {
+    const long long gch = (nbytes + GRAN_PAYLOAD - 1) / GRAN_PAYLOAD;
+    const int ggrid = (int)(gch < CAR_GRID ? gch : CAR_GRID);
+    const char* ip = static_cast<const char*>(in);
+#define JLA_GRAN(OPV, BFV)                                                                                          \
+  car_gran_kernel<OPV, BFV><<<ggrid, GRAN_THREADS, 0, s>>>(ip, out, h, hb, nbytes, st->d, OPV == OP_RESID ? hb_pack : nullptr, \
+                                                          OPV == OP_RESID ? pack_cols : 0)
+    if (op == OP_SUM) {
+      if (is_bf16) JLA_GRAN(OP_SUM, true); else JLA_GRAN(OP_SUM, false);
+    } else {
+      if (is_bf16) JLA_GRAN(OP_RESID, true); else JLA_GRAN(OP_RESID, false);
+    }
+#undef JLA_GRAN
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
   const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
   const int grid = (int)(nchunks < CAR_GRID ? nchunks : CAR_GRID);
   if (op == OP_SUM) {

@@ -1082,8 +1082,13 @@ static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv)
 static int g_v3_kpg_mult = 0;
 void attn_set_v3_kpg(int mult) { g_v3_kpg_mult = mult >= 4 ? 4 : (mult >= 2 ? 2 : (mult == 1 ? 1 : 0)); }
 // v5 (split small-batch kernel) below g_attn_v5_max_pairs (row, kv head) pairs, ahead of v3
+// (measured with tools/bench_attn_decode.py, profiles/r3_attn_decode_v5_vs_v3.jsonl: at rep 8 -- Llama-3-70B at MP 8 --
+// v3 is compute-bound on one CU per pair, so v5 wins 1.5-2x up to 32 pairs and further; at rep 4 -- Llama-3-8B -- the
+// two tie at 64 pairs and v3 wins at 128)
 static bool use_v5(int B, int Hkv, int rep) {
-  return g_attn_impl == 2 && rep <= 16 && (rep & (rep - 1)) == 0 && B * Hkv <= g_attn_v5_max_pairs;
+  const int pairs = B * Hkv;
+  return g_attn_impl == 2 && rep <= 16 && (rep & (rep - 1)) == 0 &&
+         (pairs <= g_attn_v5_max_pairs || (rep >= 8 && pairs <= 4 * g_attn_v5_max_pairs));
 }
 int attn_decode_packs(int B, int Hkv, int rep) { return (use_v5(B, Hkv, rep) || use_v3(B, Hkv, rep)) ? 1 : 0; }
 

@@ -14,6 +14,7 @@ int embedding(const int32_t* ids, const bf16_t* table, float* out, bf16_t* mirro
 int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int residual_add(float* h, const void* p, int p_bf16, bf16_t* hb, long long n, hipStream_t s);
+int prefetch(const void* p, long long nbytes, int grid, unsigned* sink, hipStream_t s);
 int gemm_f32(const float* x, const float* w, float* y, int M, int N, int K, hipStream_t s);
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
 
@@ -128,6 +129,7 @@ int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t*
 // all-gather of (fp32, int32 + idx_offset) pairs: mode 0 = first max over ranks per pair, mode 1 = [n/k][world*k]
 int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_offset, long long n, int k,
               float* out_a, int32_t* out_b, hipStream_t s);
+void car_set_gran_max(long long n);  // granule one-shot up to n payload bytes per rank (0: flag protocol only)
 int car_error(void* state);
 int car_world(void* state);
 void car_destroy(void* state);

@@ -155,6 +155,35 @@ int residual_add(float* h, const void* p, int p_bf16, bf16_t* hb, long long n, h
   return 0;
 }
 
+// Cache warm-up of a stream: every byte of [p, p + n16 * 16) is loaded with the default cache policy (allocates in the
+// 256 MiB Infinity Cache) and discarded. Diagnostic (tools/bench_prefetch.py, tools/graph_concurrency.py): a decode
+// GEMV whose weights were just warmed this way runs no faster (profiles/r3_prefetch_gemv.jsonl), so the model does
+// not use it. 16 loads in flight per lane; the xor keeps the loads alive (the sink is written only when it
+// matches `key`, a condition the compiler cannot see through and the host never arranges).
+__global__ void __launch_bounds__(256) prefetch_kernel(const u32x4* __restrict__ p, long long n16,
+                                                       unsigned* __restrict__ sink, unsigned key) {
+  constexpr int U = 16;
+  unsigned acc = 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u][0] ^ v[u][3];
+  }
+  for (; i < n16; i += stride) acc ^= p[i][1];
+  if (acc == key) sink[0] = acc;  // (practically) never true, but the loads must happen to know
+}
+
+int prefetch(const void* p, long long nbytes, int grid, unsigned* sink, hipStream_t s) {
+  if (nbytes <= 0) return 0;
+  prefetch_kernel<<<grid, 256, 0, s>>>(static_cast<const u32x4*>(p), nbytes / 16, sink, 0x9e3779b9u);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 JLA_BOUNDS_ACCESSOR(norm_embed)
 
 }  // namespace jla

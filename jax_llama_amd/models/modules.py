@@ -66,6 +66,7 @@ class LLaMAMLP:
         m, lw = self.model, self.model.layers[self.layer_idx]
         g = ops.linear_swiglu(hb, lw.gu, rms_eps=m.eps, x_packed=pk.hb_in() if pk else None,
                               out_packed=pk.act if pk else None)
+
         m._row_parallel(g, lw.down, h, hb, x_packed=pk.act if pk else None, mirror_packed=pk.hb if pk else None)
 
 

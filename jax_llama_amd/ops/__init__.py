@@ -112,6 +112,15 @@ def residual_add_(h: torch.Tensor, p: torch.Tensor, mirror: Optional[torch.Tenso
     return h
 
 
+PREFETCH_GRID = int(os.environ.get("JLA_PREFETCH_GRID", "128"))
+
+
+def prefetch(t: torch.Tensor) -> None:
+    """Load every byte of ``t`` with the default cache policy (warms the Infinity Cache; GPU only, no result)."""
+    if _is_gpu(t):
+        ext().prefetch(t, PREFETCH_GRID)
+
+
 def linear_f32(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x [M, K] @ w [N, K]^T`` with fp32 inputs, accumulation and output (precision='highest' lm_head; GPU: the
     exact-f32 MFMA kernel, csrc/kernels/gemm_f32.hip)."""

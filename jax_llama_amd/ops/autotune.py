@@ -198,24 +198,45 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
 
 
 def _measure(x, w, run, cands) -> int:
+    """Time every candidate on rotating scratch weights (> the Infinity Cache, so each call streams from HBM).
+    Decode GEMVs take 3-20 us, below the host's launch rate, so eager back-to-back calls would time the host: the
+    calls are captured into one hipGraph per candidate and the graph replay is timed (as the decode step runs them)."""
     nbytes = w.weight.numel() * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws = [torch.empty_like(w.weight).normal_(0, 0.02) for _ in range(copies)]
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for v in cands:
+    for v in cands:  # warm-up: code objects, workspaces (nothing may be allocated under capture)
         for i in range(2):
             run(v, x, ws[i % copies])
-    times = {v: float("inf") for v in cands}
+    torch.cuda.synchronize()
     iters = 2 * copies
+    graphs = {}
+    for v in cands:
+        if v == TILED_VARIANT:  # its plan (and workspace) is chosen per call: timed eagerly (a long kernel anyway)
+            graphs[v] = None
+            continue
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                for i in range(iters):
+                    run(v, x, ws[i % copies])
+            graphs[v] = g
+        except RuntimeError:  # a candidate that cannot be captured is timed eagerly
+            graphs[v] = None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    times = {v: float("inf") for v in cands}
     for _ in range(TUNE_ROUNDS):  # interleaved rounds, min per candidate (see _measure_plan)
         for v in cands:
+            g = graphs[v]
             ev0.record()
-            for i in range(iters):
-                run(v, x, ws[i % copies])
+            if g is not None:
+                g.replay()
+            else:
+                for i in range(iters):
+                    run(v, x, ws[i % copies])
             ev1.record()
             ev1.synchronize()
             times[v] = min(times[v], ev0.elapsed_time(ev1) / iters)
-    del ws
+    del ws, graphs
     return min(cands, key=times.get)
 
 

@@ -9,6 +9,7 @@ There is exactly one GPU implementation per op (no backend selection, no Triton)
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Optional
 
@@ -44,9 +45,20 @@ class _Workspace:
         # bumped on every (re)allocation: a captured hipGraph that recorded these buffers' addresses is
         # stale once it changes (runtime/engine.py recaptures)
         self.generation = 0
+        self._scope = ""
+
+    @contextlib.contextmanager
+    def scope(self, tag: str):
+        """Buffers requested inside get their own copies under ``tag``: work issued concurrently on another stream
+        (the engine's decode micro-batches) must not share split-K slabs, tickets or attention partials."""
+        prev, self._scope = self._scope, tag + "/"
+        try:
+            yield
+        finally:
+            self._scope = prev
 
     def get(self, name: str, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
-        key = (name, device, dtype)
+        key = (self._scope + name, device, dtype)
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < numel:
             buf = torch.empty(max(numel, 1), dtype=dtype, device=device)
@@ -56,7 +68,7 @@ class _Workspace:
 
     def get_zeroed(self, name: str, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
         """Zero-initialised on (re)allocation only: for self-resetting device counters."""
-        key = ("zeroed:" + name, device, dtype)
+        key = ("zeroed:" + self._scope + name, device, dtype)
         buf = self._bufs.get(key)
         if buf is None or buf.numel() < numel:
             buf = torch.zeros(max(numel, 1), dtype=dtype, device=device)

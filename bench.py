@@ -259,8 +259,8 @@ def _tp_rank_proxy(args):
     from jax_llama_amd.parallel import TPRankProxyComm
     from jax_llama_amd.runtime.benchmark import decode_latency
 
-    comm = TPRankProxyComm.create(args.proxy_tp)
     cfg = get_preset(args.proxy_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+    comm = TPRankProxyComm.create(args.proxy_tp, fused_hidden=cfg.hidden_size)
     model = LLaMAForCausalLM(cfg, device="cuda", comm=comm, _do_init=False).init_random(seed=4321)
     out = {"model": args.proxy_model, "mp": args.proxy_tp, "rank": 0,
            "note": "one rank's shards and launches; collectives on a world-1 instance of the custom kernels "
@@ -306,9 +306,10 @@ def _tp_points(args, ctx, res):
            args.prompt_len + args.gen_len}
     try:
         ctx.setup_mesh(tp=world)
-        comm = TPComm.from_context(ctx)
-        out["custom_allreduce"] = comm.custom is not None
         cfg = get_preset(tp_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+        comm = TPComm.from_context(ctx, fused_hidden=cfg.hidden_size)
+        out["custom_allreduce"] = comm.custom is not None
+        out["fused_row_parallel"] = comm.fused is not None
         model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm, _do_init=False).init_random(seed=4321)
         out["weight_gb_per_gpu"] = round(model.weight_bytes() / 1e9, 3)
         out["hbm_roofline_ms_per_token"] = round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)

@@ -133,7 +133,9 @@ def build_C(jobs: int, force: bool, debug_bounds: bool = False) -> Path:
     bobj = odir / "bindings.o"
     if force or _stale(bobj, [bsrc, *headers]):
         inc = [f"-I{p}" for p in tinc] + [f"-I{_py_include()}", f"-I{CSRC}"]
-        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
+        # host code only (no kernels in the bindings): skip the device pass
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "--offload-host-only",
+              "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM",
               f"-DTORCH_EXTENSION_NAME={name}", *extra, "-DTORCH_API_INCLUDE_EXTENSION_H", "-D_GLIBCXX_USE_CXX11_ABI=1",
               "-Wno-deprecated-declarations", "-Wno-unused-result", *inc, "-c", str(bsrc), "-o", str(bobj)])
     out = PKG / f"{name}{EXT_SUFFIX}"

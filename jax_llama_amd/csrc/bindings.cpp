@@ -9,6 +9,7 @@
 #include "kernels/launchers.h"
 
 #define MODE_QKV_ID 3
+#define MODE_TPRESID_ID 9
 #define MODE_ARGMAX_ID 8  // common.h MODE_ARGMAX
 
 namespace {
@@ -626,6 +627,34 @@ void car_allreduce_residual(int64_t state, Tensor partial, Tensor h, Tensor hb, 
      "car_allreduce_residual");
 }
 
+// fused row-parallel decode projection (gemv.hip MODE_TPRESID): h (fp32) += sum over the TP group of x @ W^T, the
+// partials exchanged as tagged granules in the GEMV's own epilogue; hb = bf16(h) (+ its packed copy). `state` is a
+// custom all-reduce instance reserved for this path (its per-workgroup counters must not be shared)
+void linear_tp_residual(int64_t state, Tensor x, Tensor w, int64_t n, int64_t k, Tensor h, Tensor hb, int64_t variant,
+                        c10::optional<Tensor> x_packed, c10::optional<Tensor> hb_pack) {
+  check_gpu(x, "x");
+  check_gpu(h, "h");
+  check_gpu(hb, "hb");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
+  const int64_t m = x.size(0);
+  check(m >= 1 && m <= SKINNY_MAX_M, "linear_tp_residual: 1 <= M <= 64");
+  check(h.scalar_type() == torch::kFloat32 && h.numel() == m * n && hb.scalar_type() == torch::kBFloat16 &&
+            hb.numel() == m * n, "h fp32 / hb bf16 [M, N]");
+  check(variant != 0 && variant != 4 && variant != 7, "linear_tp_residual: GEMV variants only");
+  void* st = reinterpret_cast<void*>(state);
+  // one TPRES_REGION per workgroup (at most 4096 workgroups: the counters), inside one slot
+  const int64_t groups = n / 16;  // upper bound (1 tile per workgroup)
+  check(groups <= jla::CAR_WG_COUNTERS && groups * jla::TPRES_REGION <= jla::car_max_bytes(st),
+        "linear_tp_residual: too many workgroups for the buffer");
+  jla::QKVArgs qa{};
+  qa.res_bf16 = bf(hb);
+  qa.pack = packed_ptr(hb_pack, m, n, "hb_pack");
+  qa.tp = jla::car_device(st);
+  run_skinny(x, w, n, k, h.data_ptr(), MODE_TPRESID_ID, -1.0, true, true, &qa, variant, Tensor(), Tensor(),
+             packed_ptr(x_packed, m, k, "x_packed"));
+}
+
 // (value fp32, index int32) all-gathers of the vocab-parallel sampler. mode 0: out_i[n] = index of the first max over
 // ranks (out_v optional); mode 1: out_v/out_i [n / k, world * k]
 void car_pairs(int64_t state, int64_t mode, Tensor vals, Tensor idx, int64_t idx_offset, int64_t k,
@@ -712,6 +741,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);
+  m.def("linear_tp_residual", &linear_tp_residual, py::arg("state"), py::arg("x"), py::arg("w"), py::arg("n"),
+        py::arg("k"), py::arg("h"), py::arg("hb"), py::arg("variant"), py::arg("x_packed") = py::none(),
+        py::arg("hb_pack") = py::none());
   m.def("bounds_error", [](bool reset) {
     const int r = reset ? 1 : 0;
     return (int64_t)(jla::jla_bounds_norm_embed(r) | jla::jla_bounds_rope_kv(r) | jla::jla_bounds_sample(r) |

@@ -43,13 +43,12 @@
 //   car_pairs_kernel<MODE>    all-gather of (fp32 value, int32 index) pairs (8-byte granules):
 //         MODE_ARGMAX  per row the first max in rank order (vocab-parallel greedy token)
 //         MODE_TOPK    per-rank top-k candidates laid out [B][world * k] for the final merge/sample
+#include "car.h"
 #include "common.h"
 #include "launchers.h"
 
 namespace jla {
 
-constexpr int CAR_MAX_WORLD = 8;
-constexpr int CAR_BLOCKS = 64;   // signal rows (one per block)
 constexpr int CAR_GRID = 63;     // chunk c -> block c % CAR_GRID on every call (fixed mapping)
 constexpr int CAR_THREADS = 256;
 constexpr int CAR_CHUNK = CAR_THREADS * 16;  // input bytes per block iteration
@@ -58,36 +57,6 @@ constexpr int CAR_PAIRS_PER_THREAD = CAR_PAIR_CHUNK / CAR_THREADS;
 
 enum { OP_SUM = 0, OP_RESID = 1 };
 enum { PAIRS_ARGMAX = 0, PAIRS_TOPK = 1 };
-
-struct CarDevice {
-  char* buf[CAR_MAX_WORLD];     // every rank's buffer (A then R), mapped here
-  int* sig[CAR_MAX_WORLD];      // every rank's flags [CAR_BLOCKS][CAR_MAX_WORLD]
-  int2* ctr;                    // [CAR_BLOCKS] {calls made, barriers passed} by block b (local): ONE 8-byte load
-                                // at the start of a call gives both the parity and the flag epoch
-  int* error;                   // 1 once a wait timed out
-  long long max_bytes;          // A slot size; R holds 2 * max_bytes per parity
-  long long timeout_ticks;      // wall-clock ticks (s_memrealtime, 100 MHz) before giving up
-  int rank, world;
-};
-
-// ---- system-scope (sc0 sc1) vector accesses through buffer resources ---------------------------
-constexpr int SYS = 17;  // cache policy bits: sc0 | sc1
-
-JLA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-}
-JLA_DEV void st_sys16(__amdgpu_buffer_rsrc_t r, long long off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, SYS);
-}
-JLA_DEV u32x4 ld_sys16(__amdgpu_buffer_rsrc_t r, long long off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, SYS);
-}
-JLA_DEV void st_sys8(__amdgpu_buffer_rsrc_t r, long long off, u32x2 v) {
-  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, SYS);
-}
-JLA_DEV u32x2 ld_sys8(__amdgpu_buffer_rsrc_t r, long long off) {
-  return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, SYS);
-}
 
 // Per-call state of block b, in LDS: the call and barrier counters are read once at the start (uncached memory:
 // every access is a memory round trip) and written back once at the end.
@@ -308,7 +277,6 @@ constexpr int GRAN_THREADS = 128;
 constexpr int GRAN_PAYLOAD = GRAN_THREADS * 16;  // payload bytes per chunk (4 KiB of granules)
 static_assert(2 * GRAN_PAYLOAD == CAR_CHUNK, "a granule chunk covers one reduce chunk's bytes");
 
-JLA_DEV unsigned gran_tag(int calls) { return 0x7FC00000u | ((unsigned)calls & 0x003FFFFFu); }
 
 template <int OP, bool BF16>
 __global__ void __launch_bounds__(GRAN_THREADS)
@@ -444,7 +412,11 @@ struct CarHost {
 size_t car_buffer_bytes(long long max_bytes, int world) {
   return (size_t)2 * world * max_bytes + (size_t)2 * 2 * max_bytes;
 }
-size_t car_signal_bytes() { return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 1024; }
+// flags [CAR_BLOCKS][CAR_MAX_WORLD], then ctr [CAR_BLOCKS] (int2), the error word, and the per-workgroup call counters
+// of the fused row-parallel GEMV (gemv.hip MODE_TPRESID)
+size_t car_signal_bytes() {
+  return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 1024 + (size_t)CAR_WG_COUNTERS * sizeof(int);
+}
 
 int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemHandle_t* hbuf,
               hipIpcMemHandle_t* hsig) {
@@ -516,6 +488,7 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   int* tail = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int));
   st->h.ctr = reinterpret_cast<int2*>(tail);  // [CAR_BLOCKS] {calls, barriers}
   st->h.error = tail + 2 * CAR_BLOCKS;
+  st->h.wg_ctr = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 1024);
   st->d = nullptr;
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&st->d), sizeof(CarDevice));
   if (e == hipSuccess) e = hipMemcpy(st->d, &st->h, sizeof(CarDevice), hipMemcpyHostToDevice);
@@ -601,6 +574,8 @@ int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_o
 }
 
 int car_world(void* state) { return static_cast<CarHost*>(state)->h.world; }
+const void* car_device(void* state) { return static_cast<CarHost*>(state)->d; }
+long long car_max_bytes(void* state) { return static_cast<CarHost*>(state)->h.max_bytes; }
 
 int car_error(void* state) {
   CarHost* st = static_cast<CarHost*>(state);

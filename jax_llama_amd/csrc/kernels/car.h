@@ -1,0 +1,46 @@
+// Custom xGMI collective state shared by the collective kernels (allreduce.hip) and the GEMV's fused row-parallel
+// epilogue (gemv.hip MODE_TPRESID): every rank's IPC-mapped buffers, counters, the error word, and the system-scope
+// (sc0 sc1) buffer accesses every hand-off byte goes through.
+#pragma once
+#include "common.h"
+#include "launchers.h"
+
+namespace jla {
+
+constexpr int CAR_MAX_WORLD = 8;
+constexpr int CAR_BLOCKS = 64;         // signal rows (one per collective block)
+
+struct CarDevice {
+  char* buf[CAR_MAX_WORLD];     // every rank's buffer (A then R), mapped here
+  int* sig[CAR_MAX_WORLD];      // every rank's flags [CAR_BLOCKS][CAR_MAX_WORLD]
+  int2* ctr;                    // [CAR_BLOCKS] {calls made, barriers passed} by block b (local): ONE 8-byte load
+                                // at the start of a call gives both the parity and the flag epoch
+  int* error;                   // 1 once a wait timed out
+  int* wg_ctr;                  // [CAR_WG_COUNTERS] calls made by fused-GEMV workgroup w (local; parity + tag)
+  long long max_bytes;          // A slot size; R holds 2 * max_bytes per parity
+  long long timeout_ticks;      // wall-clock ticks (s_memrealtime, 100 MHz) before giving up
+  int rank, world;
+};
+
+constexpr int SYS = 17;  // cache policy bits: sc0 | sc1
+
+JLA_DEV __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+JLA_DEV void st_sys16(__amdgpu_buffer_rsrc_t r, long long off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, SYS);
+}
+JLA_DEV u32x4 ld_sys16(__amdgpu_buffer_rsrc_t r, long long off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, SYS);
+}
+JLA_DEV void st_sys8(__amdgpu_buffer_rsrc_t r, long long off, u32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, SYS);
+}
+JLA_DEV u32x2 ld_sys8(__amdgpu_buffer_rsrc_t r, long long off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, SYS);
+}
+
+// granule tag of a call: a quiet-NaN pattern (never a payload of a working model) carrying the call count
+JLA_DEV unsigned gran_tag(int calls) { return 0x7FC00000u | ((unsigned)calls & 0x003FFFFFu); }
+
+}  // namespace jla

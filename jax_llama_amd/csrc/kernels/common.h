@@ -25,6 +25,7 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #define MODE_SWIGLU 2
 #define MODE_QKV 3
 #define MODE_ARGMAX 8
+#define MODE_TPRESID 9  // row-parallel partial -> granule all-reduce over the TP group -> residual (gemv.hip)
 
 // ---- bounds-checked debug build (python build.py --debug-bounds -> jax_llama_amd/_C_dbg*.so, loaded when
 // JLA_DEBUG_BOUNDS=1). The kernels clamp or skip out-of-range indices that come from device state (token ids,

@@ -23,6 +23,7 @@
 //     interleaved [w1;w3] weight, or (QKV mode) rotates q/k pairs with RoPE and writes q plus the
 //     k/v cache rows at the device-side cache slot.
 // No atomics: results are deterministic and the residual add happens exactly once.
+#include "car.h"
 #include "common.h"
 #include "launchers.h"
 #include "ring.h"
@@ -59,6 +60,14 @@ __global__ void __launch_bounds__(NW * 64)
   }
   const u32x4* zfrag = g_zero_frag + lane;
   const XT* zx = reinterpret_cast<const XT*>(g_zero_frag);
+  // MODE_TPRESID: this workgroup's call counter (parity + granule tag), read now so the uncached round trip hides
+  // behind the weight stream
+  int tp_calls = 0;
+  if constexpr (MODE == MODE_TPRESID) {
+    if (threadIdx.x == 0)
+      tp_calls = __hip_atomic_load(static_cast<const CarDevice*>(qa.tp)->wg_ctr + blockIdx.x, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   const int n = (KS - w + NW - 1) / NW;  // k-steps of this wave: ks = w + i*NW, i < n
 
@@ -139,6 +148,9 @@ __global__ void __launch_bounds__(NW * 64)
       if (lane < 16) red_ss[(w * MT + mt) * 16 + lane] = s;
     }
   }
+  if constexpr (MODE == MODE_TPRESID) {
+    if (threadIdx.x == 0) reinterpret_cast<int*>(inv_rms + MT * 16)[0] = tp_calls + 1;
+  }
   __syncthreads();
   if (threadIdx.x < MT * 16) {
     float r = 1.f;
@@ -176,6 +188,70 @@ __global__ void __launch_bounds__(NW * 64)
         if (qa.pack) qa.pack[pack_off(m, (gtile >> 1) * 16 + c, F)] = r;
       }
     }
+  } else if constexpr (MODE == MODE_TPRESID) {
+    // ---- row-parallel partial all-reduced in the epilogue (no separate collective launch): every rank's workgroup
+    // blockIdx.x computes the same (rows, columns) of its own K shard. Each even-column lane packs its value and its
+    // neighbour's (RNE to bf16, as the unfused partial) into one 8-byte granule {2 x bf16, tag} and stores it into
+    // slot [parity][rank] of every peer (this workgroup's fixed TPRES_REGION), then polls the same granule of every
+    // rank's slot in its own buffer until it carries this call's tag, sums in rank order in fp32 and applies the
+    // residual epilogue (h += sum, mirror, packed mirror). Workgroup w pairs only with workgroup w of the peers and
+    // its counter orders its calls, so the parity argument of allreduce.hip holds per workgroup; bit-identical to
+    // partial + car_reduce_kernel (same roundings, same order).
+    const CarDevice& d = *static_cast<const CarDevice*>(qa.tp);
+    const int calls = reinterpret_cast<const int*>(inv_rms + MT * 16)[0];
+    const unsigned tag = gran_tag(calls);
+    const long long wg_base = (long long)blockIdx.x * TPRES_REGION;
+    const long long par_base = (long long)(calls & 1) * d.world * d.max_bytes;
+    const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
+    float* h = static_cast<float*>(out);
+    for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
+      const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
+      const int m = mt * 16 + ml;
+      const int ln = (ml >> 2) * 16 + c, i = ml & 3;
+      const float v = reduced(mt, t, ln, i);
+      const float vn = __shfl_down(v, 1, 64);  // column c + 1 (lanes e, e + 1 are adjacent)
+      if ((c & 1) || m >= M || nt0 + t >= NTT) continue;
+      const long long g = wg_base + ((long long)m * (NT * 16) + t * 16 + c) * 4;  // granule (m, c / 2): 8 bytes
+      const u32x2 gv = {pack2bf(v, vn), tag};
+      for (int p = 0; p < d.world; ++p) st_sys8(rsrc(d.buf[p]), par_base + (long long)d.rank * d.max_bytes + g, gv);
+    }
+    const bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
+      const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
+      const int m = mt * 16 + ml;
+      if ((c & 1) || m >= M || nt0 + t >= NTT) continue;
+      const long long g = wg_base + ((long long)m * (NT * 16) + t * 16 + c) * 4;
+      float s0 = 0.f, s1 = 0.f;
+      for (int p = 0; p < d.world; ++p) {
+        const long long off = par_base + (long long)p * d.max_bytes + g;
+        u32x2 r = ld_sys8(mine, off);
+        if (r[1] != tag && !give_up) {  // slow path only: the common case is one load per granule
+          const long long t0 = (long long)wall_clock64();
+          while (r[1] != tag) {
+            if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
+              __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              break;
+            }
+            // another workgroup already gave up: stop too (one timeout per failure, not one per resident wave)
+            if (__hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+            __builtin_amdgcn_s_sleep(1);
+            r = ld_sys8(mine, off);
+          }
+        }
+        s0 += __uint_as_float(r[0] << 16);
+        s1 += __uint_as_float(r[0] & 0xffff0000u);
+      }
+      const int col = (nt0 + t) * 16 + c;
+      const size_t idx = (size_t)m * N + col;
+      const float2 hv = *reinterpret_cast<const float2*>(h + idx);
+      const float n0 = hv.x + s0, n1 = hv.y + s1;
+      *reinterpret_cast<float2*>(h + idx) = make_float2(n0, n1);
+      const uint32_t pk = pack2bf(n0, n1);
+      if (qa.res_bf16) *reinterpret_cast<uint32_t*>(qa.res_bf16 + idx) = pk;
+      if (qa.pack) *reinterpret_cast<uint32_t*>(qa.pack + pack_off(m, col, N)) = pk;
+    }
+    if (threadIdx.x == 0)
+      __hip_atomic_store(d.wg_ctr + blockIdx.x, calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
       const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
@@ -260,7 +336,7 @@ static int launch_skinny(const void* x, const void* W, void* out, int M, int N, 
   constexpr int U = DEEP ? 2 * U1 : U1;
   const int NTT = N >> 4;
   const int grid = (NTT + NT - 1) / NT;
-  const size_t lds = sizeof(float) * (NW * MT * NT * 256 + NW * MT * 16 + MT * 16);
+  const size_t lds = sizeof(float) * (NW * MT * NT * 256 + NW * MT * 16 + MT * 16 + 4);
   auto kern = &linear_skinny_kernel<XT, MT, NT, MODE, NW, U, XP>;
   if (lds > 65536) {  // opt in to > 64 KiB of dynamic LDS once (not a stream op: capture-safe)
     static bool attr_set = false;
@@ -357,12 +433,24 @@ static int dispatch_mt(const void* x, const void* W, void* out, int M, int N, in
   return dispatch_nt<XT, 4, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
 }
 
+// the fused TP epilogue reads the bf16 decode activations only (no fp32-input instantiation)
+template <typename XT>
+static int dispatch_tp(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
+                       int accumulate, const QKVArgs& qa, int variant, hipStream_t s) {
+  if constexpr (sizeof(XT) == 2) {
+    return dispatch_mt<XT, MODE_TPRESID>(x, W, out, M, N, K, eps, use_rms, accumulate, 1, qa, variant, s);
+  } else {
+    return -1;
+  }
+}
+
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s) {
   if (M <= 0) return 0;
   if (M > SKINNY_MAX_M || (N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   if (mode == MODE_QKV && (!qkv || qkv->Dh % 16 || M % qkv->S)) return -1;
+  if (mode == MODE_TPRESID && (!qkv || !qkv->tp)) return -1;
   const int use_rms = rms_eps >= 0.f;
   const float eps = use_rms ? rms_eps : 0.f;
   QKVArgs qa{};
@@ -375,6 +463,7 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
     case MODE_SWIGLU: return dispatch_mt<XT, MODE_SWIGLU>(JLA_ARGS, 0, qa, variant, s);              \
     case MODE_QKV: return dispatch_mt<XT, MODE_QKV>(JLA_ARGS, 0, qa, variant, s);                    \
     case MODE_ARGMAX: return dispatch_mt<XT, MODE_ARGMAX>(JLA_ARGS, 0, qa, variant, s);              \
+    case MODE_TPRESID: return dispatch_tp<XT>(JLA_ARGS, qa, variant, s);                             \
     default: return -1;                                                                              \
   }
   if (x_is_f32) {

@@ -31,7 +31,11 @@ struct QKVArgs {
   bf16_t* res_bf16;           // MODE_RESIDUAL: optional bf16 mirror of the updated residual (next A operand)
   bf16_t* pack;               // optional packed-layout copy (common.h pack_off) of the bf16 output: RESIDUAL -> the
                               // mirror, SWIGLU -> the activation (GEMV only; the next projection's packed-x input)
+  const void* tp;             // MODE_TPRESID: the TP group's CarDevice (car.h) the partials are all-reduced through
 };
+// MODE_TPRESID: granule bytes each workgroup of the fused row-parallel GEMV owns in every (parity, source rank) slot
+constexpr int CAR_WG_COUNTERS = 4096;  // per-workgroup call counters of the fused GEMV (workgroups per launch)
+constexpr long long TPRES_REGION = 64 * 64 * 4;  // up to 64 rows x 64 columns x 2 bf16 per 8-byte granule
 
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
@@ -131,6 +135,8 @@ int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_o
               float* out_a, int32_t* out_b, hipStream_t s);
 void car_set_gran_max(long long n);  // granule one-shot up to n payload bytes per rank (0: flag protocol only)
 int car_error(void* state);
+const void* car_device(void* state);      // the device-side CarDevice (car.h) of an instance (MODE_TPRESID)
+long long car_max_bytes(void* state);
 int car_world(void* state);
 void car_destroy(void* state);
 int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,

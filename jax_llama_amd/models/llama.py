@@ -336,6 +336,8 @@ class LLaMAForCausalLM:
         (``comm.all_reduce_residual_``; reference ``partition.py:67,70``)."""
         if self.comm.size == 1:
             ops.linear_residual(x, w, h, mirror=hb, x_packed=x_packed, mirror_packed=mirror_packed)
+        elif self.comm.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=mirror_packed):
+            pass  # decode: the GEMV exchanged its partials itself (one kernel; comm.FUSED)
         else:
             part = ops.linear(x, w, out_dtype=self.comm.reduce_dtype, x_packed=x_packed)
             self.comm.all_reduce_residual_(part, h, hb, hb_pack=mirror_packed)

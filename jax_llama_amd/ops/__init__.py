@@ -266,6 +266,23 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None, x_packed=None
                         -1.0 if rms_eps is None else float(rms_eps), bool(accumulate), v, ws, tk, mirror)
 
 
+def linear_tp_residual(x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, state: int,
+                       x_packed: Optional[torch.Tensor] = None, hb_pack: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row-parallel decode projection with its all-reduce in the GEMV epilogue (csrc/kernels/gemv.hip
+    MODE_TPRESID): ``h (fp32) += sum over the TP group of x @ W^T``, ``hb = bf16(h)`` (+ ``hb_pack``, its packed
+    copy). ``state``: a custom all-reduce instance reserved for this path. Bit-identical to ``linear`` (bf16
+    partial) + ``TPComm.all_reduce_residual_``, minus one launch and the partial's round trip through HBM."""
+    e = ext()
+    m = x.shape[0]
+    assert x.dtype == BF16 and x.is_contiguous() and m <= e.SKINNY_MAX_M, (x.dtype, x.shape)
+    # the exchange lives in the GEMV epilogue: tune among the GEMV variants (``pack_out`` excludes split-K / tiled)
+    v = _variant(e, x, w, MODE_RESIDUAL, x_packed, pack_out=True)
+    if v in (4, TILED):
+        v = 1
+    e.linear_tp_residual(state, x, w.weight, w.n, w.k, h, hb, v, x_packed if v in XP_VARIANTS else None, hb_pack)
+    return h
+
+
 TILED = 7  # decode-kernel "variant" id of the 128x128 MFMA GEMM (split-K for mid M)
 
 

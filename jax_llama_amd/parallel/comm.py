@@ -25,23 +25,34 @@ import torch
 import torch.distributed as dist
 
 
+# GEMV-fused row-parallel all-reduce at decode (csrc/kernels/gemv.hip MODE_TPRESID); JLA_TP_FUSED=0: a separate
+# collective kernel after each row-parallel GEMV
+FUSED = os.environ.get("JLA_TP_FUSED", "1") != "0"
+
+
 def _default_reduce_dtype():
     return torch.float32 if os.environ.get("JLA_TP_REDUCE_DTYPE", "bf16") == "fp32" else torch.bfloat16
 
 
 class TPComm:
     def __init__(self, size: int = 1, rank: int = 0, group=None, custom=None,
-                 reduce_dtype: Optional[torch.dtype] = None):
+                 reduce_dtype: Optional[torch.dtype] = None, fused=None):
         self.size = size
         self.rank = rank
         self.group = group
         self.custom = custom  # parallel.custom_allreduce.CustomAllReduce or None
         self.reduce_dtype = reduce_dtype or _default_reduce_dtype()
+        # a second custom instance reserved for the GEMV-fused row-parallel all-reduce (its per-workgroup counters
+        # and slots must not interleave with the standalone collectives'); None: the standalone path only
+        self.fused = fused
 
     @classmethod
     def from_context(cls, ctx, use_custom: bool = True, max_bytes: int = 16 << 20,
-                     reduce_dtype: Optional[torch.dtype] = None, timeout_s: float = 10.0) -> "TPComm":
-        custom = None
+                     reduce_dtype: Optional[torch.dtype] = None, timeout_s: float = 10.0,
+                     fused_hidden: Optional[int] = None) -> "TPComm":
+        """``fused_hidden``: hidden size of the model, to size the GEMV-fused row-parallel all-reduce (``FUSED``;
+        default 16384 columns)."""
+        custom = fused = None
         if ctx.tp_size > 1 and ctx.device.type == "cuda" and use_custom:
             try:
                 from .custom_allreduce import CustomAllReduce
@@ -55,9 +66,17 @@ class TPComm:
                     import logging
                     logging.getLogger(__name__).warning("custom all-reduce disabled: %s", ex)
                     custom = None
+                if custom is not None and FUSED:
+                    try:
+                        fused = CustomAllReduce.create(ctx, max_bytes=CustomAllReduce.fused_bytes(
+                            fused_hidden or 16384), timeout_s=timeout_s)
+                    except CustomAllReduceError as ex:
+                        import logging
+                        logging.getLogger(__name__).warning("fused row-parallel all-reduce disabled: %s", ex)
+                        fused = None
         if reduce_dtype is None and ctx.device.type != "cuda":
             reduce_dtype = torch.float32  # CPU (gloo) runs: the oracle-comparison path keeps fp32 partials
-        return cls(ctx.tp_size, ctx.tp_rank, ctx.tp_group, custom, reduce_dtype)
+        return cls(ctx.tp_size, ctx.tp_rank, ctx.tp_group, custom, reduce_dtype, fused)
 
     def _host_staged(self, t: torch.Tensor) -> bool:
         # GPU tensors over a gloo group (multi-process tests sharing one GPU): stage through the host
@@ -101,6 +120,18 @@ class TPComm:
         from .. import ops
         ops.residual_add_(h, p.view_as(h), hb)
         return h
+
+    def linear_residual_(self, x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor,
+                         x_packed: Optional[torch.Tensor] = None, hb_pack: Optional[torch.Tensor] = None) -> bool:
+        """The row-parallel projection + its all-reduce as ONE kernel when the fused path applies (decode rows,
+        bf16 partials, a reserved instance): ``h += sum_ranks(x @ W^T)``, ``hb = bf16(h)``. Returns False (nothing
+        done) otherwise -- the caller then runs ``linear`` + ``all_reduce_residual_``."""
+        f = self.fused
+        if (f is None or self.size == 1 or self.reduce_dtype != torch.bfloat16 or not x.is_cuda
+                or x.dtype != torch.bfloat16 or not f.can_fuse(x.shape[0], w.n)):
+            return False
+        f.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=hb_pack)
+        return True
 
     def packs_residual(self, nbytes: int) -> bool:
         """Whether ``all_reduce_residual_`` of an ``nbytes`` partial can also write a packed hb copy."""
@@ -150,6 +181,14 @@ class TPComm:
         error). Called by the decode loop at its periodic host poll."""
         if self.custom is not None:
             self.custom.check()
+        if self.fused is not None:
+            self.fused.check()
+
+    def close(self):
+        for c in (self.custom, self.fused):
+            if c is not None:
+                c.close()
+        self.custom = self.fused = None
 
 
 NO_COMM = TPComm()
@@ -165,13 +204,14 @@ class TPRankProxyComm(TPComm):
     What it leaves out is the xGMI link: peer writes and peer flags land in local memory. Larger messages (prefill)
     are the identity sum (the RCCL call is skipped). Not a correctness path: the numbers are one shard's."""
 
-    def __init__(self, size: int, custom=None, reduce_dtype: Optional[torch.dtype] = None):
-        super().__init__(size=size, rank=0, group=None, custom=custom, reduce_dtype=reduce_dtype)
+    def __init__(self, size: int, custom=None, reduce_dtype: Optional[torch.dtype] = None, fused=None):
+        super().__init__(size=size, rank=0, group=None, custom=custom, reduce_dtype=reduce_dtype, fused=fused)
 
     @classmethod
-    def create(cls, size: int, max_bytes: int = 16 << 20) -> "TPRankProxyComm":
+    def create(cls, size: int, max_bytes: int = 16 << 20, fused_hidden: Optional[int] = None) -> "TPRankProxyComm":
         from .custom_allreduce import CustomAllReduce
-        return cls(size, CustomAllReduce.local(max_bytes=max_bytes))
+        fused = CustomAllReduce.local(max_bytes=CustomAllReduce.fused_bytes(fused_hidden or 16384)) if FUSED else None
+        return cls(size, CustomAllReduce.local(max_bytes=max_bytes), fused=fused)
 
     def _host_staged(self, t: torch.Tensor) -> bool:
         return False
@@ -194,7 +234,3 @@ class TPRankProxyComm(TPComm):
             return self.custom.topk_pairs(vals, idx, 0)
         return vals, idx
 
-    def close(self):
-        if self.custom is not None:
-            self.custom.close()
-            self.custom = None

@@ -24,6 +24,7 @@ once, so nothing hangs); ``check()`` raises on it and the object refuses every l
 from __future__ import annotations
 
 import os
+import socket
 
 import torch
 import torch.distributed as dist
@@ -44,11 +45,14 @@ class CustomAllReduceError(RuntimeError):
 class CustomAllReduce:
     DTYPES = (torch.bfloat16, torch.float32)
 
-    def __init__(self, state: int, rank: int, world: int, max_bytes: int):
+    def __init__(self, state: int, rank: int, world: int, max_bytes: int, share: int = 1):
         self.state = state
         self.rank = rank
         self.world = world
         self.max_bytes = max_bytes
+        # most ranks of the group on one device (1 on a real node; > 1 when test ranks share a GPU): the fused GEMV's
+        # workgroups spin for their peers', so every rank's grid must fit on a shared device at once
+        self.share = share
         self.failed = False  # set once a timeout was seen: the per-block counters are out of step for good
 
     def _live(self) -> int:
@@ -98,7 +102,12 @@ class CustomAllReduce:
                 e.car_free(buf, sig)
             raise CustomAllReduceError(f"custom all-reduce setup failed on ranks "
                                        f"{[r for r, ok in enumerate(oks) if not ok]}: {err}")
-        car = cls(state, rank, world, max_bytes)
+        dev = torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(dev)
+        key = (socket.gethostname(), p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        keys = [None] * world
+        dist.all_gather_object(keys, key, group=group)
+        car = cls(state, rank, world, max_bytes, share=max(keys.count(k) for k in keys))
         # protocol self-test on the real links: a known sum, checked on the host by every rank
         ok = car.self_test()
         dist.all_gather_object(oks, ok, group=group)
@@ -162,6 +171,29 @@ class CustomAllReduce:
         (``ops.packed_rows`` x D, the next projection's packed-x input)."""
         ts = self.use_two_shot(partial.numel() * partial.element_size()) if two_shot is None else bool(two_shot)
         ext().car_allreduce_residual(self._live(), partial, h, hb, ts, hb_pack)
+
+    # fused row-parallel GEMV (gemv.hip MODE_TPRESID): one TPRES_REGION of the slot per workgroup (<= 1 per 16
+    # output columns), at most WG_COUNTERS workgroups
+    TPRES_REGION = 64 * 64 * 4
+    WG_COUNTERS = 4096
+
+    SHARED_MAX_GROUPS = 256  # ranks sharing a device: all their workgroups resident at once (<= 16 waves, 64 KiB LDS)
+
+    def can_fuse(self, m: int, n: int) -> bool:
+        groups = n // 16
+        return (1 <= m <= 64 and n % 16 == 0 and groups <= self.WG_COUNTERS and groups * self.TPRES_REGION <=
+                self.max_bytes and (self.share == 1 or self.share * groups <= self.SHARED_MAX_GROUPS))
+
+    def linear_residual_(self, x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, x_packed=None, hb_pack=None):
+        """``h += sum_ranks(x @ W^T)``, ``hb = bf16(h)``: the GEMV exchanges its bf16 partials itself (no separate
+        collective). Uses this instance's per-workgroup counters: reserve an instance for it."""
+        from .. import ops
+        ops.linear_tp_residual(x, w, h, hb, self._live(), x_packed=x_packed, hb_pack=hb_pack)
+
+    @staticmethod
+    def fused_bytes(hidden: int) -> int:
+        """Slot bytes the fused path needs for a row-parallel output of ``hidden`` columns."""
+        return max(CHUNK_BYTES, (hidden // 16) * CustomAllReduce.TPRES_REGION)
 
     def argmax_pairs(self, val: torch.Tensor, idx: torch.Tensor, idx_offset: int, out_val=None) -> torch.Tensor:
         """First max over ranks of each row's local ``(val, idx + idx_offset)``: int32 ``[B]``."""

@@ -6,6 +6,7 @@ across xGMI peers). Three behaviours:
     is 1, ``check()`` raises ``CustomAllReduceError``, later kernels give up at once, and the object refuses every
     later call until it is re-created;
   * the same inside ``DecodeEngine.run`` (prefill + hipGraph-replayed decode): the engine's periodic poll raises;
+  * the GEMV-fused row-parallel all-reduce with a skipped call: the same timeout + error word;
   * a setup failure on ONE rank (its IPC import raises) moves EVERY rank to the RCCL/gloo fallback, and no rank
     keeps its buffers."""
 from __future__ import annotations
@@ -85,6 +86,46 @@ def _missing_peer(rank, world, port, q):
         q.put(("err", rank, traceback.format_exc()))
 
 
+def _fused_missing_peer(rank, world, port, q):
+    """The GEMV-fused row-parallel all-reduce (csrc/kernels/gemv.hip MODE_TPRESID) with a peer that skips a call."""
+    try:
+        dist = _init(rank, world, port)
+        from jax_llama_amd.models.weights import PackedLinear
+        from jax_llama_amd.parallel.custom_allreduce import CustomAllReduce, CustomAllReduceError
+        n, k, m = 512, 256, 4
+        car = CustomAllReduce.create_for(rank, world, None, max_bytes=CustomAllReduce.fused_bytes(n),
+                                         timeout_s=TIMEOUT_S)
+        assert car.can_fuse(m, n)
+        w = PackedLinear.random(n, k, "cuda", 0.02, torch.Generator(device="cuda").manual_seed(7))  # same on both
+        x = torch.full((m, k), 1.0 / 64, dtype=torch.bfloat16, device="cuda")
+        h = torch.zeros(m, n, dtype=torch.float32, device="cuda")
+        hb = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+        res = {}
+        car.linear_residual_(x, w, h, hb)  # both ranks: a good round (h = 2 x the local partial)
+        part = (x.float() @ w.dense().float().t()).to(torch.bfloat16).float()
+        torch.cuda.synchronize()
+        res["first_ok"] = bool(torch.allclose(h, 2 * part, rtol=1e-2, atol=1e-3)) and car.error() == 0
+        dist.barrier()
+        if rank == 0:  # rank 1 skips this one
+            t0 = time.perf_counter()
+            car.linear_residual_(x, w, h, hb)
+            torch.cuda.synchronize()
+            res["timeout_wait_s"] = time.perf_counter() - t0
+            res["error_word"] = car.error()
+            try:
+                car.check()
+                res["check_raised"] = False
+            except CustomAllReduceError:
+                res["check_raised"] = True
+        dist.barrier()
+        car.close()
+        dist.destroy_process_group()
+        q.put(("ok", rank, res))
+    except Exception:  # pragma: no cover - surfaced in the parent
+        import traceback
+        q.put(("err", rank, traceback.format_exc()))
+
+
 def _engine_missing_peer(rank, world, port, q):
     try:
         dist = _init(rank, world, port)
@@ -117,7 +158,7 @@ def _engine_missing_peer(rank, world, port, q):
             res["elapsed_s"] = time.perf_counter() - t0
             del eng
         dist.barrier()
-        comm.custom.close()
+        comm.close()
         dist.destroy_process_group()
         q.put(("ok", rank, res))
     except Exception:  # pragma: no cover
@@ -199,6 +240,15 @@ def test_missing_peer_times_out_and_poisons():
     assert 0.8 * TIMEOUT_S <= r0["timeout_wait_s"] < 10 * TIMEOUT_S, r0["timeout_wait_s"]
     assert r0["after_error_wait_s"] < 0.5 * TIMEOUT_S, r0["after_error_wait_s"]
     assert r0["check_raised"] and r0["refuses_after"]
+
+
+@pytest.mark.timeout(300)
+def test_fused_row_parallel_missing_peer_times_out():
+    res = _spawn(_fused_missing_peer)
+    assert res[0]["first_ok"] and res[1]["first_ok"], res
+    r0 = res[0]
+    assert r0["error_word"] == 1 and r0["check_raised"], r0
+    assert 0.8 * TIMEOUT_S <= r0["timeout_wait_s"] < 10 * TIMEOUT_S, r0["timeout_wait_s"]
 
 
 @pytest.mark.timeout(300)

@@ -59,6 +59,39 @@ def _gpu_params(cfg, seed):
     return meta_state_dict_to_params(gpu_meta_state_dict(cfg, seed), cfg.num_hidden_layers)
 
 
+def _fused_row_parallel_check(comm, rank, n):
+    """GEMV-fused row-parallel all-reduce (csrc/kernels/gemv.hip MODE_TPRESID) vs linear + the standalone residual
+    all-reduce: bit-identical h, mirror and packed mirror at every decode m-tile count, row-major and packed x
+    inputs, over several calls (both parities, counters advancing)."""
+    from jax_llama_amd import ops
+    from jax_llama_amd.models.weights import PackedLinear
+    g = torch.Generator(device="cuda").manual_seed(100 + rank)
+    w = PackedLinear.random(n, n, "cuda", 0.02, g)
+    ok = True
+    saved = ops.GEMV_VARIANT
+    for m, v in ((1, 1), (5, 5), (12, 13), (17, 6), (33, 15), (64, 1), (1, 3), (12, 12)):
+        ops.GEMV_VARIANT = v  # both paths on the same GEMV variant: the same per-wave K order, the same partial
+        # x and its packed copy as decode produces them: the mirror (+ packed mirror) of a residual all-reduce
+        hx = torch.randn(m, n, device="cuda", generator=g)
+        x = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+        xp = ops.packed_empty(m, n, "cuda").zero_()
+        comm.all_reduce_residual_(torch.randn(m, n, device="cuda", generator=g).to(torch.bfloat16), hx, x, hb_pack=xp)
+        h0 = torch.randn(m, n, device="cuda", generator=g)
+        for rep in range(3):
+            xpi = xp if rep != 1 else None
+            h1, h2 = h0.clone(), h0.clone()
+            hb1 = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            hb2 = torch.empty_like(hb1)
+            pk1, pk2 = ops.packed_empty(m, n, "cuda").zero_(), ops.packed_empty(m, n, "cuda").zero_()
+            assert comm.linear_residual_(x, w, h1, hb1, x_packed=xpi, hb_pack=pk1)
+            part = ops.linear(x, w, out_dtype=torch.bfloat16, x_packed=xpi)
+            comm.all_reduce_residual_(part, h2, hb2, hb_pack=pk2)
+            torch.cuda.synchronize()
+            ok = ok and torch.equal(h1, h2) and torch.equal(hb1, hb2) and torch.equal(pk1, pk2)
+    ops.GEMV_VARIANT = saved
+    return bool(ok)
+
+
 def _worker(rank, world, port, kind, q, rows=4):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -106,12 +139,27 @@ def _worker(rank, world, port, kind, q, rows=4):
         eng_mod.FUSED_GREEDY = True
         ops.ARGMAX_FUSED_MIN_M = saved
         res["fused_eq_unfused"] = torch.equal(st_fused, st_unfused)
-        # bf16 partials (production default)
+        # bf16 partials (production default): decode's row-parallel GEMVs exchange their partials themselves
         comm.reduce_dtype = torch.bfloat16
+        assert comm.fused is not None, "fused row-parallel all-reduce not created"
         lt16 = tp_model(toks, attention_mask=mask, position_ids=pos).logits.float().cpu()
         sb_graph = greedy(True)
         sb_eager = greedy(False)
         res["graph_eq_eager_bf16"] = torch.equal(sb_graph, sb_eager)
+        # the standalone collective kernels: the same tokens, bit for bit (one pinned GEMV variant for both, so the
+        # partials are summed over K in the same order)
+        ops.GEMV_VARIANT, saved_v = 1, ops.GEMV_VARIANT
+        sb_fused = greedy(True)
+        fused, comm.fused = comm.fused, None
+        sb_unfused = greedy(True)
+        comm.fused = fused
+        ops.GEMV_VARIANT = saved_v
+        res["fused_ar_eq_unfused"] = torch.equal(sb_fused, sb_unfused)
+        res["fused_used"] = comm.fused.can_fuse(toks.shape[0], cfg.hidden_size)
+        # ranks sharing this one GPU: a width whose workgroups all fit at once (csrc: they spin for their peers')
+        n_chk = min(cfg.hidden_size, 16 * (comm.fused.SHARED_MAX_GROUPS // comm.fused.share))
+        res["fused_ar_bits"] = _fused_row_parallel_check(comm, rank, n_chk)
+        res["fused_err"] = comm.fused.error()
         gcs = GenerationConfig(max_length=12 + gen_len, do_sample=True, temperature=0.8, top_p=0.95, top_k=50,
                                pad_token_id=2, eos_token_id=-1, seed=5)
         ss = tp_model.generate(toks, attention_mask=mask, generation_config=gcs).sequences.cpu()
@@ -174,6 +222,8 @@ def test_tp_decode_matches_single_process(world, kind, rows):
         assert status == "ok", payload
     res = {rank: payload for _, rank, payload in outs}
     r0 = res[0]
+    if kind == "small":  # the model's own decode took the fused path (70B dims on a shared GPU cannot)
+        assert r0["fused_used"]
     assert r0["err_fp32"] < 2e-2, r0["err_fp32"]
     assert r0["err_bf16"] < 2e-2, r0["err_bf16"]
     # every token the TP decode chose is TP1's argmax up to rounding (exact equality of whole sequences is
@@ -187,5 +237,6 @@ def test_tp_decode_matches_single_process(world, kind, rows):
     for r in range(world):
         assert res[r]["graph_eq_eager_fp32"] and res[r]["graph_eq_eager_bf16"], r
         assert res[r]["fused_eq_unfused"], r
+        assert res[r]["fused_ar_eq_unfused"] and res[r]["fused_ar_bits"] and res[r]["fused_err"] == 0, r
         assert res[r]["car_err"] == 0, r
         assert res[r]["sampled"] == r0["sampled"], r  # every rank sampled the same tokens

@@ -33,12 +33,13 @@ def main():
     comm = None
     if args.tp_proxy > 1:
         from jax_llama_amd.parallel import TPRankProxyComm
-        comm = TPRankProxyComm.create(args.tp_proxy)
+        comm = TPRankProxyComm.create(args.tp_proxy, fused_hidden=cfg.hidden_size)
     m = LLaMAForCausalLM(cfg, device="cuda", comm=comm, _do_init=False).init_random(seed=1)
     for b in args.batch:
         r = decode_latency(m, b, args.prompt_len, args.gen_len, steps=args.steps, do_sample=args.sample)
         r["model"] = args.model
         r["mp"] = args.tp_proxy
+        r["fused_row_parallel"] = comm is not None and comm.fused is not None
         r["hbm_roofline_ms"] = round(m.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()

@@ -426,6 +426,8 @@ int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemH
   hipError_t e = hipExtMallocWithFlags(buf, car_buffer_bytes(max_bytes, world), hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipExtMallocWithFlags(sig, car_signal_bytes(), hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemset(*sig, 0, car_signal_bytes());
+  // zeroed slots: no granule tag (car.h) can be a leftover of an earlier allocation at this address
+  if (e == hipSuccess) e = hipMemset(*buf, 0, car_buffer_bytes(max_bytes, world));
   if (e == hipSuccess) e = hipIpcGetMemHandle(hbuf, *buf);
   if (e == hipSuccess) e = hipIpcGetMemHandle(hsig, *sig);
   if (e != hipSuccess) {

@@ -42,5 +42,8 @@ JLA_DEV u32x2 ld_sys8(__amdgpu_buffer_rsrc_t r, long long off) {
 
 // granule tag of a call: a quiet-NaN pattern (never a payload of a working model) carrying the call count
 JLA_DEV unsigned gran_tag(int calls) { return 0x7FC00000u | ((unsigned)calls & 0x003FFFFFu); }
+// the fused GEMV's tags (gemv.hip MODE_TPRESID): the negative quiet NaNs, so granules the standalone kernels left in
+// the same slots (the instance's self-test) never carry a fused call's tag
+JLA_DEV unsigned gran_tag_fused(int calls) { return 0xFFC00000u | ((unsigned)calls & 0x003FFFFFu); }
 
 }  // namespace jla

@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(NW * 64)
     // partial + car_reduce_kernel (same roundings, same order).
     const CarDevice& d = *static_cast<const CarDevice*>(qa.tp);
     const int calls = reinterpret_cast<const int*>(inv_rms + MT * 16)[0];
-    const unsigned tag = gran_tag(calls);
+    const unsigned tag = gran_tag_fused(calls);
     const long long wg_base = (long long)blockIdx.x * TPRES_REGION;
     const long long par_base = (long long)(calls & 1) * d.world * d.max_bytes;
     const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);

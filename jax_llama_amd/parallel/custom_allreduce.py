@@ -45,10 +45,12 @@ class CustomAllReduceError(RuntimeError):
 class CustomAllReduce:
     DTYPES = (torch.bfloat16, torch.float32)
 
-    def __init__(self, state: int, rank: int, world: int, max_bytes: int, share: int = 1):
+    def __init__(self, state: int, rank: int, world: int, max_bytes: int, share: int = 1, group=None):
         self.state = state
         self.rank = rank
         self.world = world
+        self.size = world  # (autotune.tp_scope reads size / rank / group)
+        self.group = group
         self.max_bytes = max_bytes
         # most ranks of the group on one device (1 on a real node; > 1 when test ranks share a GPU): the fused GEMV's
         # workgroups spin for their peers', so every rank's grid must fit on a shared device at once
@@ -107,7 +109,7 @@ class CustomAllReduce:
         key = (socket.gethostname(), p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
         keys = [None] * world
         dist.all_gather_object(keys, key, group=group)
-        car = cls(state, rank, world, max_bytes, share=max(keys.count(k) for k in keys))
+        car = cls(state, rank, world, max_bytes, share=max(keys.count(k) for k in keys), group=group)
         # protocol self-test on the real links: a known sum, checked on the host by every rank
         ok = car.self_test()
         dist.all_gather_object(oks, ok, group=group)
@@ -186,9 +188,11 @@ class CustomAllReduce:
 
     def linear_residual_(self, x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, x_packed=None, hb_pack=None):
         """``h += sum_ranks(x @ W^T)``, ``hb = bf16(h)``: the GEMV exchanges its bf16 partials itself (no separate
-        collective). Uses this instance's per-workgroup counters: reserve an instance for it."""
+        collective). Uses this instance's per-workgroup counters: reserve an instance for it. Every rank must launch
+        the same GEMV variant (workgroup w of every rank covers the same columns): rank 0 picks it."""
         from .. import ops
-        ops.linear_tp_residual(x, w, h, hb, self._live(), x_packed=x_packed, hb_pack=hb_pack)
+        with ops.autotune.tp_scope(self):
+            ops.linear_tp_residual(x, w, h, hb, self._live(), x_packed=x_packed, hb_pack=hb_pack)
 
     @staticmethod
     def fused_bytes(hidden: int) -> int:

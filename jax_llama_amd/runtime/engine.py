@@ -57,7 +57,8 @@ class GenerationConfig:
 FUSED_GREEDY = os.environ.get("JLA_FUSED_ARGMAX", "1") != "0"
 # Decode micro-batches (TP = 1, batch >= MICROBATCH_MIN_ROWS): the step's rows are split in two halves whose layer
 # chains run on two streams of the captured graph (one fork, one join per step), so one half's memory-bound decode
-# attention can run beside the other half's compute-bound GEMMs. JLA_MICROBATCH=1 turns it off.
+# attention can run beside the other half's compute-bound GEMMs. Opt-in (JLA_MICROBATCH=2): measured 3.7 % slower at
+# B = 2048 (profiles/r3_decode_microbatch_ab.jsonl).
 MICROBATCH = int(os.environ.get("JLA_MICROBATCH", "1"))
 MICROBATCH_MIN_ROWS = int(os.environ.get("JLA_MICROBATCH_MIN_ROWS", "512"))
 

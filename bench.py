@@ -268,7 +268,9 @@ def _tp_rank_proxy(args):
            "prompt_len": args.prompt_len, "cache_len": args.prompt_len + args.gen_len,
            "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
            "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
-           "launches_per_layer": 7}
+           # qkv, attention, wo, w1|w3, w2 (+ the two all-reduce launches when the row-parallel GEMVs do not fuse them)
+           "fused_row_parallel": comm.fused is not None,
+           "launches_per_layer_decode": 5 if comm.fused is not None else 7}
     try:
         out["points"] = [decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=11)
                          for b in args.proxy_batches]

@@ -161,8 +161,8 @@ void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* ou
   const int64_t m = x.size(0);
   const bool f32 = x.scalar_type() == torch::kFloat32;
   if (variant == 0) variant = (m == 1) ? 1 : 4;
-  const bool xp_variant = variant >= 12 && variant <= 15;
-  check(xp_variant == (x_packed != nullptr), "packed-x variants (12-15) need x_packed, the others must not get it");
+  const bool xp_variant = jla::gemv_xp_variant((int)variant);
+  check(xp_variant == (x_packed != nullptr), "packed-x variants (12-15, 18, 19) need x_packed, the others must not");
   check(!xp_variant || !f32, "packed-x variants read bf16 activations");
   check(!(xp_variant && mode == 2 && (variant == 12 || variant == 14)), "SwiGLU packed-x variants: 13 / 15");
   if (variant == 4) {
@@ -173,8 +173,21 @@ void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* ou
                           ptr<float>(ws), ws.numel(), ptr<int32_t>(tickets), tickets.numel(), stream()),
        "linear_splitk");
   } else {
+    jla::QKVArgs qs = *qa;
+    if (jla::gemv_split_variant((int)variant)) {
+      // split-K GEMV: partial slabs + self-resetting tickets (the shared skinny workspace, sized for both)
+      check_gpu(ws, "ws");
+      check_gpu(tickets, "tickets");
+      check(ws.scalar_type() == torch::kFloat32 && tickets.scalar_type() == torch::kInt32, "ws/tickets dtypes");
+      check((size_t)ws.numel() >= jla::gemv_split_workspace_floats(m, n) && ws.numel() < (1LL << 29) &&
+                tickets.numel() >= jla::gemv_split_tickets(n) && jla::gemv_split_tickets(n) > 0,
+            "split-K GEMV: workspace / tickets too small, or too many column groups");
+      qs.sk_ws = ptr<float>(ws);
+      qs.sk_tk = ptr<int32_t>(tickets);
+      qs.sk_ws_floats = (int)ws.numel();
+    }
     rc(jla::linear_skinny(x_packed ? (const void*)x_packed : x.data_ptr(), f32, w.data_ptr(), out, m, n, k, mode,
-                          (float)rms_eps, accumulate, out_f32, qa, variant, stream()),
+                          (float)rms_eps, accumulate, out_f32, &qs, variant, stream()),
        "linear_skinny");
   }
 }
@@ -227,8 +240,11 @@ void linear_skinny_argmax(Tensor x, Tensor w, int64_t n, int64_t k, double rms_e
   rc(jla::argmax_partials(ptr<float>(part), n / 16, m, ptr<int32_t>(idx), ptr<float>(val), stream()), "argmax_partials");
 }
 
+// the decode workspace shared by the split-K skinny GEMM (variant 4) and the split-K GEMV variants (16-19)
 py::tuple skinny_workspace(int64_t m, int64_t n, int64_t k, int64_t mode) {
-  return py::make_tuple((int64_t)jla::skinny_workspace_floats(m, n, k, mode), jla::skinny_tickets(m, n, k, mode));
+  return py::make_tuple((int64_t)std::max(jla::skinny_workspace_floats(m, n, k, mode),
+                                          jla::gemv_split_workspace_floats(m, n)),
+                        (int64_t)std::max(jla::skinny_tickets(m, n, k, mode), jla::gemv_split_tickets(n)));
 }
 
 // RoPE + KV-cache epilogue arguments of the fused qkv projection (validated here)
@@ -631,7 +647,8 @@ void car_allreduce_residual(int64_t state, Tensor partial, Tensor h, Tensor hb, 
 // partials exchanged as tagged granules in the GEMV's own epilogue; hb = bf16(h) (+ its packed copy). `state` is a
 // custom all-reduce instance reserved for this path (its per-workgroup counters must not be shared)
 void linear_tp_residual(int64_t state, Tensor x, Tensor w, int64_t n, int64_t k, Tensor h, Tensor hb, int64_t variant,
-                        c10::optional<Tensor> x_packed, c10::optional<Tensor> hb_pack) {
+                        c10::optional<Tensor> x_packed, c10::optional<Tensor> hb_pack, c10::optional<Tensor> ws,
+                        c10::optional<Tensor> tickets) {
   check_gpu(x, "x");
   check_gpu(h, "h");
   check_gpu(hb, "hb");
@@ -651,8 +668,9 @@ void linear_tp_residual(int64_t state, Tensor x, Tensor w, int64_t n, int64_t k,
   qa.res_bf16 = bf(hb);
   qa.pack = packed_ptr(hb_pack, m, n, "hb_pack");
   qa.tp = jla::car_device(st);
-  run_skinny(x, w, n, k, h.data_ptr(), MODE_TPRESID_ID, -1.0, true, true, &qa, variant, Tensor(), Tensor(),
-             packed_ptr(x_packed, m, k, "x_packed"));
+  // split-K variants (16-19) take the shared decode workspace: only the last arriver of a column group exchanges
+  run_skinny(x, w, n, k, h.data_ptr(), MODE_TPRESID_ID, -1.0, true, true, &qa, variant, ws ? *ws : Tensor(),
+             tickets ? *tickets : Tensor(), packed_ptr(x_packed, m, k, "x_packed"));
 }
 
 // (value fp32, index int32) all-gathers of the vocab-parallel sampler. mode 0: out_i[n] = index of the first max over
@@ -743,7 +761,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("linear_skinny_argmax", &linear_skinny_argmax);
   m.def("linear_tp_residual", &linear_tp_residual, py::arg("state"), py::arg("x"), py::arg("w"), py::arg("n"),
         py::arg("k"), py::arg("h"), py::arg("hb"), py::arg("variant"), py::arg("x_packed") = py::none(),
-        py::arg("hb_pack") = py::none());
+        py::arg("hb_pack") = py::none(), py::arg("ws") = py::none(), py::arg("tickets") = py::none());
   m.def("bounds_error", [](bool reset) {
     const int r = reset ? 1 : 0;
     return (int64_t)(jla::jla_bounds_norm_embed(r) | jla::jla_bounds_rope_kv(r) | jla::jla_bounds_sample(r) |

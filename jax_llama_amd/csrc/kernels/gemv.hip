@@ -32,7 +32,7 @@ namespace jla {
 
 __device__ u32x4 g_zero_frag[64];  // 1 KiB of zeros (static storage is zero-initialised)
 
-template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false>
+template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false>
 __global__ void __launch_bounds__(NW * 64)
     linear_skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out,
                          int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa) {
@@ -46,17 +46,23 @@ __global__ void __launch_bounds__(NW * 64)
   const int KS = K >> 5;
   const int NTT = N >> 4;
   const int nt0 = blockIdx.x * NT;
+  // SPLIT: K is cut over gridDim.y workgroups per column group; this one streams k-steps [kb, kb + kn)
+  int kb = 0, kn = KS;
+  if constexpr (SPLIT) {
+    kb = (int)((long long)KS * blockIdx.y / gridDim.y);
+    kn = (int)((long long)KS * (blockIdx.y + 1) / gridDim.y) - kb;
+  }
 
   const u32x4* wt[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) wt[t] = W + (size_t)min(nt0 + t, NTT - 1) * KS * 64 + lane;
+  for (int t = 0; t < NT; ++t) wt[t] = W + ((size_t)min(nt0 + t, NTT - 1) * KS + kb) * 64 + lane;
   const XT* xp[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int row = min(mt * 16 + (lane & 15), M - 1);  // padding rows re-read the last row (not stored)
     // XP: activations pre-packed as MFMA A fragments [MT][KS][64 lanes][8] (1 KiB contiguous per k-step,
     // like the weights) instead of row-major (16 rows x 64 B = 16 half-used cache lines per fragment)
-    xp[mt] = XP ? x + ((size_t)mt * KS * 64 + lane) * 8 : x + (size_t)row * K + 8 * (lane >> 4);
+    xp[mt] = XP ? x + (((size_t)mt * KS + kb) * 64 + lane) * 8 : x + (size_t)row * K + (size_t)kb * 32 + 8 * (lane >> 4);
   }
   const u32x4* zfrag = g_zero_frag + lane;
   const XT* zx = reinterpret_cast<const XT*>(g_zero_frag);
@@ -69,7 +75,7 @@ __global__ void __launch_bounds__(NW * 64)
                                    __HIP_MEMORY_SCOPE_AGENT);
   }
 
-  const int n = (KS - w + NW - 1) / NW;  // k-steps of this wave: ks = w + i*NW, i < n
+  const int n = (kn - w + NW - 1) / NW;  // k-steps of this wave: ks = kb + w + i*NW, i < n
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -152,11 +158,59 @@ __global__ void __launch_bounds__(NW * 64)
     if (threadIdx.x == 0) reinterpret_cast<int*>(inv_rms + MT * 16)[0] = tp_calls + 1;
   }
   __syncthreads();
+  // SPLIT: the workgroup's wave-summed partial (and RMS row sums) go to its own slab with write-through (sc1) stores;
+  // every storing wave drains them, one agent-scope ticket add per workgroup picks the group's last arriver, which
+  // sums the splits in split order (sc1 loads: cdna_hip_programming.md Guideline 16, sc1-store + agent ticket +
+  // sc1-load form) into wave 0's slot of `red` and runs the normal epilogue from there. Deterministic; the
+  // ticket resets itself for the next call.
+  constexpr int NWR = SPLIT ? 1 : NW;  // wave slots of `red` / `red_ss` the epilogue sums
+  if constexpr (SPLIT) {
+    constexpr int E = MT * NT * 256, SLAB = E + MT * 16;
+    const int ns = gridDim.y, grp = blockIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(qa.sk_ws, 0, qa.sk_ws_floats * 4, 0x00020000);
+    const int mine = (grp * ns + blockIdx.y) * SLAB * 4;
+    for (int e = threadIdx.x; e < E; e += NW * 64) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += red[ww * E + e];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, mine + e * 4, 0, 16);
+    }
+    if (use_rms && threadIdx.x < MT * 16) {
+      float v = 0.f;
+      for (int ww = 0; ww < NW; ++ww) v += red_ss[ww * MT * 16 + threadIdx.x];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, mine + (E + threadIdx.x) * 4, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last_flag = reinterpret_cast<int*>(inv_rms + MT * 16) + 1;
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(qa.sk_tk + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == ns - 1;
+      if (last) __hip_atomic_store(qa.sk_tk + grp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last_flag = last;
+    }
+    __syncthreads();
+    if (!*last_flag) return;
+    const int first = grp * ns * SLAB * 4;
+    for (int e = threadIdx.x; e < E; e += NW * 64) {
+      float v = 0.f;
+      for (int sp = 0; sp < ns; ++sp)
+        v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, first + (sp * SLAB + e) * 4, 0, 16));
+      red[e] = v;
+    }
+    if (use_rms && threadIdx.x < MT * 16) {
+      float v = 0.f;
+      for (int sp = 0; sp < ns; ++sp)
+        v += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, first + (sp * SLAB + E + threadIdx.x) * 4, 0, 16));
+      red_ss[threadIdx.x] = v;
+    }
+    __syncthreads();
+  }
   if (threadIdx.x < MT * 16) {
     float r = 1.f;
     if (use_rms) {
       float s = 0.f;
-      for (int ww = 0; ww < NW; ++ww) s += red_ss[ww * MT * 16 + threadIdx.x];
+      for (int ww = 0; ww < NWR; ++ww) s += red_ss[ww * MT * 16 + threadIdx.x];
       r = rsqrtf(s / (float)K + eps);
     }
     inv_rms[threadIdx.x] = r;
@@ -166,7 +220,7 @@ __global__ void __launch_bounds__(NW * 64)
   auto reduced = [&](int mt, int t, int ln, int i) {
     float v = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) v += red[(((ww * MT + mt) * NT + t) * 64 + ln) * 4 + i];
+    for (int ww = 0; ww < NWR; ++ww) v += red[(((ww * MT + mt) * NT + t) * 64 + ln) * 4 + i];
     return v;
   };
 
@@ -324,9 +378,9 @@ __global__ void __launch_bounds__(NW * 64)
   }
 }
 
-template <typename XT, int MT, int NT, int MODE, int NW, int DEEP = 0, bool XP = false>
+template <typename XT, int MT, int NT, int MODE, int NW, int DEEP = 0, bool XP = false, bool SPLIT = false>
 static int launch_skinny(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
-                         int accumulate, int out_f32, const QKVArgs& qa, hipStream_t s) {
+                         int accumulate, int out_f32, const QKVArgs& qa, hipStream_t s, int ksplit = 1) {
   // k-steps in flight per wave: 8 KiB of weights per wave at MT = 1; fp32 activations double the
   // activation registers, so MT > 1 keeps fewer steps in flight to stay spill-free. DEEP = 1 doubles
   // the ring (bf16 activations at M = 17..64: more bytes in flight per wave).
@@ -337,7 +391,7 @@ static int launch_skinny(const void* x, const void* W, void* out, int M, int N, 
   const int NTT = N >> 4;
   const int grid = (NTT + NT - 1) / NT;
   const size_t lds = sizeof(float) * (NW * MT * NT * 256 + NW * MT * 16 + MT * 16 + 4);
-  auto kern = &linear_skinny_kernel<XT, MT, NT, MODE, NW, U, XP>;
+  auto kern = &linear_skinny_kernel<XT, MT, NT, MODE, NW, U, XP, SPLIT>;
   if (lds > 65536) {  // opt in to > 64 KiB of dynamic LDS once (not a stream op: capture-safe)
     static bool attr_set = false;
     if (!attr_set) {
@@ -345,8 +399,12 @@ static int launch_skinny(const void* x, const void* W, void* out, int M, int N, 
       attr_set = true;
     }
   }
-  kern<<<grid, NW * 64, lds, s>>>(static_cast<const XT*>(x), static_cast<const u32x4*>(W), out, M, N, K, eps,
-                                  use_rms, accumulate, out_f32, qa);
+  if (SPLIT && (ksplit < 2 || grid > GEMV_SPLIT_MAX_GROUPS || !qa.sk_ws || !qa.sk_tk ||
+                (size_t)qa.sk_ws_floats < (size_t)grid * ksplit * (MT * NT * 256 + MT * 16) ||
+                (K >> 5) < ksplit))
+    return -3;  // split plan and workspace must fit (host checks the buffers' sizes against these)
+  kern<<<dim3(grid, SPLIT ? ksplit : 1), NW * 64, lds, s>>>(static_cast<const XT*>(x), static_cast<const u32x4*>(W),
+                                                            out, M, N, K, eps, use_rms, accumulate, out_f32, qa);
   JLA_CHECK_LAUNCH();
   return 0;
 }
@@ -401,6 +459,21 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       if (variant == 10)
         return launch_skinny<XT, MT, 2, MODE, 4, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
     }
+    // split-K variants (bf16 activations): K cut over 2 (16, 18) or 4 (17, 19) workgroups per column group, the last
+    // arriver sums the splits and runs the epilogue -- for projections with few column groups (tensor-parallel qkv
+    // shards, N = 1280 at Llama-3-70B MP 8: 80 one-tile workgroups leave most CUs idle); 18 / 19 read packed x.
+    // 1 tile per workgroup (SwiGLU: the gate/up pair), 4 waves at M <= 16, 8 above.
+    if constexpr (sizeof(XT) == 2 && MODE != MODE_ARGMAX) {
+      if (gemv_split_variant(variant)) {
+        constexpr int SNT = MODE == MODE_SWIGLU ? 2 : 1, SNW = MT == 1 ? 4 : 8;
+        const int ks = (variant == 16 || variant == 18) ? 2 : 4;
+        if (variant >= 18)
+          return launch_skinny<XT, MT, SNT, MODE, SNW, 0, true, true>(x, W, out, M, N, K, eps, use_rms, accumulate,
+                                                                      out_f32, qa, s, ks);
+        return launch_skinny<XT, MT, SNT, MODE, SNW, 0, false, true>(x, W, out, M, N, K, eps, use_rms, accumulate,
+                                                                     out_f32, qa, s, ks);
+      }
+    }
     // packed-x variants (x is the packed copy, common.h pack_off, padded to MT * 16 rows): 12 = 1 tile x 8 waves,
     // 13 = 2 tiles x 4 waves, 14 / 15 = the same with a doubled ring
     if constexpr (sizeof(XT) == 2) {
@@ -444,6 +517,14 @@ static int dispatch_tp(const void* x, const void* W, void* out, int M, int N, in
   }
 }
 
+size_t gemv_split_workspace_floats(int M, int N) {
+  const int groups = N >> 4;  // upper bound: 1 tile per column group
+  if (groups > GEMV_SPLIT_MAX_GROUPS || M < 1 || M > SKINNY_MAX_M) return 0;
+  const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
+  return (size_t)groups * 4 * (mt * 256 + mt * 16);
+}
+int gemv_split_tickets(int N) { return (N >> 4) > GEMV_SPLIT_MAX_GROUPS ? 0 : (N >> 4); }
+
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s) {
   if (M <= 0) return 0;
@@ -451,6 +532,7 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   if (mode == MODE_QKV && (!qkv || qkv->Dh % 16 || M % qkv->S)) return -1;
   if (mode == MODE_TPRESID && (!qkv || !qkv->tp)) return -1;
+  if (gemv_split_variant(variant) && (x_is_f32 || mode == MODE_ARGMAX)) return -1;
   const int use_rms = rms_eps >= 0.f;
   const float eps = use_rms ? rms_eps : 0.f;
   QKVArgs qa{};

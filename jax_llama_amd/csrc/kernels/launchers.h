@@ -32,6 +32,9 @@ struct QKVArgs {
   bf16_t* pack;               // optional packed-layout copy (common.h pack_off) of the bf16 output: RESIDUAL -> the
                               // mirror, SWIGLU -> the activation (GEMV only; the next projection's packed-x input)
   const void* tp;             // MODE_TPRESID: the TP group's CarDevice (car.h) the partials are all-reduced through
+  float* sk_ws;               // split-K GEMV variants (gemv.hip, 16-19): per-(group, split) partial slabs
+  int32_t* sk_tk;             //   and per-group tickets (zero-initialised once, reset by each group's last arriver)
+  int sk_ws_floats;           //   slab buffer size (buffer-descriptor range)
 };
 // MODE_TPRESID: granule bytes each workgroup of the fused row-parallel GEMV owns in every (parity, source rank) slot
 constexpr int CAR_WG_COUNTERS = 4096;  // per-workgroup call counters of the fused GEMV (workgroups per launch)
@@ -39,6 +42,13 @@ constexpr long long TPRES_REGION = 64 * 64 * 4;  // up to 64 rows x 64 columns x
 
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
+// split-K GEMV variants 16-19 (K over gridDim.y workgroups per column group, last arriver sums + epilogue): their slab
+// floats / tickets (0 when N has too many column groups for them)
+constexpr int GEMV_SPLIT_MAX_GROUPS = 1024;
+size_t gemv_split_workspace_floats(int M, int N);
+int gemv_split_tickets(int N);
+inline bool gemv_split_variant(int v) { return v >= 16 && v <= 19; }
+inline bool gemv_xp_variant(int v) { return (v >= 12 && v <= 15) || v == 18 || v == 19; }
 // split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
 // skinny_workspace_floats / skinny_tickets (tickets zero-initialised once, self-resetting)
 size_t skinny_workspace_floats(int M, int N, int K, int mode);

@@ -234,7 +234,8 @@ PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
 PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "32"))
 PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
 SKINNY_M = 64  # decode GEMV rows (csrc: SKINNY_MAX_M): packed copies exist only on that path
-XP_VARIANTS = (12, 13, 14, 15)
+XP_VARIANTS = (12, 13, 14, 15, 18, 19)  # packed-x GEMV variants (18 / 19: split-K)
+SPLIT_VARIANTS = (16, 17, 18, 19)  # split-K GEMV variants (the shared skinny workspace holds their slabs)
 
 
 def packed_rows(m: int) -> int:
@@ -279,7 +280,11 @@ def linear_tp_residual(x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, st
     v = _variant(e, x, w, MODE_RESIDUAL, x_packed, pack_out=True)
     if v in (4, TILED):
         v = 1
-    e.linear_tp_residual(state, x, w.weight, w.n, w.k, h, hb, v, x_packed if v in XP_VARIANTS else None, hb_pack)
+    ws = tk = None
+    if v in SPLIT_VARIANTS:
+        ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_RESIDUAL, x.device)
+    e.linear_tp_residual(state, x, w.weight, w.n, w.k, h, hb, v, x_packed if v in XP_VARIANTS else None, hb_pack,
+                         ws, tk)
     return h
 
 
@@ -356,14 +361,15 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
     e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
 
 
-def _variant(e, x, w, mode, x_packed=None, pack_out=None) -> int:
+def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int:
     """Decode-kernel variant for this shape: pinned (JLA_GEMV_VARIANT / ops.GEMV_VARIANT) or
     measured once per shape on the device (ops/autotune.py). With ``x_packed`` the packed-x variants are
     candidates too; with ``pack_out`` only GEMV variants qualify (their epilogue writes the packed copy)."""
     xp_in, p_out = x_packed is not None, pack_out is not None
     if GEMV_VARIANT:
         v = GEMV_VARIANT
-        if (v in XP_VARIANTS and not xp_in) or (p_out and v in (4, TILED)):
+        if (v in XP_VARIANTS and not xp_in) or (p_out and v in (4, TILED)) or (v in SPLIT_VARIANTS and (
+                no_split or x.dtype != BF16 or w.n // 16 > autotune.SPLIT_MAX_GROUPS)):
             v = 1
         if v in (12, 14) and mode == MODE_SWIGLU:
             v += 1
@@ -387,7 +393,7 @@ def _variant(e, x, w, mode, x_packed=None, pack_out=None) -> int:
         else:
             e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk)
 
-    return autotune.choose(e, x, w, pmode, run, xp_in=xp_in, pack_out=p_out)
+    return autotune.choose(e, x, w, pmode, run, xp_in=xp_in, pack_out=p_out, no_split=no_split)
 
 
 _SK_SIZES = {}
@@ -539,7 +545,7 @@ def linear_argmax(x: torch.Tensor, w, rms_eps: Optional[float] = None):
         return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
     if m <= ext().SKINNY_MAX_M and SKINNY_ARGMAX:
         e = ext()
-        v = _variant(e, x, w, MODE_STORE)  # same main loop as the logits GEMV: the tuned variant applies
+        v = _variant(e, x, w, MODE_STORE, no_split=True)  # the logits GEMV's main loop: its tuned variant applies
         if v in (1, 2, 3, 5, 6, 8, 9):
             part = workspace.get("skinny_argmax", m * (w.n // 16) * 2, torch.float32, x.device)
             idx = torch.empty(m, dtype=torch.int32, device=x.device)

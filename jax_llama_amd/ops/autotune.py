@@ -78,8 +78,11 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
+TUNE_VERSION = 2  # bumped when a candidate set changes (16-19: split-K GEMV), so older persisted picks are re-measured
+
+
 def _key_str(kind: str, key: Tuple) -> str:
-    return kind + ":" + ",".join(str(k).replace("torch.", "") for k in key)
+    return f"{kind}@{TUNE_VERSION}:" + ",".join(str(k).replace("torch.", "") for k in key)
 
 
 def _load():
@@ -157,22 +160,30 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
             c.extend([9, 11, 10])
         # (variant 8 -- 16 waves -- measured no faster than 1/4/6/7 at M = 32:
         # profiles/r2_decode_m32_variants_8_9.jsonl; kept as an explicit choice, not tuned)
+    if bf16_x and n // 16 <= SPLIT_MAX_GROUPS:
+        # split-K GEMV (K over 2 / 4 workgroups per column group, in-kernel last-arriver sum): few column groups
+        c.extend([16, 17])
     return tuple(c)
+
+
+SPLIT_MAX_GROUPS = 1024  # csrc GEMV_SPLIT_MAX_GROUPS
 
 
 TILED_VARIANT = 7
 
 
-XP_CANDIDATES = (12, 13, 14, 15)  # packed-x GEMV variants (gemv.hip dispatch_nt)
+XP_CANDIDATES = (12, 13, 14, 15, 18, 19)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 split-K)
 
 
-def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False) -> int:
+def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False,
+           no_split: bool = False) -> int:
     """``run(variant, x, weight_tensor)`` launches the op once. ``xp_in``: a packed copy of x exists, so the
     packed-x variants compete too; ``pack_out``: the epilogue must also write a packed copy of its output,
-    which only the GEMV variants do (no split-K skinny 4, no tiled 7)."""
+    which only the GEMV variants do (no split-K skinny 4, no tiled 7); ``no_split``: without the split-K GEMV
+    variants (16-19; the fused-argmax lm_head GEMV has no split form)."""
     m = x.shape[0]
     # (TP-scoped decisions are cached apart: every rank of the group must take the same collective path)
-    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out, _SCOPE["comm"] is not None)
+    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out, no_split, _SCOPE["comm"] is not None)
     v = _CACHE.get(key)
     if v is not None:
         return v
@@ -180,7 +191,10 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     if pack_out:
         cands = [c for c in cands if c not in (4, TILED_VARIANT)]
     if xp_in and x.dtype == torch.bfloat16:
-        cands += [c for c in XP_CANDIDATES if mode != 2 or c in (13, 15)]
+        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19)) and
+                  (c < 18 or w.n // 16 <= SPLIT_MAX_GROUPS)]
+    if no_split:
+        cands = [c for c in cands if not 16 <= c <= 19]
     if not ENABLED or torch.cuda.is_current_stream_capturing():
         h = heuristic(m, w.n, w.k, mode)
         return h if h in cands else 1

@@ -386,6 +386,42 @@ def test_linear_qkv_rope_fused(m, s, k, xdt):
     _close(vg, vc, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("variant", [16, 17])
+@pytest.mark.parametrize("m,s,k", [(1, 1, 8192), (16, 1, 4096), (32, 1, 8192), (64, 1, 1024), (6, 3, 256)])
+def test_split_gemv_qkv_rope(m, s, k, variant):
+    """Split-K GEMV (K over 2 / 4 workgroups per column group, last arriver sums + runs the epilogue): the fused
+    qkv projection (RMS statistics summed over the splits, RoPE, KV-cache write) at tensor-parallel shard widths
+    (10 heads = 80 column tiles, as Llama-3-70B at MP 8) against the fp32 oracle, and repeatable bit for bit (the
+    tickets reset themselves)."""
+    h, hkv, dh, t = 8, 1, 128, 80
+    b = m // s
+    n = (h + 2 * hkv) * dh
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    x = torch.randn(m, k).to(BF16).float()
+    table = ref.rope_table(dh, 256, 500000.0)
+    pos = torch.randint(0, 200, (m,), dtype=torch.int32)
+    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+    vc = torch.zeros_like(kc)
+    q = ref.linear_qkv_rope(x, w, 1e-5, table, pos, kc, vc, 7, s, h, hkv, dh)
+    pg = PackedLinear.from_dense(w, DEV)
+    ops.GEMV_VARIANT = variant
+    try:
+        outs = []
+        for _ in range(3):
+            kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+            qg = ops.linear_qkv_rope(x.to(BF16).to(DEV), pg, 1e-5, table.to(DEV), pos.to(DEV), kg, vg,
+                                     torch.tensor([7], dtype=torch.int32, device=DEV), s, h, hkv, dh)
+            outs.append((qg.cpu(), kg.cpu(), vg.cpu()))
+    finally:
+        ops.GEMV_VARIANT = 0
+    qg, kg, vg = outs[0]
+    _close(qg, q, 2e-2, 2e-2)
+    _close(kg, kc, 2e-2, 2e-2)
+    _close(vg, vc, 2e-2, 2e-2)
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
+
+
 def test_gemv_variants_agree():
     x = torch.randn(16, 2048, device=DEV)
     w = PackedLinear.from_dense((torch.randn(512, 2048) * 0.05).to(BF16), DEV)
@@ -399,7 +435,7 @@ def test_gemv_variants_agree():
 
 
 @pytest.mark.parametrize("k", [256, 4096])
-@pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11])
+@pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11, 16, 17])
 @pytest.mark.parametrize("m", [1, 9, 16, 40, 64])
 def test_decode_linear_paths_all_modes(variant, m, k):
     """Both decode GEMM designs (and the GEMV's tile / ring-depth variants: at M > 16 the hand-counted
@@ -837,7 +873,7 @@ def _qkv_rope_stream_k(e, m, s):
     _close(vg, vc, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("variant", [12, 13, 14, 15])
+@pytest.mark.parametrize("variant", [12, 13, 14, 15, 18, 19])
 @pytest.mark.parametrize("m", [1, 12, 16, 20, 32, 40])
 def test_packed_x_variants_and_packed_epilogues(m, variant):
     """Packed-x GEMV variants read the packed copy (ref.pack_act) and match the fp32 reference; the residual /

@@ -30,7 +30,9 @@ def proxy_model():
 
 
 @pytest.mark.timeout(240)
-def test_proxy_fused_row_parallel_matches_standalone(proxy_model):
+@pytest.mark.parametrize("variant", [1, 16])
+def test_proxy_fused_row_parallel_matches_standalone(proxy_model, variant):
+    """variant 16: the split-K GEMV (2 workgroups per column group; only the last arriver exchanges)."""
     from jax_llama_amd import ops
     from jax_llama_amd.runtime.engine import DecodeEngine, GenerationConfig
     cfg, comm, model = proxy_model
@@ -45,7 +47,7 @@ def test_proxy_fused_row_parallel_matches_standalone(proxy_model):
 
     assert comm.fused.can_fuse(toks.shape[0], cfg.hidden_size)
     saved = ops.GEMV_VARIANT
-    ops.GEMV_VARIANT = 1
+    ops.GEMV_VARIANT = variant
     try:
         fused_graph = greedy(True)
         fused_eager = greedy(False)

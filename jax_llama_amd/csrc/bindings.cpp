@@ -778,6 +778,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_set_v3_kpg", [](int64_t m) { jla::attn_set_v3_kpg((int)m); });
   m.def("attn_set_v3_max_pairs", [](int64_t n) { jla::attn_set_v3_max_pairs((int)n); });
   m.def("attn_set_v5_max_pairs", [](int64_t n) { jla::attn_set_v5_max_pairs((int)n); });
+  m.def("attn_set_v5_fold", [](int64_t n) { jla::attn_set_v5_fold((int)n); });
   m.def("attn_set_v1_min_wgs", [](int64_t n) { jla::attn_set_v1_min_wgs((int)n); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),

@@ -424,11 +424,16 @@ __global__ void __launch_bounds__(AD3_WAVES * 64)
 // projection). Splits outside the valid key range exit at once (the grid covers the whole cache, the valid range is
 // device state), so the ticket counts only the active splits; a pair with one active split writes directly.
 constexpr int AD5_WAVES = 4;
+// splits the last arriver merges per round (all of a round's partial loads in flight together): 4 or 12; by default
+// 12 from 16 (row, kv head) pairs on (70B MP 8 B = 32 T = 384: 13.9 -> 12.8 us) and 4 below (B = 1: 8.8 vs 9.4 us;
+// profiles/r3_attn_decode_v5_fold_ab.jsonl). attn_set_v5_fold(4 / 12) pins one (A/B), 0 = by pairs.
+static int g_attn_v5_fold = 0;
+void attn_set_v5_fold(int n) { g_attn_v5_fold = (n == 4 || n == 12) ? n : 0; }
 static int g_attn_v5_max_pairs = 64;  // v5 up to this many (row, kv head) pairs (0: off)
 void attn_set_v5_max_pairs(int n) { g_attn_v5_max_pairs = n < 0 ? 64 : n; }
 static int kpg5(int rep) { return rep >= 16 ? 1 : (rep == 8 ? 2 : (rep == 4 ? 4 : 8)); }
 
-template <int REP, int KPG>
+template <int REP, int KPG, int AD5_FOLD>
 __global__ void __launch_bounds__(AD5_WAVES * 64)
     attn_decode_v5_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
@@ -603,22 +608,19 @@ __global__ void __launch_bounds__(AD5_WAVES * 64)
       for (int e = 0; e < 4; ++e) Or[e] = Or[e] * a + f * __uint_as_float(ov[e]);
       Mr = mn;
     };
-    int s = s_lo;
-    for (; s + 4 <= s_hi; s += 4) {
-      u32x4 ml[4], ov[4];
+    // AD5_FOLD splits per round, all loads of a round in flight together (one dependent L2 round trip per round,
+    // not one per 4 splits: T = 384 at rep 8 is 12 splits); past the end the last split is re-read, never folded
+    for (int s = s_lo; s < s_hi; s += AD5_FOLD) {
+      u32x4 ml[AD5_FOLD], ov[AD5_FOLD];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int off = ((s + u) * PS + h * HS) * 4;
+      for (int u = 0; u < AD5_FOLD; ++u) {
+        const int off = (min(s + u, s_hi - 1) * PS + h * HS) * 4;
         ml[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
         ov[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + (4 + d) * 4, 0, 16);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) fold(ml[u], ov[u]);
-    }
-    for (; s < s_hi; ++s) {
-      const int off = (s * PS + h * HS) * 4;
-      fold(__builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16),
-           __builtin_amdgcn_raw_buffer_load_b128(rs, off + (4 + d) * 4, 0, 16));
+      for (int u = 0; u < AD5_FOLD; ++u)
+        if (s + u < s_hi) fold(ml[u], ov[u]);
     }
     float v[4];
 #pragma unroll
@@ -1125,9 +1127,14 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
     dim3 grid5(nsplit, Hkv, B);
 #define JLA_AD5(R, K)                                                                                          \
   if (rep == R) {                                                                                              \
-    attn_decode_v5_kernel<R, K><<<grid5, AD5_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, \
-                                                                 out, ws, tickets, H, Hkv, T, t_cap, nsplit,   \
-                                                                 scale, out_pack);                             \
+    if (g_attn_v5_fold == 4 || (g_attn_v5_fold == 0 && B * Hkv < 16))                                          \
+      attn_decode_v5_kernel<R, K, 4><<<grid5, AD5_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask,     \
+                                                                      mask_len, out, ws, tickets, H, Hkv, T,   \
+                                                                      t_cap, nsplit, scale, out_pack);         \
+    else                                                                                                       \
+      attn_decode_v5_kernel<R, K, 12><<<grid5, AD5_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask,    \
+                                                                       mask_len, out, ws, tickets, H, Hkv, T,  \
+                                                                       t_cap, nsplit, scale, out_pack);        \
     JLA_CHECK_LAUNCH();                                                                                        \
     return 0;                                                                                                  \
   }

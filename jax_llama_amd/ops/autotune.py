@@ -251,11 +251,21 @@ def _measure(x, w, run, cands) -> int:
             ev1.synchronize()
             times[v] = min(times[v], ev0.elapsed_time(ev1) / iters)
     del ws, graphs
+    _TIMES[(x.shape[0], w.n, w.k, len(_TIMES))] = {v: round(t * 1000.0, 2) for v, t in times.items()}
     return min(cands, key=times.get)
+
+
+_TIMES: Dict[Tuple, Dict[int, float]] = {}  # (m, n, k, seq) -> {variant: us per call} of every measured GEMV choice
 
 
 def table() -> Dict[Tuple, int]:
     return dict(_CACHE)
+
+
+def measured() -> Dict[Tuple, Dict[int, float]]:
+    """Graph-timed microseconds per candidate of every GEMV choice measured in this process (tools/decode_point.py
+    --tune-report)."""
+    return dict(_TIMES)
 
 
 # ----------------------------------------------------------------------------------------------

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--sample", action="store_true")
     ap.add_argument("--tp-proxy", type=int, default=1, help="> 1: ONE rank of that MP degree on this GPU "
                     "(parallel/comm.py TPRankProxyComm; bench.py tp_rank_proxy)")
+    ap.add_argument("--tune-report", action="store_true", help="print the decode-kernel choices and the graph-timed "
+                    "microseconds of every candidate measured (ops/autotune.py)")
     args = ap.parse_args()
     import torch
     from jax_llama_amd.config import get_preset
@@ -43,6 +45,10 @@ def main():
         r["hbm_roofline_ms"] = round(m.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
+    if args.tune_report:
+        from jax_llama_amd.ops import autotune
+        for (m, n, k, _), t in autotune.measured().items():
+            print(json.dumps({"tune": "gemv", "m": m, "n": n, "k": k, "us": t, "best": min(t, key=t.get)}), flush=True)
 
 
 if __name__ == "__main__":

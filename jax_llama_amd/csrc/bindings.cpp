@@ -334,7 +334,7 @@ SkWs check_sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& t
 // tile 4 -> data-parallel whole waves + stream-K tail (ws/tickets from gemm_sk_workspace).
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate,
           c10::optional<Tensor> mirror, int64_t ksplit, c10::optional<Tensor> ws, double rms_eps, int64_t tile,
-          c10::optional<Tensor> tickets) {
+          c10::optional<Tensor> tickets, c10::optional<Tensor> pack_out) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -343,6 +343,16 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   const int64_t m = x.size(0);
   check_linear_out(out, m, n, mode);
   jla::bf16_t* mir = mode == 1 ? mirror_ptr(mirror, out.numel()) : nullptr;
+  // packed copy of the bf16 output (decode M <= 64; the residual's mirror / the SwiGLU activation): written by the
+  // split-K reduce epilogue, so only on that path
+  jla::QKVArgs pqa{};
+  if (pack_out.has_value()) {
+    check(m <= SKINNY_MAX_M && (mode == 1 || mode == 2) && (mode != 1 || mir), "gemm pack_out: decode M, residual "
+          "(with its mirror) or SwiGLU");
+    check(ksplit > 1 && tile != 4 && tile != 6 && !(tickets.has_value() && jla::gemm_fixup_enabled()),
+          "gemm pack_out: the split-K reduce-kernel path only");
+    pqa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
+  }
   if (tile == 4) {
     check(ksplit <= 1, "gemm tile 4: no K split");
     const SkWs sk = check_sk_ws(ws, tickets, m, n, k);
@@ -383,7 +393,7 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   }
   check_gemm_ws(ws, ksplit, m, n, rms_eps >= 0);
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-               out.scalar_type() == torch::kFloat32, mir, nullptr,
+               out.scalar_type() == torch::kFloat32, mir, pqa.pack ? &pqa : nullptr,
                ksplit > 1 ? ptr<float>(*ws) : nullptr, ksplit > 1 ? ws->numel() : 0, ksplit, stream(),
                (float)rms_eps, (int)tile),
      "gemm");
@@ -720,7 +730,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("pack_out") = py::none());
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
-        py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none());
+        py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none(),
+        py::arg("pack_out") = py::none());
   m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
     return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
   }, "(slab floats, tickets) of the in-kernel split-K fixup");

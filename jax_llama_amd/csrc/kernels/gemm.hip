@@ -1229,8 +1229,11 @@ __global__ void __launch_bounds__(256)
       }();
       const float uu[4] = {u.x, u.y, u.z, u.w};
       bf16_t* o = static_cast<bf16_t*>(out) + (size_t)m * (N >> 1) + (tile >> 1) * 16 + c0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = f2bf(silu(vv[q]) * uu[q]);
+      const uint2 pk = make_uint2(pack2bf(silu(vv[0]) * uu[0], silu(vv[1]) * uu[1]),
+                                  pack2bf(silu(vv[2]) * uu[2], silu(vv[3]) * uu[3]));
+      *reinterpret_cast<uint2*>(o) = pk;
+      // decode M: also the packed copy (common.h pack_off) the next projection's packed-x GEMV reads
+      if (qa.pack) *reinterpret_cast<uint2*>(qa.pack + pack_off(m, (tile >> 1) * 16 + c0, N >> 1)) = pk;
     }
   } else if constexpr (MODE == MODE_RESIDUAL) {
     float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + idx);
@@ -1244,7 +1247,11 @@ __global__ void __launch_bounds__(256)
       r = make_float4(vv[0], vv[1], vv[2], vv[3]);
     }
     *o = r;
-    if (mirror) *reinterpret_cast<uint2*>(mirror + idx) = make_uint2(pack2bf(r.x, r.y), pack2bf(r.z, r.w));
+    if (mirror) {
+      const uint2 pk = make_uint2(pack2bf(r.x, r.y), pack2bf(r.z, r.w));
+      *reinterpret_cast<uint2*>(mirror + idx) = pk;
+      if (qa.pack) *reinterpret_cast<uint2*>(qa.pack + pack_off(m, col, N)) = pk;  // packed copy of the mirror
+    }
   } else if constexpr (MODE == MODE_QKV) {
     const int head = col / qa.Dh, d0 = col - head * qa.Dh;
     const int b = m / qa.S, sq = m - b * qa.S;

@@ -91,8 +91,9 @@ class PackedActs:
     residual epilogue of the step (the embedding writes only the row-major mirror)."""
 
     def __init__(self, rows: int, model, device, full: bool = True):
-        # full = False (33-64 rows): only the attention output is packed (wo reads it); hb / the SwiGLU output stay
-        # row-major so w1|w3 and w2 keep the tiled GEMM, which wins there (profiles/r2_packed_x_decode_ab.jsonl)
+        # full = False (rows above ops.PACKED_X_MAX_M): only the attention output is packed (wo reads it); hb / the
+        # SwiGLU output stay row-major (profiles/r2_packed_x_decode_ab.jsonl). Since the tiled split-K GEMM's reduce
+        # epilogue writes packed copies too, full packing reaches 64 rows (profiles/r3_packed_x_m64_ab.jsonl)
         self.hb = ops.packed_empty(rows, model.config.hidden_size, device) if full else None
         self.att = ops.packed_empty(rows, model.n_heads * model.head_dim, device)
         self.act = ops.packed_empty(rows, model.ffn, device) if full else None

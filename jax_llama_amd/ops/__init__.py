@@ -231,7 +231,9 @@ def linear_swiglu(x: torch.Tensor, w, rms_eps: Optional[float] = None, x_packed:
 # (profiles/r2_decode_m32_asm_ring.jsonl: o 15.6 -> 10.5 us, down 36.6 -> 30.7 us at M = 32).
 PACKED_X = os.environ.get("JLA_PACKED_X", "1") != "0"
 PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
-PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "32"))
+# up to 64 rows: from 33 rows the tiled split-K GEMM's reduce epilogue writes the packed copies too, so the producers
+# keep the tiled GEMM where it wins (w2 at M = 33-64) and the consumers read packed x (profiles/r3_packed_x_m64_ab.jsonl)
+PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "64"))
 PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
 SKINNY_M = 64  # decode GEMV rows (csrc: SKINNY_MAX_M): packed copies exist only on that path
 XP_VARIANTS = (12, 13, 14, 15, 18, 19)  # packed-x GEMV variants (18 / 19: split-K)
@@ -255,8 +257,10 @@ def _gpu_linear(x, w, out, mode, rms_eps, accumulate, mirror=None, x_packed=None
     if m > e.SKINNY_MAX_M:
         x_packed = pack_out = None
     v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, mode, x_packed, pack_out)
+    if v == TILED and pack_out is not None and not _tiled_packs(e, m, w.n, w.k, x.device, mode, rms_eps):
+        v = 1  # (a plan that cannot pack: the GEMV writes the packed copy)
     if v == TILED:
-        _tiled(e, x, w.weight, w.n, w.k, out, mode, rms_eps, accumulate, mirror)
+        _tiled(e, x, w.weight, w.n, w.k, out, mode, rms_eps, accumulate, mirror, pack_out)
     elif x_packed is not None or pack_out is not None:
         ws, tk = _skinny_ws(e, m, w.n, w.k, mode, x.device)
         e.linear_skinny(x, w.weight, w.n, w.k, out, mode, -1.0 if rms_eps is None else float(rms_eps),
@@ -352,13 +356,24 @@ def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
     return ks, tm, ws, None
 
 
-def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None):
+def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None, pack_out=None):
     """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups, or a stream-K tail,
-    when the output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip)."""
+    when the output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip). ``pack_out``: the split-K
+    reduce epilogue also writes the packed copy of the bf16 output (plans that ``_tiled_packs``)."""
     fused = _fused_rms(e, mode, rms_eps)
     xb = _tiled_input(x, rms_eps, fused)
     ks, tm, ws, tk = _gemm_ws(e, x.shape[0], n, k, x.device, mode, fused)
-    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
+    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk,
+           pack_out)
+
+
+def _tiled_packs(e, m, n, k, device, mode, rms_eps) -> bool:
+    """Whether the tiled GEMM's tuned plan for this decode shape can write a packed output copy: the plain split-K
+    path, whose reduce kernel runs the epilogue (not ks = 1, the stream-K / hybrid tiles or the in-kernel fixup)."""
+    if e is None or m > SKINNY_M or mode not in (MODE_RESIDUAL, MODE_SWIGLU):
+        return False
+    ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, _fused_rms(e, mode, rms_eps))
+    return ks > 1 and tm not in (SK_TILE, autotune.HYBRID_TILE) and not e.gemm_fixup_enabled()
 
 
 def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int:
@@ -368,7 +383,9 @@ def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int
     xp_in, p_out = x_packed is not None, pack_out is not None
     if GEMV_VARIANT:
         v = GEMV_VARIANT
-        if (v in XP_VARIANTS and not xp_in) or (p_out and v in (4, TILED)) or (v in SPLIT_VARIANTS and (
+        if (v in XP_VARIANTS and not xp_in) or (p_out and v == 4) or (p_out and v == TILED and not _tiled_packs(
+                e, x.shape[0], w.n, w.k, x.device, mode, None if mode == MODE_RESIDUAL else 1e-5)) or (
+                v in SPLIT_VARIANTS and (
                 no_split or x.dtype != BF16 or w.n // 16 > autotune.SPLIT_MAX_GROUPS)):
             v = 1
         if v in (12, 14) and mode == MODE_SWIGLU:
@@ -384,16 +401,20 @@ def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int
         p_out and pmode == MODE_RESIDUAL) else None
     pscratch = workspace.get("tune_pack", packed_rows(m) * ncols, BF16, x.device).view(-1, ncols) if p_out else None
 
+    tiled_packs = p_out and _tiled_packs(e, m, w.n, w.k, x.device, pmode, None if pmode == MODE_RESIDUAL else 1e-5)
+
     def run(v, xx, wt):
         if v == TILED:
-            _tiled(e, xx, wt, w.n, w.k, scratch, pmode, 1e-5, True)
+            _tiled(e, xx, wt, w.n, w.k, scratch, pmode, None if pmode == MODE_RESIDUAL else 1e-5, True, mirror,
+                   pscratch if tiled_packs else None)
         elif xp_in or p_out:
             e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk, mirror,
                             x_packed if v in XP_VARIANTS else None, pscratch)
         else:
             e.linear_skinny(xx, wt, w.n, w.k, scratch, pmode, 1e-5, True, v, ws, tk)
 
-    return autotune.choose(e, x, w, pmode, run, xp_in=xp_in, pack_out=p_out, no_split=no_split)
+    return autotune.choose(e, x, w, pmode, run, xp_in=xp_in, pack_out=p_out, no_split=no_split,
+                           tiled_packs=tiled_packs)
 
 
 _SK_SIZES = {}

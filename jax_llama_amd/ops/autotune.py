@@ -176,20 +176,20 @@ XP_CANDIDATES = (12, 13, 14, 15, 18, 19)  # packed-x GEMV variants (gemv.hip dis
 
 
 def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False,
-           no_split: bool = False) -> int:
+           no_split: bool = False, tiled_packs: bool = False) -> int:
     """``run(variant, x, weight_tensor)`` launches the op once. ``xp_in``: a packed copy of x exists, so the
     packed-x variants compete too; ``pack_out``: the epilogue must also write a packed copy of its output,
-    which only the GEMV variants do (no split-K skinny 4, no tiled 7); ``no_split``: without the split-K GEMV
+    which the GEMV variants do, and the tiled GEMM when ``tiled_packs`` (its split-K plan); ``no_split``: without the split-K GEMV
     variants (16-19; the fused-argmax lm_head GEMV has no split form)."""
     m = x.shape[0]
     # (TP-scoped decisions are cached apart: every rank of the group must take the same collective path)
-    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out, no_split, _SCOPE["comm"] is not None)
+    key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out, no_split, tiled_packs, _SCOPE["comm"] is not None)
     v = _CACHE.get(key)
     if v is not None:
         return v
     cands = list(candidates(m, w.n, swiglu=(mode == 2), bf16_x=(x.dtype == torch.bfloat16)))
-    if pack_out:
-        cands = [c for c in cands if c not in (4, TILED_VARIANT)]
+    if pack_out:  # the tiled GEMM qualifies when its split-K reduce epilogue writes the copy (``tiled_packs``)
+        cands = [c for c in cands if c != 4 and (c != TILED_VARIANT or tiled_packs)]
     if xp_in and x.dtype == torch.bfloat16:
         cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19)) and
                   (c < 18 or w.n // 16 <= SPLIT_MAX_GROUPS)]

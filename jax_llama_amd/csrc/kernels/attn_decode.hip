@@ -1071,11 +1071,25 @@ void attn_set_impl(int impl, int waves_target) {
 // v2 streams whole (b, kv head) pairs; below ~4096 pairs (B = 512 at 8 kv heads) v1's
 // chunk-per-workgroup design is as fast or faster (profiles/r1_attn_decode_v2_ab.jsonl,
 // r1_attn_decode_v2_geometry.jsonl), so smaller batches stay on v1.
-static bool use_v2(int B, int Hkv) { return g_attn_impl == 2 && B * Hkv >= g_attn_v2_min_pairs; }
+// The one-split register-ring stream (v4) also serves batches above the decode GEMV's rows (B > 64) below the v2
+// threshold: at rep <= 4 from there on, at rep 8 from 2048 (row, kv head) pairs. Graph-timed with cold K/V
+// (profiles/r3_attn_decode_v4_midbatch.jsonl): Llama-3-8B B = 128 / 256 (T 384) 71.9 / 129 us (v3) -> 57.9 / 70.5;
+// Llama-3-70B B = 256 (T 256 / 384) 158 / 206 -> 87 / 125; v3 stays ahead at B <= 64 (where it also writes the
+// packed copy the o projection's GEMV reads) and at rep 8 below 2048 pairs.
+static bool v4_midbatch(int B, int Hkv, int rep) {
+  return g_attn_impl == 2 && g_attn_v4 && g_attn_v2_min_pairs == 4096 && B > SKINNY_MAX_M && rep <= 8 &&
+         (rep <= 4 || B * Hkv >= 2048);
+}
+static bool use_v2(int B, int Hkv, int rep) {
+  return g_attn_impl == 2 && (B * Hkv >= g_attn_v2_min_pairs || v4_midbatch(B, Hkv, rep));
+}
+
 // v3 (one workgroup per (row, kv head), no split merge) below this many (row, kv head) pairs
 static int g_attn_v3_max_pairs = 4096;  // up to the v2 threshold: faster than v1 at B = 1..256 (8 kv heads)
 void attn_set_v3_max_pairs(int n) { g_attn_v3_max_pairs = n; }
-static bool use_v3(int B, int Hkv, int rep) { return rep <= 8 && !use_v2(B, Hkv) && B * Hkv <= g_attn_v3_max_pairs; }
+static bool use_v3(int B, int Hkv, int rep) {
+  return rep <= 8 && !use_v2(B, Hkv, rep) && B * Hkv <= g_attn_v3_max_pairs;
+}
 // v3 keys per lane-group row per chunk = base KPG (REP * KPG = 8) x this multiplier (1, 2, 4; capped at 8 rows):
 // fewer, larger chunks = fewer dependent load round trips on the latency-bound small-batch path
 // 0 = by size: x2 up to 128 (row, kv head) pairs (B <= 16 at 8 kv heads: B = 1 T = 384 12.4 -> 11.0 us, B = 8
@@ -1097,16 +1111,17 @@ int attn_decode_packs(int B, int Hkv, int rep) { return (use_v5(B, Hkv, rep) || 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
   if (use_v5(B, Hkv, rep)) return 16 * kpg5(rep);
   if (use_v3(B, Hkv, rep)) return T;
-  return use_v2(B, Hkv) ? 4 * kpg_v2(rep, B * Hkv) : 16 * kpg_v1(rep, B, Hkv, T);
+  return use_v2(B, Hkv, rep) ? 4 * kpg_v2(rep, B * Hkv) : 16 * kpg_v1(rep, B, Hkv, T);
 }
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
   if (use_v5(B, Hkv, rep)) return (T + 16 * kpg5(rep) - 1) / (16 * kpg5(rep));
   if (use_v3(B, Hkv, rep)) return 1;
-  if (!use_v2(B, Hkv)) {
+  if (!use_v2(B, Hkv, rep)) {
     const int ch = 16 * kpg_v1(rep, B, Hkv, T);
     return (T + ch - 1) / ch;
   }
+  if (v4_midbatch(B, Hkv, rep)) return 1;  // one split: the v4 stream (v2 with a key mask)
   const int pairs = B * Hkv;
   const int max_split = T > 64 ? (T + 63) / 64 : 1;  // >= 64 keys per split
   int ns = (g_attn_waves_target + pairs - 1) / pairs;
@@ -1162,7 +1177,7 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
 #undef JLA_AD3
     return -1;
   }
-  if (!use_v2(B, Hkv)) {
+  if (!use_v2(B, Hkv, rep)) {
     dim3 grid(nsplit, Hkv, B);
     const int kpg = kpg_v1(rep, B, Hkv, t_cap);
 #define JLA_AD(R, K)                                                                                           \
@@ -1182,14 +1197,17 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
 #undef JLA_AD
   }
   const int items = B * Hkv * nsplit;
-  if (g_attn_v4 && nsplit == 1 && !key_mask && rep <= 4) {
-#define JLA_AD4(R)                                                                                               \
+  if (g_attn_v4 && nsplit == 1 && !key_mask && rep <= 8) {
+#define JLA_AD4(R, K, U)                                                                                         \
   if (rep == R) {                                                                                                \
-    attn_decode_v4_kernel<R, 4, 3><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale); \
+    attn_decode_v4_kernel<R, K, U><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale); \
     JLA_CHECK_LAUNCH();                                                                                          \
     return 0;                                                                                                    \
   }
-    JLA_AD4(1) JLA_AD4(2) JLA_AD4(4)
+    JLA_AD4(1, 4, 3) JLA_AD4(2, 4, 3) JLA_AD4(4, 4, 3)
+    // rep 8 (Llama-3-70B: 8 q heads per kv head): twice the q / o registers of rep 4, so 8-key chunks, 3 in flight
+    // (16-key chunks x 3 slots at rep 8 fail the ring check: the compiler reuses in-flight ring registers)
+    JLA_AD4(8, 2, 4)
 #undef JLA_AD4
   }
   int split_len = (t_cap + nsplit - 1) / nsplit;

@@ -175,13 +175,15 @@ def test_attention_decode_streaming_v2(rep, t, slot, masked):
     assert got[2].float().abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize("rep", [1, 2, 4])
+@pytest.mark.parametrize("b", [512, 256, 128])
+@pytest.mark.parametrize("rep", [1, 2, 4, 8])
 @pytest.mark.parametrize("t,slot", [(300, 299), (520, 260)])
-def test_attention_decode_v4_large_batch(rep, t, slot):
-    """Large batch, one split, no key mask: the register-ring streaming kernel (v4) serves it; compare with the
-    fp32 reference and with the v2 LDS-DMA kernel (impl 4: same 16-key chunking -> same summation order)."""
+def test_attention_decode_v4_large_batch(rep, t, slot, b):
+    """Large batch, one split, no key mask: the register-ring streaming kernel (v4) serves it (from 4096 (row, kv
+    head) pairs, and mid-batch above 64 rows: every rep <= 4, rep 8 from 2048 pairs); compare with the fp32 reference
+    and with the v2 LDS-DMA kernel (impl 4)."""
     e = ops.ext()
-    b, hkv, dh = 4096 // 8, 8, 128
+    hkv, dh = 8, 128
     h = hkv * rep
     kc, vc = _cache(b, hkv, t, dh)
     q = torch.randn(b, 1, h, dh).to(BF16)

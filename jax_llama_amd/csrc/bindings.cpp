@@ -807,6 +807,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("car_pairs", &car_pairs, py::arg("state"), py::arg("mode"), py::arg("vals"), py::arg("idx"),
         py::arg("idx_offset"), py::arg("k"), py::arg("out_v").none(true), py::arg("out_i"));
   m.def("car_set_gran_max", [](int64_t n) { jla::car_set_gran_max(n); });
+  m.def("car_set_grid", [](int64_t st, int64_t grid) {
+    rc(jla::car_set_grid(reinterpret_cast<void*>(st), (int)grid), "car_set_grid");
+  });
   m.def("car_error", [](int64_t st) { return jla::car_error(reinterpret_cast<void*>(st)); });
   m.def("car_destroy", [](int64_t st) { jla::car_destroy(reinterpret_cast<void*>(st)); });
   m.def("car_free", [](int64_t buf, int64_t sig) {

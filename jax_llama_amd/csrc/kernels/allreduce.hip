@@ -18,7 +18,7 @@
 //   No release/acquire fences: the L2 write-back a system-scope release needs is both slow and subject
 //   to a known compiler hazard (the vmcnt wait after buffer_wbl2 can be dropped).
 //
-// Block b of every rank handles chunks c == b (mod CAR_GRID) of every message, so block b only ever
+// Block b of every rank handles chunks c == b (mod the instance grid, d.grid) of every message, so block b only ever
 // pairs with block b of its peers; barriers count per block and flags are monotonic. Every kernel maps
 // chunk c to the SAME bytes of a slot -- [c * CAR_CHUNK, (c + 1) * CAR_CHUNK) of A, and
 // [c * 2 * CAR_CHUNK, (c + 1) * 2 * CAR_CHUNK) of R whatever the element type -- so a block's slot bytes are
@@ -49,7 +49,11 @@
 
 namespace jla {
 
-constexpr int CAR_GRID = 63;     // chunk c -> block c % CAR_GRID on every call (fixed mapping)
+// chunk c -> block c % d.grid on every call (fixed mapping per instance): 63 blocks while ranks share a device, 255 with
+// one rank per GPU -- a 4 MiB message (the row-parallel partial of Llama-3-70B at MP 8, B = 256) then spreads over
+// every CU instead of 63 (profiles/r3_car_grid_ab.jsonl)
+static_assert(CAR_GRID_MAX <= CAR_BLOCKS && CAR_GRID_SHARED <= CAR_GRID_MAX && 2 * CAR_BLOCKS * 4 + 64 <= CAR_TAIL_BYTES,
+              "signal layout");
 constexpr int CAR_THREADS = 256;
 constexpr int CAR_CHUNK = CAR_THREADS * 16;  // input bytes per block iteration
 constexpr int CAR_PAIR_CHUNK = CAR_CHUNK / 8;  // pairs per block iteration: the same slot bytes as a reduce chunk
@@ -205,7 +209,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
   const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
 
   // 1. push this rank's input: to every peer (one-shot) or to the chunk's owner (two-shot)
-  for (long long c = b; c < nchunks; c += CAR_GRID) {
+  for (long long c = b; c < nchunks; c += d.grid) {
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
     const u32x4 v = c == b ? in0 : *reinterpret_cast<const u32x4*>(in + off);
@@ -220,7 +224,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
 
   if (!TWO_SHOT) {
     // 2. sum the slots in rank order, apply the op
-    for (long long c = b; c < nchunks; c += CAR_GRID) {
+    for (long long c = b; c < nchunks; c += d.grid) {
       const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
       if (off >= nbytes) continue;
       Piece<BF16> acc;
@@ -232,7 +236,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
     return;
   }
   // 2. owner: sum its chunks in rank order, push the fp32 sum to every rank's R region
-  for (long long c = b; c < nchunks; c += CAR_GRID) {
+  for (long long c = b; c < nchunks; c += d.grid) {
     if ((int)(c % d.world) != d.rank) continue;
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
@@ -250,7 +254,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
   }
   car_barrier(d, b, &st);
   // 3. every rank: apply the op to every chunk from the gathered sums
-  for (long long c = b; c < nchunks; c += CAR_GRID) {
+  for (long long c = b; c < nchunks; c += d.grid) {
     const long long off = c * CAR_CHUNK + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
     const long long roff = r_off + c * 2 * CAR_CHUNK + ((off - c * CAR_CHUNK) / ESZ) * 4;
@@ -307,7 +311,7 @@ __global__ void __launch_bounds__(GRAN_THREADS)
   const long long a_off = (long long)parity * d.world * slot;
   const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
   // 1. push: granules of this rank's payload into slot `rank` of every peer
-  for (long long c = b; c < nchunks; c += CAR_GRID) {
+  for (long long c = b; c < nchunks; c += d.grid) {
     const long long off = c * GRAN_PAYLOAD + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
     const u32x4 v = c == b ? in0 : *reinterpret_cast<const u32x4*>(in + off);
@@ -320,7 +324,7 @@ __global__ void __launch_bounds__(GRAN_THREADS)
   }
   // 2. per 16 payload bytes: poll every rank's two granule pairs until they carry this call's tag, sum in rank order
   const bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-  for (long long c = b; c < nchunks; c += CAR_GRID) {
+  for (long long c = b; c < nchunks; c += d.grid) {
     const long long off = c * GRAN_PAYLOAD + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
     Piece<BF16> acc;
@@ -361,7 +365,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
   const long long slot = d.max_bytes;
   const long long a_off = (long long)parity * d.world * slot;
   const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
-  for (long long c = blk; c < nchunks; c += CAR_GRID) {
+  for (long long c = blk; c < nchunks; c += d.grid) {
 #pragma unroll
     for (int t = 0; t < CAR_PAIRS_PER_THREAD; ++t) {
       const long long i = c * CAR_PAIR_CHUNK + t * CAR_THREADS + threadIdx.x;
@@ -371,7 +375,7 @@ __global__ void __launch_bounds__(CAR_THREADS)
     }
   }
   car_barrier(d, blk, &st);
-  for (long long c = blk; c < nchunks; c += CAR_GRID) {
+  for (long long c = blk; c < nchunks; c += d.grid) {
    for (int t = 0; t < CAR_PAIRS_PER_THREAD; ++t) {
     const long long i = c * CAR_PAIR_CHUNK + t * CAR_THREADS + threadIdx.x;
     if (i >= n) continue;
@@ -415,7 +419,7 @@ size_t car_buffer_bytes(long long max_bytes, int world) {
 // flags [CAR_BLOCKS][CAR_MAX_WORLD], then ctr [CAR_BLOCKS] (int2), the error word, and the per-workgroup call counters
 // of the fused row-parallel GEMV (gemv.hip MODE_TPRESID)
 size_t car_signal_bytes() {
-  return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 1024 + (size_t)CAR_WG_COUNTERS * sizeof(int);
+  return (size_t)CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + CAR_TAIL_BYTES + (size_t)CAR_WG_COUNTERS * sizeof(int);
 }
 
 int car_alloc(long long max_bytes, int world, void** buf, void** sig, hipIpcMemHandle_t* hbuf,
@@ -458,6 +462,7 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   st->n_opened = 0;
   st->h.rank = rank;
   st->h.world = world;
+  st->h.grid = CAR_GRID_SHARED;
   st->h.max_bytes = max_bytes;
   int dev = 0, rate_khz = 0;
   (void)hipGetDevice(&dev);
@@ -490,7 +495,8 @@ int car_init(int rank, int world, long long max_bytes, void* own_buf, void* own_
   int* tail = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int));
   st->h.ctr = reinterpret_cast<int2*>(tail);  // [CAR_BLOCKS] {calls, barriers}
   st->h.error = tail + 2 * CAR_BLOCKS;
-  st->h.wg_ctr = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) + 1024);
+  st->h.wg_ctr = reinterpret_cast<int*>(static_cast<char*>(own_sig) + CAR_BLOCKS * CAR_MAX_WORLD * sizeof(int) +
+                                        CAR_TAIL_BYTES);
   st->d = nullptr;
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&st->d), sizeof(CarDevice));
   if (e == hipSuccess) e = hipMemcpy(st->d, &st->h, sizeof(CarDevice), hipMemcpyHostToDevice);
@@ -530,7 +536,7 @@ int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t*
   if (two_shot && st->h.world == 1) two_shot = 0;
   if (!two_shot && nbytes <= g_car_gran_max && 2 * nbytes <= st->h.max_bytes) {
     const long long gch = (nbytes + GRAN_PAYLOAD - 1) / GRAN_PAYLOAD;
-    const int ggrid = (int)(gch < CAR_GRID ? gch : CAR_GRID);
+    const int ggrid = (int)(gch < st->h.grid ? gch : st->h.grid);
     const char* ip = static_cast<const char*>(in);
 #define JLA_GRAN(OPV, BFV)                                                                                          \
   car_gran_kernel<OPV, BFV><<<ggrid, GRAN_THREADS, 0, s>>>(ip, out, h, hb, nbytes, st->d, OPV == OP_RESID ? hb_pack : nullptr, \
@@ -545,7 +551,7 @@ int car_reduce(void* state, int op, const void* in, void* out, float* h, bf16_t*
     return 0;
   }
   const long long nchunks = (nbytes + CAR_CHUNK - 1) / CAR_CHUNK;
-  const int grid = (int)(nchunks < CAR_GRID ? nchunks : CAR_GRID);
+  const int grid = (int)(nchunks < st->h.grid ? nchunks : st->h.grid);
   if (op == OP_SUM) {
     if (is_bf16) launch_reduce<OP_SUM, true>(two_shot, grid, in, out, h, hb, nbytes, st->d, s, nullptr, 0);
     else launch_reduce<OP_SUM, false>(two_shot, grid, in, out, h, hb, nbytes, st->d, s, nullptr, 0);
@@ -566,13 +572,22 @@ int car_pairs(void* state, int mode, const float* a, const int32_t* b, int idx_o
   if (n * 8 > st->h.max_bytes) return -2;
   if (mode == PAIRS_TOPK && (k <= 0 || n % k || !out_a)) return -1;
   const long long nchunks = (n + CAR_PAIR_CHUNK - 1) / CAR_PAIR_CHUNK;
-  const int grid = (int)(nchunks < CAR_GRID ? nchunks : CAR_GRID);
+  const int grid = (int)(nchunks < st->h.grid ? nchunks : st->h.grid);
   if (mode == PAIRS_ARGMAX)
     car_pairs_kernel<PAIRS_ARGMAX><<<grid, CAR_THREADS, 0, s>>>(a, b, idx_offset, n, k, out_a, out_b, st->d);
   else
     car_pairs_kernel<PAIRS_TOPK><<<grid, CAR_THREADS, 0, s>>>(a, b, idx_offset, n, k, out_a, out_b, st->d);
   JLA_CHECK_LAUNCH();
   return 0;
+}
+
+// collective blocks per launch of this instance (every rank of the group must set the same value, before first use)
+int car_set_grid(void* state, int grid) {
+  CarHost* st = static_cast<CarHost*>(state);
+  if (grid == 0) grid = CAR_GRID_MAX;
+  if (!st || grid < 1 || grid > CAR_GRID_MAX) return -1;
+  st->h.grid = grid;
+  return (int)hipMemcpy(st->d, &st->h, sizeof(CarDevice), hipMemcpyHostToDevice);
 }
 
 int car_world(void* state) { return static_cast<CarHost*>(state)->h.world; }

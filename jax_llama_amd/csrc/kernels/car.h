@@ -8,7 +8,10 @@
 namespace jla {
 
 constexpr int CAR_MAX_WORLD = 8;
-constexpr int CAR_BLOCKS = 64;         // signal rows (one per collective block)
+constexpr int CAR_BLOCKS = 256;        // signal rows (one per collective block)
+constexpr int CAR_TAIL_BYTES = 4096;   // after the flags: ctr [CAR_BLOCKS] (int2) and the error word
+constexpr int CAR_GRID_SHARED = 63;    // ranks sharing one GPU (tests): 8 x 63 blocks stay co-resident
+constexpr int CAR_GRID_MAX = 255;      // one rank per GPU: a 4 MiB message spreads over every CU
 
 struct CarDevice {
   char* buf[CAR_MAX_WORLD];     // every rank's buffer (A then R), mapped here
@@ -20,6 +23,9 @@ struct CarDevice {
   long long max_bytes;          // A slot size; R holds 2 * max_bytes per parity
   long long timeout_ticks;      // wall-clock ticks (s_memrealtime, 100 MHz) before giving up
   int rank, world;
+  int grid;                     // collective blocks per launch (chunk c -> block c % grid on every call, every rank):
+                                // CAR_GRID_SHARED while ranks share a device (every rank's blocks co-resident), else
+                                // CAR_GRID_MAX; fixed for the life of the instance
 };
 
 constexpr int SYS = 17;  // cache policy bits: sc0 | sc1

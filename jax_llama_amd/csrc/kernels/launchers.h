@@ -149,6 +149,7 @@ int car_error(void* state);
 const void* car_device(void* state);      // the device-side CarDevice (car.h) of an instance (MODE_TPRESID)
 long long car_max_bytes(void* state);
 int car_world(void* state);
+int car_set_grid(void* state, int grid);  // collective blocks per launch (0: the maximum; same on every rank, before first use)
 void car_destroy(void* state);
 int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,
                   int32_t* positions, int32_t* slot, int B, int L, int pad, int eos, hipStream_t s);

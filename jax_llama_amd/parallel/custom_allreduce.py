@@ -110,6 +110,14 @@ class CustomAllReduce:
         keys = [None] * world
         dist.all_gather_object(keys, key, group=group)
         car = cls(state, rank, world, max_bytes, share=max(keys.count(k) for k in keys), group=group)
+        grid = int(os.environ.get("JLA_CAR_GRID", "0"))  # tests: pin the grid (the same on every rank)
+        if grid > 0:
+            e.car_set_grid(state, grid)
+        elif car.share == 1:
+            # one rank per GPU: up to 255 collective blocks (a 4 MiB partial over every CU); ranks sharing a device
+            # keep 63 so every rank's blocks stay co-resident (they spin for each other). Same value on every rank,
+            # set before the first call (the self-test): the chunk -> block map must never change under an instance.
+            e.car_set_grid(state, 0)
         # protocol self-test on the real links: a known sum, checked on the host by every rank
         ok = car.self_test()
         dist.all_gather_object(oks, ok, group=group)
@@ -130,6 +138,8 @@ class CustomAllReduce:
         except RuntimeError:
             e.car_free(buf, sig)
             raise
+        # the only rank on its GPU: the full collective grid, as a TP rank on its own GPU (JLA_CAR_GRID pins one: A/B)
+        e.car_set_grid(state, int(os.environ.get("JLA_CAR_GRID", "0")))
         return cls(state, 0, 1, max_bytes)
 
     def self_test(self) -> bool:

@@ -132,9 +132,11 @@ def _run(rank, world, q):
     return car
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, grid=0):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if grid:
+            os.environ["JLA_CAR_GRID"] = str(grid)
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -149,12 +151,14 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_custom_collectives_exact(world):
+@pytest.mark.parametrize("world,grid", [(2, 0), (4, 0), (8, 0), (2, 255)])
+def test_custom_collectives_exact(world, grid):
+    """grid 0: the shared-device default (63 blocks); 255: the one-rank-per-GPU grid, pinned (2 x 255 blocks still fit
+    co-resident on the one test GPU)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, grid)) for r in range(world)]
     for p in procs:
         p.start()
     outs = []

@@ -432,33 +432,50 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
 static int g_attn_prefill_impl = 2;
 void attn_prefill_set_impl(int impl) { g_attn_prefill_impl = impl; }
 
+// v2 launch with NW waves per workgroup: NW / rep position blocks (rep < NW) or NW of the rep q heads (rep >= NW) share
+// each K/V tile the workgroup stages; `paired_only`: always the (heavy, light) pair per workgroup (impl 4 / 6)
+template <int NW>
+static void launch_prefill_v2(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot,
+                              const int32_t* kv_start, const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S,
+                              int H, int Hkv, int T, int rep, bool paired_only, hipStream_t s) {
+  const int npb = rep >= NW ? 1 : NW / rep;    // position blocks per workgroup
+  const int hpw = NW / npb;                    // q heads per workgroup
+  const int hgroups = rep / hpw;
+  const float sl2 = 1.4426950408889634f / sqrtf((float)AP_DH);
+  const int n_qb = (S + 32 * npb - 1) / (32 * npb);
+  const int pairs = (n_qb + 1) / 2 * Hkv * hgroups * B;
+  // fewer pairs than two workgroups per CU (B = 1 prefill): each half of a pair is its own workgroup, so a CU
+  // holds two resident workgroups instead of one
+  const bool split = !paired_only && pairs < 2 * 256;
+  if (split) {
+    attn_prefill_v2_kernel<NW, 1><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
+        q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H, Hkv, T, sl2, npb, hgroups, n_qb, 1);
+  } else {
+    dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
+    attn_prefill_v2_kernel<NW, 1><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
+                                                             Hkv, T, sl2, npb, hgroups, n_qb, 0);
+  }
+}
+
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,
                  hipStream_t s) {
   if (B <= 0 || S <= 0) return 0;
   if (Dh != AP_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
-  constexpr int NW = 4;
-  if ((g_attn_prefill_impl == 2 || g_attn_prefill_impl == 4) && (rep % NW == 0 || NW % rep == 0)) {
-    const int npb = rep >= NW ? 1 : NW / rep;    // position blocks per workgroup
-    const int hpw = NW / npb;                    // q heads per workgroup
-    const int hgroups = rep / hpw;
-    const float sl2 = 1.4426950408889634f / sqrtf((float)Dh);
-    {
-      const int n_qb = (S + 32 * npb - 1) / (32 * npb);
-      const int pairs = (n_qb + 1) / 2 * Hkv * hgroups * B;
-      // fewer pairs than two workgroups per CU (B = 1 prefill): each half of a pair is its own workgroup, so a CU
-      // holds two resident workgroups (8 waves) instead of one; impl 4 = always paired (A/B)
-      const bool split = g_attn_prefill_impl == 2 && pairs < 2 * 256;
-      if (split) {
-        attn_prefill_v2_kernel<NW, 1><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
-            q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H, Hkv, T, sl2, npb, hgroups, n_qb, 1);
-      } else {
-        dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
-        attn_prefill_v2_kernel<NW, 1><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out,
-                                                                S, H, Hkv, T, sl2, npb, hgroups, n_qb, 0);
-      }
-    }
+  const int impl = g_attn_prefill_impl;
+  // impl 2 (default) / 4 (always paired): 4 waves per workgroup; 5 / 6: the same with 8 waves (A/B). The default
+  // takes the 8-wave paired launch for long prompts and rep >= 8, where twice the queries per staged K/V tile pay
+  // (interleaved A/B, profiles/r3_attn_prefill_nw8_ab.jsonl: 8B S = 8192 826 -> 877 TFLOP/s, 70B S = 2048 689 -> 716;
+  // 4 waves stay ahead at S = 2048 with rep 4 and at S = 128)
+  const bool auto8 = impl == 2 && (rep == 1 || rep == 2 || rep == 4 || rep == 8) && (S >= 4096 || (rep >= 8 && S >= 1024));
+  const bool eight = impl == 5 || impl == 6 || auto8;
+  const int nw = eight ? 8 : 4;
+  if ((impl == 2 || impl == 4 || eight) && (rep % nw == 0 || nw % rep == 0)) {
+    if (eight)
+      launch_prefill_v2<8>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, impl != 5, s);
+    else
+      launch_prefill_v2<4>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, impl == 4, s);
     JLA_CHECK_LAUNCH();
     return 0;
   }

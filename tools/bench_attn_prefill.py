@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Prefill attention throughput (causal, GQA) at real model shapes: TFLOP/s of impl 2 (GQA-shared
-32x32x16 MFMA flash kernel, 32 queries per wave), impl 4 (always paired launch) and impl 1 (v1). FLOPs counted for the causal triangle only:
+32x32x16 MFMA flash kernel, 32 queries per wave), impl 4 (always paired launch), impl 5 / 6 (the
+same with 8 waves per workgroup: twice the queries per staged K/V tile) and impl 1 (v1). FLOPs counted for the causal triangle only:
 4 * B * H * Dh * S (S + 1) / 2. Prints one JSON line per (shape, impl)."""
 from __future__ import annotations
 
@@ -25,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default=None, help="run only this shape name (profiling)")
     ap.add_argument("--impl", type=int, default=None, help="run only this impl (profiling)")
+    ap.add_argument("--impls", type=int, nargs="*", default=None, help="impls to compare (default 2 4 5 6 1)")
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     e = ops.ext()
     for name, b, s, h, hkv in SHAPES:
@@ -38,26 +41,30 @@ def main():
         slot = torch.zeros(1, dtype=torch.int32, device="cuda")
         flops = 4.0 * b * h * 128 * s * (s + 1) / 2
         ref = None
-        for impl in (2, 4, 3, 1):
-            if impl == 1 and s * s * b * h > 2048 * 2048 * 16 * 32:
-                continue
-            if args.impl is not None and impl != args.impl:
-                continue
+        impls = [i for i in (args.impls or (2, 4, 5, 6, 1)) if not (i == 1 and s * s * b * h > 2048 * 2048 * 16 * 32)
+                 and (args.impl is None or i == args.impl)]
+        best, diffs = {i: float("inf") for i in impls}, {}
+        for impl in impls:  # warm-up + correctness vs the first impl
             e.attn_prefill_set_impl(impl)
             o = ops.attention(q, kc, vc, slot, ks)
             torch.cuda.synchronize()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            n = 5
-            ev[0].record()
-            for _ in range(n):
-                ops.attention(q, kc, vc, slot, ks)
-            ev[1].record()
-            torch.cuda.synchronize()
-            us = ev[0].elapsed_time(ev[1]) * 1000 / n
-            diff = 0.0 if ref is None else float((o.float() - ref.float()).abs().max())
+            diffs[impl] = 0.0 if ref is None else float((o.float() - ref.float()).abs().max())
             ref = o if ref is None else ref
-            print(json.dumps({"shape": name, "impl": impl, "us": round(us, 1),
-                              "tflops": round(flops / us / 1e6, 1), "max_diff_vs_impl2": round(diff, 5)}), flush=True)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for _ in range(args.rounds):  # interleaved rounds, min per impl (DVFS drift between impls)
+            for impl in impls:
+                e.attn_prefill_set_impl(impl)
+                n = 5
+                ev[0].record()
+                for _ in range(n):
+                    ops.attention(q, kc, vc, slot, ks)
+                ev[1].record()
+                torch.cuda.synchronize()
+                best[impl] = min(best[impl], ev[0].elapsed_time(ev[1]) * 1000 / n)
+        for impl in impls:
+            us = best[impl]
+            print(json.dumps({"shape": name, "impl": impl, "us": round(us, 1), "tflops": round(flops / us / 1e6, 1),
+                              "max_diff_vs_first": round(diffs[impl], 5)}), flush=True)
         e.attn_prefill_set_impl(2)
         del kc, vc, q
         torch.cuda.empty_cache()

@@ -224,8 +224,8 @@ void linear_skinny_argmax(Tensor x, Tensor w, int64_t n, int64_t k, double rms_e
         "x must be fp32/bf16 [M, K]");
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_skinny_argmax: M too large");
-  check(variant == 1 || variant == 2 || variant == 3 || (variant >= 5 && variant <= 11 && variant != 7),
-        "argmax: GEMV variants only");
+  check(variant == 1 || variant == 2 || variant == 3 || (variant >= 5 && variant <= 11 && variant != 7) || variant == 20,
+        "argmax: GEMV variants only (row-major x)");
   check_gpu(part, "part");
   check(part.scalar_type() == torch::kFloat32 && part.numel() >= m * (n / 16) * 2, "argmax partials too small");
   check_gpu(idx, "idx");

@@ -474,6 +474,14 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
                                                                      out_f32, qa, s, ks);
       }
     }
+    // 2 tiles x 8 waves (20 row-major, 21 packed x): twice the bytes in flight per workgroup of the 2-tile variants
+    // for wide projections with few column groups (w1|w3 at Llama-3-70B MP 8: 224 workgroups of the SwiGLU pairs)
+    if (variant == 20)
+      return launch_skinny<XT, MT, 2, MODE, 8>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    if constexpr (sizeof(XT) == 2) {
+      if (variant == 21)
+        return launch_skinny<XT, MT, 2, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    }
     // packed-x variants (x is the packed copy, common.h pack_off, padded to MT * 16 rows): 12 = 1 tile x 8 waves,
     // 13 = 2 tiles x 4 waves, 14 / 15 = the same with a doubled ring
     if constexpr (sizeof(XT) == 2) {

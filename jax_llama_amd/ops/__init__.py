@@ -236,7 +236,7 @@ PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
 PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "64"))
 PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
 SKINNY_M = 64  # decode GEMV rows (csrc: SKINNY_MAX_M): packed copies exist only on that path
-XP_VARIANTS = (12, 13, 14, 15, 18, 19)  # packed-x GEMV variants (18 / 19: split-K)
+XP_VARIANTS = (12, 13, 14, 15, 18, 19, 21)  # packed-x GEMV variants (18 / 19: split-K; 21: 2 tiles x 8 waves)
 SPLIT_VARIANTS = (16, 17, 18, 19)  # split-K GEMV variants (the shared skinny workspace holds their slabs)
 
 
@@ -567,7 +567,7 @@ def linear_argmax(x: torch.Tensor, w, rms_eps: Optional[float] = None):
     if m <= ext().SKINNY_MAX_M and SKINNY_ARGMAX:
         e = ext()
         v = _variant(e, x, w, MODE_STORE, no_split=True)  # the logits GEMV's main loop: its tuned variant applies
-        if v in (1, 2, 3, 5, 6, 8, 9):
+        if v in (1, 2, 3, 5, 6, 8, 9, 20):
             part = workspace.get("skinny_argmax", m * (w.n // 16) * 2, torch.float32, x.device)
             idx = torch.empty(m, dtype=torch.int32, device=x.device)
             val = torch.empty(m, dtype=torch.float32, device=x.device)

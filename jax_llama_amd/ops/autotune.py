@@ -160,6 +160,8 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
             c.extend([9, 11, 10])
         # (variant 8 -- 16 waves -- measured no faster than 1/4/6/7 at M = 32:
         # profiles/r2_decode_m32_variants_8_9.jsonl; kept as an explicit choice, not tuned)
+    if n // 32 < 512:
+        c.append(20)  # 2 tiles x 8 waves: few column groups (w1|w3 shards)
     if bf16_x and n // 16 <= SPLIT_MAX_GROUPS:
         # split-K GEMV (K over 2 / 4 workgroups per column group, in-kernel last-arriver sum): few column groups
         c.extend([16, 17])
@@ -172,7 +174,7 @@ SPLIT_MAX_GROUPS = 1024  # csrc GEMV_SPLIT_MAX_GROUPS
 TILED_VARIANT = 7
 
 
-XP_CANDIDATES = (12, 13, 14, 15, 18, 19)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 split-K)
+XP_CANDIDATES = (12, 13, 14, 15, 18, 19, 21)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 split-K)
 
 
 def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False,
@@ -191,8 +193,8 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     if pack_out:  # the tiled GEMM qualifies when its split-K reduce epilogue writes the copy (``tiled_packs``)
         cands = [c for c in cands if c != 4 and (c != TILED_VARIANT or tiled_packs)]
     if xp_in and x.dtype == torch.bfloat16:
-        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19)) and
-                  (c < 18 or w.n // 16 <= SPLIT_MAX_GROUPS)]
+        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19, 21)) and
+                  (c not in (18, 19) or w.n // 16 <= SPLIT_MAX_GROUPS) and (c != 21 or w.n // 32 < 512)]
     if no_split:
         cands = [c for c in cands if not 16 <= c <= 19]
     if not ENABLED or torch.cuda.is_current_stream_capturing():

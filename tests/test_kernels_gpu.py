@@ -327,7 +327,7 @@ def test_attention_decode_8k(rep):
 
 
 @pytest.mark.parametrize("m", [1, 5, 17, 40, 64])
-@pytest.mark.parametrize("variant", [1, 5, 6, 9, 10, 11])
+@pytest.mark.parametrize("variant", [1, 5, 6, 9, 10, 11, 20])
 def test_linear_skinny_argmax(m, variant):
     """Decode lm_head with the argmax in the GEMV epilogue == stored fp32 logits + first-max argmax,
     bit for bit (same accumulation order), including an exact tie across two 16-column tiles."""
@@ -437,7 +437,7 @@ def test_gemv_variants_agree():
 
 
 @pytest.mark.parametrize("k", [256, 4096])
-@pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11, 16, 17])
+@pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11, 16, 17, 20])
 @pytest.mark.parametrize("m", [1, 9, 16, 40, 64])
 def test_decode_linear_paths_all_modes(variant, m, k):
     """Both decode GEMM designs (and the GEMV's tile / ring-depth variants: at M > 16 the hand-counted
@@ -875,7 +875,7 @@ def _qkv_rope_stream_k(e, m, s):
     _close(vg, vc, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("variant", [12, 13, 14, 15, 18, 19, 7])
+@pytest.mark.parametrize("variant", [12, 13, 14, 15, 18, 19, 21, 7])
 @pytest.mark.parametrize("m", [1, 12, 16, 20, 32, 40, 64])
 def test_packed_x_variants_and_packed_epilogues(m, variant):
     """Packed-x GEMV variants read the packed copy (ref.pack_act) and match the fp32 reference; the residual /

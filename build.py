@@ -90,7 +90,10 @@ def _scratch_users(remarks: str):
 # spill-free at this bound: its 256 accumulators + two fragment sets use the whole 512-register file).
 SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20,
               # gemm2 FA + fused RMS: a 3-dword spill in the split-K fixup tail (after the main loop)
-              "gemm2_kernelILi0ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16, "gemm2_kernelILi2ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16}
+              "gemm2_kernelILi0ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16, "gemm2_kernelILi2ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16,
+              # gemm2 FA + fused RMS, direct RoPE / KV-write epilogue (MODE_QKV): 3 dwords spilled and reloaded in
+              # the LDS-staged epilogue, after the last MFMA (checked in the .s)
+              "gemm2_kernelILi3ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1ELi2E": 16}
 
 
 def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):

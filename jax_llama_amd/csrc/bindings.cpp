@@ -403,7 +403,7 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
 // applies the fused RMSNorm statistic, otherwise x must already be scaled).
 void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor positions, Tensor kc, Tensor vc,
               Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q, int64_t ksplit,
-              Tensor ws, double rms_eps, int64_t tile, c10::optional<Tensor> tickets) {
+              c10::optional<Tensor> ws, double rms_eps, int64_t tile, c10::optional<Tensor> tickets) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -417,9 +417,17 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
        "gemm_qkv");
     return;
   }
-  check(ksplit >= 2, "gemm_qkv: ksplit >= 2");
+  if (ksplit <= 1) {  // no K split: the GEMM's own RoPE / KV-write epilogue (default FA pipeline, fused norm)
+    check(rms_eps >= 0 && jla::gemm_qkv_direct_ok((int)m, (int)tile), "gemm_qkv without a K split: 256 x 256 FA "
+          "tiles with the fused norm (gemm_qkv_direct_ok)");
+    rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, nullptr, 0, 1, stream(),
+                 (float)rms_eps, (int)tile),
+       "gemm_qkv");
+    return;
+  }
+  check(ws.has_value(), "gemm_qkv: a K split needs the slab workspace");
   check_gemm_ws(ws, ksplit, m, n, rms_eps >= 0);
-  rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(ws), ws.numel(),
+  rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(*ws), ws->numel(),
                ksplit, stream(), (float)rms_eps, (int)tile),
      "gemm_qkv");
 }
@@ -732,6 +740,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
         py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none(),
         py::arg("pack_out") = py::none());
+  m.def("gemm_qkv_direct_ok", [](int64_t m, int64_t tile) { return jla::gemm_qkv_direct_ok((int)m, (int)tile) != 0; });
   m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
     return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
   }, "(slab floats, tickets) of the in-kernel split-K fixup");

@@ -902,7 +902,7 @@ JLA_DEV void ad_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-template <int REP, int KPG, int U>
+template <int REP, int KPG, int U, bool DIAG = false>
 __global__ void __launch_bounds__(64)
     attn_decode_v4_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
@@ -1003,7 +1003,11 @@ __global__ void __launch_bounds__(64)
         for (int e = 0; e < L; ++e) ad_pin(ring[u][e]);
 #pragma unroll
         for (int h = 0; h < REP; ++h) ad_pin(qp[h]);
-        if (c < nc) compute(ring[u], ring[u] + KPG, c);
+        if constexpr (DIAG) {  // tools only (attn_set_diag): the stream without the math (the pins keep it live)
+          (void)c;
+        } else {
+          if (c < nc) compute(ring[u], ring[u] + KPG, c);
+        }
       }
     }
     // retire the past-the-end refills, keeping every ring register live until then
@@ -1204,6 +1208,11 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
     JLA_CHECK_LAUNCH();                                                                                          \
     return 0;                                                                                                    \
   }
+    if (g_attn_diag && rep == 4) {  // tools only: stream-only build of the rep-4 kernel (wrong results)
+      attn_decode_v4_kernel<4, 4, 3, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale);
+      JLA_CHECK_LAUNCH();
+      return 0;
+    }
     JLA_AD4(1, 4, 3) JLA_AD4(2, 4, 3) JLA_AD4(4, 4, 3)
     // rep 8 (Llama-3-70B: 8 q heads per kv head): twice the q / o registers of rep 4, so 8-key chunks, 3 in flight
     // (16-key chunks x 3 slots at rep 8 fail the ring check: the compiler reuses in-flight ring registers)

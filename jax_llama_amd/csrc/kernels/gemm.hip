@@ -231,7 +231,7 @@ template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                 float rms_eps, float* __restrict__ ssq_ws, G2Fix fix) {
+                 float rms_eps, float* __restrict__ ssq_ws, G2Fix fix, QKVArgs qa) {
   // wave tile: MT m-tiles x NTW n-tiles of 16x16 (128 x 64 by default; 64 x 32 for the 128 x 128 tile)
   constexpr int NW = 4 * WM, BM = 16 * MT * WM, BN = 64 * NTW;
   constexpr int RPW = MT / 4;  // RMS: m-tiles whose row statistics each wave accumulates
@@ -821,6 +821,70 @@ __global__ void __launch_bounds__(256 * WM)
         const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
         if (c == 0 && row < M) o[(size_t)row * P + slot] = make_float2(bv, __int_as_float(bi));
       }
+  } else if constexpr (MODE == MODE_QKV) {
+    // fused qkv projection without a K split (decode B = 2048, prefill): the (norm-scaled) accumulators are staged
+    // through LDS one wave row (128 x 256 fp32) at a time, then every thread takes 4 consecutive columns of a row --
+    // two RoPE pairs -- rotates the q / k heads and writes q, or the k / v cache row at slot[0] + (position in the
+    // sequence), 8 bytes per store; replaces the bf16 store + rope_kv_kernel round trip (same arithmetic as
+    // gemm_reduce_kernel<MODE_QKV>; reference model.py:58-92, :169-199)
+    static_assert(WM == 2 && MT == 8 && NTW == 4, "QKV epilogue: 256 x 256 tiles");
+    float* ep = reinterpret_cast<float*>(lds);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is past its last read of the tile buffers
+#pragma unroll 1
+    for (int half = 0; half < 2; ++half) {
+      if (wr == half) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTW; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = i * 16 + 4 * (lane >> 4) + r;
+              const int col = ((wc * NTW + j) * 16 + c) ^ (((row >> 2) & 3) << 4);
+              ep[row * BN + col] = acc[i][j][r];
+            }
+      }
+      __syncthreads();
+#pragma unroll 2
+      for (int qq = 0; qq < 16; ++qq) {
+        const int e = threadIdx.x + 512 * qq;
+        const int row = e >> 6, c4 = (e & 63) * 4;
+        const int grow = m0 + half * 128 + row, gcol = n0 + c4;
+        const float4 v = *reinterpret_cast<const float4*>(ep + row * BN + (c4 ^ (((row >> 2) & 3) << 4)));
+        if (grow >= M || gcol >= N) continue;
+        float v0 = v.x, v1 = v.y, v2 = v.z, v3 = v.w;
+        const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
+        const int b = grow / qa.S, sq = grow - b * qa.S;
+        if (head < qa.H + qa.Hkv) {
+          int pos = qa.positions[grow];
+          if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
+          pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
+          const float4 cs = *reinterpret_cast<const float4*>(qa.table + (size_t)pos * (qa.Dh >> 1) + (d0 >> 1));
+          const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
+          const float r2 = v2 * cs.z - v3 * cs.w, r3 = v2 * cs.w + v3 * cs.z;
+          v0 = r0;
+          v1 = r1;
+          v2 = r2;
+          v3 = r3;
+        }
+        const uint2 packed = make_uint2(pack2bf(v0, v1), pack2bf(v2, v3));
+        if (head < qa.H) {
+          *reinterpret_cast<uint2*>(qa.q + ((size_t)grow * qa.H + head) * qa.Dh + d0) = packed;
+        } else {
+          const int cslot = qa.slot[0] + sq;
+          if (cslot < qa.T) {
+            const bool is_k = head < qa.H + qa.Hkv;
+            const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
+            bf16_t* cache = is_k ? qa.kc : qa.vc;
+            *reinterpret_cast<uint2*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + cslot) * qa.Dh + d0) = packed;
+          } else {
+            JLA_FLAG(JLA_BOUNDS_KV_SLOT);
+          }
+        }
+      }
+      __syncthreads();  // the half-tile is consumed before the other wave row overwrites it
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
@@ -1361,11 +1425,14 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 //   3: 128 x 128, 8 waves (two ping-pong rows) of 64 x 32 -- 64 KiB of LDS, so two workgroups can share a CU;
 //      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
+int gemm_qkv_direct_ok(int M, int tile) {
+  return g_gemm_impl == 2 && g_g2_var == 5 && (tile == 0 || tile == 1) && tile_cfg(tile, M) == 1;
+}
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
-                      int grid_override = 0, G2Fix fix = G2Fix{}) {
+                      int grid_override = 0, G2Fix fix = G2Fix{}, const QKVArgs& qa = QKVArgs{}) {
   const int cfg = tile_cfg(tile, M);
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
@@ -1373,11 +1440,14 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int grid = grid_override > 0 ? grid_override : (fix.tile_count > 0 ? fix.tile_count : tm * tn) * ksplit;
 #define JLA_G2S(WMV, NB, LATE, R, MTV, NTV, SB)                                                             \
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
-      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix)
+      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix, qa)
 #define JLA_G2(WMV, NB, LATE, R, MTV, NTV) JLA_G2S(WMV, NB, LATE, R, MTV, NTV, 1)
 #define JLA_G2FA(R, FM)                                                                                      \
   gemm2_kernel<MODE, 2, 4, true, R, 8, 4, 1, true, FM><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate,     \
-                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix)
+                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix, qa)
+  if constexpr (MODE == MODE_QKV) {  // the direct RoPE / KV-write epilogue: the default 256 x 256 FA pipeline only
+    JLA_G2FA(true, 2);
+  } else {
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   if constexpr (MODE != MODE_RESIDUAL) {
     if (rms) {  // fused RMSNorm statistic (default pipeline variant only)
@@ -1412,6 +1482,7 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     JLA_G2FA(false, 0);
   else
     JLA_G2(2, 4, false, false, 8, 4);
+  }
 #undef JLA_G2FA
 #undef JLA_G2
 #undef JLA_G2S
@@ -1563,15 +1634,19 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
     if (mode == MODE_QKV) return -1;
     tile = 1;  // whole waves only: the plain data-parallel launch
   }
-  if (mode == MODE_QKV && (!qkv || ksplit < 2)) return -1;  // qkv epilogue only in the reduce kernel
+  if (mode == MODE_QKV && !qkv) return -1;
   const int KS = K >> 5;
   if (ksplit < 1) ksplit = 1;
   const int kc = (KS + ksplit - 1) / ksplit;
   ksplit = (KS + kc - 1) / kc;
-  if (mode == MODE_QKV && ksplit < 2) return -1;
+  // qkv without a K split: the RoPE / KV-write epilogue of the default FA pipeline (256 x 256 tiles, fused norm)
+  if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile) && rms)) return -1;
   const u32x4* w = static_cast<const u32x4*>(W);
   if (ksplit == 1) {
     switch (mode) {
+      case MODE_QKV:
+        launch_g2<MODE_QKV>(x, w, nullptr, M, N, K, 0, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s, 0, G2Fix{}, *qkv);
+        break;
       case MODE_STORE:
         launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile, s);
         break;
@@ -1728,10 +1803,10 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   const u32x4* w = static_cast<const u32x4*>(W);
   if (rms_eps >= 0.f)
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, true, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
-        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{});
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{}, QKVArgs{});
   else
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, false, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
-        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{});
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{}, QKVArgs{});
   JLA_CHECK_LAUNCH();
   launch_argmax_partials(reinterpret_cast<const float2*>(ws), tn * 4, M, idx, val, s);
   JLA_CHECK_LAUNCH();

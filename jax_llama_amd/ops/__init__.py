@@ -293,6 +293,9 @@ def linear_tp_residual(x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, st
 
 
 TILED = 7  # decode-kernel "variant" id of the 128x128 MFMA GEMM (split-K for mid M)
+# qkv projection without a K split (B = 2048 decode, prefill): RoPE + KV write in the GEMM epilogue (JLA_QKV_DIRECT=0:
+# plain GEMM + rope_kv_kernel, for A/B)
+QKV_DIRECT = os.environ.get("JLA_QKV_DIRECT", "1") != "0"
 
 
 def _fused_rms(e, mode, rms_eps) -> bool:
@@ -475,6 +478,14 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
             tk = None  # split QKV: partial slabs + the RoPE / KV-write reduce kernel
         if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):
             tm = 1  # the stream-K plan has a data-parallel part here: plain GEMM + RoPE kernel
+        fused = _fused_rms(e, MODE_QKV, rms_eps)
+        if ks == 1 and tm != SK_TILE and fused and QKV_DIRECT and e.gemm_qkv_direct_ok(m, tm):
+            # enough tiles, no K split: the GEMM's own RoPE / KV-write epilogue (no qkv round trip, no rope kernel)
+            q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
+            e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
+                       k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
+                       int(head_dim), q, 1, None, float(rms_eps), tm, None)
+            return q
         if ks == 1 and tm != SK_TILE:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
             qkv = linear(x, w, rms_eps=rms_eps)
             return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads,

@@ -523,6 +523,51 @@ def test_qkv_rope_tiled_splitk(m, s):
         ops.GEMV_VARIANT = 0
 
 
+@pytest.mark.parametrize("m,s,n_heads", [(512, 512, 8), (256, 1, 32), (300, 3, 8)])
+def test_qkv_rope_direct_epilogue(m, s, n_heads):
+    """qkv projection without a K split: the RoPE / KV-cache write runs in the GEMM's own (LDS-staged) epilogue
+    (gemm2 FA, 256 x 256 tiles, fused norm) -- against the fp32 oracle, the plain GEMM + RoPE-kernel path, and
+    bit for bit across repeated calls; row counts that are not a multiple of the tile included."""
+    e = ops.ext()
+    hkv, dh, k, t = 8, 128, 4096, 600
+    h = n_heads
+    b = m // s
+    n = (h + 2 * hkv) * dh
+    assert e.gemm_qkv_direct_ok(m, 1)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    x = torch.randn(m, k).to(BF16)
+    table = ref.rope_table(dh, 1024, 500000.0)
+    pos = torch.randint(0, 1000, (m,), dtype=torch.int32)
+    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+    vc = torch.zeros_like(kc)
+    q = ref.linear_qkv_rope(x.float(), w, 1e-5, table, pos, kc, vc, 11, s, h, hkv, dh)
+    pg = PackedLinear.from_dense(w, DEV)
+    args = (table.to(DEV), pos.to(DEV))
+    outs = []
+    for _ in range(2):
+        kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+        qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
+        e.gemm_qkv(x.to(DEV), pg.weight, n, k, args[0], args[1], kg, vg, torch.tensor([11], dtype=torch.int32,
+                   device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, 1, None)
+        outs.append((qg.cpu(), kg.cpu(), vg.cpu()))
+    qg, kg, vg = outs[0]
+    _close(qg, q, 2e-2, 2e-2)
+    _close(kg, kc, 2e-2, 2e-2)
+    _close(vg, vc, 2e-2, 2e-2)
+    assert all(torch.equal(a, c) for a, c in zip(outs[0], outs[1]))
+    # the un-fused path (bf16 qkv store + rope_kv_kernel) agrees to bf16 rounding of the pre-RoPE values
+    saved = ops.QKV_DIRECT
+    ops.QKV_DIRECT = False
+    try:
+        kg2, vg2 = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+        qg2 = ops.linear_qkv_rope(x.to(DEV), pg, 1e-5, args[0], args[1], kg2, vg2,
+                                  torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh)
+    finally:
+        ops.QKV_DIRECT = saved
+    _close(qg2.cpu(), qg, 2e-2, 2e-2)
+    _close(kg2.cpu(), kg, 2e-2, 2e-2)
+
+
 def test_rms_scale_bf16_input():
     x = (torch.randn(70, 4096) * 3).to(BF16)
     out = ops.rms_scale(x.to(DEV), 1e-5)

@@ -946,17 +946,28 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
       for (int r = 0; r < KPG; ++r) ad_load_nt(sl[KPG + r], vbase + (size_t)min(jb + 4 * r, k1 - 1) * AD_DH);
     };
+    // base-2 softmax (scale pre-multiplied by log2 e, v_exp_f32 directly). Chunk 0 always holds key k0, so after it
+    // every running max is finite: exp2(-inf - max) = 0 for masked keys and for the first rescale (m = -inf) without
+    // selects; only the last chunk (keys past k1) masks scores, behind a wave-uniform branch.
+    const float scale2 = scale * 1.4426950408889634f;
     auto compute = [&](const u32x4* kr, const u32x4* vr, int c) __attribute__((always_inline)) {
       const int jb = k0 + c * CK + g;
+      const bool full = k0 + (c + 1) * CK <= k1;
       float sc[REP][KPG];
 #pragma unroll
       for (int r = 0; r < KPG; ++r) {
-        const bool valid = jb + 4 * r < k1;
 #pragma unroll
         for (int h = 0; h < REP; ++h) {
-          float d = dot8_bf16(kr[r], qp[h], 0.f);
-          d = row16_sum(d) * scale;
-          sc[h][r] = valid ? d : -INFINITY;
+          const float d = dot8_bf16(kr[r], qp[h], 0.f);
+          sc[h][r] = row16_sum(d) * scale2;
+        }
+      }
+      if (!full) {
+#pragma unroll
+        for (int r = 0; r < KPG; ++r) {
+          const bool valid = jb + 4 * r < k1;
+#pragma unroll
+          for (int h = 0; h < REP; ++h) sc[h][r] = valid ? sc[h][r] : -INFINITY;
         }
       }
 #pragma unroll
@@ -967,7 +978,7 @@ __global__ void __launch_bounds__(64)
         cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
         cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
         const float mn = fmaxf(m_h[h], cm);
-        const float alpha = (m_h[h] == -INFINITY) ? 0.f : __expf(m_h[h] - mn);
+        const float alpha = __builtin_amdgcn_exp2f(m_h[h] - mn);
         m_h[h] = mn;
         l_h[h] *= alpha;
 #pragma unroll
@@ -981,7 +992,7 @@ __global__ void __launch_bounds__(64)
           vf[i] = f32x2_t{__uint_as_float(vr[r][i] << 16), __uint_as_float(vr[r][i] & 0xffff0000u)};
 #pragma unroll
         for (int h = 0; h < REP; ++h) {
-          const float pr = (sc[h][r] == -INFINITY) ? 0.f : __expf(sc[h][r] - m_h[h]);
+          const float pr = __builtin_amdgcn_exp2f(sc[h][r] - m_h[h]);
           l_h[h] += pr;
           const f32x2_t pp = {pr, pr};
 #pragma unroll

@@ -906,7 +906,8 @@ template <int REP, int KPG, int U, bool DIAG = false>
 __global__ void __launch_bounds__(64)
     attn_decode_v4_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
-                          bf16_t* __restrict__ out, int H, int Hkv, int T, int t_cap, float scale) {
+                          bf16_t* __restrict__ out, int H, int Hkv, int T, int t_cap, float scale,
+                          bf16_t* __restrict__ out_pack) {
   constexpr int CK = 4 * KPG;  // keys per chunk
   constexpr int L = 2 * KPG;   // loads per chunk and lane: KPG K rows + KPG V rows (16 B each)
   const int lane = threadIdx.x;
@@ -1048,7 +1049,10 @@ __global__ void __launch_bounds__(64)
       float r8[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) r8[e] = o[h][e >> 1][e & 1] * inv;
-      *reinterpret_cast<u32x4*>(out + ((size_t)b * H + h0 + h) * AD_DH + 8 * li) = pack8(r8);
+      const u32x4 pk = pack8(r8);
+      *reinterpret_cast<u32x4*>(out + ((size_t)b * H + h0 + h) * AD_DH + 8 * li) = pk;
+      // decode rows <= 64: also the packed copy (common.h pack_off) the o projection's packed-x GEMV reads
+      if (out_pack) *reinterpret_cast<u32x4*>(out_pack + pack_off(b, (h0 + h) * AD_DH + 8 * li, H * AD_DH)) = pk;
     }
   }
 }
@@ -1092,8 +1096,8 @@ void attn_set_impl(int impl, int waves_target) {
 // Llama-3-70B B = 256 (T 256 / 384) 158 / 206 -> 87 / 125; v3 stays ahead at B <= 64 (where it also writes the
 // packed copy the o projection's GEMV reads) and at rep 8 below 2048 pairs.
 static bool v4_midbatch(int B, int Hkv, int rep) {
-  return g_attn_impl == 2 && g_attn_v4 && g_attn_v2_min_pairs == 4096 && B > SKINNY_MAX_M && rep <= 8 &&
-         (rep <= 4 || B * Hkv >= 2048);
+  return g_attn_impl == 2 && g_attn_v4 && g_attn_v2_min_pairs == 4096 && rep <= 8 &&
+         ((rep <= 4 && B > 32) || (rep == 8 && B * Hkv >= 2048));
 }
 static bool use_v2(int B, int Hkv, int rep) {
   return g_attn_impl == 2 && (B * Hkv >= g_attn_v2_min_pairs || v4_midbatch(B, Hkv, rep));
@@ -1121,7 +1125,10 @@ static bool use_v5(int B, int Hkv, int rep) {
   return g_attn_impl == 2 && rep <= 16 && (rep & (rep - 1)) == 0 &&
          (pairs <= g_attn_v5_max_pairs || (rep >= 8 && pairs <= 4 * g_attn_v5_max_pairs));
 }
-int attn_decode_packs(int B, int Hkv, int rep) { return (use_v5(B, Hkv, rep) || use_v3(B, Hkv, rep)) ? 1 : 0; }
+// the kernels that also write the packed output copy: v5, v3, and v4 at decode rows <= 64 (mid-batch)
+int attn_decode_packs(int B, int Hkv, int rep) {
+  return (use_v5(B, Hkv, rep) || use_v3(B, Hkv, rep) || (B <= SKINNY_MAX_M && v4_midbatch(B, Hkv, rep))) ? 1 : 0;
+}
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
   if (use_v5(B, Hkv, rep)) return 16 * kpg5(rep);
@@ -1149,6 +1156,8 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
                 int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s, bf16_t* out_pack) {
   if (B <= 0) return 0;
   if (out_pack && !attn_decode_packs(B, Hkv, H / Hkv)) return -3;  // only the small-batch kernels write the packed copy
+  // (a key mask sends the mid-batch rows to v2, which does not write it)
+  if (out_pack && key_mask && !use_v5(B, Hkv, H / Hkv) && !use_v3(B, Hkv, H / Hkv)) return -3;
   if (Dh != AD_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   if (attn_decode_splits(B, Hkv, t_cap, rep) != nsplit) return -2;
@@ -1215,12 +1224,14 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   if (g_attn_v4 && nsplit == 1 && !key_mask && rep <= 8) {
 #define JLA_AD4(R, K, U)                                                                                         \
   if (rep == R) {                                                                                                \
-    attn_decode_v4_kernel<R, K, U><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale); \
+    attn_decode_v4_kernel<R, K, U><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale,   \
+                                                        out_pack);                                               \
     JLA_CHECK_LAUNCH();                                                                                          \
     return 0;                                                                                                    \
   }
     if (g_attn_diag && rep == 4) {  // tools only: stream-only build of the rep-4 kernel (wrong results)
-      attn_decode_v4_kernel<4, 4, 3, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale);
+      attn_decode_v4_kernel<4, 4, 3, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale,
+                                                                nullptr);
       JLA_CHECK_LAUNCH();
       return 0;
     }

@@ -49,7 +49,7 @@ class LLaMAAttention:
             a, weights = ref.attention(q4, kc, vc, s0, kv_start, key_mask, return_weights=True)
             a = a.reshape(b * seq_len, -1)
         else:
-            att_p = pk.att if pk is not None and ops.attention_packs(q4, kc) else None
+            att_p = pk.att if pk is not None and ops.attention_packs(q4, kc, key_mask) else None
             a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask, out_packed=att_p)
         m._row_parallel(a, lw.o, h, hb, x_packed=att_p, mirror_packed=pk.hb if pk else None)
         if pk is not None and pk.hb is not None:

@@ -505,10 +505,16 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     return q
 
 
-def attention_packs(q: torch.Tensor, k_cache: torch.Tensor) -> bool:
-    """Whether ``attention(..., out_packed=...)`` can write the packed copy for this decode shape."""
+def attention_packs(q: torch.Tensor, k_cache: torch.Tensor, key_mask: Optional[torch.Tensor] = None) -> bool:
+    """Whether ``attention(..., out_packed=...)`` can write the packed copy for this decode shape (with a key mask
+    only the small-batch kernels, v3 / v5, do: mid-batch rows then go to v2)."""
     bsz, s, h, _ = q.shape
-    return s == 1 and bool(ext().attn_decode_packs(bsz, k_cache.shape[1], h // k_cache.shape[1]))
+    if s != 1:
+        return False
+    e = ext()
+    if key_mask is not None and bsz > 32:
+        return False
+    return bool(e.attn_decode_packs(bsz, k_cache.shape[1], h // k_cache.shape[1]))
 
 
 def attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor,

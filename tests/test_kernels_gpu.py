@@ -954,8 +954,9 @@ def test_packed_x_variants_and_packed_epilogues(m, variant):
         ops.GEMV_VARIANT = 0
 
 
-@pytest.mark.parametrize("b", [1, 12, 32])
+@pytest.mark.parametrize("b", [1, 12, 32, 48, 64])
 def test_attention_decode_packed_output(b):
+    """v5 / v3 (small batch) and the mid-batch v4 stream (33-64 rows) write the packed copy of their output."""
     h, hkv, dh, t = 32, 8, 128, 96
     q = torch.randn(b, 1, h, dh).to(BF16)
     kc = torch.randn(b, hkv, t, dh).to(BF16)

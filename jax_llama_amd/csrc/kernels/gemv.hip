@@ -481,6 +481,15 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
     if constexpr (sizeof(XT) == 2) {
       if (variant == 21)
         return launch_skinny<XT, MT, 2, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      // 4 tiles x 4 waves reading packed x (22): half the activation bytes per weight byte of the 2-tile variants,
+      // for wide projections at M = 17..64 (w1|w3: 1792 column tiles at Llama-3-8B)
+      if (variant == 22 || variant == 23) {  // (x is the packed copy: never fall through to a row-major variant)
+        if (N & 63) return -1;
+        if (variant == 23)  // the same with 8 waves
+          return launch_skinny<XT, MT, 4, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa,
+                                                            s);
+        return launch_skinny<XT, MT, 4, MODE, 4, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+      }
     }
     // packed-x variants (x is the packed copy, common.h pack_off, padded to MT * 16 rows): 12 = 1 tile x 8 waves,
     // 13 = 2 tiles x 4 waves, 14 / 15 = the same with a doubled ring

@@ -48,7 +48,7 @@ constexpr int GEMV_SPLIT_MAX_GROUPS = 1024;
 size_t gemv_split_workspace_floats(int M, int N);
 int gemv_split_tickets(int N);
 inline bool gemv_split_variant(int v) { return v >= 16 && v <= 19; }
-inline bool gemv_xp_variant(int v) { return (v >= 12 && v <= 15) || v == 18 || v == 19 || v == 21; }
+inline bool gemv_xp_variant(int v) { return (v >= 12 && v <= 15) || v == 18 || v == 19 || (v >= 21 && v <= 23); }
 // split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
 // skinny_workspace_floats / skinny_tickets (tickets zero-initialised once, self-resetting)
 size_t skinny_workspace_floats(int M, int N, int K, int mode);

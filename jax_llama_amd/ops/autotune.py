@@ -174,7 +174,7 @@ SPLIT_MAX_GROUPS = 1024  # csrc GEMV_SPLIT_MAX_GROUPS
 TILED_VARIANT = 7
 
 
-XP_CANDIDATES = (12, 13, 14, 15, 18, 19, 21)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 split-K)
+XP_CANDIDATES = (12, 13, 14, 15, 18, 19, 21, 22, 23)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 split-K)
 
 
 def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False,
@@ -193,8 +193,9 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     if pack_out:  # the tiled GEMM qualifies when its split-K reduce epilogue writes the copy (``tiled_packs``)
         cands = [c for c in cands if c != 4 and (c != TILED_VARIANT or tiled_packs)]
     if xp_in and x.dtype == torch.bfloat16:
-        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19, 21)) and
-                  (c not in (18, 19) or w.n // 16 <= SPLIT_MAX_GROUPS) and (c != 21 or w.n // 32 < 512)]
+        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19, 21, 22, 23)) and
+                  (c not in (18, 19) or w.n // 16 <= SPLIT_MAX_GROUPS) and (c != 21 or w.n // 32 < 512) and
+                  (c not in (22, 23) or (w.n % 64 == 0 and w.n // 64 >= 64))]
     if no_split:
         cands = [c for c in cands if not 16 <= c <= 19]
     if not ENABLED or torch.cuda.is_current_stream_capturing():

@@ -299,11 +299,7 @@ def _tp_points(args, ctx, res):
                 res["tp_points"] = {"status": "timeout", "timeout_s": args.tp_timeout}
                 _emit(res, args.json_out)
             sys.stdout.flush()
-            print(f"tp_points: no result within {args.tp_timeout:.0f} s; the headline line above is complete",
-                  file=sys.stderr, flush=True)
-            # every rank's watchdog fires within seconds of the others; the headline measurement finished before
-            # this phase began, so the run exits cleanly with the timeout recorded in its line
-            os._exit(0)
+            os._exit(3)  # the headline line is out, but a stuck phase is not a clean run
 
     threading.Thread(target=watchdog, daemon=True).start()
     world = ctx.world

@@ -162,7 +162,7 @@ void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* ou
   const bool f32 = x.scalar_type() == torch::kFloat32;
   if (variant == 0) variant = (m == 1) ? 1 : 4;
   const bool xp_variant = jla::gemv_xp_variant((int)variant);
-  check(xp_variant == (x_packed != nullptr), "packed-x variants (12-15, 18, 19) need x_packed, the others must not");
+  check(xp_variant == (x_packed != nullptr), "packed-x variants (12-15, 18, 19, 21-23, 26) need x_packed, the others must not");
   check(!xp_variant || !f32, "packed-x variants read bf16 activations");
   check(!(xp_variant && mode == 2 && (variant == 12 || variant == 14)), "SwiGLU packed-x variants: 13 / 15");
   if (variant == 4) {

@@ -464,6 +464,14 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
     // shards, N = 1280 at Llama-3-70B MP 8: 80 one-tile workgroups leave most CUs idle); 18 / 19 read packed x.
     // 1 tile per workgroup (SwiGLU: the gate/up pair), 4 waves at M <= 16, 8 above.
     if constexpr (sizeof(XT) == 2 && MODE != MODE_ARGMAX) {
+      // 26: 4 tiles x 8 waves per workgroup on packed x with K over 4 workgroups -- the 4-tile x re-read ratio of 22/23
+      // for the narrow, deep projections at M = 17..64 (w2 at N = 4096: 64 column groups alone leave most CUs idle).
+      // The 4-wave forms with 2 / 4 splits never won a shape (profiles/r3_gemv_split4tile_candidates.jsonl).
+      if (variant == 26) {
+        if (N & 63) return -1;
+        return launch_skinny<XT, MT, 4, MODE, 8, 0, true, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32,
+                                                                qa, s, 4);
+      }
       if (gemv_split_variant(variant)) {
         constexpr int SNT = MODE == MODE_SWIGLU ? 2 : 1, SNW = MT == 1 ? 4 : 8;
         const int ks = (variant == 16 || variant == 18) ? 2 : 4;

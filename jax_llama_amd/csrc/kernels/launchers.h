@@ -47,8 +47,8 @@ int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, 
 constexpr int GEMV_SPLIT_MAX_GROUPS = 1024;
 size_t gemv_split_workspace_floats(int M, int N);
 int gemv_split_tickets(int N);
-inline bool gemv_split_variant(int v) { return v >= 16 && v <= 19; }
-inline bool gemv_xp_variant(int v) { return (v >= 12 && v <= 15) || v == 18 || v == 19 || (v >= 21 && v <= 23); }
+inline bool gemv_split_variant(int v) { return (v >= 16 && v <= 19) || v == 26; }
+inline bool gemv_xp_variant(int v) { return (v >= 12 && v <= 15) || v == 18 || v == 19 || (v >= 21 && v <= 23) || v == 26; }
 // split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
 // skinny_workspace_floats / skinny_tickets (tickets zero-initialised once, self-resetting)
 size_t skinny_workspace_floats(int M, int N, int K, int mode);

@@ -236,8 +236,9 @@ PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
 PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "64"))
 PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
 SKINNY_M = 64  # decode GEMV rows (csrc: SKINNY_MAX_M): packed copies exist only on that path
-XP_VARIANTS = (12, 13, 14, 15, 18, 19, 21, 22, 23)  # packed-x GEMV variants (18 / 19 split-K; 21-23: 2x8 / 4x4 / 4x8)
-SPLIT_VARIANTS = (16, 17, 18, 19)  # split-K GEMV variants (the shared skinny workspace holds their slabs)
+XP_VARIANTS = (12, 13, 14, 15, 18, 19, 21, 22, 23, 26)  # packed-x GEMV variants (18 / 19 / 26 split-K; 21-23: 2x8 / 4x4 / 4x8;
+#   26: 4 tiles x 8 waves, K over 4)
+SPLIT_VARIANTS = (16, 17, 18, 19, 26)  # split-K GEMV variants (the shared skinny workspace holds their slabs)
 
 
 def packed_rows(m: int) -> int:

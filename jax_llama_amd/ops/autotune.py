@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 2  # bumped when a candidate set changes (16-19: split-K GEMV), so older persisted picks are re-measured
+TUNE_VERSION = 3  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -169,12 +169,14 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
 
 
 SPLIT_MAX_GROUPS = 1024  # csrc GEMV_SPLIT_MAX_GROUPS
+SPLIT_GEMV = (16, 17, 18, 19, 26)  # split-K GEMV variants (gemv.hip gemv_split_variant)
 
 
 TILED_VARIANT = 7
 
 
-XP_CANDIDATES = (12, 13, 14, 15, 18, 19, 21, 22, 23)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 split-K)
+XP_CANDIDATES = (12, 13, 14, 15, 18, 19, 21, 22, 23, 26)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 / 26
+#   split-K)
 
 
 def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False,
@@ -193,11 +195,13 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     if pack_out:  # the tiled GEMM qualifies when its split-K reduce epilogue writes the copy (``tiled_packs``)
         cands = [c for c in cands if c != 4 and (c != TILED_VARIANT or tiled_packs)]
     if xp_in and x.dtype == torch.bfloat16:
-        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19, 21, 22, 23)) and
+        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19, 21, 22, 23, 26)) and
                   (c not in (18, 19) or w.n // 16 <= SPLIT_MAX_GROUPS) and (c != 21 or w.n // 32 < 512) and
-                  (c not in (22, 23) or (w.n % 64 == 0 and w.n // 64 >= 64))]
+                  (c not in (22, 23) or (w.n % 64 == 0 and w.n // 64 >= 64)) and
+                  # 4-tile split-K: narrow outputs only (few 64-column groups), M > 16
+                  (c != 26 or (m > 16 and w.n % 64 == 0 and w.n // 64 < 256))]
     if no_split:
-        cands = [c for c in cands if not 16 <= c <= 19]
+        cands = [c for c in cands if c not in SPLIT_GEMV]
     if not ENABLED or torch.cuda.is_current_stream_capturing():
         h = heuristic(m, w.n, w.k, mode)
         return h if h in cands else 1

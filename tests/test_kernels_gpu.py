@@ -920,7 +920,7 @@ def _qkv_rope_stream_k(e, m, s):
     _close(vg, vc, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("variant", [12, 13, 14, 15, 18, 19, 21, 22, 23, 7])
+@pytest.mark.parametrize("variant", [12, 13, 14, 15, 18, 19, 21, 22, 23, 26, 7])
 @pytest.mark.parametrize("m", [1, 12, 16, 20, 32, 40, 64])
 def test_packed_x_variants_and_packed_epilogues(m, variant):
     """Packed-x GEMV variants read the packed copy (ref.pack_act) and match the fp32 reference; the residual /

@@ -30,9 +30,10 @@ def proxy_model():
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("variant", [1, 16])
+@pytest.mark.parametrize("variant", [1, 16, 26])
 def test_proxy_fused_row_parallel_matches_standalone(proxy_model, variant):
-    """variant 16: the split-K GEMV (2 workgroups per column group; only the last arriver exchanges)."""
+    """variant 16: the split-K GEMV (2 workgroups per column group; only the last arriver exchanges); 26: 4 tiles x 8 waves
+    per workgroup on packed x, K over 4 workgroups."""
     from jax_llama_amd import ops
     from jax_llama_amd.runtime.engine import DecodeEngine, GenerationConfig
     cfg, comm, model = proxy_model

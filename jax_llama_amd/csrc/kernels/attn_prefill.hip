@@ -13,6 +13,8 @@
 //   S = Q K^T: 2 key sub-tiles x 4 d-steps of v_mfma_f32_16x16x32_bf16 (Q fragments live in VGPRs);
 //   online softmax on the accumulator layout (row stats reduced over 16 lanes);
 //   P goes through a small per-wave LDS tile to become the A operand; O += P V: 8 MFMAs.
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -215,17 +217,26 @@ JLA_DEV u32x2 ld_tr(const char* lds, int off) {
 // fragment (2 x ds_read_b64_tr_b16) read from LDS feeds QB MFMAs instead of one. With QB = 1 four waves x two
 // workgroups re-read each 32-KiB K/V tile per 32 MFMAs per wave -- about the LDS read rate; QB = 2 halves the
 // LDS bytes per MFMA at the price of one workgroup per CU (O^T, S^T, Q^T and P for 64 queries: ~340 registers).
-template <int NW, int QB>
+//
+// PIPE (QB = 1): the scores of tile i+1 are issued before the softmax of tile i, so one wave's MFMA pipe works
+// through S(i+1) while its VALU runs exp / sum / pack of tile i (independent instructions in one basic block).
+// K and V each get a 2-slot LDS ring (64 KiB per workgroup): K(i+1) and V(i) are resident during tile i while
+// the registers stage K(i+2) and V(i+1) into the slots freed by tile i-1, so each tile ends with ONE barrier.
+// LAZY: the running max (and with it the O / l rescale) moves only when a lane's tile max exceeds it by more
+// than 8 (log2 units): exp2 of the rest stays <= 256, exact in fp32 and bf16-representable for P; the 64 O
+// multiplies per tile run only in a wave-uniform branch when some lane needs them (mostly the first tiles).
+template <int NW, int QB, int PIPE = 0, int LAZY = 0>
 __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
     attn_prefill_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                            const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                            const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int S, int H,
                            int Hkv, int T, float scale_log2, int npb, int hgroups, int n_qb, int split) {
+  static_assert(!PIPE || QB == 1, "the pipelined loop holds one query block per wave");
   constexpr int NT = NW * 64;
   constexpr int TILE_BYTES = FA_KT * AP_DH * 2;            // 16 KiB
   constexpr int CH_PER_T = FA_KT * 16 / NT;                 // 16-byte chunks per thread per tile (K or V)
   constexpr int QW = 32 * QB;                               // queries per wave
-  __shared__ __attribute__((aligned(16))) char lds[2 * TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[(PIPE ? 4 : 2) * TILE_BYTES];
   char* Ks = lds;
   char* Vs = lds + TILE_BYTES;
 
@@ -312,16 +323,129 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
       *reinterpret_cast<u32x4*>(Vs + fa_off(row, ch)) = sv[i];
     }
   };
+  // per-lane LDS read offsets: K row reads (key block kb, dk step ks -> chunk 2 ks + hi)
+  // V transposed reads: 16-lane group G = lane >> 4 covers d columns 16 (G & 1) .. +15 of a 32-wide d tile,
+  // lane 4q + p of the group addresses row q of the 4-key block, columns 4p .. 4p + 3.
+  const int gq = (lane & 15) >> 2, gp = lane & 3, G = lane >> 4;
+  if constexpr (PIPE) {
+    // LDS-DMA staging (no VGPRs held across the tile): wave w fills 1-KiB blocks w, w + NW, ... of a tile
+    // image; lane L of block bi writes row 4 bi + L / 16, slot L % 16, so it fetches the source chunk that
+    // fa_off's swizzle puts in that slot
+    auto Kr = [&](int i) { return lds + i * TILE_BYTES; };
+    auto Vr = [&](int i) { return lds + (2 + i) * TILE_BYTES; };
+    auto dma = [&](const bf16_t* src, int t0, char* dst) {
+#pragma unroll
+      for (int i = 0; i < 16 / NW; ++i) {
+        const int bi = w + NW * i, row = 4 * bi + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        glds16(src + (size_t)min(t0 + row, T - 1) * AP_DH + 8 * ch, dst + 1024 * bi);
+      }
+    };
+    auto scores = [&](const char* Kt, f32x16 (&s)[2]) {
+#pragma unroll
+      for (int kbk = 0; kbk < 2; ++kbk) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kbk][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+          s[kbk] = mfma32(*reinterpret_cast<const u32x4*>(Kt + fa_off(32 * kbk + col, 2 * ks + hi)), qf[0][ks], s[kbk]);
+      }
+    };
+    const int n_t = t_begin <= last_key ? (last_key - t_begin) / FA_KT + 1 : 0;
+    const int qfirst = slot0 + p0, qslot = qfirst + col;
+    f32x16 st[2];
+    if (n_t > 0) {
+      dma(kb, t_begin, Kr(0));
+      dma(vb, t_begin, Vr(0));
+    }
+    if (n_t > 1) dma(kb, t_begin + FA_KT, Kr(1));
+    wait_vmcnt<0>();
+    __syncthreads();
+    if (n_t > 0 && t_begin <= wave_last_slot) scores(Kr(0), st);
+    for (int it = 0; it < n_t; ++it) {
+      const int t0 = t_begin + it * FA_KT, cur = it & 1;
+      const bool has1 = it + 1 < n_t, has2 = it + 2 < n_t;
+      // K(i+2) into K(i)'s slot and V(i+1) into V(i-1)'s: both last read before the previous barrier
+      if (has2) dma(kb, t0 + 2 * FA_KT, Kr(cur));
+      if (has1) dma(vb, t0 + FA_KT, Vr(cur ^ 1));
+      if (t0 <= wave_last_slot) {  // wave-uniform; every later tile is inactive too
+        // masking (wave-uniform branch: only tiles crossing kv_start, the diagonal, T, or a key mask)
+        const bool full = !mrow && t0 >= lo && t0 + FA_KT - 1 <= qfirst && t0 + FA_KT - 1 < T;
+        if (!full) {
+#pragma unroll
+          for (int kbk = 0; kbk < 2; ++kbk)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int j = t0 + 32 * kbk + (i & 3) + 8 * (i >> 2) + 4 * hi;
+              bool ok = j >= lo && j <= qslot && j < T;
+              if (mrow) ok = ok && j < mask_len && mrow[j] != 0;
+              st[kbk][i] = ok ? st[kbk][i] : -INFINITY;
+            }
+        }
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int kbk = 0; kbk < 2; ++kbk)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, st[kbk][i]);
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * scale_log2;  // scale > 0: max of the scaled scores
+        if (__ballot(tmax > m_run[0] + 8.f)) {
+          const float m_new = fmaxf(m_run[0], tmax);
+          const float alpha = __builtin_amdgcn_exp2f(m_run[0] - (m_new == -INFINITY ? 0.f : m_new));
+          l_run[0] *= alpha;
+          m_run[0] = m_new;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[0][dt][i] *= alpha;
+        }
+        const float m_use = m_run[0] == -INFINITY ? 0.f : m_run[0];
+        // one straight-line block: S(i+1) on the matrix pipe beside exp / sum / pack of tile i (VALU), then
+        // O += V(i) P(i); NEXT is a compile-time copy so no branch splits the MFMAs from the VALU work
+        auto body = [&](auto NEXT) {
+          f32x16 sn[2];
+          if constexpr (decltype(NEXT)::value) scores(Kr(cur ^ 1), sn);
+          // key step s: 8 exps -> one P fragment -> its 4 PV MFMAs (one fragment live, exp beside the MFMAs)
+          float rs = 0.f;
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            float e[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              e[j] = __builtin_amdgcn_exp2f(fmaf(st[s >> 1][8 * (s & 1) + j], scale_log2, -m_use));
+              rs += e[j];
+            }
+            const u32x4 pf = pack8(e);
+            const int r0 = 16 * s + 4 * (G >> 1) + gq;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+              const int c0 = 4 * dt + 2 * (G & 1) + (gp >> 1);
+              const u32x2 lo4 = ld_tr(Vr(cur), fa_off(r0, c0) + 8 * (gp & 1));
+              const u32x2 hi4 = ld_tr(Vr(cur), fa_off(r0 + 8, c0) + 8 * (gp & 1));
+              const u32x4 vf = {lo4[0], lo4[1], hi4[0], hi4[1]};
+              o[0][dt] = mfma32(vf, pf, o[0][dt]);
+            }
+          }
+          rs += __shfl_xor(rs, 32, 64);
+          l_run[0] += rs;
+          if constexpr (decltype(NEXT)::value) {
+            st[0] = sn[0];
+            st[1] = sn[1];
+          }
+        };
+        if (has1 && t0 + FA_KT <= wave_last_slot)
+          body(std::true_type{});
+        else
+          body(std::false_type{});
+      }
+      wait_vmcnt<0>();
+      __syncthreads();
+    }
+  } else {
   if (t_begin <= last_key) {
     load_tile(t_begin);
     store_tile();
   }
   __syncthreads();
-
-  // per-lane LDS read offsets: K row reads (key block kb, dk step ks -> chunk 2 ks + hi)
-  // V transposed reads: 16-lane group G = lane >> 4 covers d columns 16 (G & 1) .. +15 of a 32-wide d tile,
-  // lane 4q + p of the group addresses row q of the 4-key block, columns 4p .. 4p + 3.
-  const int gq = (lane & 15) >> 2, gp = lane & 3, G = lane >> 4;
   for (int t0 = t_begin; t0 <= last_key; t0 += FA_KT) {
     const bool has_next = t0 + FA_KT <= last_key;
     if (has_next) load_tile(t0 + FA_KT);
@@ -364,9 +488,21 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
             tmax = fmaxf(tmax, v);
           }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float m_new = fmaxf(m_run[qq], tmax);
+        if constexpr (LAZY) {
+          if (__ballot(tmax > m_run[qq] + 8.f)) {
+            const float m_new = fmaxf(m_run[qq], tmax);
+            const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - (m_new == -INFINITY ? 0.f : m_new));
+            l_run[qq] *= alpha;
+            m_run[qq] = m_new;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
+          }
+        }
+        const float m_new = LAZY ? m_run[qq] : fmaxf(m_run[qq], tmax);
         const float m_use = m_new == -INFINITY ? 0.f : m_new;
-        const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - m_use);  // m_run = -inf -> 0
+        const float alpha = LAZY ? 1.f : __builtin_amdgcn_exp2f(m_run[qq] - m_use);  // m_run = -inf -> 0
         float rs = 0.f;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -381,10 +517,12 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
         rs += __shfl_xor(rs, 32, 64);
         l_run[qq] = l_run[qq] * alpha + rs;
         m_run[qq] = m_new;
+        if constexpr (!LAZY) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+          for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
+            for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
+        }
       }
       // ---- O^T += V^T P^T; A element j of lane half hi = V[key 16 s + 8 (j >> 2) + 4 hi + (j & 3)][d]
 #pragma unroll
@@ -407,6 +545,7 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
       __syncthreads();
     }
   }
+  }  // !PIPE
 
   // ---- epilogue: lane (query pos, half hi) holds d = 32 dt + 8 g + 4 hi + (0..3) in o[dt][4 g .. 4 g + 3]
 #pragma unroll
@@ -434,7 +573,7 @@ void attn_prefill_set_impl(int impl) { g_attn_prefill_impl = impl; }
 
 // v2 launch with NW waves per workgroup: NW / rep position blocks (rep < NW) or NW of the rep q heads (rep >= NW) share
 // each K/V tile the workgroup stages; `paired_only`: always the (heavy, light) pair per workgroup (impl 4 / 6)
-template <int NW>
+template <int NW, int PIPE = 0, int LAZY = 0>
 static void launch_prefill_v2(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot,
                               const int32_t* kv_start, const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S,
                               int H, int Hkv, int T, int rep, bool paired_only, hipStream_t s) {
@@ -448,11 +587,11 @@ static void launch_prefill_v2(const bf16_t* q, const bf16_t* kc, const bf16_t* v
   // holds two resident workgroups instead of one
   const bool split = !paired_only && pairs < 2 * 256;
   if (split) {
-    attn_prefill_v2_kernel<NW, 1><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
+    attn_prefill_v2_kernel<NW, 1, PIPE, LAZY><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
         q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H, Hkv, T, sl2, npb, hgroups, n_qb, 1);
   } else {
     dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
-    attn_prefill_v2_kernel<NW, 1><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
+    attn_prefill_v2_kernel<NW, 1, PIPE, LAZY><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
                                                              Hkv, T, sl2, npb, hgroups, n_qb, 0);
   }
 }
@@ -471,6 +610,17 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   const bool auto8 = impl == 2 && (rep == 1 || rep == 2 || rep == 4 || rep == 8) && (S >= 4096 || (rep >= 8 && S >= 1024));
   const bool eight = impl == 5 || impl == 6 || auto8;
   const int nw = eight ? 8 : 4;
+  // impl 7 / 9: the software-pipelined loop with lazy rescale (4 / 8 waves), 8: lazy rescale only (A/B)
+  if ((impl == 7 || impl == 8 || impl == 9) && (rep % (impl == 9 ? 8 : 4) == 0 || (impl == 9 ? 8 : 4) % rep == 0)) {
+    if (impl == 7)
+      launch_prefill_v2<4, 1, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
+    else if (impl == 8)
+      launch_prefill_v2<4, 0, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
+    else
+      launch_prefill_v2<8, 1, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, true, s);
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
   if ((impl == 2 || impl == 4 || eight) && (rep % nw == 0 || nw % rep == 0)) {
     if (eight)
       launch_prefill_v2<8>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, impl != 5, s);

@@ -902,7 +902,7 @@ JLA_DEV void ad_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-template <int REP, int KPG, int U, bool DIAG = false, bool LAZY = false>
+template <int REP, int KPG, int U, bool DIAG = false>
 __global__ void __launch_bounds__(64)
     attn_decode_v4_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
@@ -971,35 +971,19 @@ __global__ void __launch_bounds__(64)
           for (int h = 0; h < REP; ++h) sc[h][r] = valid ? sc[h][r] : -INFINITY;
         }
       }
-      float cm[REP];
 #pragma unroll
       for (int h = 0; h < REP; ++h) {
-        cm[h] = sc[h][0];
+        float cm = sc[h][0];
 #pragma unroll
-        for (int r = 1; r < KPG; ++r) cm[h] = fmaxf(cm[h], sc[h][r]);
-        cm[h] = fmaxf(cm[h], __shfl_xor(cm[h], 16, 64));
-        cm[h] = fmaxf(cm[h], __shfl_xor(cm[h], 32, 64));
-      }
-      auto rescale = [&]() __attribute__((always_inline)) {
+        for (int r = 1; r < KPG; ++r) cm = fmaxf(cm, sc[h][r]);
+        cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+        const float mn = fmaxf(m_h[h], cm);
+        const float alpha = __builtin_amdgcn_exp2f(m_h[h] - mn);
+        m_h[h] = mn;
+        l_h[h] *= alpha;
 #pragma unroll
-        for (int h = 0; h < REP; ++h) {
-          const float mn = fmaxf(m_h[h], cm[h]);
-          const float alpha = __builtin_amdgcn_exp2f(m_h[h] - mn);
-          m_h[h] = mn;
-          l_h[h] *= alpha;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) o[h][i] *= alpha;
-        }
-      };
-      if constexpr (LAZY) {
-        // the running max moves only when some head's chunk max exceeds it by more than 8 (log2 units): the
-        // exp2 values stay <= 256 (exact in fp32), and most chunks skip the rescale (wave-uniform branch)
-        bool need = false;
-#pragma unroll
-        for (int h = 0; h < REP; ++h) need |= cm[h] > m_h[h] + 8.f;
-        if (__ballot(need)) rescale();
-      } else {
-        rescale();
+        for (int i = 0; i < 4; ++i) o[h][i] *= alpha;
       }
 #pragma unroll
       for (int r = 0; r < KPG; ++r) {
@@ -1240,16 +1224,12 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   if (g_attn_v4 && nsplit == 1 && !key_mask && rep <= 8) {
 #define JLA_AD4(R, K, U)                                                                                         \
   if (rep == R) {                                                                                                \
-    if (g_attn_diag == 2)                                                                                        \
-      attn_decode_v4_kernel<R, K, U, false, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, \
-                                                                       t_cap, scale, out_pack);                 \
-    else                                                                                                         \
-      attn_decode_v4_kernel<R, K, U><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale, \
-                                                          out_pack);                                             \
+    attn_decode_v4_kernel<R, K, U><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale,   \
+                                                        out_pack);                                               \
     JLA_CHECK_LAUNCH();                                                                                          \
     return 0;                                                                                                    \
   }
-    if (g_attn_diag == 1 && rep == 4) {  // tools only: stream-only build of the rep-4 kernel (wrong results)
+    if (g_attn_diag && rep == 4) {  // tools only: stream-only build of the rep-4 kernel (wrong results)
       attn_decode_v4_kernel<4, 4, 3, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, out, H, Hkv, T, t_cap, scale,
                                                                 nullptr);
       JLA_CHECK_LAUNCH();
@@ -1267,11 +1247,11 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   if (key_mask)                                                                                                     \
     attn_decode_v2_kernel<R, KPG, NS, true><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
                                                                  ws, tickets, B, H, Hkv, T, t_cap, nsplit, split_len, \
-                                                                 scale, g_attn_diag == 1);                            \
+                                                                 scale, g_attn_diag);                              \
   else                                                                                                              \
     attn_decode_v2_kernel<R, KPG, NS, false><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
                                                                   ws, tickets, B, H, Hkv, T, t_cap, nsplit,          \
-                                                                  split_len, scale, g_attn_diag == 1);
+                                                                  split_len, scale, g_attn_diag);
   const int geo = geo_v2(B * Hkv);
   switch (rep) {
     case 1:

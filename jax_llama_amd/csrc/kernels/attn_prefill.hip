@@ -602,15 +602,31 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   if (B <= 0 || S <= 0) return 0;
   if (Dh != AP_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
-  const int impl = g_attn_prefill_impl;
-  // impl 2 (default) / 4 (always paired): 4 waves per workgroup; 5 / 6: the same with 8 waves (A/B). The default
-  // takes the 8-wave paired launch for long prompts and rep >= 8, where twice the queries per staged K/V tile pay
-  // (interleaved A/B, profiles/r3_attn_prefill_nw8_ab.jsonl: 8B S = 8192 826 -> 877 TFLOP/s, 70B S = 2048 689 -> 716;
-  // 4 waves stay ahead at S = 2048 with rep 4 and at S = 128)
-  const bool auto8 = impl == 2 && (rep == 1 || rep == 2 || rep == 4 || rep == 8) && (S >= 4096 || (rep >= 8 && S >= 1024));
+  const bool pow2rep = rep == 1 || rep == 2 || rep == 4 || rep == 8;
+  int impl = g_attn_prefill_impl;
+  // default (impl 2): lazy rescale everywhere; the software-pipelined loop from S = 512 (a query block needs a few
+  // tiles to pipeline), with 8 waves per workgroup when that paired grid still fills the CUs (>= 256 workgroups:
+  // twice the queries per staged K/V tile), else 4 waves. Interleaved A/B (profiles/r3_attn_prefill_pipe_ab.jsonl,
+  // TFLOP/s, previous default -> now): 8B B = 1 S = 2048 454 -> 509, B = 16 S = 2048 672 -> 746, S = 8192 854 -> 903,
+  // B = 2048 S = 128 186 -> 198, 70B S = 2048 698 -> 733, 7B (MHA) B = 16 615 -> 651.
+  // impl 10: the previous default dispatch (A/B); 4 / 5 / 6: the unpipelined 4 / 8-wave launches
+  if (impl == 2 && pow2rep) {
+    if (S <= 256) {
+      impl = 8;
+    } else {
+      const int npb8 = rep >= 8 ? 1 : 8 / rep;
+      const int n_qb8 = (S + 32 * npb8 - 1) / (32 * npb8);
+      const int wg8 = (n_qb8 + 1) / 2 * Hkv * (rep / (8 / npb8)) * B;
+      impl = wg8 >= 256 ? 9 : 7;
+    }
+  }
+  if (impl == 10) impl = 2;
+  // impl 2 here (previous default) / 4 (always paired): 4 waves per workgroup; 5 / 6: the same with 8 waves. The
+  // previous default takes the 8-wave paired launch for long prompts and rep >= 8
+  const bool auto8 = impl == 2 && pow2rep && (S >= 4096 || (rep >= 8 && S >= 1024));
   const bool eight = impl == 5 || impl == 6 || auto8;
   const int nw = eight ? 8 : 4;
-  // impl 7 / 9: the software-pipelined loop with lazy rescale (4 / 8 waves), 8: lazy rescale only (A/B)
+  // impl 7 / 9: the software-pipelined loop with lazy rescale (4 / 8 waves), 8: lazy rescale only
   if ((impl == 7 || impl == 8 || impl == 9) && (rep % (impl == 9 ? 8 : 4) == 0 || (impl == 9 ? 8 : 4) % rep == 0)) {
     if (impl == 7)
       launch_prefill_v2<4, 1, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);

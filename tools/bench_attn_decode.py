@@ -7,8 +7,7 @@ evicts L2 and the Infinity Cache, as the weight stream of a real step does). Tim
 
 impl (ext.attn_set_impl / attn_set_v3_max_pairs): 2 = default dispatch; 1 = the split v1 kernel (v3 off);
 5 = split small-batch kernel (v5) where it applies; 6 = v5 with the first merge (4 splits per load round);
-7 = v4 (register ring, one split) forced; 12 = v4 forced with the lazy rescale (attn_set_diag(2));
-9 = v2 (LDS-DMA ring) forced. Prints one JSON line per (shape, impl).
+7 = v4 (register ring, one split) forced; 9 = v2 (LDS-DMA ring) forced. Prints one JSON line per (shape, impl).
 """
 from __future__ import annotations
 
@@ -28,14 +27,13 @@ from jax_llama_amd.config import get_preset  # noqa: E402
 def set_impl(e, impl):
     e.attn_set_impl(2, 4096)
     e.attn_set_v3_max_pairs(0 if impl == 1 else 4096)
-    e.attn_set_diag(2 if impl == 12 else 0)
-    if impl in (7, 9, 12):
-        # the streaming kernels at any pair count, one split: 7 / 12 = v4 register ring, 9 = v2 (LDS-DMA ring)
+    if impl in (7, 9):
+        # the streaming kernels at any pair count, one split: 7 = v4 register ring, 9 = v2 (LDS-DMA ring)
         e.attn_set_impl(3 if impl == 9 else 2, 1)  # waves target 1 -> one split
         e.attn_set_impl(3 if impl == 9 else 2, -1)  # v2/v4 down to 1 pair
         e.attn_set_v3_max_pairs(0)
     if hasattr(e, "attn_set_v5_max_pairs"):
-        e.attn_set_v5_max_pairs(4096 if impl in (5, 6) else (0 if impl in (1, 3, 7, 9, 12) else -1))
+        e.attn_set_v5_max_pairs(4096 if impl in (5, 6) else (0 if impl in (1, 3, 7, 9) else -1))
     if hasattr(e, "attn_set_v5_fold"):
         e.attn_set_v5_fold(4 if impl == 6 else (12 if impl == 5 else 0))
 

@@ -432,9 +432,9 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
             st[1] = sn[1];
           }
         };
-        // PIPE 2: always the NEXT copy (no branch for LLVM to hoist the shared softmax above; the last tile's
-        // extra scores MFMAs read a stale but allocated K slot and are dropped)
-        if (PIPE == 2 || (has1 && t0 + FA_KT <= wave_last_slot))
+        // (the branch lets LLVM hoist the shared exp block above the scores MFMAs; a branch-free variant that always
+        // runs the NEXT copy interleaves them but measured neutral: profiles/r3_attn_prefill_branchfree_ab.jsonl)
+        if (has1 && t0 + FA_KT <= wave_last_slot)
           body(std::true_type{});
         else
           body(std::false_type{});
@@ -629,13 +629,8 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   const bool eight = impl == 5 || impl == 6 || auto8;
   const int nw = eight ? 8 : 4;
   // impl 7 / 9: the software-pipelined loop with lazy rescale (4 / 8 waves), 8: lazy rescale only
-  if ((impl == 7 || impl == 8 || impl == 9 || impl == 11 || impl == 12) &&
-      (rep % (impl == 9 || impl == 12 ? 8 : 4) == 0 || (impl == 9 || impl == 12 ? 8 : 4) % rep == 0)) {
-    if (impl == 11)  // 11 / 12: 7 / 9 with the NEXT body on every tile (one straight-line block, A/B)
-      launch_prefill_v2<4, 2, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
-    else if (impl == 12)
-      launch_prefill_v2<8, 2, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, true, s);
-    else if (impl == 7)
+  if ((impl == 7 || impl == 8 || impl == 9) && (rep % (impl == 9 ? 8 : 4) == 0 || (impl == 9 ? 8 : 4) % rep == 0)) {
+    if (impl == 7)
       launch_prefill_v2<4, 1, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
     else if (impl == 8)
       launch_prefill_v2<4, 0, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);

@@ -87,11 +87,11 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     ctx.setup_mesh(tp=args.tp)
-    comm = TPComm.from_context(ctx)
     dev = ctx.device
     overrides = {} if args.layers is None else {"num_hidden_layers": args.layers}
     max_len = args.prompt_len + args.gen_len
     cfg = get_preset(args.model, max_seq_len=max(2048, max_len), **overrides)
+    comm = TPComm.from_context(ctx, fused_hidden=cfg.hidden_size)
     model = LLaMAForCausalLM(cfg, device=dev, comm=comm, _do_init=False).init_random(seed=1234)
     torch.cuda.synchronize(dev)
 

@@ -16,6 +16,7 @@ random-init model of a named architecture with synthetic prompt ids (no checkpoi
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import sys
 import time
@@ -37,7 +38,9 @@ def load(ckpt_dir: str, tokenizer_path: str, is_llama3: bool, max_seq_len: int =
     """Reference ``load`` (jax_example.py:10-31) on the MI355X runtime."""
     ctx = init_distributed()
     ctx.setup_mesh(tp=ctx.world)
-    comm = TPComm.from_context(ctx)
+    with open(os.path.join(ckpt_dir, "params.json")) as f:
+        hidden = int(json.load(f)["dim"])
+    comm = TPComm.from_context(ctx, fused_hidden=hidden)
     tokenizer = LLaMA3Tokenizer(tokenizer_path) if is_llama3 else LLaMA2Tokenizer(tokenizer_path)
     params, config = load_meta_rank(ckpt_dir, tokenizer, ctx.tp_rank, ctx.tp_size, max_seq_len=max_seq_len)
     config.bos_token_id, config.eos_token_id = tokenizer.bos_id, tokenizer.eos_id
@@ -63,8 +66,8 @@ def synthetic(model_name: str, batch: int, prompt_len: int, max_gen_len: int, te
     from jax_llama_amd.runtime.engine import GenerationConfig
     ctx = init_distributed()
     ctx.setup_mesh(tp=ctx.world)
-    comm = TPComm.from_context(ctx)
     cfg = get_preset(model_name, max_seq_len=max(2048, prompt_len + max_gen_len))
+    comm = TPComm.from_context(ctx, fused_hidden=cfg.hidden_size)
     model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm, _do_init=False).init_random(seed=0)
     toks = torch.randint(3, cfg.vocab_size, (batch, prompt_len), generator=torch.Generator().manual_seed(0),
                          dtype=torch.int32)

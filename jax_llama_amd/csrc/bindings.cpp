@@ -418,7 +418,7 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
     return;
   }
   if (ksplit <= 1) {  // no K split: the GEMM's own RoPE / KV-write epilogue (default FA pipeline, fused norm)
-    check(rms_eps >= 0 && jla::gemm_qkv_direct_ok((int)m, (int)tile), "gemm_qkv without a K split: 256 x 256 FA "
+    check(rms_eps >= 0 && jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k), "gemm_qkv without a K split: 256 x 256 FA "
           "tiles with the fused norm (gemm_qkv_direct_ok)");
     rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, nullptr, 0, 1, stream(),
                  (float)rms_eps, (int)tile),
@@ -740,7 +740,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
         py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none(),
         py::arg("pack_out") = py::none());
-  m.def("gemm_qkv_direct_ok", [](int64_t m, int64_t tile) { return jla::gemm_qkv_direct_ok((int)m, (int)tile) != 0; });
+  m.def("gemm_qkv_direct_ok", [](int64_t m, int64_t tile, int64_t k) {
+    return jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k) != 0;
+  });
+  m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
   m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
     return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
   }, "(slab floats, tickets) of the in-kernel split-K fixup");

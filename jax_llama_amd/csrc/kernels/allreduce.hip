@@ -323,7 +323,10 @@ __global__ void __launch_bounds__(GRAN_THREADS)
     }
   }
   // 2. per 16 payload bytes: poll every rank's two granule pairs until they carry this call's tag, sum in rank order
-  const bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  // give_up: once any wait of any block (or an earlier call) has timed out, every later wait -- further peers, further
+  // chunks of this block -- returns at once; the error word is re-read inside each poll loop and after a local timeout,
+  // so one launch stalls for at most ~timeout_s however many peers are missing
+  bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
   for (long long c = b; c < nchunks; c += d.grid) {
     const long long off = c * GRAN_PAYLOAD + (long long)threadIdx.x * 16;
     if (off >= nbytes) continue;
@@ -334,8 +337,13 @@ __global__ void __launch_bounds__(GRAN_THREADS)
       if (!give_up && (g0[1] != tag || g0[3] != tag || g1[1] != tag || g1[3] != tag)) {
         const long long t0 = (long long)wall_clock64();
         while (g0[1] != tag || g0[3] != tag || g1[1] != tag || g1[3] != tag) {
+          if (__hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+            give_up = true;
+            break;
+          }
           if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
             __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            give_up = true;
             break;
           }
           __builtin_amdgcn_s_sleep(1);

@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "gemm4w.h"
 #include "launchers.h"
 
 namespace jla {
@@ -916,7 +917,239 @@ __global__ void __launch_bounds__(256 * WM)
   }
 }
 
+
 // ---------------------------------------------------------------------------------------------
+// gemm4: the 4-wave 256 x 256 main loop of gemm4w.h (one wave per SIMD, 128 x 128 per wave, 64-deep K-tiles)
+// with every epilogue of gemm2. The accumulators are C^T fragments: lane (c = lane & 15, q = lane >> 4) holds,
+// per (n-tile j, m-tile i) of its wave block, output row m0 + wr*128 + 16i + c at the 4 consecutive columns
+// n0 + wc*128 + 16j + 4q + 0..3 -- so SwiGLU gate/up pairs (adjacent n-tiles), RoPE pairs (adjacent columns) and
+// the fp32 residual (one float4) are all in-lane, and every store is 8 or 16 bytes. Split-K: MODE_PARTIAL slabs
+// [split][M][N] (+ the fused-RMS partial sums [split][M]) summed by gemm_reduce_kernel, as gemm2's.
+template <int MODE, bool RMS>
+__global__ void __launch_bounds__(256, 1)
+    gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                 int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
+                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa) {
+  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];  // the two K-tile slots (the epilogue's staging), + 1 KiB of row scales
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  // XCD-aware bijective remap, then (split, M-grouped tile) order (as gemm2)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int split = wgid / tiles, pid = wgid - split * tiles;
+  int tm, tn;
+  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int t0 = split * kc, KT = min(K >> 6, t0 + kc) - t0;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+  const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
+  g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+
+  const int c = lane & 15, q = lane >> 4, NTT = N >> 4;
+  const int rbase = m0 + wr * 128 + c;  // + 16 i: this lane's output row in m-tile i
+  float sc[8];                           // RMS: per m-tile row scale
+  if constexpr (RMS) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // complete each row's sum over the 4 lanes holding its k-chunks
+      ss[i] += __shfl_xor(ss[i], 16, 64);
+      ss[i] += __shfl_xor(ss[i], 32, 64);
+    }
+    if constexpr (MODE == MODE_PARTIAL) {
+      if (q == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = m0 + wr * 128 + (4 * wc + i) * 16 + c;
+          if (row < M) ssq_ws[(size_t)split * M + row] = ss[i];
+        }
+      }
+    } else {
+      float* rs = reinterpret_cast<float*>(lds + 2 * G4_SLOT_U4);  // beside the staging space
+      __syncthreads();  // every wave is past its last fragment read
+      if (q == 0) {
+        const float fk = (float)K;  // (t / K exactly as gemm_reduce_kernel and gemm2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rs[wr * 128 + (4 * wc + i) * 16 + c] = 1.f / sqrtf(ss[i] / fk + rms_eps);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sc[i] = rs[wr * 128 + 16 * i + c];
+    }
+  }
+  // one accumulator tile at a time, scaled by its row's norm: g4_take keeps hipcc from copying all 256 AGPRs to
+  // VGPRs at once (which spilled)
+  auto tile_val = [&](int j, int i) -> f32x4 {
+    f32x4 v = g4_take(acc[j][i]);
+    if constexpr (RMS && MODE != MODE_PARTIAL) v *= sc[i];
+    return v;
+  };
+
+  // bf16 outputs go through the wave's 32 KiB of LDS (g4_stage_put / g4_stage_rows); every wave must be past its
+  // last fragment read first (the RMS path above already synchronised)
+  char* const wl = reinterpret_cast<char*>(lds) + wu * 32768;
+  constexpr bool STAGED = MODE == MODE_SWIGLU || MODE == MODE_QKV || MODE == MODE_STORE;
+  if constexpr (STAGED && !(RMS && MODE != MODE_PARTIAL)) __syncthreads();
+  const int mrow0 = m0 + wr * 128;  // first output row of the wave block
+  if constexpr (MODE == MODE_SWIGLU) {
+    // gate tile j (even) and up tile j + 1 -> 16 activation columns; the wave block's 64 columns = 128-byte rows
+    const int F = N >> 1;
+    bf16_t* o = static_cast<bf16_t*>(out);
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f32x4 gv = tile_val(j, i), uv = tile_val(j + 1, i);
+        const u32x2 p = {pack2bf(silu(gv[0]) * uv[0], silu(gv[1]) * uv[1]),
+                         pack2bf(silu(gv[2]) * uv[2], silu(gv[3]) * uv[3])};
+        g4_stage_put<128>(wl, 16 * i + c, 16 * j + 8 * q, p);
+      }
+    }
+    const int fcol0 = ((n0 >> 4) + wc * 8) * 8;  // first activation column of the wave block
+    g4_stage_rows<128>(wl, lane, [&](int r, int ch, u32x4 v) {
+      const int row = mrow0 + r, col = fcol0 + 8 * ch;
+      if (row < M && col < F) *reinterpret_cast<u32x4*>(o + (size_t)row * F + col) = v;
+    });
+  } else if constexpr (MODE == MODE_ARGMAX) {
+    // per row: the first maximum over this wave's 128 columns -> one (value, index) partial at
+    // [row][n0 / 128 + wc] (P = 2 tiles_n slots per row); argmax_partials_kernel finishes the row
+    float2* o = static_cast<float2*>(out);
+    const int P = tiles_n * 2, slot = (n0 >> 7) + wc;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tile = (n0 >> 4) + wc * 8 + j;
+        const f32x4 tv = tile_val(j, i);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = tv[r];
+          if (tile < NTT && v > bv) {  // ascending columns in-lane, strict >: the first max
+            bv = v;
+            bi = tile * 16 + 4 * q + r;
+          }
+        }
+      }
+#pragma unroll
+      for (int sh = 16; sh < 64; sh <<= 1) {
+        const float ov = __shfl_xor(bv, sh, 64);
+        const int oi = __shfl_xor(bi, sh, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      const int row = rbase + 16 * i;
+      if (q == 0 && row < M) o[(size_t)row * P + slot] = make_float2(bv, __int_as_float(bi));
+    }
+  } else if constexpr (MODE == MODE_QKV) {
+    // RoPE on the two (even, odd) pairs of the lane's 4 columns in fp32, then staged: 16-byte pieces of a row go to
+    // q or to the k / v cache row at slot[0] + (position in the sequence); same arithmetic as gemm2's /
+    // gemm_reduce_kernel's QKV epilogue (reference model.py:58-92, :169-199)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int gcol = n0 + wc * 128 + 16 * j + 4 * q;
+      const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int grow = min(rbase + 16 * i, M - 1);
+        const f32x4 tv = tile_val(j, i);
+        float v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3];
+        if (head < qa.H + qa.Hkv) {
+          int pos = qa.positions[grow];
+          if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
+          pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
+          const float4 cs = *reinterpret_cast<const float4*>(qa.table + (size_t)pos * (qa.Dh >> 1) + (d0 >> 1));
+          const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
+          const float r2 = v2 * cs.z - v3 * cs.w, r3 = v2 * cs.w + v3 * cs.z;
+          v0 = r0;
+          v1 = r1;
+          v2 = r2;
+          v3 = r3;
+        }
+        g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v0, v1), pack2bf(v2, v3)});
+      }
+    }
+    g4_stage_rows<256>(wl, lane, [&](int r, int ch, u32x4 v) {
+      const int grow = mrow0 + r, gcol = n0 + wc * 128 + 8 * ch;
+      if (grow >= M || gcol >= N) return;
+      const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
+      if (head < qa.H) {
+        *reinterpret_cast<u32x4*>(qa.q + ((size_t)grow * qa.H + head) * qa.Dh + d0) = v;
+      } else {
+        const int b = grow / qa.S, sq = grow - b * qa.S;
+        const int cslot = qa.slot[0] + sq;
+        if (cslot < qa.T) {
+          const bool is_k = head < qa.H + qa.Hkv;
+          const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
+          bf16_t* cache = is_k ? qa.kc : qa.vc;
+          *reinterpret_cast<u32x4*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + cslot) * qa.Dh + d0) = v;
+        } else {
+          JLA_FLAG(JLA_BOUNDS_KV_SLOT);
+        }
+      }
+    });
+  } else if constexpr (MODE == MODE_STORE) {
+    if (out_f32) {  // fp32 logits (16-byte pieces, direct)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tile = (n0 >> 4) + wc * 8 + j;
+        if (tile >= NTT) continue;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int row = rbase + 16 * i;
+          const f32x4 v = tile_val(j, i);
+          if (row < M) *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)row * N + tile * 16 + 4 * q) = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const f32x4 v = tile_val(j, i);
+          g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+        }
+      bf16_t* o = static_cast<bf16_t*>(out);
+      g4_stage_rows<256>(wl, lane, [&](int r, int ch, u32x4 v) {
+        const int row = mrow0 + r, col = n0 + wc * 128 + 8 * ch;
+        if (row < M && col < N) *reinterpret_cast<u32x4*>(o + (size_t)row * N + col) = v;
+      });
+    }
+  } else {  // PARTIAL / RESIDUAL: fp32, one 16-byte piece per lane per tile
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tile = (n0 >> 4) + wc * 8 + j;
+      if (tile >= NTT) continue;
+      const int col = tile * 16 + 4 * q;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = rbase + 16 * i;
+        if (row >= M) continue;
+        const size_t idx = (size_t)row * N + col;
+        const f32x4 v = tile_val(j, i);
+        if constexpr (MODE == MODE_PARTIAL) {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = v;
+        } else {
+          f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(out) + idx);
+          const f32x4 nv = accumulate ? *o + v : v;
+          *o = nv;
+          if (mirror) *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
+        }
+      }
+    }
+  }
+}
+
 // Stream-K tail of the 256 x 256 ping-pong GEMM (tile config 4). Decode-sized outputs rarely have a
 // multiple of 256 tiles (Llama-3-8B at M = 2048: qkv 192, o/down 128, gate_up 896 tiles), so the
 // last wave of whole tiles leaves CUs idle, and split-K pays a second kernel that re-reads fp32
@@ -1425,14 +1658,44 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 //   3: 128 x 128, 8 waves (two ping-pong rows) of 64 x 32 -- 64 KiB of LDS, so two workgroups can share a CU;
 //      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
-int gemm_qkv_direct_ok(int M, int tile) {
-  return g_gemm_impl == 2 && g_g2_var == 5 && (tile == 0 || tile == 1) && tile_cfg(tile, M) == 1;
+static bool use_g4(int tile, int M, int K);
+int gemm_qkv_direct_ok(int M, int tile, int K) {
+  return (g_gemm_impl == 2 && g_g2_var == 5 && (tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
+         use_g4(tile, M, K);
+}
+
+// gemm4 (tile config 7; the default for tile 0 once g_g4_default is set): the 4-wave 256 x 256 kernel of gemm4w.h.
+// Needs K % 64 == 0; data-parallel or plain split-K (MODE_PARTIAL + reduce kernel) only -- the stream-K tail,
+// hybrid and in-kernel fixup plans stay on gemm2.
+constexpr int G4_TILE = 7;
+static bool g_g4_default = true;
+void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
+static bool use_g4(int tile, int M, int K) {
+  return g_gemm_impl == 2 && (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
+}
+
+template <int MODE>
+static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
+                      bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa) {
+  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
+  const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
+  const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
+  if (rms)
+    gemm4_kernel<MODE, true><<<tm * tn * ksplit, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
+                                                               tn, rms_eps, ssq, qa);
+  else
+    gemm4_kernel<MODE, false><<<tm * tn * ksplit, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc,
+                                                                tm, tn, rms_eps, ssq, qa);
 }
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
                       int grid_override = 0, G2Fix fix = G2Fix{}, const QKVArgs& qa = QKVArgs{}) {
+  if (grid_override == 0 && fix.ksplit <= 1 && fix.tile_count == 0 && use_g4(tile, M, K)) {
+    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa);
+    return;
+  }
   const int cfg = tile_cfg(tile, M);
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
@@ -1640,7 +1903,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   const int kc = (KS + ksplit - 1) / ksplit;
   ksplit = (KS + kc - 1) / kc;
   // qkv without a K split: the RoPE / KV-write epilogue of the default FA pipeline (256 x 256 tiles, fused norm)
-  if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile) && rms)) return -1;
+  if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile, K) && rms)) return -1;
   const u32x4* w = static_cast<const u32x4*>(W);
   if (ksplit == 1) {
     switch (mode) {
@@ -1801,6 +2064,13 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   if (ws == nullptr || ws_floats < gemm_argmax_workspace_floats(M, N)) return -3;
   const int tm = (M + 255) / 256, tn = (N + G2_BN - 1) / G2_BN;
   const u32x4* w = static_cast<const u32x4*>(W);
+  if (use_g4(0, M, K)) {  // 2 partials per 256-column tile (one per wave column)
+    launch_g4<MODE_ARGMAX>(x, w, ws, M, N, K, 0, 1, nullptr, 1, rms_eps, nullptr, s, QKVArgs{});
+    JLA_CHECK_LAUNCH();
+    launch_argmax_partials(reinterpret_cast<const float2*>(ws), tn * 2, M, idx, val, s);
+    JLA_CHECK_LAUNCH();
+    return 0;
+  }
   if (rms_eps >= 0.f)
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, true, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
         x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{}, QKVArgs{});

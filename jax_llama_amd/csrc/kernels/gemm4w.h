@@ -1,0 +1,241 @@
+// gemm4w: the 256 x 256 GEMM main loop with ONE wave per SIMD (4 waves per workgroup, 2 x 2), each wave owning a
+// 128 x 128 output block = 8 x 8 v_mfma_f32_16x16x32_bf16 accumulators (256 fp32 registers: the accumulator half of
+// gfx950's 512-entry unified register file). K advances 64 per LDS tile (two 32-deep MFMA sub-steps), two LDS slots
+// of 64 KiB each (x 32 KiB + W 32 KiB), both filled by LDS-DMA (global_load_lds_dwordx4, no VGPR staging):
+//
+//   sub-step (t, 0): 64 MFMAs on register set 0 (tile t, k 0..31) | ds_read set 1 <- tile t, k 32..63
+//   -- lgkmcnt(0), vmcnt(0) (this wave's part of tile t+1 has landed), s_barrier --
+//   sub-step (t, 1): 64 MFMAs on register set 1 | LDS-DMA of tile t+2 into tile t's slot | ds_read set 0 <- tile t+1
+//
+// so the single wave of a SIMD keeps its own MFMA pipe fed: every LDS read and DMA issue sits in the shadow of the
+// MFMAs (sched_group_barrier pins a 4 MFMA : 1 ds_read : 1 DMA interleave), one barrier per 64-deep K-tile, and a
+// DMA has one to two sub-steps (~1-2k cycles) to land. Per MFMA a wave reads 256 B of fragments from LDS (the
+// 8-wave 128 x 64-per-wave ping-pong of gemm2 reads 384 B and pays a barrier pair per 32 MFMAs).
+//
+// LDS images (both lane-linear per DMA instruction, so each A / B fragment read is one conflict-free ds_read_b128):
+//   x  : [256 rows][8 x 16-B cells] per slot, 8 rows x 128 B per DMA (full cache lines); cell c of row r holds the
+//        row's 16-B k-chunk c ^ ((r & 15) >> 1) (the source address is permuted, the destination stays linear);
+//   W  : the packed weight fragments (common.h: 16 n x 32 k per 1 KiB) copied verbatim, fragment (n-tile, k half).
+// The MFMA runs with the weight fragment as the A operand, so each lane ends up holding 4 CONSECUTIVE output columns
+// of one output row per 16 x 16 tile (C^T fragments): RoPE pairs, SwiGLU gate/up pairs and 8-byte packed stores
+// fall out in-lane.
+//
+// Reference ops: jax_llama/model.py:210 (q/k/v projections), :294 (wo), :338 (SwiGLU MLP), :736 (lm_head).
+#pragma once
+#include "common.h"
+
+namespace jla {
+
+constexpr int G4_BM = 256, G4_BN = 256, G4_BK = 64, G4_GROUP_M = 8;
+constexpr int G4_A_U4 = G4_BM * G4_BK * 2 / 16;  // 2048 u32x4 = 32 KiB
+constexpr int G4_B_U4 = G4_BN * G4_BK * 2 / 16;  // 2048 u32x4 = 32 KiB
+constexpr int G4_SLOT_U4 = G4_A_U4 + G4_B_U4;    // 64 KiB
+
+// launch-order tile index -> (m tile, n tile), M-grouped by G4_GROUP_M so consecutive workgroups share W columns
+JLA_DEV void g4_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int in_group = G4_GROUP_M * tiles_n;
+  const int first_m = (pid / in_group) * G4_GROUP_M;
+  const int gsz = min(tiles_m - first_m, G4_GROUP_M);
+  tm = first_m + (pid % in_group) % gsz;
+  tn = (pid % in_group) / gsz;
+}
+
+// The accumulators are pinned to AGPRs through inline asm: with the intrinsic, hipcc (ROCm 7.2) splits the 256
+// loop-carried accumulators between the two register files and shuffles them with v_accvgpr moves around every
+// MFMA. Volatile, so the MFMAs keep their program order relative to the DMA issues and fragment reads placed between
+// them. Hazards: the A / B fragments come from ds_reads (counted by hipcc: the asm names them as inputs), each
+// accumulator is read by one MFMA per 64, and g4_acc_fence() pads the MFMA -> v_accvgpr_read hand-off after the loop.
+JLA_DEV void g4_mfma(f32x4& acc, const u32x4& a, const u32x4& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// an accumulator tile for the epilogue, read out of its AGPRs at this point in program order
+JLA_DEV f32x4 g4_take(f32x4& a) {
+  asm volatile("" : "+a"(a));
+  return a;
+}
+JLA_DEV void g4_acc_fence() { asm volatile("s_nop 7\n\ts_nop 7" ::: "memory"); }
+
+struct G4Args {
+  const bf16_t* x;  // [M][K] row-major activations
+  const u32x4* W;   // packed [N/16][K/32][64] fragments
+  void* out;
+  int M, N, K;
+  int kc;           // 64-deep K-tiles per split (split = workgroup index / tiles)
+  int tiles_m, tiles_n;
+};
+
+// The main loop; leaves the C^T accumulators of this wave in acc[j][i] (n-tile j, m-tile i of the wave's block).
+// Returns nothing else; the caller's epilogue reads acc. `lds` is the workgroup's 128 KiB staging array.
+// RMS: also accumulate the row sums of squares of x (the fused RMSNorm statistic, reference model.py:42-48) from
+// the x fragments already in registers: wave (wr, wc) takes m-tiles 4wc..4wc+3 of its row block, ss[i] holds lane
+// (row lane & 15, k-chunk lane >> 4)'s partial of m-tile 4wc + i, k32 step after k32 step in K order.
+template <bool RMS = false, typename Acc>
+JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc,
+                         float* ss = nullptr) {
+  const int wr = wu >> 1, wc = wu & 1;
+  const int K = g.K, KS = K >> 5, NTT = g.N >> 4;
+
+  // ---- DMA sources (saddr form: a wave-uniform base per operand + a 32-bit per-lane offset)
+  // x piece P = wu + 4j (j = 0..7): rows 8P + (lane >> 3), cell lane & 7 <- k-chunk (lane & 7) ^ swz(row)
+  const char* const baseA = reinterpret_cast<const char*>(g.x + (size_t)m0 * K + (size_t)t0 * 64);
+  const char* const baseB = reinterpret_cast<const char*>(g.W + ((size_t)(n0 >> 4) * KS + 2 * t0) * 64);
+  unsigned offA[8], offB[8];
+  const int mlast = g.M - 1 - m0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int P = wu + 4 * j;
+    const int row = min(8 * P + (lane >> 3), mlast);
+    const int chunk = (lane & 7) ^ (4 * (P & 1) + (lane >> 4));
+    offA[j] = (unsigned)row * (unsigned)K * 2u + 16u * (unsigned)chunk;
+    // W fragment f = wu + 4j: n-tile f >> 1, k half f & 1 (= wu & 1)
+    const int f = wu + 4 * j;
+    const int nt = min((n0 >> 4) + (f >> 1), NTT - 1) - (n0 >> 4);
+    offB[j] = ((unsigned)nt * (unsigned)KS + (unsigned)(f & 1)) * 1024u + 16u * (unsigned)lane;
+  }
+  auto dma = [&](int t, int j) {  // the j-th of this wave's 16 DMAs of K-tile t (0..7 x, 8..15 W)
+    u32x4* slot = lds + (t & 1) * G4_SLOT_U4;
+    if (j < 8) {
+      glds16(baseA + (size_t)t * 128 + offA[j], slot + (wu + 4 * j) * 64);
+    } else {
+      glds16(baseB + (size_t)t * 2048 + offB[j - 8], slot + G4_A_U4 + (wu + 4 * (j - 8)) * 64);
+    }
+  };
+
+  // ---- fragment reads: A operand = W fragment of n-tile (wc*8 + j), B operand = x fragment of m-tile (wr*8 + i)
+  // x: row r = wr*128 + 16i + (lane & 15), k-chunk 4h + (lane >> 4), stored at cell chunk ^ ((r & 15) >> 1)
+  const int xrd = (wr * 128 + (lane & 15)) * 8;
+  const int xc0 = (0 + (lane >> 4)) ^ ((lane >> 1) & 7), xc1 = (4 + (lane >> 4)) ^ ((lane >> 1) & 7);
+  auto rd = [&](u32x4& dst, int slot, int h, int q) {  // q 0..7: W n-tile q; 8..15: x m-tile q - 8
+    const u32x4* s = lds + slot * G4_SLOT_U4;
+    if (q < 8)
+      dst = s[G4_A_U4 + ((wc * 8 + q) * 2 + h) * 64 + lane];
+    else
+      dst = s[xrd + (q - 8) * 128 + (h ? xc1 : xc0)];
+  };
+
+  u32x4 w0[8], x0[8], w1[8], x1[8];
+
+  // one 64-MFMA sub-step on (wf, xf), interleaved with up to 16 fragment reads into (wn, xn) and 16 DMAs of tile td
+  auto substep = [&](u32x4 (&wf)[8], u32x4 (&xf)[8], u32x4 (&wn)[8], u32x4 (&xn)[8], bool do_rd, int rslot, int rh,
+                     bool do_dma, int td) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = 4 * q + u, j = e >> 3, i = e & 7;
+        g4_mfma(acc[j][i], wf[j], xf[i]);
+      }
+      if (do_rd) rd(q < 8 ? wn[q] : xn[q - 8], rslot, rh, q);
+      if (do_dma) dma(td, q);
+      if constexpr (RMS) {
+        if (q < 4) {  // m-tile 4wc + q: the runtime wc selects between two named fragments (no indexed array)
+          const u32x4 f = wc ? xf[4 + q] : xf[q];
+          ss[q] = dot8_bf16(f, f, ss[q]);
+        }
+      }
+    }
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed, set 0 <- tile 0 k 0..31
+  if (KT > 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(0, j);
+  }
+  if (KT > 1) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(1, j);
+    wait_vmcnt<16>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (KT > 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rd(q < 8 ? w0[q] : x0[q - 8], 0, 0, q);
+  }
+
+  auto mid_barrier = [&]() {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0), visible to hipcc's own wait bookkeeping
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  int t = 0;
+  for (; t + 2 < KT; ++t) {  // steady state: reads of tile t+1 and DMA of tile t+2 in every K-tile
+    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    mid_barrier();
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, true, t + 2);
+  }
+  if (t + 1 < KT) {  // second to last: nothing left to DMA
+    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    mid_barrier();
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, false, 0);
+    ++t;
+  }
+  if (t < KT) {  // last K-tile
+    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    substep(w1, x1, w0, x0, false, 0, 0, false, 0);
+  }
+  g4_acc_fence();
+}
+
+// Staged bf16 epilogue, in two steps on the wave's private 32 KiB of the (now idle) staging array:
+//  g4_stage_put: lane (c, q) puts its 4 bf16 of an output row (8 bytes at logical byte cb of local row r) -- rows of
+//    CB bytes, 8-byte granules XOR-swizzled by (r & 15) so the 16 rows a lane group writes hit distinct banks;
+//  g4_stage_rows: after lgkmcnt(0), each lane takes 16 contiguous bytes of a row (CB / 16 lanes per row) and hands
+//    them to store(local row, 16-byte chunk index, data) -- full-row global stores instead of 16-row x 32-byte pieces
+//    (the direct form cost 10+ % at prefill sizes: the epilogue runs with the CU's MFMA pipes idle).
+template <int CB>
+JLA_DEV void g4_stage_put(char* wl, int r, int cb, u32x2 v) {
+  *reinterpret_cast<u32x2*>(wl + r * CB + (cb ^ ((r & 15) << 3))) = v;
+}
+template <int CB, typename F>
+JLA_DEV void g4_stage_rows(const char* wl, int lane, F&& store) {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's own puts landed (the region is wave-private)
+  constexpr int LPR = CB / 16, RPI = 64 / LPR;
+  const int ch = lane % LPR;
+#pragma unroll 4
+  for (int s = 0; s < 128 / RPI; ++s) {
+    const int r = RPI * s + lane / LPR;
+    const int sw = (r & 15) << 3;
+    u32x4 v = *reinterpret_cast<const u32x4*>(wl + r * CB + ((16 * ch) ^ (sw & ~15)));
+    if (sw & 8) v = u32x4{v[2], v[3], v[0], v[1]};
+    store(r, ch, v);
+  }
+}
+
+// bf16 store of the wave's 128 x 128 block through LDS: each lane packs its 4 consecutive columns per tile into
+// one 8-byte ds_write (row-XOR-swizzled at 8-byte granularity: conflict-free for the 16 rows of a lane group), then
+// reads back 16 B of a row per lane and writes full 256-B row segments (32 x 16-B stores per lane). The caller has
+// passed a barrier after the last fragment read; the wave uses its own 32 KiB of the staging array.
+template <typename Acc>
+JLA_DEV void g4_store_bf16(Acc& acc, u32x4* lds, bf16_t* out, int M, int N, int m0, int n0, int wu, int lane) {
+  const int wr = wu >> 1, wc = wu & 1;
+  char* const wl = reinterpret_cast<char*>(lds) + wu * 32768;
+  const int c = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 16 * i + c;  // local row
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 v = acc[j][i];
+      const u32x2 p = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      const int cb = (32 * j + 8 * q) ^ (c << 3);
+      *reinterpret_cast<u32x2*>(wl + r * 256 + cb) = p;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own writes landed (the region is wave-private)
+  const int gcol = n0 + wc * 128 + 8 * c;
+#pragma unroll 8
+  for (int s = 0; s < 32; ++s) {
+    const int r = 4 * s + q;
+    const int sw = (r & 15) << 3;
+    u32x4 v = *reinterpret_cast<const u32x4*>(wl + r * 256 + ((16 * c) ^ (sw & ~15)));
+    if (sw & 8) v = u32x4{v[2], v[3], v[0], v[1]};
+    const int grow = m0 + wr * 128 + r;
+    if (grow < M && gcol < N) *reinterpret_cast<u32x4*>(out + (size_t)grow * N + gcol) = v;
+  }
+}
+
+}  // namespace jla

@@ -331,9 +331,11 @@ class LLaMAForCausalLM:
                       x_packed: Optional[torch.Tensor] = None, mirror_packed: Optional[torch.Tensor] = None) -> None:
         """``h += x @ W^T`` where W is row-sharded. TP=1: the GEMM epilogue adds into the fp32 residual
         ``h`` and writes its bf16 mirror ``hb`` (the A operand of the next projection). TP>1: the GEMM
-        writes only this rank's partial (``comm.reduce_dtype``, bf16 by default) and one collective
-        kernel sums the partials in rank order, adds them to ``h`` and rewrites ``hb``
-        (``comm.all_reduce_residual_``; reference ``partition.py:67,70``)."""
+        writes only this rank's partial (``comm.reduce_dtype``, bf16 by default). Decode-sized partials: one
+        custom collective kernel (or the GEMV itself, ``comm.FUSED``) sums them in fp32 in rank order, adds them to
+        ``h`` and rewrites ``hb``. Prefill-sized partials: RCCL sums them upcast to fp32 (RCCL's order; bf16 on the
+        wire only with ``JLA_TP_RCCL_BF16=1``), then one kernel adds into ``h`` (``comm.all_reduce_residual_``;
+        reference ``partition.py:67,70``)."""
         if self.comm.size == 1:
             ops.linear_residual(x, w, h, mirror=hb, x_packed=x_packed, mirror_packed=mirror_packed)
         elif self.comm.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=mirror_packed):

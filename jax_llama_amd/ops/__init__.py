@@ -480,7 +480,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
         if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):
             tm = 1  # the stream-K plan has a data-parallel part here: plain GEMM + RoPE kernel
         fused = _fused_rms(e, MODE_QKV, rms_eps)
-        if ks == 1 and tm != SK_TILE and fused and QKV_DIRECT and e.gemm_qkv_direct_ok(m, tm):
+        if ks == 1 and tm != SK_TILE and fused and QKV_DIRECT and e.gemm_qkv_direct_ok(m, tm, w.k):
             # enough tiles, no K split: the GEMM's own RoPE / KV-write epilogue (no qkv round trip, no rope kernel)
             q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
             e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),

@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 3  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26), so older persisted picks are re-measured
+TUNE_VERSION = 4  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -282,7 +282,7 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
+TILE_CANDIDATES = (1, 2, 3, 7)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg); 7: gemm4;
 # plus (1, SK_TILE) -- 256x256 with a stream-K tail -- for shapes whose tile count is not a multiple of the CUs
 TUNE_MAX_M = 2048
 

@@ -28,6 +28,8 @@ import torch.distributed as dist
 # GEMV-fused row-parallel all-reduce at decode (csrc/kernels/gemv.hip MODE_TPRESID); JLA_TP_FUSED=0: a separate
 # collective kernel after each row-parallel GEMV
 FUSED = os.environ.get("JLA_TP_FUSED", "1") != "0"
+# prefill-sized row-parallel partials over RCCL in bf16 (half the bytes, bf16 accumulation) instead of fp32
+RCCL_BF16 = os.environ.get("JLA_TP_RCCL_BF16", "0") == "1"
 
 
 def _default_reduce_dtype():
@@ -106,12 +108,14 @@ class TPComm:
             return h
         if hb_pack is not None:
             raise RuntimeError("all_reduce_residual_: the packed hb copy needs the custom all-reduce path")
-        # prefill-sized messages: the partials go over RCCL in reduce_dtype as they are (bf16 by default: half the
-        # bytes of fp32), then ONE kernel adds the sum into h and rewrites the mirror (ops.residual_add_)
+        # prefill-sized messages go over RCCL / gloo, which accumulate in the dtype on the wire: bf16 partials are
+        # upcast so the sum is an fp32 sum like the custom kernels' (a bf16 ring sum would round up to world-1 times,
+        # in an order RCCL picks); RCCL_BF16 (JLA_TP_RCCL_BF16=1) keeps them bf16 for half the bytes. Then ONE kernel
+        # adds the sum into h and rewrites the mirror (ops.residual_add_)
         if self.size > 1:
             p = partial if partial.is_contiguous() else partial.contiguous()
-            if p.dtype == torch.bfloat16 and (not p.is_cuda or self._host_staged(p)):
-                p = p.float()  # gloo: sum in fp32
+            if p.dtype == torch.bfloat16 and not (RCCL_BF16 and p.is_cuda and not self._host_staged(p)):
+                p = p.float()
             elif p.data_ptr() == partial.data_ptr():
                 p = p.clone()  # never reduce the caller's buffer in place
             self.all_reduce_(p)

@@ -22,6 +22,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 TIMEOUT_S = 0.5
+TIMEOUT3_S = 2.0
 
 
 def _free_port():
@@ -78,6 +79,38 @@ def _missing_peer(rank, world, port, q):
             except CustomAllReduceError:
                 res["refuses_after"] = True
         dist.barrier()  # rank 0's kernels are done before rank 1 unmaps its buffers
+        car.close()
+        dist.destroy_process_group()
+        q.put(("ok", rank, res))
+    except Exception:  # pragma: no cover - surfaced in the parent
+        import traceback
+        q.put(("err", rank, traceback.format_exc()))
+
+
+def _two_missing_peers(rank, world, port, q):
+    """World 3, ranks 1 and 2 both skip a granule all-reduce: rank 0's blocks must give up on the second missing peer
+    as soon as the first has timed out (the error word is re-read inside every poll loop), so the call ends after
+    about one timeout, not one per missing peer."""
+    try:
+        dist = _init(rank, world, port)
+        from jax_llama_amd.parallel.custom_allreduce import CustomAllReduce
+        car = CustomAllReduce.create_for(rank, world, None, max_bytes=1 << 20, timeout_s=TIMEOUT3_S)
+        n = 16 * 1024  # 32 KiB of bf16 per rank: the granule path, 16 chunks
+        x = torch.full((n,), float(rank + 1), dtype=torch.bfloat16, device="cuda")
+        h = torch.zeros(n, dtype=torch.float32, device="cuda")
+        hb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        res = {}
+        car.all_reduce_residual_(x, h, hb)  # every rank: a good round
+        torch.cuda.synchronize()
+        res["first_ok"] = bool((h == 6.0).all()) and car.error() == 0
+        dist.barrier()
+        if rank == 0:
+            t0 = time.perf_counter()
+            car.all_reduce_residual_(x, h, hb)
+            torch.cuda.synchronize()
+            res["timeout_wait_s"] = time.perf_counter() - t0
+            res["error_word"] = car.error()
+        dist.barrier()
         car.close()
         dist.destroy_process_group()
         q.put(("ok", rank, res))
@@ -248,6 +281,16 @@ def test_missing_peer_times_out_and_poisons():
     assert 0.8 * TIMEOUT_S <= r0["timeout_wait_s"] < 10 * TIMEOUT_S, r0["timeout_wait_s"]
     assert r0["after_error_wait_s"] < 0.5 * TIMEOUT_S, r0["after_error_wait_s"]
     assert r0["check_raised"] and r0["refuses_after"]
+
+
+@pytest.mark.timeout(300)
+def test_two_missing_peers_wait_one_timeout():
+    res = _spawn(_two_missing_peers, world=3)
+    assert all(res[r]["first_ok"] for r in range(3)), res
+    r0 = res[0]
+    assert r0["error_word"] == 1, r0
+    # before the fix: one full timeout per missing peer (>= 2 x TIMEOUT3_S)
+    assert 0.8 * TIMEOUT3_S <= r0["timeout_wait_s"] < 1.5 * TIMEOUT3_S, r0["timeout_wait_s"]
 
 
 @pytest.mark.timeout(300)

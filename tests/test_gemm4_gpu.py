@@ -1,0 +1,156 @@
+"""gemm4 -- the 4-wave 256 x 256 GEMM (one wave per SIMD, 128 x 128 AGPR accumulators per wave, 64-deep K-tiles;
+csrc/kernels/gemm4w.h) -- against the pure-PyTorch fp32 reference and against gemm2 (tile config 1) for every
+epilogue: bf16 / fp32 store, SwiGLU, residual + mirror, the RoPE / KV-cache write, the fused argmax; with and
+without the fused RMSNorm statistic; data-parallel and split-K (partial slabs + reduce kernel); ragged M and N.
+Reference ops: jax_llama/model.py:210, :294, :338, :736."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from jax_llama_amd import ops
+from jax_llama_amd.models.weights import PackedLinear
+from jax_llama_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF16 = torch.bfloat16
+G4 = 7  # tile config of gemm4 (csrc/kernels/gemm.hip G4_TILE)
+
+
+def _close(a, b, rtol, atol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item()
+    assert err <= atol + rtol * scale, f"max err {err:.3e} (ref max {scale:.3e})"
+
+
+def _run_all(e, xg, pg, gp, h0, n, k, ks, ws, tile):
+    outs = []
+    for eps in (-1.0, 1e-5):
+        o = torch.empty(xg.shape[0], n, dtype=torch.float32, device=DEV)
+        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile)
+        ob = torch.empty(xg.shape[0], n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile)
+        o2 = torch.empty(xg.shape[0], n // 2, dtype=BF16, device=DEV)
+        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile)
+        outs += [o, ob, o2]
+    hg, mir = h0.clone(), torch.empty(h0.shape, dtype=BF16, device=DEV)
+    e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, tile)
+    torch.cuda.synchronize()
+    return outs + [hg, mir]
+
+
+@pytest.mark.parametrize("m,n,k,ks", [(200, 768, 1024, 1), (512, 1056, 1024, 1), (700, 2560, 4096, 1),
+                                      (300, 768, 2048, 3), (2048, 4096, 4096, 2), (1000, 6144, 1536, 1)])
+def test_gemm4_every_epilogue(m, n, k, ks):
+    e = ops.ext()
+    torch.manual_seed(m + n + k)
+    x = torch.randn(m, k).to(BF16)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    pg = PackedLinear.from_dense(w, DEV)
+    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+    gp = PackedLinear.from_dense(gu, DEV)
+    xg = x.to(DEV)
+    h0 = torch.randn(m, n).to(DEV)
+    ws = torch.empty(ks * m * (n + 1), dtype=torch.float32, device=DEV) if ks > 1 else None
+    g4 = _run_all(e, xg, pg, gp, h0, n, k, ks, ws, G4)
+    again = _run_all(e, xg, pg, gp, h0, n, k, ks, ws, G4)
+    g2 = _run_all(e, xg, pg, gp, h0, n, k, ks, ws, 1)
+    for i, (a, b) in enumerate(zip(g4, again)):
+        assert torch.equal(a, b), f"output {i}: not reproducible"
+    # vs gemm2: the same MFMA products in the same K order per output element; the row statistic of the fused norm
+    # is summed in the same order, so the outputs agree to the last bit or within one rounding of bf16 outputs
+    for i, (a, b) in enumerate(zip(g4, g2)):
+        _close(a, b, 1e-2, 1e-3)
+    _close(g4[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+    _close(g4[1], ref.linear(x, w, None, torch.float32), 2e-2, 2e-2)
+    _close(g4[3], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+    _close(g4[2], ref.linear_swiglu(x, gu, None), 3e-2, 3e-2)
+    _close(g4[5], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
+    _close(g4[6], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
+    torch.testing.assert_close(g4[7].cpu(), g4[6].cpu().to(BF16), rtol=0, atol=0)
+    exact = [torch.equal(a, b) for a, b in zip(g4, g2)]
+    print("bit-identical to gemm2:", exact)
+
+
+@pytest.mark.parametrize("m,s,n_heads", [(512, 512, 8), (256, 1, 32), (300, 3, 8)])
+def test_gemm4_qkv_rope_epilogue(m, s, n_heads):
+    """The RoPE / KV-cache write in gemm4's epilogue (rotation in fp32 on the lane's two column pairs) against the
+    fp32 oracle and gemm2's LDS-staged epilogue."""
+    e = ops.ext()
+    hkv, dh, k, t = 8, 128, 4096, 600
+    h = n_heads
+    b = m // s
+    n = (h + 2 * hkv) * dh
+    assert e.gemm_qkv_direct_ok(m, G4, k)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    x = torch.randn(m, k).to(BF16)
+    table = ref.rope_table(dh, 1024, 500000.0)
+    pos = torch.randint(0, 1000, (m,), dtype=torch.int32)
+    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
+    vc = torch.zeros_like(kc)
+    q = ref.linear_qkv_rope(x.float(), w, 1e-5, table, pos, kc, vc, 11, s, h, hkv, dh)
+    pg = PackedLinear.from_dense(w, DEV)
+    outs = {}
+    for tile in (G4, 1):
+        kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
+        qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
+        e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
+                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile, None)
+        outs[tile] = (qg.cpu(), kg.cpu(), vg.cpu())
+    qg, kg, vg = outs[G4]
+    _close(qg, q, 2e-2, 2e-2)
+    _close(kg, kc, 2e-2, 2e-2)
+    _close(vg, vc, 2e-2, 2e-2)
+    for a, c in zip(outs[G4], outs[1]):
+        _close(a, c, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 1008, 512), (300, 4096, 1024), (700, 2560, 1024)])
+def test_gemm4_argmax(m, n, k):
+    """gemm_argmax on gemm4 (2 partials per 256-column tile): exactly the stored-logits argmax (index and value),
+    planted exact ties included."""
+    e = ops.ext()
+    x = torch.randn(m, k).to(BF16)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    for src, dst in ((3, 700 % n), (17, 18), (n - 300, n - 1), (64, 63), (100, 200)):
+        w[src] = (w[src].float() * 8).to(BF16)
+        w[dst] = w[src]
+    pg = PackedLinear.from_dense(w, DEV)
+    xg = x.to(DEV)
+    try:
+        e.gemm_set_g4_default(1)
+        for eps in (-1.0, 1e-5):
+            logits = torch.empty(m, n, dtype=torch.float32, device=DEV)
+            e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, G4)
+            i0 = torch.empty(m, dtype=torch.int32, device=DEV)
+            v0 = torch.empty(m, dtype=torch.float32, device=DEV)
+            e.argmax(logits, i0, v0)
+            ws = torch.empty(e.gemm_argmax_workspace(m, n), dtype=torch.float32, device=DEV)
+            i1, v1 = torch.empty_like(i0), torch.empty_like(v0)
+            e.gemm_argmax(xg, pg.weight, n, k, ws, eps, i1, v1)
+            torch.cuda.synchronize()
+            assert torch.equal(i0.cpu(), i1.cpu()), (eps, (i0 != i1).nonzero()[:8])
+            assert torch.equal(v0.cpu(), v1.cpu())
+    finally:
+        e.gemm_set_g4_default(0)
+
+
+def test_gemm4_model_prefill_matches_gemm2():
+    """A whole prefill (M = 2 x 160 rows: every projection on the tiled GEMM) with gemm4 as the tile-0 default vs
+    gemm2: logits agree to bf16 rounding."""
+    from helpers import gpu_config
+    from jax_llama_amd.models import LLaMAForCausalLM
+    e = ops.ext()
+    cfg = gpu_config(hidden_size=512, intermediate_size=1536, num_attention_heads=4, num_key_value_heads=2,
+                     vocab_size=1024)
+    model = LLaMAForCausalLM(cfg, device=DEV, seed=0)
+    toks = torch.randint(3, cfg.vocab_size, (2, 160), dtype=torch.int32)
+    base = model(toks).logits.float().cpu()
+    try:
+        e.gemm_set_g4_default(1)
+        got = model(toks).logits.float().cpu()
+    finally:
+        e.gemm_set_g4_default(0)
+    _close(got, base, 2e-2, 2e-2)

@@ -230,7 +230,9 @@ def test_tp_decode_matches_single_process(world, kind, rows):
     # not a property of a K-split sum: a near-tie can break the other way and the sequences then differ)
     # (the TP1 decode and its teacher-forced prefill round the logits at different points: near-ties within
     # bf16 rounding of the logits, ~1e-3 of their scale at V = 32000, can break either way)
-    assert r0["tp1_argmax_gap"] < 5e-3, r0["tp1_argmax_gap"]
+    # per kind: the V = 32000 MHA configs (13b / 65b) carry near-ties up to ~1e-3 of the logit scale; the small and
+    # 70b configs keep the tight bound
+    assert r0["tp1_argmax_gap"] < (5e-3 if kind in ("13b", "65b") else 1e-4), r0["tp1_argmax_gap"]
     # (a near-tie broken the other way costs at most the logits' rounding error: err_fp32 above is < 2e-2)
     assert r0["tp_argmax_gap"] < 1e-2, (r0["tp_argmax_gap"], r0["greedy_eq_tp1"])
     assert r0["greedy_bf16_first_eq"]

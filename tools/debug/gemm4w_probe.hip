@@ -1,0 +1,129 @@
+// Standalone probe of the gemm4w main loop (csrc/kernels/gemm4w.h): correctness against a naive fp32 GPU
+// reference and timing on random operands, weights rotated over copies larger than the Infinity Cache.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -I jax_llama_amd/csrc/kernels \
+//     tools/debug/gemm4w_probe.hip -o build/gemm4w_probe
+//   build/gemm4w_probe M N K [iters]
+// Prints one JSON line per shape: us, TFLOP/s, max relative error.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "gemm4w.h"
+
+using namespace jla;
+
+__global__ void __launch_bounds__(256, 1) gemm4_store_kernel(G4Args g) {
+  __shared__ u32x4 lds[2 * G4_SLOT_U4];
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int split = wgid / tiles, pid = wgid - split * tiles;
+  int tm, tn;
+  g4_tile_coords(pid, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int t0 = split * g.kc, KT = min(g.K >> 6, t0 + g.kc) - t0;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  g4_mainloop(g, lds, m0, n0, t0, KT, wu, lane, acc);
+  __syncthreads();
+  g4_store_bf16(acc, lds, static_cast<bf16_t*>(g.out), g.M, g.N, m0, n0, wu, lane);
+}
+
+__device__ inline unsigned hash32(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352d; x ^= x >> 15; x *= 0x846ca68b; x ^= x >> 16;
+  return x;
+}
+__global__ void fill_rand(bf16_t* p, size_t n, unsigned seed, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float u = (hash32((unsigned)i * 2654435761u ^ seed) >> 8) * (1.f / 16777216.f) * 2.f - 1.f;
+    p[i] = f2bf(u * scale);
+  }
+}
+// out[m][n] = sum_k x[m][k] W[n][k]; W in the packed fragment layout
+__global__ void ref_kernel(const bf16_t* x, const bf16_t* Wp, float* out, int M, int N, int K, int rows) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x, m = blockIdx.y;
+  if (n >= N || m >= rows) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const size_t off = ((size_t)((n >> 4) * (K >> 5) + (k >> 5)) * 64 + (n & 15) + 16 * ((k & 31) >> 3)) * 8 + (k & 7);
+    s += bf2f(x[(size_t)m * K + k]) * bf2f(Wp[off]);
+  }
+  out[(size_t)m * N + n] = s;
+}
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 2048, N = argc > 2 ? atoi(argv[2]) : 28672,
+            K = argc > 3 ? atoi(argv[3]) : 4096, iters = argc > 4 ? atoi(argv[4]) : 20;
+  const int ksplit = argc > 5 ? atoi(argv[5]) : 1;
+  if (N % 16 || K % 64) {
+    fprintf(stderr, "shape\n");
+    return 2;
+  }
+  const size_t wbytes = (size_t)N * K * 2;
+  const int copies = (int)std::max<size_t>(2, (700ull << 20) / wbytes + 1);
+  bf16_t *x, *out;
+  std::vector<bf16_t*> w(copies);
+  CK(hipMalloc(&x, (size_t)M * K * 2));
+  CK(hipMalloc(&out, (size_t)M * N * 2));
+  for (int c = 0; c < copies; ++c) {
+    CK(hipMalloc(&w[c], wbytes));
+    fill_rand<<<2048, 256>>>(w[c], (size_t)N * K, 1234 + c, 0.05f);
+  }
+  fill_rand<<<2048, 256>>>(x, (size_t)M * K, 99, 1.f);
+  CK(hipDeviceSynchronize());
+  const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+  const int KT64 = K / 64, kc = (KT64 + ksplit - 1) / ksplit;
+  auto launch = [&](int c) {
+    G4Args g{x, reinterpret_cast<const u32x4*>(w[c]), out, M, N, K, kc, tm, tn};
+    gemm4_store_kernel<<<tm * tn * ksplit, 256>>>(g);
+  };
+  // correctness (first rows; ksplit must be 1 for a meaningful check)
+  launch(0);
+  CK(hipDeviceSynchronize());
+  const int rows = std::min(M, 512);
+  float* ref;
+  CK(hipMalloc(&ref, (size_t)rows * N * 4));
+  ref_kernel<<<dim3((N + 255) / 256, rows), 256>>>(x, w[0], ref, M, N, K, rows);
+  CK(hipDeviceSynchronize());
+  std::vector<float> hr((size_t)rows * N);
+  std::vector<bf16_t> ho((size_t)rows * N);
+  CK(hipMemcpy(hr.data(), ref, hr.size() * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(ho.data(), out, ho.size() * 2, hipMemcpyDeviceToHost));
+  double maxerr = 0, maxref = 0;
+  for (size_t i = 0; i < hr.size(); ++i) {
+    const float g = __builtin_bit_cast(float, (unsigned)ho[i] << 16);
+    maxerr = std::max(maxerr, (double)fabsf(g - hr[i]));
+    maxref = std::max(maxref, (double)fabsf(hr[i]));
+  }
+  // timing
+  for (int i = 0; i < 3; ++i) launch(i % copies);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) launch(i % copies);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1000.0 / iters;
+  printf("{\"kernel\": \"gemm4w\", \"m\": %d, \"n\": %d, \"k\": %d, \"ksplit\": %d, \"us\": %.2f, \"tflops\": %.1f, "
+         "\"rel_err\": %.2e}\n",
+         M, N, K, ksplit, us, 2.0 * M * N * K / us / 1e6, maxerr / std::max(maxref, 1e-6));
+  return 0;
+}

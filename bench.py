@@ -68,6 +68,10 @@ def main():
     ap.add_argument("--proxy-model", default="llama3-70b", help="model of the one-GPU TP rank proxy ('' = skip)")
     ap.add_argument("--proxy-tp", type=int, default=8)
     ap.add_argument("--proxy-batches", type=int, nargs="*", default=[1, 32, 256])
+    ap.add_argument("--mp1-model", default="llama3-70b", help="one-GPU (MP 1) decode point of this model at "
+                    "--mp1-batch ('' = skip): all 80 layers of Llama-3-70B on one 288 GB GPU")
+    ap.add_argument("--mp1-batch", type=int, default=256)
+    ap.add_argument("--no-calibration", action="store_true")
     ap.add_argument("--json-out", default=None)
     args = ap.parse_args()
 
@@ -79,7 +83,8 @@ def main():
     from jax_llama_amd.ops import autotune
     from jax_llama_amd.parallel import TPComm, init_distributed
     from jax_llama_amd.runtime import engine as eng_mod
-    from jax_llama_amd.runtime.benchmark import decode_latency, generate_tokens_per_sec, time_to_first_token
+    from jax_llama_amd.runtime.benchmark import (calibration, decode_latency, generate_tokens_per_sec,
+                                                 time_to_first_token)
     from jax_llama_amd.runtime.engine import GenerationConfig, get_engine
 
     ctx = init_distributed()
@@ -189,7 +194,7 @@ def main():
     def latency_points():
         lat = []
         for b in args.latency_batches:
-            lat.append(decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=7, barrier=ctx.barrier))
+            lat.append(decode_latency(model, b, args.prompt_len, args.gen_len, seed=7, barrier=ctx.barrier))
         for p in lat:  # the slowest rank's number
             p["decode_ms_per_token"] = ctx.all_reduce_max([p["decode_ms_per_token"]])[0]
             p["decode_tokens_per_sec"] = round(p["batch"] * 1000.0 / p["decode_ms_per_token"], 2)
@@ -222,12 +227,19 @@ def main():
         extra("sampled", sampled)
     if world == 1 and args.proxy_model and args.proxy_batches:
         extra("tp_rank_proxy", lambda: res.__setitem__("tp_rank_proxy", _tp_rank_proxy(args)))
+    if world == 1 and args.mp1_model:
+        del model
+        eng_mod._ENGINES.clear()
+        torch.cuda.empty_cache()
+        extra("mp1_point", lambda: res.__setitem__("mp1_point", _mp1_point(args)))
+    if not args.no_calibration:  # last: the GEMM / copy probes of this box, next to the numbers above
+        extra("calibration", lambda: res.__setitem__("calibration", calibration(dev)))
     res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}{'_rms' if k[4] else ''}": f"ks{v[0]}_tile{v[1]}"
                                for k, v in autotune.ksplit_table().items()}
 
     # ---- tensor-parallel points: the BASELINE model of MP = world over every GPU of the job, under a watchdog
     if world > 1 and args.tp == 1 and args.tp_model and args.tp_batches and not failed["any"]:
-        del model
+        model = None
         torch.cuda.empty_cache()
         res["tp_points"] = _tp_points(args, ctx, res)
 
@@ -272,13 +284,34 @@ def _tp_rank_proxy(args):
            "fused_row_parallel": comm.fused is not None,
            "launches_per_layer_decode": 5 if comm.fused is not None else 7}
     try:
-        out["points"] = [decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=11)
+        out["points"] = [decode_latency(model, b, args.prompt_len, args.gen_len, seed=11)
                          for b in args.proxy_batches]
     finally:
         del model
         comm.close()
         torch.cuda.empty_cache()
     return out
+
+
+def _mp1_point(args):
+    """``--mp1-model`` (default Llama-3-70B, 141 GB of bf16 weights) on this one GPU: decode ms/token at
+    ``--mp1-batch`` over the full generation window, next to its HBM roofline."""
+    import torch
+
+    from jax_llama_amd.config import get_preset
+    from jax_llama_amd.models import LLaMAForCausalLM
+    from jax_llama_amd.runtime.benchmark import decode_latency
+
+    cfg = get_preset(args.mp1_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+    model = LLaMAForCausalLM(cfg, device="cuda", _do_init=False).init_random(seed=77)
+    try:
+        p = decode_latency(model, args.mp1_batch, args.prompt_len, args.gen_len, seed=12)
+        return {"model": args.mp1_model, "mp": 1, "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
+                "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
+                "point": p}
+    finally:
+        del model
+        torch.cuda.empty_cache()
 
 
 def _tp_points(args, ctx, res):
@@ -312,12 +345,13 @@ def _tp_points(args, ctx, res):
         comm = TPComm.from_context(ctx, fused_hidden=cfg.hidden_size)
         out["custom_allreduce"] = comm.custom is not None
         out["fused_row_parallel"] = comm.fused is not None
+        out["litmus"] = comm.litmus()  # the paths verified on these links before use (else RCCL carries them)
         model = LLaMAForCausalLM(cfg, device=ctx.device, comm=comm, _do_init=False).init_random(seed=4321)
         out["weight_gb_per_gpu"] = round(model.weight_bytes() / 1e9, 3)
         out["hbm_roofline_ms_per_token"] = round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4)
         pts = []
         for b in args.tp_batches:
-            p = decode_latency(model, b, args.prompt_len, args.gen_len, steps=64, seed=9, barrier=ctx.barrier)
+            p = decode_latency(model, b, args.prompt_len, args.gen_len, seed=9, barrier=ctx.barrier)
             p["decode_ms_per_token"] = ctx.all_reduce_max([p["decode_ms_per_token"]])[0]
             p["decode_tokens_per_sec"] = round(b * 1000.0 / p["decode_ms_per_token"], 2)
             pts.append(p)

@@ -332,9 +332,20 @@ SkWs check_sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& t
 
 // Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel;
 // tile 4 -> data-parallel whole waves + stream-K tail (ws/tickets from gemm_sk_workspace).
+// rms_ws: optional fp32 scratch (>= M floats) for the row statistic of the fused norm on gemm4 plans without a K
+// split (computed ahead of the GEMM by rms_rowinv); absent: the statistic is summed inside the main loop.
+static float* rms_ws_ptr(const c10::optional<Tensor>& rws, int64_t m, size_t* floats) {
+  *floats = 0;
+  if (!rws.has_value()) return nullptr;
+  check_gpu(*rws, "rms_ws");
+  check(rws->scalar_type() == torch::kFloat32 && rws->numel() >= m, "rms_ws: fp32, >= M floats");
+  *floats = rws->numel();
+  return ptr<float>(*rws);
+}
+
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate,
           c10::optional<Tensor> mirror, int64_t ksplit, c10::optional<Tensor> ws, double rms_eps, int64_t tile,
-          c10::optional<Tensor> tickets, c10::optional<Tensor> pack_out) {
+          c10::optional<Tensor> tickets, c10::optional<Tensor> pack_out, c10::optional<Tensor> rms_ws) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -392,10 +403,12 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
     return;
   }
   check_gemm_ws(ws, ksplit, m, n, rms_eps >= 0);
+  size_t rfl = 0;
+  float* rws = rms_ws_ptr(rms_ws, m, &rfl);
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
                out.scalar_type() == torch::kFloat32, mir, pqa.pack ? &pqa : nullptr,
                ksplit > 1 ? ptr<float>(*ws) : nullptr, ksplit > 1 ? ws->numel() : 0, ksplit, stream(),
-               (float)rms_eps, (int)tile),
+               (float)rms_eps, (int)tile, nullptr, 0, rws, rfl),
      "gemm");
 }
 
@@ -403,7 +416,8 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
 // applies the fused RMSNorm statistic, otherwise x must already be scaled).
 void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor positions, Tensor kc, Tensor vc,
               Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q, int64_t ksplit,
-              c10::optional<Tensor> ws, double rms_eps, int64_t tile, c10::optional<Tensor> tickets) {
+              c10::optional<Tensor> ws, double rms_eps, int64_t tile, c10::optional<Tensor> tickets,
+              c10::optional<Tensor> rms_ws) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -420,8 +434,10 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
   if (ksplit <= 1) {  // no K split: the GEMM's own RoPE / KV-write epilogue (default FA pipeline, fused norm)
     check(rms_eps >= 0 && jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k), "gemm_qkv without a K split: 256 x 256 FA "
           "tiles with the fused norm (gemm_qkv_direct_ok)");
+    size_t rfl = 0;
+    float* rws = rms_ws_ptr(rms_ws, m, &rfl);
     rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, nullptr, 0, 1, stream(),
-                 (float)rms_eps, (int)tile),
+                 (float)rms_eps, (int)tile, nullptr, 0, rws, rfl),
        "gemm_qkv");
     return;
   }
@@ -515,7 +531,8 @@ void argmax(Tensor logits, Tensor idx, Tensor val) {
 
 // Greedy lm_head: tiled GEMM (fused RMS when rms_eps >= 0) with the argmax in its epilogue; the fp32
 // logits are never written. ws: fp32 >= gemm_argmax_workspace(m, n) floats.
-void gemm_argmax(Tensor x, Tensor w, int64_t n, int64_t k, Tensor ws, double rms_eps, Tensor idx, Tensor val) {
+void gemm_argmax(Tensor x, Tensor w, int64_t n, int64_t k, Tensor ws, double rms_eps, Tensor idx, Tensor val,
+                 c10::optional<Tensor> rms_ws) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -528,8 +545,10 @@ void gemm_argmax(Tensor x, Tensor w, int64_t n, int64_t k, Tensor ws, double rms
   check(idx.scalar_type() == torch::kInt32 && val.scalar_type() == torch::kFloat32 && idx.numel() == m &&
             val.numel() == m,
         "gemm_argmax outputs");
+  size_t rfl = 0;
+  float* rws = rms_ws_ptr(rms_ws, m, &rfl);
   rc(jla::gemm_argmax(cbf(x), w.data_ptr(), ptr<float>(ws), ws.numel(), m, n, k, (float)rms_eps, ptr<int32_t>(idx),
-                      ptr<float>(val), stream()),
+                      ptr<float>(val), stream(), rws, rfl),
      "gemm_argmax");
 }
 
@@ -739,7 +758,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
         py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none(),
-        py::arg("pack_out") = py::none());
+        py::arg("pack_out") = py::none(), py::arg("rms_ws") = py::none());
   m.def("gemm_qkv_direct_ok", [](int64_t m, int64_t tile, int64_t k) {
     return jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k) != 0;
   });
@@ -762,9 +781,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm_qkv", &gemm_qkv, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("table"),
         py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"), py::arg("h"),
         py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("ksplit"), py::arg("ws"), py::arg("rms_eps") = -1.0,
-        py::arg("tile") = 0, py::arg("tickets") = py::none());
+        py::arg("tile") = 0, py::arg("tickets") = py::none(), py::arg("rms_ws") = py::none());
   m.def("gemm_argmax", &gemm_argmax, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("ws"),
-        py::arg("rms_eps"), py::arg("idx"), py::arg("val"));
+        py::arg("rms_eps"), py::arg("idx"), py::arg("val"), py::arg("rms_ws") = py::none());
   m.def("gemm_argmax_workspace", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_argmax_workspace_floats(m, n); });
   m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
   m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });

@@ -15,8 +15,21 @@
 //     stores the flag (relaxed, system scope = sc0 sc1 store);
 //   * consumer: one lane per peer polls its flag (relaxed system-scope load, bounded by a wall-clock
 //     timeout that raises the error word instead of hanging), __syncthreads, then the payload loads.
-//   No release/acquire fences: the L2 write-back a system-scope release needs is both slow and subject
-//   to a known compiler hazard (the vmcnt wait after buffer_wbl2 can be dropped).
+//   No release/acquire fences, and why none is needed (gfx950 memory model, peer-mapped memory):
+//   - a release fence exists to write back dirty cache lines before the flag becomes visible; here no handed-off
+//     byte is ever cached dirty: the buffers are uncached allocations and every hand-off store is sc0 sc1
+//     (system-scope write-through), so it leaves the CU's caches and the XCD L2 immediately;
+//   - s_waitcnt vmcnt(0) after the payload stores returns only once each store is acknowledged by the memory side
+//     it targets (for a peer's buffer: across xGMI), and the flag store is issued after that wait, on the same
+//     path -- so a peer that reads the flag's new value reads after the payload landed;
+//   - an acquire fence exists to invalidate stale cached copies before the payload loads; here every load of
+//     handed-off bytes is sc0 sc1 (system scope: it bypasses the non-coherent caches), so nothing stale is read;
+//   - the granule protocol (below) needs no ordering at all: data and tag travel in one 8-byte store.
+//   A fence would add the slow L2 write-back and the compiler hazard where the vmcnt wait after buffer_wbl2 is
+//   dropped (MI355X_MICROARCH.md). The argument is verified, not assumed, on every new set of links: before an
+//   instance is used, parallel/custom_allreduce.py self_test() runs rounds of every path (granule, flag one-shot,
+//   two-shot, pair gather, the GEMV-fused exchange) with rank-dependent data checked word by word on the host, and
+//   any mismatch moves every rank to RCCL.
 //
 // Block b of every rank handles chunks c == b (mod the instance grid, d.grid) of every message, so block b only ever
 // pairs with block b of its peers; barriers count per block and flags are monotonic. Every kernel maps

@@ -925,11 +925,14 @@ __global__ void __launch_bounds__(256 * WM)
 // n0 + wc*128 + 16j + 4q + 0..3 -- so SwiGLU gate/up pairs (adjacent n-tiles), RoPE pairs (adjacent columns) and
 // the fp32 residual (one float4) are all in-lane, and every store is 8 or 16 bytes. Split-K: MODE_PARTIAL slabs
 // [split][M][N] (+ the fused-RMS partial sums [split][M]) summed by gemm_reduce_kernel, as gemm2's.
-template <int MODE, bool RMS>
+// RMSM (fused RMSNorm statistic): 0 none; 1 summed inside the main loop from the x fragments (split-K partial
+// slabs: per-split sums to ssq_ws); 2 read from rms_inv[M], computed ahead of the GEMM by rms_rowinv_kernel.
+template <int MODE, int RMSM>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa) {
+                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv) {
+  constexpr bool RMS = RMSM == 1;
   __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];  // the two K-tile slots (the epilogue's staging), + 1 KiB of row scales
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -957,6 +960,10 @@ __global__ void __launch_bounds__(256, 1)
   const int c = lane & 15, q = lane >> 4, NTT = N >> 4;
   const int rbase = m0 + wr * 128 + c;  // + 16 i: this lane's output row in m-tile i
   float sc[8];                           // RMS: per m-tile row scale
+  if constexpr (RMSM == 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sc[i] = rms_inv[min(rbase + 16 * i, M - 1)];
+  }
   if constexpr (RMS) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // complete each row's sum over the 4 lanes holding its k-chunks
@@ -988,7 +995,7 @@ __global__ void __launch_bounds__(256, 1)
   // VGPRs at once (which spilled)
   auto tile_val = [&](int j, int i) -> f32x4 {
     f32x4 v = g4_take(acc[j][i]);
-    if constexpr (RMS && MODE != MODE_PARTIAL) v *= sc[i];
+    if constexpr (RMSM != 0 && MODE != MODE_PARTIAL) v *= sc[i];
     return v;
   };
 
@@ -1676,24 +1683,33 @@ static bool use_g4(int tile, int M, int K) {
 
 template <int MODE>
 static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                      bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa) {
+                      bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa,
+                      float* rms_ws = nullptr) {
   const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
   const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
-  if (rms)
-    gemm4_kernel<MODE, true><<<tm * tn * ksplit, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
-                                                               tn, rms_eps, ssq, qa);
-  else
-    gemm4_kernel<MODE, false><<<tm * tn * ksplit, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc,
-                                                                tm, tn, rms_eps, ssq, qa);
+  const int grid = tm * tn * ksplit;
+#define JLA_G4(R, INV)                                                                                        \
+  gemm4_kernel<MODE, R><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, \
+                                             ssq, qa, INV)
+  if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
+    if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;  // (K % 8 == 0 always holds here)
+    JLA_G4(2, rms_ws);
+  } else if (rms) {
+    JLA_G4(1, nullptr);
+  } else {
+    JLA_G4(0, nullptr);
+  }
+#undef JLA_G4
 }
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
-                      int grid_override = 0, G2Fix fix = G2Fix{}, const QKVArgs& qa = QKVArgs{}) {
+                      int grid_override = 0, G2Fix fix = G2Fix{}, const QKVArgs& qa = QKVArgs{},
+                      float* rms_ws = nullptr) {
   if (grid_override == 0 && fix.ksplit <= 1 && fix.tile_count == 0 && use_g4(tile, M, K)) {
-    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa);
+    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
     return;
   }
   const int cfg = tile_cfg(tile, M);
@@ -1754,10 +1770,11 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
 template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
                          int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile,
-                         hipStream_t s) {
+                         hipStream_t s, float* rms_ws = nullptr) {
 
   if (g_gemm_impl == 2) {
-    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s);
+    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s, 0, G2Fix{},
+                    QKVArgs{}, rms_ws);
   } else {
     dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
     gemm_kernel<MODE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc);
@@ -1858,7 +1875,8 @@ static int gemm_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps, int tile, int32_t* tickets, int n_tickets) {
+         float rms_eps, int tile, int32_t* tickets, int n_tickets, float* rms_ws, size_t rms_ws_floats) {
+  if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
@@ -1908,16 +1926,19 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (ksplit == 1) {
     switch (mode) {
       case MODE_QKV:
-        launch_g2<MODE_QKV>(x, w, nullptr, M, N, K, 0, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s, 0, G2Fix{}, *qkv);
+        launch_g2<MODE_QKV>(x, w, nullptr, M, N, K, 0, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s, 0, G2Fix{}, *qkv,
+                            rms_ws);
         break;
       case MODE_STORE:
-        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile, s);
+        launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile, s,
+                                 rms_ws);
         break;
       case MODE_RESIDUAL:
         launch_tiled<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, 1, -1.f, nullptr, tile, s);
         break;
       case MODE_SWIGLU:
-        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s);
+        launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s,
+                                  rms_ws);
         break;
       default: return -1;
     }
@@ -2057,7 +2078,8 @@ int argmax_partials(const float* part, int P, int M, int32_t* idx, float* val, h
 size_t gemm_argmax_workspace_floats(int M, int N) { return (size_t)M * ((N + G2_BN - 1) / G2_BN) * 4 * 2; }
 
 int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
-                int32_t* idx, float* val, hipStream_t s) {
+                int32_t* idx, float* val, hipStream_t s, float* rms_ws, size_t rms_ws_floats) {
+  if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (g_gemm_impl != 2) return -1;
@@ -2065,7 +2087,7 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   const int tm = (M + 255) / 256, tn = (N + G2_BN - 1) / G2_BN;
   const u32x4* w = static_cast<const u32x4*>(W);
   if (use_g4(0, M, K)) {  // 2 partials per 256-column tile (one per wave column)
-    launch_g4<MODE_ARGMAX>(x, w, ws, M, N, K, 0, 1, nullptr, 1, rms_eps, nullptr, s, QKVArgs{});
+    launch_g4<MODE_ARGMAX>(x, w, ws, M, N, K, 0, 1, nullptr, 1, rms_eps, nullptr, s, QKVArgs{}, rms_ws);
     JLA_CHECK_LAUNCH();
     launch_argmax_partials(reinterpret_cast<const float2*>(ws), tn * 2, M, idx, val, s);
     JLA_CHECK_LAUNCH();

@@ -13,6 +13,7 @@ int embedding(const int32_t* ids, const bf16_t* table, float* out, bf16_t* mirro
               hipStream_t s);
 int rms_scale(const float* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
 int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStream_t s);
+int rms_rowinv(const bf16_t* x, float* inv, int M, int D, float eps, hipStream_t s);  // inv[M] = 1/sqrt(mean(x^2)+eps)
 int residual_add(float* h, const void* p, int p_bf16, bf16_t* hb, long long n, hipStream_t s);
 int prefetch(const void* p, long long nbytes, int grid, unsigned* sink, hipStream_t s);
 int gemm_f32(const float* x, const float* w, float* y, int M, int N, int K, hipStream_t s);
@@ -73,7 +74,10 @@ size_t gemm_workspace_floats(int M, int N, int K);
 // once, self-resetting; MODE_QKV supported when every tile is in the tail)
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0);
+         float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0,
+         float* rms_ws = nullptr, size_t rms_ws_floats = 0);
+// rms_ws (>= M floats): with the fused norm, a gemm4 plan without a K split computes the row statistic ahead of
+// the GEMM into it (rms_rowinv) instead of inside its main loop; null: in-loop statistic
 // split-K with tickets (ksplit > 1, tile 0-3, not MODE_QKV): the in-kernel fixup (no reduce kernel) on
 // ws >= gemm_fix_workspace_floats(M, N, ksplit) slabs and >= gemm_fix_tiles(M, N) zero-initialised tickets
 size_t gemm_fix_workspace_floats(int M, int N, int ksplit);
@@ -85,7 +89,7 @@ void gemm_set_fixup(int on);  // A/B: 0 = partial slabs + reduce kernel even whe
 int gemm_fixup_enabled();
 // greedy lm_head: GEMM + first-max argmax epilogue (ws >= gemm_argmax_workspace_floats(M, N) floats)
 int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
-                int32_t* idx, float* val, hipStream_t s);
+                int32_t* idx, float* val, hipStream_t s, float* rms_ws = nullptr, size_t rms_ws_floats = 0);
 size_t gemm_argmax_workspace_floats(int M, int N);
 // first max per row over [M][P] (value, index) float2 partials
 int argmax_partials(const float* part, int P, int M, int32_t* idx, float* val, hipStream_t s);

@@ -103,6 +103,36 @@ __global__ void __launch_bounds__(256) rms_bf16_kernel(const bf16_t* __restrict_
   }
 }
 
+// inv[row] = 1 / sqrt(mean(x[row]^2) + eps) of bf16 rows (reference model.py:42-43), one wave per row, 4 rows per
+// block: the fused-RMSNorm statistic of a tiled GEMM computed ahead of it (gemm.hip gemm4, RMS mode 2), so the
+// GEMM's MFMA stream carries no sum-of-squares VALU work (that cost gemm4 ~10 %).
+__global__ void __launch_bounds__(256) rms_rowinv_kernel(const bf16_t* __restrict__ x, float* __restrict__ inv, int M,
+                                                         int D, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * D);
+  float s0 = 0.f, s1 = 0.f;
+  for (int i = lane; i < D / 8; i += 64) {
+    const u32x4 v = xr[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float lo = __uint_as_float(v[e] << 16), hi = __uint_as_float(v[e] & 0xffff0000u);
+      s0 = fmaf(lo, lo, s0);
+      s1 = fmaf(hi, hi, s1);
+    }
+  }
+  const float t = wave_sum(s0 + s1);
+  if (lane == 0) inv[row] = 1.f / sqrtf(t / (float)D + eps);
+}
+
+int rms_rowinv(const bf16_t* x, float* inv, int M, int D, float eps, hipStream_t s) {
+  if (D % 8) return -1;
+  if (M == 0) return 0;
+  rms_rowinv_kernel<<<(M + 3) / 4, 256, 0, s>>>(x, inv, M, D, eps);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStream_t s) {
   if (D % 8) return -1;
   if (M == 0) return 0;

@@ -360,6 +360,14 @@ def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
     return ks, tm, ws, None
 
 
+def _rms_ws(x, fused: bool, ks: int):
+    """fp32 [M] scratch for the row statistic of the fused norm, computed ahead of a gemm4 GEMM without a K split
+    (csrc/kernels/norm_embed.hip rms_rowinv; the main loop then carries no sum-of-squares work)."""
+    if not fused or ks > 1:
+        return None
+    return workspace.get("gemm_rms", x.shape[0], torch.float32, x.device)
+
+
 def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None, pack_out=None):
     """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups, or a stream-K tail,
     when the output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip). ``pack_out``: the split-K
@@ -368,7 +376,7 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None, pack
     xb = _tiled_input(x, rms_eps, fused)
     ks, tm, ws, tk = _gemm_ws(e, x.shape[0], n, k, x.device, mode, fused)
     e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk,
-           pack_out)
+           pack_out, _rms_ws(x, fused, ks))
 
 
 def _tiled_packs(e, m, n, k, device, mode, rms_eps) -> bool:
@@ -485,7 +493,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
             q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
             e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                        k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                       int(head_dim), q, 1, None, float(rms_eps), tm, None)
+                       int(head_dim), q, 1, None, float(rms_eps), tm, None, _rms_ws(x, fused, 1))
             return q
         if ks == 1 and tm != SK_TILE:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
             qkv = linear(x, w, rms_eps=rms_eps)
@@ -602,7 +610,8 @@ def linear_argmax(x: torch.Tensor, w, rms_eps: Optional[float] = None):
     ws = workspace.get("gemm_argmax", e.gemm_argmax_workspace(m, w.n), torch.float32, x.device)
     idx = torch.empty(m, dtype=torch.int32, device=x.device)
     val = torch.empty(m, dtype=torch.float32, device=x.device)
-    e.gemm_argmax(xb, w.weight, w.n, w.k, ws, -1.0 if rms_eps is None else float(rms_eps), idx, val)
+    e.gemm_argmax(xb, w.weight, w.n, w.k, ws, -1.0 if rms_eps is None else float(rms_eps), idx, val,
+                  _rms_ws(x, rms_eps is not None, 1))
     return idx, val
 
 

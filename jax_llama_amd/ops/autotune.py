@@ -358,6 +358,7 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     if fix_tk is None and hyb_floats:
         fix_tk = torch.zeros(e.gemm_fix_workspace(m, n, 2)[1], dtype=torch.int32, device=device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rms_ws = torch.empty(m, dtype=torch.float32, device=device)  # as ops._rms_ws: the statistic ahead of gemm4
 
     def run(c, tm, i):
         if tm == SK_TILE:
@@ -366,7 +367,7 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, ws, eps, tm, fix_tk)
         else:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm,
-                   fix_tk if c > 1 else None)
+                   fix_tk if c > 1 else None, None, rms_ws if c == 1 and eps > 0 else None)
 
     for c, tm in cands:  # warm every variant (code objects, caches) before any timing
         for i in range(2):

@@ -71,7 +71,7 @@ class TPComm:
                 if custom is not None and FUSED:
                     try:
                         fused = CustomAllReduce.create(ctx, max_bytes=CustomAllReduce.fused_bytes(
-                            fused_hidden or 16384), timeout_s=timeout_s)
+                            fused_hidden or 16384), timeout_s=timeout_s, kind="fused")
                     except CustomAllReduceError as ex:
                         import logging
                         logging.getLogger(__name__).warning("fused row-parallel all-reduce disabled: %s", ex)
@@ -180,6 +180,10 @@ class TPComm:
         return out.view((self.size,) + tuple(t.shape))
 
     # ------------------------------------------------------------------ failure detection
+    def litmus(self):
+        """Which collective paths passed the creation litmus on this group's links (None: no custom instance)."""
+        return {"collective": getattr(self.custom, "litmus", None), "fused": getattr(self.fused, "litmus", None)}
+
     def check(self):
         """Raise if a custom collective timed out waiting for a peer (bounded spins ->
         error). Called by the decode loop at its periodic host poll."""

@@ -56,6 +56,7 @@ class CustomAllReduce:
         # workgroups spin for their peers', so every rank's grid must fit on a shared device at once
         self.share = share
         self.failed = False  # set once a timeout was seen: the per-block counters are out of step for good
+        self.litmus = None  # verdict of self_test (create_for runs it)
 
     def _live(self) -> int:
         if self.failed:
@@ -65,13 +66,16 @@ class CustomAllReduce:
         return self.state
 
     @classmethod
-    def create(cls, ctx, max_bytes: int = 16 << 20, group=None, timeout_s: float = 10.0) -> "CustomAllReduce":
+    def create(cls, ctx, max_bytes: int = 16 << 20, group=None, timeout_s: float = 10.0,
+               kind: str = "collective") -> "CustomAllReduce":
         return cls.create_for(ctx.tp_rank, ctx.tp_size, ctx.tp_group if group is None else group, max_bytes,
-                              timeout_s)
+                              timeout_s, kind)
 
     @classmethod
     def create_for(cls, rank: int, world: int, group, max_bytes: int = 16 << 20,
-                   timeout_s: float = 10.0) -> "CustomAllReduce":
+                   timeout_s: float = 10.0, kind: str = "collective") -> "CustomAllReduce":
+        """``kind``: which litmus ``self_test`` runs before the instance is handed out (``collective``: the
+        standalone all-reduce / gather paths; ``fused``: the GEMV-fused row-parallel exchange)."""
         if world > 8:
             raise ValueError("custom all-reduce supports up to 8 ranks (one xGMI hop)")
         max_bytes = (max_bytes + CHUNK_BYTES - 1) // CHUNK_BYTES * CHUNK_BYTES  # whole kernel chunks
@@ -118,8 +122,13 @@ class CustomAllReduce:
             # keep 63 so every rank's blocks stay co-resident (they spin for each other). Same value on every rank,
             # set before the first call (the self-test): the chunk -> block map must never change under an instance.
             e.car_set_grid(state, 0)
-        # protocol self-test on the real links: a known sum, checked on the host by every rank
-        ok = car.self_test()
+        # protocol litmus on the real links: every path, rank-dependent data, every word checked on the host
+        try:
+            ok = car.self_test(kind)
+        except Exception as ex:  # noqa: BLE001 -- a failing path is a failed litmus, on every rank
+            import logging
+            logging.getLogger(__name__).warning("custom all-reduce litmus raised: %s", ex)
+            ok = False
         dist.all_gather_object(oks, ok, group=group)
         if not all(oks):
             car.close()
@@ -142,16 +151,84 @@ class CustomAllReduce:
         e.car_set_grid(state, int(os.environ.get("JLA_CAR_GRID", "0")))
         return cls(state, 0, 1, max_bytes)
 
-    def self_test(self) -> bool:
-        """One-shot and two-shot sums of rank-dependent data (bit-exact integers in fp32)."""
-        n = 64 * 1024
-        x = torch.arange(n, dtype=torch.float32, device="cuda") % 997 + 1000.0 * (self.rank + 1)
-        want = (torch.arange(n, dtype=torch.float32) % 997) * self.world + 1000.0 * self.world * (self.world + 1) / 2
+    LITMUS_ROUNDS = int(os.environ.get("JLA_CAR_LITMUS_ROUNDS", "8"))
+
+    @staticmethod
+    def _pattern(n: int, rank: int, rnd: int) -> torch.Tensor:
+        """Rank- and round-dependent integers in [1, 97]: exact in bf16 and fp32, and so are their sums over <= 8
+        ranks -- every rank can compute every peer's data and the exact expected result on the host."""
+        return ((torch.arange(n, dtype=torch.int64) * (2 * rnd + 1) + 31 * rank + rnd) % 97 + 1).to(torch.float32)
+
+    def self_test(self, kind: str = "collective", rounds=None) -> bool:
+        """Litmus test on the real links before the instance is declared usable (a wrong protocol on some fabric
+        must fall back to RCCL, not corrupt a generation): ``rounds`` rounds of every path with rank- and
+        round-dependent data, every word checked exactly on the host. ``collective``: granule one-shot (fp32 sum
+        and the bf16 residual epilogue), flag one-shot (> the granule limit), two-shot, and the (value, index) pair
+        gather; ``fused``: the GEMV-fused row-parallel exchange (gemv.hip MODE_TPRESID). The verdict and the paths
+        checked are kept in ``self.litmus``."""
+        rounds = self.LITMUS_ROUNDS if rounds is None else rounds
+        world, rank = self.world, self.rank
+        paths = []
         ok = True
-        for ts in (False, True):
-            got = self.all_reduce(x, two_shot=ts).cpu()
-            ok = ok and torch.equal(got, want)
-        return bool(ok and self.error() == 0)
+
+        def want_sum(n, rnd):
+            return sum(self._pattern(n, r, rnd) for r in range(world))
+
+        for rnd in range(rounds):
+            if kind == "fused":
+                from ..models.weights import PackedLinear
+                m, n, k = 4, 256, 256
+                if not self.can_fuse(m, n):
+                    break
+                # W_rank[n][k] = 1 where (n + k + rank) % 3 == rnd % 3: every partial is an exact bf16 integer
+                def wmat(r):
+                    nn = torch.arange(n)[:, None]
+                    kk = torch.arange(k)[None, :]
+                    return ((nn + kk + r) % 3 == rnd % 3).to(torch.bfloat16)
+                w = PackedLinear.from_dense(wmat(rank), "cuda")
+                x = torch.ones(m, k, dtype=torch.bfloat16, device="cuda")
+                h = (torch.arange(m * n, dtype=torch.float32) % 13).reshape(m, n).cuda()
+                hb = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+                want = (torch.arange(m * n, dtype=torch.float32) % 13).reshape(m, n) + sum(
+                    wmat(r).float().sum(1) for r in range(world))[None, :]
+                self.linear_residual_(x, w, h, hb)
+                ok = ok and torch.equal(h.cpu(), want) and torch.equal(hb.cpu(), want.to(torch.bfloat16))
+                paths = ["fused_gemv"]
+                continue
+            # granule one-shot (fp32 sum), flag one-shot (fp32, above the granule limit), two-shot (forced)
+            for name, n, ts in (("granule", 16 * 1024, False), ("flag", 192 * 1024, False), ("two_shot", 64 * 1024, True)):
+                if n * 4 > self.max_bytes:
+                    continue
+                got = self.all_reduce(self._pattern(n, rank, rnd).cuda(), two_shot=ts).cpu()
+                ok = ok and torch.equal(got, want_sum(n, rnd))
+                if rnd == 0:
+                    paths.append(name)
+            # the residual epilogue with bf16 partials, on the granule and on the flag path
+            for name, n in (("granule_resid_bf16", 8 * 1024), ("flag_resid_bf16", 256 * 1024)):
+                if n * 2 > self.max_bytes:
+                    continue
+                h0 = (torch.arange(n, dtype=torch.float32) % 13)
+                h = h0.cuda()
+                hb = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+                self.all_reduce_residual_(self._pattern(n, rank, rnd).to(torch.bfloat16).cuda(), h, hb)
+                want = h0 + want_sum(n, rnd)
+                ok = ok and torch.equal(h.cpu(), want) and torch.equal(hb.cpu(), want.to(torch.bfloat16))
+                if rnd == 0:
+                    paths.append(name)
+            # (value, index) pairs: the first max over ranks, rank order breaking ties
+            b = 256
+            vals = [((torch.arange(b) * 7 + 3 * r + rnd) % 11).to(torch.float32) for r in range(world)]
+            got = self.argmax_pairs(vals[rank].cuda(), torch.arange(b, dtype=torch.int32, device="cuda"),
+                                    rank * b).cpu()
+            stacked = torch.stack(vals)  # [world, b]
+            best = stacked.argmax(0)  # first max in rank order
+            ok = ok and torch.equal(got, (best * b + torch.arange(b)).to(torch.int32))
+            if rnd == 0:
+                paths.append("pairs")
+        torch.cuda.synchronize()
+        ok = bool(ok and self.error() == 0)
+        self.litmus = {"kind": kind, "rounds": rounds, "paths": paths, "ok": ok}
+        return ok
 
     # ------------------------------------------------------------------ capability checks
     def can_handle(self, t: torch.Tensor) -> bool:

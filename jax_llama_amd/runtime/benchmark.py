@@ -18,13 +18,16 @@ def synthetic_prompts(vocab: int, batch: int, prompt_len: int, seed: int) -> tor
     return torch.randint(3, vocab, (batch, prompt_len), generator=g, dtype=torch.int32)
 
 
-def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256, steps: int = 64,
+def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256, steps: Optional[int] = None,
                    seed: int = 0, barrier=None, do_sample: bool = False) -> Dict[str, float]:
     """Prefill ``batch`` prompts into a ``prompt_len + gen_len`` cache (``prefill_ms``: the second, warm prefill; the
-    first autotunes), then time ``steps`` replays of
-    the captured decode step (every layer, lm_head, sampler, state update). Every rank of a TP group
-    must call this with the same arguments (the step contains the TP collectives)."""
-    assert steps + 2 < gen_len, "replays must stay inside the cache"
+    first autotunes), capture the decode step (every layer, lm_head, sampler, state update), prefill again, then time
+    ``steps`` replays of it -- by default every step of a ``gen_len``-token generation (``gen_len - 1`` replays after
+    the prefill's first token, cache length from ``prompt_len + 1`` up), so attention is weighted as in a real
+    generation (``kv_len_mean`` reports the mean cache length the steps covered; reference generation.py:35:
+    max_length = S + max_gen_len). Every rank of a TP group must call this with the same arguments."""
+    steps = gen_len - 1 if steps is None else steps
+    assert 1 <= steps <= gen_len - 1, "replays must stay inside the cache"
     max_len = prompt_len + gen_len
     eng = DecodeEngine(model, batch, max_len, use_graph=True)
     gc = GenerationConfig(max_length=max_len, do_sample=do_sample, temperature=0.8, top_p=0.95, top_k=50,
@@ -44,6 +47,8 @@ def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256,
     eng._graph.replay()
     torch.cuda.synchronize(dev)
     ttft_ms = ev0.elapsed_time(ev1)
+    eng.prefill(prompts, None)  # back to the first decode position: the timed replays cover the whole window
+    torch.cuda.synchronize(dev)
     if barrier is not None:
         barrier()
     ev0.record()
@@ -55,7 +60,8 @@ def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256,
     model.comm.check()
     del eng
     return {"batch": batch, "decode_ms_per_token": round(ms, 4),
-            "decode_tokens_per_sec": round(batch * 1000.0 / ms, 2), "prefill_ms": round(ttft_ms, 3)}
+            "decode_tokens_per_sec": round(batch * 1000.0 / ms, 2), "prefill_ms": round(ttft_ms, 3),
+            "steps": steps, "kv_len_mean": round(prompt_len + 1 + (steps - 1) / 2, 1)}
 
 
 def time_to_first_token(model, batch: int, prompt_len: int, reps: int = 3, seed: int = 0,
@@ -103,3 +109,55 @@ def generate_tokens_per_sec(model, batch: int, prompt_len: int, gen_len: int, gc
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
     return {"batch": batch, "ms_per_generate": round(1000 * dt, 2), "tokens_per_sec": round(batch * gen_len / dt, 2)}
+
+
+def calibration(device) -> Dict[str, object]:
+    """Fixed-work probes that tell a slower box from a kernel regression (bench.py ``calibration``): bf16 GEMM
+    TFLOP/s of one fixed 8192^3 shape on this framework's tiled GEMM and on the vendor library (torch.mm ->
+    hipBLASLt), HBM copy TB/s (read + write bytes), and the current shader clock level if sysfs exposes it."""
+    import glob
+
+    from .. import ops
+    from ..models.weights import PackedLinear
+    out: Dict[str, object] = {}
+    n = 8192
+    g = torch.Generator(device=device).manual_seed(1)
+    x = torch.randn(n, n, device=device, generator=g).to(torch.bfloat16)
+    w = (torch.randn(n, n, device=device, generator=g) * 0.02).to(torch.bfloat16)
+    pw = PackedLinear.from_dense(w, device)
+    y = torch.empty(n, n, device=device, dtype=torch.bfloat16)
+    e = ops.ext()
+
+    def timed(fn, iters):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(device)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(iters):
+            fn()
+        ev1.record()
+        torch.cuda.synchronize(device)
+        return ev0.elapsed_time(ev1) / iters
+
+    flop = 2.0 * n * n * n
+    ms = timed(lambda: e.gemm(x, pw.weight, n, n, y, ops.MODE_STORE, False, None, 1, None, -1.0, 0), 10)
+    out["gemm_8192_tflops"] = round(flop / ms / 1e9, 1)
+    ms = timed(lambda: torch.mm(x, w.t(), out=y), 10)
+    out["hipblaslt_8192_tflops"] = round(flop / ms / 1e9, 1)
+    del x, w, pw, y
+    src = torch.empty(1 << 29, dtype=torch.float32, device=device).fill_(1.0)  # 2 GiB
+    dst = torch.empty_like(src)
+    ms = timed(lambda: dst.copy_(src), 5)
+    out["copy_tbps"] = round(2 * src.numel() * 4 / ms / 1e9, 2)
+    del src, dst
+    torch.cuda.empty_cache()
+    try:
+        for f in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
+            cur = [ln.strip() for ln in open(f) if ln.strip().endswith("*")]
+            if cur:
+                out["sclk"] = cur[0]
+                break
+    except OSError:
+        pass
+    return out

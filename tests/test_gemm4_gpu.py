@@ -25,15 +25,17 @@ def _close(a, b, rtol, atol):
     assert err <= atol + rtol * scale, f"max err {err:.3e} (ref max {scale:.3e})"
 
 
-def _run_all(e, xg, pg, gp, h0, n, k, ks, ws, tile):
+def _run_all(e, xg, pg, gp, h0, n, k, ks, ws, tile, rms_ws=None):
+    """rms_ws: the fused norm's row statistic computed ahead of the GEMM (gemm4 without a K split)."""
     outs = []
     for eps in (-1.0, 1e-5):
+        rw = rms_ws if eps > 0 else None
         o = torch.empty(xg.shape[0], n, dtype=torch.float32, device=DEV)
-        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile)
+        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, rw)
         ob = torch.empty(xg.shape[0], n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, rw)
         o2 = torch.empty(xg.shape[0], n // 2, dtype=BF16, device=DEV)
-        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile)
+        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile, None, None, rw)
         outs += [o, ob, o2]
     hg, mir = h0.clone(), torch.empty(h0.shape, dtype=BF16, device=DEV)
     e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, tile)
@@ -72,6 +74,14 @@ def test_gemm4_every_epilogue(m, n, k, ks):
     torch.testing.assert_close(g4[7].cpu(), g4[6].cpu().to(BF16), rtol=0, atol=0)
     exact = [torch.equal(a, b) for a, b in zip(g4, g2)]
     print("bit-identical to gemm2:", exact)
+    if ks == 1:  # the row statistic computed ahead of the GEMM (rms_rowinv): fp32-reference close, near the in-loop one
+        pre = _run_all(e, xg, pg, gp, h0, n, k, ks, ws, G4, torch.empty(m, device=DEV))
+        for i in (0, 1, 2, 6, 7):  # no norm: the same kernel
+            assert torch.equal(pre[i], g4[i]), i
+        _close(pre[3], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+        _close(pre[5], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
+        for i in (3, 4, 5):
+            _close(pre[i], g4[i], 1e-2, 1e-3)
 
 
 @pytest.mark.parametrize("m,s,n_heads", [(512, 512, 8), (256, 1, 32), (300, 3, 8)])
@@ -97,7 +107,8 @@ def test_gemm4_qkv_rope_epilogue(m, s, n_heads):
         kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
         qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
         e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
-                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile, None)
+                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile, None,
+                   torch.empty(m, device=DEV) if tile == G4 else None)
         outs[tile] = (qg.cpu(), kg.cpu(), vg.cpu())
     qg, kg, vg = outs[G4]
     _close(qg, q, 2e-2, 2e-2)
@@ -133,6 +144,13 @@ def test_gemm4_argmax(m, n, k):
             torch.cuda.synchronize()
             assert torch.equal(i0.cpu(), i1.cpu()), (eps, (i0 != i1).nonzero()[:8])
             assert torch.equal(v0.cpu(), v1.cpu())
+            if eps > 0:  # the precomputed statistic: same as the stored-logits path with the same statistic
+                rw = torch.empty(m, device=DEV)
+                e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, G4, None, None, rw)
+                e.argmax(logits, i0, v0)
+                e.gemm_argmax(xg, pg.weight, n, k, ws, eps, i1, v1, rw)
+                torch.cuda.synchronize()
+                assert torch.equal(i0.cpu(), i1.cpu()) and torch.equal(v0.cpu(), v1.cpu())
     finally:
         e.gemm_set_g4_default(0)
 

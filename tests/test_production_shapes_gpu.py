@@ -79,3 +79,29 @@ def test_bench_regime_greedy_matches_small_batch(llama3_8b_2l):
     assert gap_small < 1e-2, (gap_small, agree)
     assert agree > 0.5, agree
     assert int(big.min()) >= 0 and int(big.max()) < cfg.vocab_size
+
+
+@pytest.mark.timeout(600)
+def test_headline_regime_b2048_prompt128(llama3_8b_2l):
+    """The exact benchmarked regime (bench.py: B = 2048, 128-token prompts): the M = 262,144-row prefill plans
+    (tile-0 GEMMs, flash prefill) and the B = 2048 decode plans (tuned tiled GEMMs, v4 attention, the fused-argmax
+    lm_head), 32 generated tokens; 8 spread rows against the same rows run at B = 8, both judged by the fp32
+    oracle's teacher-forced argmax gap (reference jax_test.py:427-490, 492-522)."""
+    from jax_llama_amd.runtime.benchmark import synthetic_prompts
+    from jax_llama_amd.runtime.engine import GenerationConfig
+    cfg, model, oracle = llama3_8b_2l
+    b, s, gen = 2048, 128, 32
+    prompts = synthetic_prompts(cfg.vocab_size, b, s, seed=21)
+    gc = GenerationConfig(max_length=s + gen, do_sample=False, pad_token_id=0, eos_token_id=-1)
+    big = model.generate(prompts, generation_config=gc).sequences.cpu()
+    torch.cuda.empty_cache()
+    rows = [0, 1, 255, 256, 1023, 1024, 2000, 2047]
+    small = model.generate(prompts[rows], generation_config=gc).sequences.cpu()
+    ones = torch.ones(len(rows), s, dtype=torch.int32)
+    gap_big = argmax_gap(oracle, big[rows], ones, s)
+    gap_small = argmax_gap(oracle, small, ones, s)
+    agree = (big[rows][:, s:] == small[:, s:]).float().mean().item()
+    assert gap_big < 1e-2, (gap_big, agree)
+    assert gap_small < 1e-2, (gap_small, agree)
+    assert agree > 0.5, agree
+    assert int(big.min()) >= 0 and int(big.max()) < cfg.vocab_size

@@ -50,7 +50,14 @@ def main():
                     "1 in-kernel fixup (tickets); tile 6 always uses the fixup")
     ap.add_argument("--tile", type=int, nargs="+", default=[0], help="gemm2 tile config(s): 0 auto, 1 256x256, "
                     "2 128x256, 3 128x128")
+    ap.add_argument("--mode", default="store", choices=["store", "swiglu", "residual"],
+                    help="epilogue (the model's: qkv/lm_head store, gate_up swiglu, o/down residual)")
+    ap.add_argument("--rms", action="store_true", help="fused RMSNorm statistic (store / swiglu)")
+    ap.add_argument("--data", default="normal", choices=["normal", "uniform"],
+                    help="operand distribution (uniform: as tools/debug/gemm4w_probe.hip)")
     args = ap.parse_args()
+    mode = {"store": 0, "residual": 1, "swiglu": 2}[args.mode]
+    eps = 1e-5 if args.rms and mode != 1 else -1.0
     cfg = get_preset(args.model)
     d, f, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
     h, hkv = cfg.num_attention_heads, cfg.num_key_value_heads
@@ -62,11 +69,22 @@ def main():
             continue
         nbytes = n * k * 2
         copies = max(2, int((700 << 20) // nbytes) + 1)
-        dense = [(torch.randn(n, k, device=DEV) * 0.02).to(torch.bfloat16) for _ in range(copies)]
+        if args.data == "uniform":
+            dense = [((torch.rand(n, k, device=DEV) * 2 - 1) * 0.05).to(torch.bfloat16) for _ in range(copies)]
+        else:
+            dense = [(torch.randn(n, k, device=DEV) * 0.02).to(torch.bfloat16) for _ in range(copies)]
         packed = [PackedLinear.from_dense(w, DEV) for w in dense]
         for m in args.m:
-            x = (torch.randn(m, k, device=DEV)).to(torch.bfloat16)
+            if args.data == "uniform":
+                x = (torch.rand(m, k, device=DEV) * 2 - 1).to(torch.bfloat16)
+            else:
+                x = (torch.randn(m, k, device=DEV)).to(torch.bfloat16)
             out = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+            if mode == 1:
+                out = torch.zeros(m, n, device=DEV, dtype=torch.float32)
+                mir = torch.empty(m, n, device=DEV, dtype=torch.bfloat16)
+            elif mode == 2:
+                out = torch.empty(m, n // 2, device=DEV, dtype=torch.bfloat16)
             flop = 2.0 * m * n * k
             iters = max(5, min(200, int(2e13 / flop)))
             res = {}
@@ -101,22 +119,29 @@ def main():
 
                       tcfg = tile
 
-                      def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk):
-                          e.gemm(x, packed[i % copies].weight, n, k, out, 0, True, None, kk,
-                                 ws if (kk > 1 or tile in (4, 6)) else None, -1.0, tile, tk)
+                      rws = torch.empty(m, device=DEV) if (eps > 0 and kk == 1) else None
+
+                      def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
+                          e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
+                                 ws if (kk > 1 or tile in (4, 6)) else None, eps, tile, tk, None, rws)
                       res[f"v{impl}_ks{kk}_t{tile}" + ("_fix" if fx and kk > 1 else "") +
                           (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                       run(0)
+                      if mode != 0:  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
+                          continue
                       got = out.float()
                       if ref is None:
-                          ref = (x.float() @ dense[0].float().t())
+                          xs = x.float()
+                          if eps > 0:
+                              xs = xs * torch.rsqrt(xs.pow(2).mean(-1, keepdim=True) + eps)
+                          ref = (xs @ dense[0].float().t())
                       err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
                       assert err < 2e-2 or (tile >= 50 and (tile - 50) & 14), (name, m, impl, kk, err)
                       if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
                           f0 = first.setdefault((kk, tile), got.clone())
                           assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
             e.gemm_set_impl(2)
-            if not args.no_blas:
+            if not args.no_blas and mode == 0:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)
             for impl, us in res.items():
                 print(json.dumps({"op": name, "m": m, "n": n, "k": k, "impl": impl, "us": round(us, 2),

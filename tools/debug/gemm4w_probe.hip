@@ -12,6 +12,7 @@
 
 using namespace jla;
 
+template <bool RDF, bool DMF, int RMSV = 0, int ABL = 0>
 __global__ void __launch_bounds__(256, 1) gemm4_store_kernel(G4Args g) {
   __shared__ u32x4 lds[2 * G4_SLOT_U4];
   const int lane = threadIdx.x & 63;
@@ -30,9 +31,63 @@ __global__ void __launch_bounds__(256, 1) gemm4_store_kernel(G4Args g) {
   for (int j = 0; j < 8; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  g4_mainloop(g, lds, m0, n0, t0, KT, wu, lane, acc);
+  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+  g4_mainloop<RMSV != 0, RDF, DMF, RMSV == 0 ? 1 : RMSV, ABL>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+  if constexpr (RMSV != 0) {  // keep the statistic live (the probe stores no scaled output)
+    if (ss[0] + ss[1] + ss[2] + ss[3] == 12345.f) acc[0][0][0] += 1.f;
+  }
   __syncthreads();
   g4_store_bf16(acc, lds, static_cast<bf16_t*>(g.out), g.M, g.N, m0, n0, wu, lane);
+}
+
+__global__ void __launch_bounds__(256, 1) gemm4_ring_kernel(G4Args g) {
+  __shared__ u32x4 lds[G4R_LDS_U4];
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int split = wgid / tiles, pid = wgid - split * tiles;
+  int tm, tn;
+  g4_tile_coords(pid, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int t0 = split * g.kc, KT = min(g.K >> 6, t0 + g.kc) - t0;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  g4_mainloop_ring(g, lds, m0, n0, t0, KT, wu, lane, acc);
+  wait_vmcnt<0>();  // the clamped tail DMAs have landed before the staging reuses LDS
+  __syncthreads();
+  g4_store_bf16(acc, lds, static_cast<bf16_t*>(g.out), g.M, g.N, m0, n0, wu, lane);
+}
+
+template <int ABL>
+__global__ void __launch_bounds__(256, 1) gemm4_32_kernel(G4Args g) {
+  __shared__ u32x4 lds[2 * G4_SLOT_U4];
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = g.tiles_m * g.tiles_n;
+  const int split = wgid / tiles, pid = wgid - split * tiles;
+  int tm, tn;
+  g4_tile_coords(pid, g.tiles_m, g.tiles_n, tm, tn);
+  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int t0 = split * g.kc, KT = min(g.K >> 6, t0 + g.kc) - t0;
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.f;
+  g4_mainloop32<ABL>(g, lds, m0, n0, t0, KT, wu, lane, acc);
+  __syncthreads();
+  g4_store32_bf16(acc, lds, static_cast<bf16_t*>(g.out), g.M, g.N, m0, n0, wu, lane);
 }
 
 __device__ inline unsigned hash32(unsigned x) {
@@ -70,6 +125,7 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 2048, N = argc > 2 ? atoi(argv[2]) : 28672,
             K = argc > 3 ? atoi(argv[3]) : 4096, iters = argc > 4 ? atoi(argv[4]) : 20;
   const int ksplit = argc > 5 ? atoi(argv[5]) : 1;
+  const int var = argc > 6 ? atoi(argv[6]) : 0;  // bit 0: reads front-loaded, bit 1: DMAs front-loaded
   if (N % 16 || K % 64) {
     fprintf(stderr, "shape\n");
     return 2;
@@ -88,12 +144,26 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   const int tm = (M + 255) / 256, tn = (N + 255) / 256;
   const int KT64 = K / 64, kc = (KT64 + ksplit - 1) / ksplit;
-  auto launch = [&](int c) {
+  auto launch = [&](int c, int var) {
     G4Args g{x, reinterpret_cast<const u32x4*>(w[c]), out, M, N, K, kc, tm, tn};
-    gemm4_store_kernel<<<tm * tn * ksplit, 256>>>(g);
+    const int grid = tm * tn * ksplit;
+    if (var == 0) gemm4_store_kernel<false, false><<<grid, 256>>>(g);
+    if (var == 1) gemm4_store_kernel<true, false><<<grid, 256>>>(g);
+    if (var == 2) gemm4_store_kernel<false, true><<<grid, 256>>>(g);
+    if (var == 3) gemm4_store_kernel<true, true><<<grid, 256>>>(g);
+    if (var == 4) gemm4_store_kernel<false, false, 1><<<grid, 256>>>(g);
+    if (var == 5) gemm4_store_kernel<false, false, 2><<<grid, 256>>>(g);
+    if (var == 6) gemm4_32_kernel<0><<<grid, 256>>>(g);  // 32x32x16 MFMAs
+    if (var == 14) gemm4_ring_kernel<<<grid, 256>>>(g);   // deeper LDS ring
+    if (var == 7) gemm4_32_kernel<3><<<grid, 256>>>(g);  // 32x32x16, no DMA / reads (wrong results)
+    if (var == 8 + 1) gemm4_store_kernel<false, false, 0, 1><<<grid, 256>>>(g);  // ablations (wrong results)
+    if (var == 8 + 2) gemm4_store_kernel<false, false, 0, 2><<<grid, 256>>>(g);
+    if (var == 8 + 3) gemm4_store_kernel<false, false, 0, 3><<<grid, 256>>>(g);
+    if (var == 8 + 4) gemm4_store_kernel<false, false, 0, 4><<<grid, 256>>>(g);
+    if (var == 8 + 5) gemm4_store_kernel<false, false, 0, 5><<<grid, 256>>>(g);
   };
   // correctness (first rows; ksplit must be 1 for a meaningful check)
-  launch(0);
+  launch(0, var < 0 ? 0 : var);  // (the check runs variant 0, or the one asked for)
   CK(hipDeviceSynchronize());
   const int rows = std::min(M, 512);
   float* ref;
@@ -110,20 +180,36 @@ int main(int argc, char** argv) {
     maxerr = std::max(maxerr, (double)fabsf(g - hr[i]));
     maxref = std::max(maxref, (double)fabsf(hr[i]));
   }
-  // timing
-  for (int i = 0; i < 3; ++i) launch(i % copies);
+  // timing: variants (var < 0: all four) interleaved over rounds in this one process, min per variant
+  // var -1: schedule variants 0-3; -2: fused-RMS statistic variants 0 (none), 4 (v_dot2), 5 (fp32 FMAs)
+  // -3: ablations 9 (no DMA), 10 (no reads), 11 (neither), 12 (no mid barrier), 13 (no DMA, no barrier)
+  const std::vector<int> vl = var == -1 ? std::vector<int>{0, 1, 2, 3}
+                              : var == -2 ? std::vector<int>{0, 4, 5}
+                              : var == -3 ? std::vector<int>{0, 9, 10, 11, 12, 13}
+                              : var == -4 ? std::vector<int>{0, 6, 7, 11}
+                              : var == -5 ? std::vector<int>{0, 1, 14} : std::vector<int>{var};
+  const int nv = (int)vl.size(), rounds = var < 0 ? 3 : 1;
+  std::vector<double> best(16, 1e30);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  CK(hipEventRecord(e0));
-  for (int i = 0; i < iters; ++i) launch(i % copies);
-  CK(hipEventRecord(e1));
-  CK(hipEventSynchronize(e1));
-  float ms = 0;
-  CK(hipEventElapsedTime(&ms, e0, e1));
-  const double us = ms * 1000.0 / iters;
-  printf("{\"kernel\": \"gemm4w\", \"m\": %d, \"n\": %d, \"k\": %d, \"ksplit\": %d, \"us\": %.2f, \"tflops\": %.1f, "
-         "\"rel_err\": %.2e}\n",
-         M, N, K, ksplit, us, 2.0 * M * N * K / us / 1e6, maxerr / std::max(maxref, 1e-6));
+  for (int rd = 0; rd < rounds; ++rd)
+    for (int vi = 0; vi < nv; ++vi) {
+      const int v = vl[vi];
+      for (int i = 0; i < 3; ++i) launch(i % copies, v);
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < iters; ++i) launch(i % copies, v);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best[v] = std::min(best[v], ms * 1000.0 / iters);
+    }
+  for (int v = 0; v < 16; ++v) {
+    if (best[v] > 1e29) continue;
+    printf("{\"kernel\": \"gemm4w\", \"var\": %d, \"m\": %d, \"n\": %d, \"k\": %d, \"ksplit\": %d, \"us\": %.2f, "
+           "\"tflops\": %.1f, \"rel_err\": %.2e}\n",
+           v, M, N, K, ksplit, best[v], 2.0 * M * N * K / best[v] / 1e6, maxerr / std::max(maxref, 1e-6));
+  }
   return 0;
 }

@@ -236,6 +236,7 @@ def main():
         extra("calibration", lambda: res.__setitem__("calibration", calibration(dev)))
     res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}{'_rms' if k[4] else ''}": f"ks{v[0]}_tile{v[1]}"
                                for k, v in autotune.ksplit_table().items()}
+    res["gemv_variant_choice"] = autotune.variant_table()
 
     # ---- tensor-parallel points: the BASELINE model of MP = world over every GPU of the job, under a watchdog
     if world > 1 and args.tp == 1 and args.tp_model and args.tp_batches and not failed["any"]:

@@ -763,6 +763,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
     return jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k) != 0;
   });
   m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
+  m.def("gemm_set_g4_ring", [](int64_t on) { jla::gemm_set_g4_ring((int)on); });
   m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
     return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
   }, "(slab floats, tickets) of the in-kernel split-K fixup");

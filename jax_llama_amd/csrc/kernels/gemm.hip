@@ -927,13 +927,16 @@ __global__ void __launch_bounds__(256 * WM)
 // [split][M][N] (+ the fused-RMS partial sums [split][M]) summed by gemm_reduce_kernel, as gemm2's.
 // RMSM (fused RMSNorm statistic): 0 none; 1 summed inside the main loop from the x fragments (split-K partial
 // slabs: per-split sums to ssq_ws); 2 read from rms_inv[M], computed ahead of the GEMM by rms_rowinv_kernel.
-template <int MODE, int RMSM>
+// RING: the main loop of g4_mainloop_ring (3-slot x ring + 4-slot W ring, all 160 KiB of LDS) instead of the
+// two 64 KiB K-tile slots of g4_mainloop.
+template <int MODE, int RMSM, bool RING>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
                  float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv) {
   constexpr bool RMS = RMSM == 1;
-  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];  // the two K-tile slots (the epilogue's staging), + 1 KiB of row scales
+  // the K-tile slots / rings; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
+  __shared__ u32x4 lds[RING ? G4R_LDS_U4 : 2 * G4_SLOT_U4 + 64];
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wu >> 1, wc = wu & 1;
@@ -955,7 +958,12 @@ __global__ void __launch_bounds__(256, 1)
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss[4] = {0.f, 0.f, 0.f, 0.f};
   const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
-  g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+  if constexpr (RING) {
+    g4_mainloop_ring<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+    wait_vmcnt<0>();  // the ring's clamped tail DMAs land before LDS is reused
+  } else {
+    g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+  }
 
   const int c = lane & 15, q = lane >> 4, NTT = N >> 4;
   const int rbase = m0 + wr * 128 + c;  // + 16 i: this lane's output row in m-tile i
@@ -979,7 +987,7 @@ __global__ void __launch_bounds__(256, 1)
         }
       }
     } else {
-      float* rs = reinterpret_cast<float*>(lds + 2 * G4_SLOT_U4);  // beside the staging space
+      float* rs = reinterpret_cast<float*>(lds + 8192);  // beside the 128 KiB staging space
       __syncthreads();  // every wave is past its last fragment read
       if (q == 0) {
         const float fk = (float)K;  // (t / K exactly as gemm_reduce_kernel and gemm2)
@@ -1677,6 +1685,8 @@ int gemm_qkv_direct_ok(int M, int tile, int K) {
 constexpr int G4_TILE = 7;
 static bool g_g4_default = true;
 void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
+static bool g_g4_ring = false;  // gemm4 main loop: the deeper LDS ring (gemm4w.h g4_mainloop_ring)
+void gemm_set_g4_ring(int on) { g_g4_ring = on != 0; }
 static bool use_g4(int tile, int M, int K) {
   return g_gemm_impl == 2 && (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
 }
@@ -1689,9 +1699,15 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   const int grid = tm * tn * ksplit;
-#define JLA_G4(R, INV)                                                                                        \
-  gemm4_kernel<MODE, R><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, \
-                                             ssq, qa, INV)
+#define JLA_G4(R, INV)                                                                                          \
+  do {                                                                                                            \
+    if (g_g4_ring)                                                                                                \
+      gemm4_kernel<MODE, R, true><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, \
+                                                       rms_eps, ssq, qa, INV);                                   \
+    else                                                                                                          \
+      gemm4_kernel<MODE, R, false><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,    \
+                                                        tn, rms_eps, ssq, qa, INV);                              \
+  } while (0)
   if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
     if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;  // (K % 8 == 0 always holds here)
     JLA_G4(2, rms_ws);

@@ -56,25 +56,3 @@ class KVCache:
             }
             for i in range(self.k.shape[0])
         }
-
-
-class KVRows:
-    """Rows [b0, b1) of a KVCache (views: per layer ``[b1 - b0, Hkv, T, Dh]`` contiguous runs), sharing its slot
-    counter -- one decode micro-batch of the engine."""
-
-    def __init__(self, cache: KVCache, b0: int, b1: int):
-        self.cache, self.b0, self.b1 = cache, b0, b1
-        self.batch_size = b1 - b0
-        self.max_length = cache.max_length
-        self.index_t = cache.index_t
-
-    @property
-    def index(self):
-        return self.cache.index
-
-    @property
-    def device(self):
-        return self.cache.device
-
-    def layer(self, i: int):
-        return self.cache.k[i, self.b0:self.b1], self.cache.v[i, self.b0:self.b1]

@@ -394,3 +394,10 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
 
 def ksplit_table() -> Dict[Tuple, int]:
     return dict(_KS_CACHE)
+
+
+def variant_table() -> Dict[str, int]:
+    """The decode-kernel variant picked per (M bucket, N, K, mode, ...) shape so far (bench.py reports it: which
+    variants production shapes actually use)."""
+    return {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}" + ("_xp" if k[5] else "") + ("_pack" if k[6] else "") +
+            ("_nosplit" if k[7] else "") + ("_tp" if k[9] else ""): v for k, v in _CACHE.items()}

@@ -55,12 +55,6 @@ class GenerationConfig:
 
 # greedy decoding takes the argmax inside the lm_head GEMM epilogue (JLA_FUSED_ARGMAX=0: logits + argmax)
 FUSED_GREEDY = os.environ.get("JLA_FUSED_ARGMAX", "1") != "0"
-# Decode micro-batches (TP = 1, batch >= MICROBATCH_MIN_ROWS): the step's rows are split in two halves whose layer
-# chains run on two streams of the captured graph (one fork, one join per step), so one half's memory-bound decode
-# attention can run beside the other half's compute-bound GEMMs. Opt-in (JLA_MICROBATCH=2): measured 3.7 % slower at
-# B = 2048 (profiles/r3_decode_microbatch_ab.jsonl).
-MICROBATCH = int(os.environ.get("JLA_MICROBATCH", "1"))
-MICROBATCH_MIN_ROWS = int(os.environ.get("JLA_MICROBATCH_MIN_ROWS", "512"))
 
 
 def _fused_greedy() -> bool:
@@ -184,43 +178,10 @@ class DecodeEngine:
     def _logits_mode(self) -> str:
         return "argmax" if _fused_greedy() and not self.gc.do_sample else "last"
 
-    def _microbatches(self) -> int:
-        if (MICROBATCH > 1 and self.device.type == "cuda" and self.model.comm.size == 1
-                and self.b >= MICROBATCH_MIN_ROWS and self.b % MICROBATCH == 0):
-            return MICROBATCH
-        return 1
-
     def _decode_step(self):
-        nmb = self._microbatches()
-        if nmb > 1:
-            return self._decode_step_microbatched(nmb)
         logits, *_ = self.model.forward_tokens(self.tokens, self.positions, self.cache, self.cache.index_t,
                                                self.kv_start, self.key_mask, logits_mode=self._logits_mode())
         self._update(self._next_token(logits))
-
-    def _decode_step_microbatched(self, nmb: int):
-        """Rows split in ``nmb`` equal micro-batches; micro-batch i > 0 runs on side stream i (forked from the main
-        stream at the top of the step, joined before the state update), each with its own scratch workspaces."""
-        from ..models.kv_cache import KVRows
-        main = torch.cuda.current_stream(self.device)
-        if not hasattr(self, "_side_streams"):
-            self._side_streams = [torch.cuda.Stream(device=self.device) for _ in range(nmb - 1)]
-        for s in self._side_streams:
-            s.wait_stream(main)
-        step = self.b // nmb
-        outs = []
-        for i in range(nmb):
-            b0, b1 = i * step, (i + 1) * step
-            stream = main if i == 0 else self._side_streams[i - 1]
-            with torch.cuda.stream(stream), ops.workspace.scope(f"mb{i}"):
-                km = None if self.key_mask is None else self.key_mask[b0:b1]
-                logits, *_ = self.model.forward_tokens(self.tokens[b0:b1], self.positions[b0:b1],
-                                                       KVRows(self.cache, b0, b1), self.cache.index_t,
-                                                       self.kv_start[b0:b1], km, logits_mode=self._logits_mode())
-                outs.append(self._next_token(logits))
-        for s in self._side_streams:
-            main.wait_stream(s)
-        self._update(torch.cat(outs))
 
     # ---------------------------------------------------------------------------------
     def prefill(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor]):
@@ -267,7 +228,7 @@ class DecodeEngine:
     def _graph_state(self):
         # the graph records buffer addresses: the scratch workspaces (ops.workspace) and the sampling mode
         return (self.gc.do_sample, self.key_mask is not None, ops.workspace.generation, _fused_greedy(),
-                ops.ARGMAX_FUSED_MIN_M, ops.SKINNY_ARGMAX, self.model.comm.reduce_dtype, self._microbatches())
+                ops.ARGMAX_FUSED_MIN_M, ops.SKINNY_ARGMAX, self.model.comm.reduce_dtype)
 
     def _ensure_graph(self):
         if self._graph is not None and self._graph_key == self._graph_state():

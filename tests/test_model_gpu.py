@@ -180,26 +180,3 @@ def test_packed_activations_decode_rows(rows):
         ops.PACKED_X = saved
     assert rel_err(a, b) < 1e-2
     assert rel_err(a, cpu(toks).logits) < 2e-2
-
-
-def test_decode_microbatches_two_streams(monkeypatch):
-    """Engine decode micro-batches (runtime/engine.py MICROBATCH): the rows' two halves run on two streams of the
-    captured step with their own scratch workspaces -- graph replay == eager bit for bit, and the tokens match the
-    single-stream step up to near-ties (the half-size GEMM plans sum in another order)."""
-    from jax_llama_amd.runtime import engine as eng_mod
-    cfg = gpu_config()
-    _, gpu, _ = _pair(cfg, seed=21)
-    b = 512
-    toks = torch.randint(3, cfg.vocab_size, (b, 6), dtype=torch.int32, generator=torch.Generator().manual_seed(3))
-    gc = GenerationConfig(max_length=22, do_sample=False, pad_token_id=0, eos_token_id=-1)
-    monkeypatch.setattr(eng_mod, "MICROBATCH_MIN_ROWS", 256)
-    monkeypatch.setattr(eng_mod, "MICROBATCH", 1)
-    single = DecodeEngine(gpu, b, 22, use_graph=True).run(toks, None, gc).clone()
-    monkeypatch.setattr(eng_mod, "MICROBATCH", 2)
-    e_graph = DecodeEngine(gpu, b, 22, use_graph=True)
-    assert e_graph._microbatches() == 2
-    mb_graph = e_graph.run(toks, None, gc).clone()
-    mb_eager = DecodeEngine(gpu, b, 22, use_graph=False).run(toks, None, gc).clone()
-    assert torch.equal(mb_graph, mb_eager)
-    agree = (mb_graph[:, 6:] == single[:, 6:]).float().mean().item()
-    assert agree > 0.9, agree

@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--mode", default="store", choices=["store", "swiglu", "residual"],
                     help="epilogue (the model's: qkv/lm_head store, gate_up swiglu, o/down residual)")
     ap.add_argument("--rms", action="store_true", help="fused RMSNorm statistic (store / swiglu)")
+    ap.add_argument("--ring", type=int, nargs="+", default=[0], help="gemm4 main loop: 0 two K-tile slots, 1 the "
+                    "160 KiB ring (gemm_set_g4_ring); only for tile 7 / tile-0 gemm4 plans")
     ap.add_argument("--data", default="normal", choices=["normal", "uniform"],
                     help="operand distribution (uniform: as tools/debug/gemm4w_probe.hip)")
     args = ap.parse_args()
@@ -93,7 +95,11 @@ def main():
             for rnd, impl in [(r, i) for r in range(args.rounds) for i in args.impl]:
                 e.gemm_set_impl(impl)
                 for ks in args.ksplit:
+                 for ring in args.ring:
+                  e.gemm_set_g4_ring(ring)
                   for tile in args.tile:
+                    if ring and tile not in (0, 7):
+                        continue
                     kk = ks or e.gemm_ksplit(m, n, k)
                     tk = None
                     for fx in args.fixup:
@@ -124,7 +130,7 @@ def main():
                       def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
                           e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
                                  ws if (kk > 1 or tile in (4, 6)) else None, eps, tile, tk, None, rws)
-                      res[f"v{impl}_ks{kk}_t{tile}" + ("_fix" if fx and kk > 1 else "") +
+                      res[f"v{impl}_ks{kk}_t{tile}" + ("_ring" if ring else "") + ("_fix" if fx and kk > 1 else "") +
                           (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                       run(0)
                       if mode != 0:  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
@@ -141,6 +147,7 @@ def main():
                           f0 = first.setdefault((kk, tile), got.clone())
                           assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
             e.gemm_set_impl(2)
+            e.gemm_set_g4_ring(0)
             if not args.no_blas and mode == 0:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)
             for impl, us in res.items():

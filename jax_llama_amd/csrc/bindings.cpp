@@ -330,6 +330,23 @@ SkWs check_sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& t
   return r;
 }
 
+// gemm4 stream-K (tile 8) workspace: slabs + self-resetting tickets
+SkWs check_g4sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& tickets, int64_t m, int64_t n) {
+  SkWs r;
+  check(ws.has_value() && tickets.has_value(), "gemm tile 8: gemm4 stream-K needs ws and tickets");
+  check_gpu(*ws, "gemm4 sk ws");
+  check_gpu(*tickets, "gemm4 sk tickets");
+  check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm4_sk_workspace_floats(),
+        "gemm4 sk ws too small (gemm4_sk_workspace)");
+  check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm4_sk_tickets(m, n),
+        "gemm4 sk tickets too small");
+  r.ws = ptr<float>(*ws);
+  r.ws_floats = ws->numel();
+  r.tk = ptr<int32_t>(*tickets);
+  r.n_tk = (int)tickets->numel();
+  return r;
+}
+
 // Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel;
 // tile 4 -> data-parallel whole waves + stream-K tail (ws/tickets from gemm_sk_workspace).
 // rms_ws: optional fp32 scratch (>= M floats) for the row statistic of the fused norm on gemm4 plans without a K
@@ -363,6 +380,19 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
     check(ksplit > 1 && tile != 4 && tile != 6 && !(tickets.has_value() && jla::gemm_fixup_enabled()),
           "gemm pack_out: the split-K reduce-kernel path only");
     pqa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
+  }
+  if (tile == 8) {
+    check(ksplit <= 1, "gemm tile 8: no K split");
+    check(pqa.pack == nullptr, "gemm tile 8: no packed output copy");
+    const SkWs sk = check_g4sk_ws(ws, tickets, m, n);
+    size_t rfl = 0;
+    float* rws = rms_ws_ptr(rms_ws, m, &rfl);
+    check(rms_eps < 0 || rws != nullptr, "gemm tile 8 with the fused norm needs rms_ws");
+    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
+                 out.scalar_type() == torch::kFloat32, mir, nullptr, sk.ws, sk.ws_floats, 1, stream(),
+                 (float)rms_eps, 8, sk.tk, sk.n_tk, rws, rfl),
+       "gemm");
+    return;
   }
   if (tile == 4) {
     check(ksplit <= 1, "gemm tile 4: no K split");
@@ -423,6 +453,16 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
   const int64_t m = x.size(0);
   jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
+  if (tile == 8) {  // gemm4 stream-K: the RoPE + cache-write epilogue runs in the GEMM itself
+    const SkWs sk = check_g4sk_ws(ws, tickets, m, n);
+    size_t rfl = 0;
+    float* rws = rms_ws_ptr(rms_ws, m, &rfl);
+    check(rms_eps < 0 || rws != nullptr, "gemm_qkv tile 8 with the fused norm needs rms_ws");
+    rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, sk.ws, sk.ws_floats, 1,
+                 stream(), (float)rms_eps, 8, sk.tk, sk.n_tk, rws, rfl),
+       "gemm_qkv");
+    return;
+  }
   if (tile == 4) {  // stream-K: the RoPE + cache-write epilogue runs in the GEMM itself
     const SkWs sk = check_sk_ws(ws, tickets, m, n, k);
     check(sk.ws != nullptr, "gemm_qkv tile 4: this shape has no stream-K tail");
@@ -764,6 +804,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   });
   m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
   m.def("gemm_set_g4_ring", [](int64_t on) { jla::gemm_set_g4_ring((int)on); });
+  m.def("gemm4_sk_workspace", [](int64_t m, int64_t n) {
+    return py::make_tuple((int64_t)jla::gemm4_sk_workspace_floats(), (int64_t)jla::gemm4_sk_tickets(m, n));
+  });
   m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
     return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
   }, "(slab floats, tickets) of the in-kernel split-K fixup");

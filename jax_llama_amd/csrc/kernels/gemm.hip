@@ -929,42 +929,31 @@ __global__ void __launch_bounds__(256 * WM)
 // slabs: per-split sums to ssq_ws); 2 read from rms_inv[M], computed ahead of the GEMM by rms_rowinv_kernel.
 // RING: the main loop of g4_mainloop_ring (3-slot x ring + 4-slot W ring, all 160 KiB of LDS) instead of the
 // two 64 KiB K-tile slots of g4_mainloop.
-template <int MODE, int RMSM, bool RING>
-__global__ void __launch_bounds__(256, 1)
-    gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                 int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv) {
+// The epilogue of one gemm4 output tile (every mode; see gemm4_kernel), shared by the data-parallel and the
+// stream-K launches. acc: this wave's finished C^T accumulators; ss: the in-loop RMS partial sums (RMSM 1).
+struct G4Epi {
+  void* out;
+  int M, N, K, accumulate, out_f32;
+  bf16_t* mirror;
+  int tiles_n;
+  float rms_eps;
+  float* ssq_ws;
+  const float* rms_inv;
+};
+template <int MODE, int RMSM, typename Acc>
+JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int m0, int n0, int split,
+                         const G4Epi& ep, const QKVArgs& qa) {
   constexpr bool RMS = RMSM == 1;
-  // the K-tile slots / rings; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
-  __shared__ u32x4 lds[RING ? G4R_LDS_U4 : 2 * G4_SLOT_U4 + 64];
-  const int lane = threadIdx.x & 63;
-  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wu >> 1, wc = wu & 1;
-  // XCD-aware bijective remap, then (split, M-grouped tile) order (as gemm2)
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tiles = tiles_m * tiles_n;
-  const int split = wgid / tiles, pid = wgid - split * tiles;
-  int tm, tn;
-  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
-  const int t0 = split * kc, KT = min(K >> 6, t0 + kc) - t0;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss[4] = {0.f, 0.f, 0.f, 0.f};
-  const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
-  if constexpr (RING) {
-    g4_mainloop_ring<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
-    wait_vmcnt<0>();  // the ring's clamped tail DMAs land before LDS is reused
-  } else {
-    g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
-  }
-
+  void* const out = ep.out;
+  const int M = ep.M, N = ep.N, K = ep.K, accumulate = ep.accumulate, out_f32 = ep.out_f32;
+  bf16_t* const mirror = ep.mirror;
+  const int tiles_n = ep.tiles_n;
+  const float rms_eps = ep.rms_eps;
+  float* const ssq_ws = ep.ssq_ws;
+  const float* const rms_inv = ep.rms_inv;
+  (void)K, (void)tiles_n, (void)rms_eps, (void)ssq_ws, (void)rms_inv, (void)split, (void)accumulate, (void)out_f32,
+      (void)mirror, (void)wc;
   const int c = lane & 15, q = lane >> 4, NTT = N >> 4;
   const int rbase = m0 + wr * 128 + c;  // + 16 i: this lane's output row in m-tile i
   float sc[8];                           // RMS: per m-tile row scale
@@ -1165,6 +1154,151 @@ __global__ void __launch_bounds__(256, 1)
   }
 }
 
+template <int MODE, int RMSM, bool RING>
+__global__ void __launch_bounds__(256, 1)
+    gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                 int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
+                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv) {
+  constexpr bool RMS = RMSM == 1;
+  // the K-tile slots / rings; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
+  __shared__ u32x4 lds[RING ? G4R_LDS_U4 : 2 * G4_SLOT_U4 + 64];
+  const int lane = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wu >> 1, wc = wu & 1;
+  // XCD-aware bijective remap, then (split, M-grouped tile) order (as gemm2)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int split = wgid / tiles, pid = wgid - split * tiles;
+  int tm, tn;
+  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int t0 = split * kc, KT = min(K >> 6, t0 + kc) - t0;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[4] = {0.f, 0.f, 0.f, 0.f};
+  const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
+  if constexpr (RING) {
+    g4_mainloop_ring<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+    wait_vmcnt<0>();  // the ring's clamped tail DMAs land before LDS is reused
+  } else {
+    g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+  }
+  g4_epilogue<MODE, RMSM>(acc, ss, lds, wu, lane, m0, n0, split,
+                          G4Epi{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, ssq_ws, rms_inv}, qa);
+}
+
+// ---------------------------------------------------------------------------------------------
+// gemm4 stream-K (tile config 8): one persistent workgroup per CU walks an equal share of ALL the launch's
+// (tile, 64-deep K-tile) iterations -- no partial last wave of tiles (Llama-3-8B at M = 2048: gate_up has 896 256 x 256
+// tiles = 3.5 waves, qkv 192 < 256 CUs). A segment that covers a whole tile runs the epilogue directly; a partial one
+// publishes its fp32 accumulators with write-through (sc1) stores into its own slab slot (slot 0: the segment that
+// opens the workgroup's range, slot 1: the one that closes it), takes the tile's agent-scope ticket, and the LAST
+// arriver sums every contributor in K order (deterministic) and runs the epilogue (cdna_hip_programming.md
+// Guideline 16: sc1 stores + vmcnt(0) + agent ticket + sc1 loads; tickets reset themselves). Nobody waits for
+// anybody. The fused norm needs the precomputed statistic (RMSM 2).
+JLA_DEV int g2sk_owner(long long it, long long iters, int P) {  // workgroup whose range holds iteration it
+  return (int)(((it + 1) * P - 1) / iters);
+}
+JLA_DEV long long g2sk_lo(int w, long long iters, int P) { return iters * w / P; }
+
+struct G4Sk {
+  long long iters;   // tiles * (K / 64)
+  float* slabs;      // [P][2][G4SK_SLAB_FLOATS]
+  int slab_bytes;    // buffer-descriptor range
+  int32_t* tickets;  // [tiles], zero-initialised once
+};
+constexpr int G4SK_SLAB_BYTES = 4 * 64 * 1024;  // 4 waves x 64 accumulator tiles x 1 KiB
+constexpr int G4SK_SLAB_FLOATS = G4SK_SLAB_BYTES / 4;
+
+template <int MODE, int RMSM>
+__global__ void __launch_bounds__(256, 1)
+    gemm4_sk_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                    int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int tiles_m, int tiles_n,
+                    float rms_eps, G4Sk sk, QKVArgs qa, const float* __restrict__ rms_inv) {
+  static_assert(RMSM != 1, "stream-K: the fused norm's statistic is precomputed");
+  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64 + 1];  // K-tile slots / staging, row scales, last-arriver flag
+  int* const sh_last = reinterpret_cast<int*>(lds + 2 * G4_SLOT_U4 + 64);
+  const int lane0 = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int KT64 = K >> 6;
+  const int P = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = P >> 3, r8 = P & 7;
+  // XCD-aware: the workgroups of one XCD get consecutive iteration ranges (neighbouring tiles share L2)
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const long long lo = g2sk_lo(wg, sk.iters, P), hi = g2sk_lo(wg + 1, sk.iters, P);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(sk.slabs, 0, sk.slab_bytes, 0x00020000);
+  const G4Args g{x, W, out, M, N, K, KT64, tiles_m, tiles_n};
+  const G4Epi ep{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, nullptr, rms_inv};
+
+  for (long long it = lo; it < hi;) {
+    const int t = (int)(it / KT64);
+    const int kb = (int)(it - (long long)t * KT64);
+    const int ke = (int)min((long long)KT64, (long long)kb + (hi - it));
+    const int slot = it == lo ? 0 : 1;
+    it += ke - kb;
+    int tm, tn;
+    g4_tile_coords(t, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+    // the lane index laundered through an opaque move once per segment: the lane-dependent address math of the
+    // main loop and the unrolled epilogue would otherwise be hoisted out of the segment loop and kept live (spills)
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+    __syncthreads();  // the previous segment's epilogue / slab reads are done with LDS
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    g4_mainloop<false>(g, lds, m0, n0, kb, ke - kb, wu, lane, acc);
+
+    if (!(kb == 0 && ke == KT64)) {
+      // ---- partial segment: publish (sc1), ticket, the last arriver sums all contributors in K order
+      const int base = (wg * 2 + slot) * G4SK_SLAB_BYTES;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, g4_take(acc[j][i])), rsrc,
+                                                 base + ((wu * 8 + j) * 8 + i) * 1024 + lane * 16, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const long long t_lo = (long long)t * KT64, t_hi = t_lo + KT64;
+      const int w_first = g2sk_owner(t_lo, sk.iters, P), w_last = g2sk_owner(t_hi - 1, sk.iters, P);
+      if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(sk.tickets + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == w_last - w_first;
+        if (last) __hip_atomic_store(sk.tickets + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *sh_last = last;
+      }
+      __syncthreads();
+      const int last = *sh_last;
+      if (!last) continue;
+      const int me = wg - w_first;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int off = ((wu * 8 + j) * 8 + i) * 1024 + lane * 16;
+          f32x4 tsum = f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 mine = g4_take(acc[j][i]);
+          for (int cw = w_first; cw <= w_last; ++cw) {
+            const int cb = (cw * 2 + (g2sk_lo(cw, sk.iters, P) >= t_lo ? 0 : 1)) * G4SK_SLAB_BYTES;
+            tsum += cw - w_first == me ? mine
+                                       : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, cb + off, 0, 16));
+          }
+          acc[j][i] = tsum;
+        }
+    }
+    g4_epilogue<MODE, RMSM>(acc, nullptr, lds, wu, lane, m0, n0, 0, ep, qa);
+  }
+}
+
 // Stream-K tail of the 256 x 256 ping-pong GEMM (tile config 4). Decode-sized outputs rarely have a
 // multiple of 256 tiles (Llama-3-8B at M = 2048: qkv 192, o/down 128, gate_up 896 tiles), so the
 // last wave of whole tiles leaves CUs idle, and split-K pays a second kernel that re-reads fp32
@@ -1191,10 +1325,6 @@ constexpr int G2SK_ACC_BYTES = 8 * 8 * 4 * 1024;                // 8 waves x 8 x
 constexpr int G2SK_SLAB_BYTES = G2SK_ACC_BYTES + 256 * 4;       // + 256 row sums of squares
 constexpr int G2SK_SLAB_FLOATS = G2SK_SLAB_BYTES / 4;
 
-JLA_DEV int g2sk_owner(long long it, long long iters, int P) {  // workgroup whose range holds iteration it
-  return (int)(((it + 1) * P - 1) / iters);
-}
-JLA_DEV long long g2sk_lo(int w, long long iters, int P) { return iters * w / P; }
 
 template <int MODE, bool RMS>
 __global__ void __launch_bounds__(512)
@@ -1719,6 +1849,35 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
 #undef JLA_G4
 }
 
+// gemm4 stream-K (tile config 8): slabs + tickets of the plan
+constexpr int G4_SK_TILE = 8;
+static int num_cus();
+size_t gemm4_sk_workspace_floats() { return (size_t)num_cus() * 2 * G4SK_SLAB_FLOATS; }
+int gemm4_sk_tickets(int M, int N) { return ((M + G4_BM - 1) / G4_BM) * ((N + G4_BN - 1) / G4_BN); }
+
+template <int MODE>
+static int launch_g4_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
+                        bf16_t* mirror, float rms_eps, const QKVArgs& qa, float* ws, size_t ws_floats,
+                        int32_t* tickets, int n_tickets, float* rms_ws, hipStream_t s) {
+  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
+  const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
+  if ((K & 63) || ws == nullptr || ws_floats < gemm4_sk_workspace_floats() || tickets == nullptr ||
+      n_tickets < tm * tn || (rms && rms_ws == nullptr))
+    return -3;
+  const int P = num_cus();
+  const G4Sk sk{(long long)tm * tn * (K >> 6), ws, (int)(gemm4_sk_workspace_floats() * 4), tickets};
+  if (rms) {
+    if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return -1;
+    gemm4_sk_kernel<MODE, 2><<<P, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, sk,
+                                                 qa, rms_ws);
+  } else {
+    gemm4_sk_kernel<MODE, 0><<<P, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, sk,
+                                                 qa, nullptr);
+  }
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
@@ -1893,6 +2052,29 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps, int tile, int32_t* tickets, int n_tickets, float* rms_ws, size_t rms_ws_floats) {
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
+  if (tile == G4_SK_TILE) {  // gemm4 stream-K over every (tile, K-tile) iteration: one persistent workgroup per CU
+    if (g_gemm_impl != 2 || ksplit > 1) return -1;
+    if ((N & 15) || (K & 31)) return -1;
+    if (mode == MODE_QKV && !qkv) return -1;
+    const u32x4* wp = static_cast<const u32x4*>(W);
+    QKVArgs qa{};
+    if (qkv) qa = *qkv;
+    switch (mode) {
+      case MODE_STORE:
+        return launch_g4_sk<MODE_STORE>(x, wp, out, M, N, K, accumulate, out_f32, nullptr, rms_eps, qa, ws, ws_floats,
+                                        tickets, n_tickets, rms_ws, s);
+      case MODE_RESIDUAL:
+        return launch_g4_sk<MODE_RESIDUAL>(x, wp, out, M, N, K, accumulate, 1, mirror, -1.f, qa, ws, ws_floats,
+                                           tickets, n_tickets, nullptr, s);
+      case MODE_SWIGLU:
+        return launch_g4_sk<MODE_SWIGLU>(x, wp, out, M, N, K, accumulate, 0, nullptr, rms_eps, qa, ws, ws_floats,
+                                         tickets, n_tickets, rms_ws, s);
+      case MODE_QKV:
+        return launch_g4_sk<MODE_QKV>(x, wp, nullptr, M, N, K, 0, 0, nullptr, rms_eps, qa, ws, ws_floats, tickets,
+                                      n_tickets, rms_ws, s);
+      default: return -1;
+    }
+  }
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;

@@ -64,7 +64,12 @@ int gemm_ksplit(int M, int N, int K);
 int gemm_qkv_direct_ok(int M, int tile, int K);  // qkv without a K split: the direct RoPE / KV-write GEMM epilogue applies
 // gemm4 (the 4-wave 256 x 256 kernel, tile config 7) as the tile-0 default for M > 128, K % 64 == 0 (on by default)
 void gemm_set_g4_default(int on);
-void gemm_set_g4_ring(int on);  // gemm4 main loop on the 160 KiB LDS ring (3 x pairs + 4 W stages in flight)
+void gemm_set_g4_ring(int on);
+// tile config 8: gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration; partial tiles
+// summed by the last arriver): ws >= gemm4_sk_workspace_floats(), tickets >= gemm4_sk_tickets(M, N) int32
+// zero-initialised once (self-resetting); the fused norm needs rms_ws; every mode incl. MODE_QKV
+size_t gemm4_sk_workspace_floats();
+int gemm4_sk_tickets(int M, int N);  // gemm4 main loop on the 160 KiB LDS ring (3 x pairs + 4 W stages in flight)
 void gemm_set_impl(int impl);  // 2 = gemm2 (default, full-line x), 4 = gemm2 fragment-shaped x, 1 = 128x128 v1 (A/B)
 int gemm_get_impl();
 size_t gemm_workspace_floats(int M, int N, int K);

@@ -339,11 +339,25 @@ def fix_workspace(e, m, n, ks, device):
     return ws, tk
 
 
+G4SK_TILE = 8  # gemm4 stream-K plan (csrc/kernels/gemm.hip gemm4_sk_kernel)
+
+
+def g4sk_workspace(e, m, n, device):
+    """Slabs + self-resetting tickets of the gemm4 stream-K plan (sized for the largest M seen; one fixed-size ticket
+    array so captured graphs never see a reallocation)."""
+    floats, tiles = e.gemm4_sk_workspace(m, n)
+    return (workspace.get("gemm4_sk", floats, torch.float32, device),
+            workspace.get_zeroed("gemm4_sk_tickets", max(FIX_TICKETS, tiles), torch.int32, device))
+
+
 def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
     """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue.
     A split plan gets fixup tickets (the GEMM sums its splits itself) except for the QKV epilogue, whose
     RoPE + cache write lives in the reduce kernel."""
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, rms)
+    if tm == G4SK_TILE:
+        ws, tk = g4sk_workspace(e, m, n, device)
+        return 1, tm, ws, tk
     if tm == SK_TILE:
         ws, tk = sk_workspace(e, m, n, k, device)
         return 1, tm, ws, tk
@@ -362,7 +376,8 @@ def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
 
 def _rms_ws(x, fused: bool, ks: int):
     """fp32 [M] scratch for the row statistic of the fused norm, computed ahead of a gemm4 GEMM without a K split
-    (csrc/kernels/norm_embed.hip rms_rowinv; the main loop then carries no sum-of-squares work)."""
+    (csrc/kernels/norm_embed.hip rms_rowinv; the main loop then carries no sum-of-squares work; the gemm4 stream-K
+    plan requires it)."""
     if not fused or ks > 1:
         return None
     return workspace.get("gemm_rms", x.shape[0], torch.float32, x.device)
@@ -385,7 +400,7 @@ def _tiled_packs(e, m, n, k, device, mode, rms_eps) -> bool:
     if e is None or m > SKINNY_M or mode not in (MODE_RESIDUAL, MODE_SWIGLU):
         return False
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, _fused_rms(e, mode, rms_eps))
-    return ks > 1 and tm not in (SK_TILE, autotune.HYBRID_TILE) and not e.gemm_fixup_enabled()
+    return ks > 1 and tm not in (SK_TILE, autotune.HYBRID_TILE, G4SK_TILE) and not e.gemm_fixup_enabled()
 
 
 def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int:
@@ -481,6 +496,13 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     if v == TILED:
         # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
         ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
+        if tm == G4SK_TILE:  # gemm4 stream-K: the RoPE / KV-write epilogue runs in the GEMM itself
+            fused = _fused_rms(e, MODE_QKV, rms_eps)
+            q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
+            e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
+                       k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
+                       int(head_dim), q, 1, ws, float(rms_eps) if fused else -1.0, tm, tk, _rms_ws(x, fused, 1))
+            return q
         if tm == autotune.HYBRID_TILE:
             tm = 1  # (only reached with ks == 1: the plain linear() below runs the hybrid plan itself)
         if tm != SK_TILE:

@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 4  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7), so older persisted picks are re-measured
+TUNE_VERSION = 5  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -322,6 +322,7 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
 
 SK_TILE = 4  # 256x256 tiles with a stream-K tail (no K split): csrc/kernels/gemm.hip gemm_sk
 HYBRID_TILE = 6  # whole waves of 256x256 tiles + the partial wave split 2-way with the in-kernel fixup
+G4SK_TILE = 8  # gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration)
 SK_MARGIN = 0.97
 TUNE_ROUNDS = 3
 
@@ -334,6 +335,12 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     sk_ws, sk_tk = sk_workspace(e, m, n, k, device)
     if sk_ws is not None:
         cands.append((1, SK_TILE))
+    g4sk = None
+    if k % 64 == 0:  # gemm4 stream-K over every (tile, K-tile) iteration
+        cands.append((1, G4SK_TILE))
+        fl, tiles = e.gemm4_sk_workspace(m, n)
+        g4sk = (torch.empty(fl, dtype=torch.float32, device=device), torch.zeros(tiles, dtype=torch.int32,
+                                                                                  device=device))
     hyb_floats = e.gemm_hybrid_workspace(m, n)[0] if e.gemm_fixup_enabled() else 0
     if hyb_floats > 0:  # whole waves data-parallel + the partial wave split 2-way (in-kernel fixup)
         cands.append((1, HYBRID_TILE))
@@ -361,7 +368,10 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     rms_ws = torch.empty(m, dtype=torch.float32, device=device)  # as ops._rms_ws: the statistic ahead of gemm4
 
     def run(c, tm, i):
-        if tm == SK_TILE:
+        if tm == G4SK_TILE:
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, g4sk[0], eps, tm, g4sk[1], None,
+                   rms_ws if eps > 0 else None)
+        elif tm == SK_TILE:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, sk_ws, eps, tm, sk_tk)
         elif tm == HYBRID_TILE:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, ws, eps, tm, fix_tk)
@@ -388,7 +398,7 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     # the stream-K tail publishes fp32 partials in-kernel: keep it only when it clearly wins
     if (1, SK_TILE) in times and times[(1, SK_TILE)] < SK_MARGIN * times[best]:
         best = (1, SK_TILE)
-    del ws_w, ws
+    del ws_w, ws, g4sk
     return best
 
 

@@ -1864,8 +1864,11 @@ static int launch_g4_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N
   if ((K & 63) || ws == nullptr || ws_floats < gemm4_sk_workspace_floats() || tickets == nullptr ||
       n_tickets < tm * tn || (rms && rms_ws == nullptr))
     return -3;
-  const int P = num_cus();
-  const G4Sk sk{(long long)tm * tn * (K >> 6), ws, (int)(gemm4_sk_workspace_floats() * 4), tickets};
+  // one workgroup per CU, never more than there are iterations: an empty range inside a tile's contributor span
+  // would never take its ticket
+  const long long iters = (long long)tm * tn * (K >> 6);
+  const int P = (int)min((long long)num_cus(), iters);
+  const G4Sk sk{iters, ws, (int)(gemm4_sk_workspace_floats() * 4), tickets};
   if (rms) {
     if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return -1;
     gemm4_sk_kernel<MODE, 2><<<P, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, sk,

@@ -109,6 +109,11 @@ def main():
                           ws, tk = ops.sk_workspace(e, m, n, k, DEV)
                           if ws is None:
                               continue
+                      elif tile == 8:  # gemm4 stream-K (persistent, every iteration)
+                          kk = 1
+                          floats, tiles = e.gemm4_sk_workspace(m, n)
+                          ws = torch.empty(floats, device=DEV, dtype=torch.float32)
+                          tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
                       elif tile == 6:  # whole waves + 2-way split tail (fixup)
                           kk = 1
                           floats, tiles = e.gemm_hybrid_workspace(m, n)
@@ -129,7 +134,7 @@ def main():
 
                       def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
                           e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
-                                 ws if (kk > 1 or tile in (4, 6)) else None, eps, tile, tk, None, rws)
+                                 ws if (kk > 1 or tile in (4, 6, 8)) else None, eps, tile, tk, None, rws)
                       res[f"v{impl}_ks{kk}_t{tile}" + ("_ring" if ring else "") + ("_fix" if fx and kk > 1 else "") +
                           (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                       run(0)

@@ -33,6 +33,7 @@ Extra keys (outside the timed region, reported alongside the headline):
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -80,6 +81,7 @@ def main():
 
     from jax_llama_amd.config import get_preset
     from jax_llama_amd.models import LLaMAForCausalLM
+    from jax_llama_amd import ops
     from jax_llama_amd.ops import autotune
     from jax_llama_amd.parallel import TPComm, init_distributed
     from jax_llama_amd.runtime import engine as eng_mod
@@ -229,7 +231,11 @@ def main():
         extra("tp_rank_proxy", lambda: res.__setitem__("tp_rank_proxy", _tp_rank_proxy(args)))
     if world == 1 and args.mp1_model:
         del model
+        # 141 GB of 70B weights: drop everything the earlier points left resident (engines, their KV caches, and
+        # the grow-only op workspaces sized by the B = 2048 prefill's split-K slabs)
         eng_mod._ENGINES.clear()
+        ops.workspace.clear()
+        gc.collect()
         torch.cuda.empty_cache()
         extra("mp1_point", lambda: res.__setitem__("mp1_point", _mp1_point(args)))
     if not args.no_calibration:  # last: the GEMM / copy probes of this box, next to the numbers above
@@ -304,10 +310,12 @@ def _mp1_point(args):
     from jax_llama_amd.runtime.benchmark import decode_latency
 
     cfg = get_preset(args.mp1_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
+    resident_gb = round(torch.cuda.memory_allocated() / 1e9, 2)  # what the earlier points left allocated
     model = LLaMAForCausalLM(cfg, device="cuda", _do_init=False).init_random(seed=77)
     try:
         p = decode_latency(model, args.mp1_batch, args.prompt_len, args.gen_len, seed=12)
         return {"model": args.mp1_model, "mp": 1, "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
+                "resident_gb_before_load": resident_gb,
                 "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
                 "point": p}
     finally:

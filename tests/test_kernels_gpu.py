@@ -533,7 +533,7 @@ def test_qkv_rope_direct_epilogue(m, s, n_heads):
     h = n_heads
     b = m // s
     n = (h + 2 * hkv) * dh
-    assert e.gemm_qkv_direct_ok(m, 1)
+    assert e.gemm_qkv_direct_ok(m, 1, k)
     w = (torch.randn(n, k) * 0.05).to(BF16)
     x = torch.randn(m, k).to(BF16)
     table = ref.rope_table(dh, 1024, 500000.0)

@@ -131,7 +131,18 @@ int attn_decode_splits(int B, int Hkv, int T, int rep);
 int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                 const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int32_t* tickets, int B, int H,
                 int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s, bf16_t* out_pack = nullptr);
-int attn_decode_packs(int B, int Hkv, int rep);  // 1: attn_decode can also write the packed-layout output
+int attn_decode_packs(int B, int Hkv, int rep);
+// persistent decode step (decode_mk.hip): every layer of one decode token for M <= 4 rows in one launch; `layers` is
+// a device array of L MkLayer records (6 pointers: wqkv, wo, wgu, wdown, k cache, v cache of the layer)
+int decode_mk_supported(int M, int D, int H, int Hkv, int Dh, int F);
+int decode_mk_grid();
+size_t decode_mk_slab_floats();
+int decode_mk_max_splits(int T);
+int decode_mk(const void* layers, int L, int M, int D, int H, int Hkv, int F, int T, float eps, float* h, bf16_t* hb,
+              bf16_t* q, bf16_t* att, bf16_t* act, float* ssq, const float2* rope, int rope_len,
+              const int32_t* positions, const int32_t* slot, const int32_t* kv_start, float* slab, size_t slab_floats,
+              int32_t* tickets, int n_tickets, unsigned* bar, int32_t* err, float* aws, size_t aws_floats, int32_t* atk,
+              hipStream_t s);  // 1: attn_decode can also write the packed-layout output
 void attn_prefill_set_impl(int impl);  // 2 = GQA-shared MFMA 32x32 flash kernel (default), 1 = v1
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,

@@ -581,7 +581,8 @@ Tensor decode_mk_table(std::vector<Tensor> wqkv, std::vector<Tensor> wo, std::ve
 
 void decode_mk(Tensor table, Tensor h, Tensor hb, Tensor q, Tensor att, Tensor act, Tensor ssq, Tensor rope,
                Tensor positions, Tensor slot, Tensor kv_start, Tensor kc, Tensor slab, Tensor tickets, Tensor bar,
-               Tensor err, Tensor aws, Tensor atk, int64_t H, int64_t Hkv, int64_t F, double eps) {
+               Tensor err, Tensor aws, Tensor atk, int64_t H, int64_t Hkv, int64_t F, double eps,
+               c10::optional<Tensor> trace, int64_t prefetch_late) {
   for (auto* t : {&table, &h, &hb, &q, &att, &act, &ssq, &rope, &positions, &slot, &kv_start, &kc, &slab, &tickets,
                   &bar, &err, &aws, &atk})
     check_gpu(*t, "decode_mk operand");
@@ -603,13 +604,20 @@ void decode_mk(Tensor table, Tensor h, Tensor hb, Tensor q, Tensor att, Tensor a
         "decode_mk: positions / kv_start / slot int32");
   check(slab.scalar_type() == torch::kFloat32 && tickets.scalar_type() == torch::kInt32 &&
             bar.scalar_type() == torch::kInt32 && err.scalar_type() == torch::kInt32 &&
-            aws.scalar_type() == torch::kFloat32 && atk.scalar_type() == torch::kInt32 && atk.numel() >= M * Hkv,
-        "decode_mk: workspace dtypes");
+            aws.scalar_type() == torch::kFloat32 && atk.scalar_type() == torch::kInt32 && atk.numel() >= 32 * M * Hkv &&
+            bar.numel() >= jla::decode_mk_bar_words(),
+        "decode_mk: workspace dtypes / sizes");
+  unsigned long long* tr = nullptr;
+  if (trace.has_value()) {
+    check_gpu(*trace, "trace");
+    check(trace->scalar_type() == torch::kInt64 && trace->numel() >= jla::decode_mk_trace_words(), "decode_mk: trace");
+    tr = reinterpret_cast<unsigned long long*>(trace->data_ptr());
+  }
   rc(jla::decode_mk(table.data_ptr(), L, M, D, H, Hkv, F, T, (float)eps, ptr<float>(h), bf(hb), bf(q), bf(att),
                     bf(act), ptr<float>(ssq), reinterpret_cast<const float2*>(rope.data_ptr()), rope.size(0),
                     ptr<int32_t>(positions), ptr<int32_t>(slot), ptr<int32_t>(kv_start), ptr<float>(slab),
                     slab.numel(), ptr<int32_t>(tickets), tickets.numel(), reinterpret_cast<unsigned*>(bar.data_ptr()),
-                    ptr<int32_t>(err), ptr<float>(aws), aws.numel(), ptr<int32_t>(atk), stream()),
+                    ptr<int32_t>(err), ptr<float>(aws), aws.numel(), ptr<int32_t>(atk), tr, (int)prefetch_late, stream()),
      "decode_mk");
 }
 
@@ -936,7 +944,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
         py::arg("nsplit"), py::arg("out_pack") = py::none());
   m.def("decode_mk_table", &decode_mk_table);
-  m.def("decode_mk", &decode_mk);
+  m.def("decode_mk", &decode_mk, py::arg("table"), py::arg("h"), py::arg("hb"), py::arg("q"), py::arg("att"),
+        py::arg("act"), py::arg("ssq"), py::arg("rope"), py::arg("positions"), py::arg("slot"), py::arg("kv_start"),
+        py::arg("kc"), py::arg("slab"), py::arg("tickets"), py::arg("bar"), py::arg("err"), py::arg("aws"),
+        py::arg("atk"), py::arg("H"), py::arg("Hkv"), py::arg("F"), py::arg("eps"), py::arg("trace") = py::none(),
+        py::arg("prefetch_late") = 0);
+  m.def("decode_mk_trace_words", []() { return jla::decode_mk_trace_words(); });
   m.def("decode_mk_supported", [](int64_t m, int64_t d, int64_t h, int64_t hkv, int64_t dh, int64_t f) {
     return jla::decode_mk_supported(m, d, h, hkv, dh, f) != 0;
   });

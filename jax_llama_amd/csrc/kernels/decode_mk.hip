@@ -41,7 +41,9 @@ constexpr int MK_MINRUN = 8;            // fewest k-steps per active wave (tiny 
 constexpr int MK_X_BYTES = 144 * 1024;  // x staging (M rows x K bf16, row pitch 2K + 16)
 constexpr int MK_DH = 128;
 constexpr int MK_KPG = 2;                         // keys per 16-lane group per attention split
-constexpr int MK_CH = MK_NW * 4 * MK_KPG;         // keys per attention split (64)
+constexpr int MK_CH = MK_NW * 4 * MK_KPG;         // keys per attention chunk (64)
+constexpr int MK_ACH = 6;                         // chunks per attention split (384 keys: all loads issued at once)
+constexpr int MK_SPK = MK_CH * MK_ACH;            // keys per attention split
 constexpr unsigned MK_SC1 = 16;                   // cache-policy bits of a write-through / coherent buffer access
 
 __device__ u32x4 g_mk_zero[64];  // zero fragment: past-the-end ring refills
@@ -68,18 +70,32 @@ JLA_DEV void st_bf(__amdgpu_buffer_rsrc_t r, int byte_off, float v) {
   __builtin_amdgcn_raw_buffer_store_b16((unsigned short)f2bf(v), r, byte_off, 0, MK_SC1);
 }
 
-// Device-wide phase barrier on a monotonic counter (zeroed by the host before the launch). The caller has drained
-// its own write-through stores (vmcnt(0)) before it issued anything it wants in flight across the barrier.
-JLA_DEV void mk_sync(unsigned* bar, unsigned target, int32_t* err, int tag) {
+// Device-wide phase barrier, two levels so no counter sees more than ~32 arrivals per phase: each workgroup adds to
+// its XCD group's counter (blockIdx % 8: the dispatcher's round-robin XCD), the group's last arriver adds to the
+// global counter, and the overall last arriver raises every group's release flag; a workgroup polls only its own
+// group's flag. Counters and flags are monotonic (phase number), each on its own 128-B line, zeroed by the host
+// before the launch. The caller has drained its own write-through stores (vmcnt(0)) before anything it wants in
+// flight across the barrier.
+constexpr int MK_BAR_WORDS = 32 * 17;  // 8 group counters, 1 global counter, 8 release flags
+JLA_DEV void mk_sync(unsigned* bar, unsigned epoch, int32_t* err) {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS reads are done before anyone restages
   __builtin_amdgcn_s_barrier();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int G = gridDim.x, ng = min(G, 8), x = blockIdx.x & 7;
+    const unsigned nx = (unsigned)(G / 8 + (x < G % 8 ? 1 : 0));
+    unsigned* flag = bar + 32 * (9 + x);
+    const unsigned old = __hip_atomic_fetch_add(bar + 32 * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == epoch * nx - 1) {  // last of its group
+      const unsigned gold = __hip_atomic_fetch_add(bar + 32 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (gold == epoch * (unsigned)ng - 1)  // last group: release every group
+        for (int i = 0; i < ng; ++i)
+          __hip_atomic_store(bar + 32 * (9 + i), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1 << 22)) {
-        __hip_atomic_store(err, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(err, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -113,16 +129,32 @@ struct MkArgs {
   const int32_t* slot;       // device int32[1]: cache slot of this token
   const int32_t* kv_start;   // [M]: first valid key (left padding)
   float* slab;             // [grid * MK_NW][MK_NSEG][64][4] partial tiles
-  int32_t* tickets;        // >= max groups, zero-initialised once, self-resetting
+  int32_t* tickets;        // [max groups][32] (one per 128-B line), zero-initialised once, self-resetting
   unsigned* bar;           // phase-barrier counter, zeroed before every launch
   int32_t* err;            // barrier timeout -> phase tag
   float* aws;              // attention partials [M][Hkv][max_splits][REP][132]
   int32_t* atk;            // [M][Hkv] attention tickets (self-resetting)
   int max_splits;
+  int prefetch_late;          // A/B: 1 = issue the ring prologue after the phase barrier instead of before
+  unsigned long long* trace;  // optional [MK_TRACE_PH][MK_TRACE_EV][grid] s_memrealtime stamps (100 MHz), else null
 };
 
-JLA_DEV long long mk_lo(int w, long long W, int P) { return W * w / P; }
-JLA_DEV int mk_owner(long long it, long long W, int P) { return (int)(((it + 1) * P - 1) / W); }
+// the first two layers, per wave (lane 0); events: entry, released, ready, streamed, done
+constexpr int MK_TRACE_PH = 10, MK_TRACE_EV = 5;
+JLA_DEV void mk_mark(const MkArgs& a, unsigned epoch, int ev) {
+  const int ph = (int)epoch - 1;
+  if (a.trace != nullptr && ph < MK_TRACE_PH && (threadIdx.x & 63) == 0)
+    a.trace[((ph * MK_TRACE_EV + ev) * gridDim.x + blockIdx.x) * MK_NW + (threadIdx.x >> 6)] =
+        __builtin_amdgcn_s_memrealtime();
+}
+
+// Run bounds in double precision: a 64-bit integer division is a ~100-instruction software routine (the last
+// arriver evaluates these per contributor); the operands stay below 2^33 and the divisor below 2^13, so a
+// non-integral quotient sits >= 2^-13 from the next integer, far above the double rounding error (exact floors).
+JLA_DEV long long mk_lo(int w, long long W, int P) { return (long long)floor((double)W * (double)w / (double)P); }
+JLA_DEV int mk_owner(long long it, long long W, int P) {
+  return (int)floor(((double)(it + 1) * (double)P - 1.0) / (double)W);
+}
 
 // ---- one GEMV phase: y = epilogue([inv_rms *] x @ W^T), N / 16 tiles x K / 32 k-steps over the active waves
 template <int MODE>
@@ -141,12 +173,23 @@ __device__ __attribute__((noinline)) void mk_gemv(const MkArgs& a, const MkLayer
   u32x4 ring[MK_U];
   const u32x4* zf = g_mk_zero + lane;
   const u32x4* wp = W + lane;
+  // (A/B: prefetch_late issues them after the barrier instead; one code path either way)
+  const bool late = a.prefetch_late != 0;
+  if (late) {
+    mk_mark(a, epoch, 0);
+    mk_sync(a.bar, epoch, a.err);
+    mk_mark(a, epoch, 1);
+  }
 #pragma unroll
   for (int u = 0; u < MK_U; ++u) {
     ring[u] = u32x4{0u, 0u, 0u, 0u};
     mk_load(ring[u], lo + u < hi ? (const void*)(wp + (size_t)(lo + u) * 64) : (const void*)zf);
   }
-  mk_sync(a.bar, epoch * gridDim.x, a.err, (int)epoch);
+  if (!late) {
+    mk_mark(a, epoch, 0);
+    mk_sync(a.bar, epoch, a.err);
+    mk_mark(a, epoch, 1);
+  }
 
   // ---- stage x [M][K] (sc1: written by other workgroups of this launch) and the norm statistic
   const int M = a.M;
@@ -154,6 +197,13 @@ __device__ __attribute__((noinline)) void mk_gemv(const MkArgs& a, const MkLayer
   {
     const __amdgpu_buffer_rsrc_t xr = mk_rsrc(x, (long long)M * K * 2);
     const int cpr = K >> 3, chunks = M * cpr;  // 16-B chunks
+    // the norm statistic's loads first (wave m < M: row m's K / 16 per-tile sums), so they share the x loads' round trip
+    const int nt = K >> 4;
+    const __amdgpu_buffer_rsrc_t sr = mk_rsrc(a.ssq, (long long)nt * 16);
+    float sv[8];
+    const bool do_rms = rms && w < M;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sv[e] = do_rms ? ld1(sr, (min(lane + 64 * e, nt - 1) * 4 + w) * 4) : 0.f;
     for (int c0 = threadIdx.x; c0 < chunks; c0 += 8 * MK_THREADS) {  // 8 loads in flight per thread
       u32x4 v[8];
 #pragma unroll
@@ -171,23 +221,18 @@ __device__ __attribute__((noinline)) void mk_gemv(const MkArgs& a, const MkLayer
         }
       }
     }
-    if (rms && w < M) {  // wave m: inv_rms of row m from the K / 16 per-tile sums (fixed order)
-      const int nt = K >> 4;
-      const __amdgpu_buffer_rsrc_t sr = mk_rsrc(a.ssq, (long long)nt * 16);
+    if (do_rms) {  // fixed order: lane-strided partials, then the wave's xor tree
       float s = 0.f;
-      for (int t0 = lane; t0 < nt; t0 += 8 * 64) {
-        float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = ld1(sr, (min(t0 + 64 * e, nt - 1) * 4 + w) * 4);
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (t0 + 64 * e < nt) s += v[e];
-      }
+      for (int e = 0; e < 8; ++e)
+        if (lane + 64 * e < nt) s += sv[e];
+      for (int t0 = lane + 512; t0 < nt; t0 += 64) s += ld1(sr, (t0 * 4 + w) * 4);  // (D > 8192 only)
       s = wave_sum(s);
       if (lane == 0) inv_s[w] = rsqrtf(s / (float)K + a.eps);
     }
   }
   __syncthreads();
+  mk_mark(a, epoch, 2);
 
   // ---- stream: fragment i = (tile i / KS, k-step i % KS); the A operand is row (lane & 15) of the staged x
   const int xrow = min(lane & 15, M - 1);
@@ -219,6 +264,7 @@ __device__ __attribute__((noinline)) void mk_gemv(const MkArgs& a, const MkLayer
   mk_wait<0>();
 #pragma unroll
   for (int u = 0; u < MK_U; ++u) mk_pin(ring[u]);
+  mk_mark(a, epoch, 3);
 
   // ---- epilogues. Accumulator layout: lane holds rows 4 (lane >> 4) + i, column lane & 15 (M <= 4: lanes 0..15)
   const int c = lane & 15, r0 = 4 * (lane >> 4);
@@ -293,79 +339,102 @@ __device__ __attribute__((noinline)) void mk_gemv(const MkArgs& a, const MkLayer
     }
   };
 
+  // Batched over the run's (<= MK_NSEG) segments so the round trips overlap: (1) direct epilogues of whole tiles and
+  // the write-through partials of the others, one vmcnt(0); (2) every ticket add issued before any result is used;
+  // (3) each group this wave completed: all contributors' partials loaded together, summed in wave (= K) order.
   const int t_first = hi > lo ? lo / KS : 0;
+  auto seg_v = [&](int s) { return s == 0 ? sa0 : (s == 1 ? sa1 : acc); };
+  auto is_direct = [&](int s) {
+    const int kb = s == 0 ? lo % KS : 0, ke = s == nseg - 1 ? (hi - 1) % KS + 1 : KS;
+    return MODE != MODE_SWIGLU && kb == 0 && ke == KS;
+  };
+  int pend = 0;  // bit s: segment s published a partial
   for (int s = 0; s < nseg; ++s) {
-    const int t = t_first + s;
-    const f32x4 v = s == 0 ? sa0 : (s == 1 ? sa1 : acc);
-    const int kb = s == 0 ? lo % KS : 0;
-    const int ke = s == nseg - 1 ? (hi - 1) % KS + 1 : KS;
-    if (MODE != MODE_SWIGLU && kb == 0 && ke == KS) {
-      epilogue(t, v, v);
-      continue;
+    if (is_direct(s)) {
+      const f32x4 v = seg_v(s);
+      epilogue(t_first + s, v, v);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, seg_v(s)), slr,
+                                             ((gw * MK_NSEG + s) * 64 + lane) * 16, 0, MK_SC1);
+      pend |= 1 << s;
     }
-    // publish the partial, take the group's ticket
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), slr, ((gw * MK_NSEG + s) * 64 + lane) * 16, 0,
-                                           MK_SC1);
+  }
+  if (pend) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int g0 = MODE == MODE_SWIGLU ? (t & ~1) : t, gn = MODE == MODE_SWIGLU ? 2 : 1;
-    int count = 0;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (q < gn) {
+    auto group_of = [&](int s) { return MODE == MODE_SWIGLU ? ((t_first + s) >> 1) : (t_first + s); };
+    auto count_of = [&](int g) {
+      const int g0 = MODE == MODE_SWIGLU ? 2 * g : g, gn = MODE == MODE_SWIGLU ? 2 : 1;
+      int count = 0;
+      for (int q = 0; q < gn; ++q) {
         const long long b0 = (long long)(g0 + q) * KS;
         count += mk_owner(b0 + KS - 1, Wt, P) - mk_owner(b0, Wt, P) + 1;
       }
-    int last = 0;
+      return count;
+    };
+    int lastm = 0;
     if (lane == 0) {
-      int32_t* tk = a.tickets + (MODE == MODE_SWIGLU ? (t >> 1) : t);
-      const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == count - 1;
-      if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    last = __shfl(last, 0, 64);
-    if (!last) continue;
-    // last arriver: every contributor's partial of each tile of the group, summed in wave (= K) order
-    f32x4 sum[2];
+      int prev[MK_NSEG];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (q >= gn) continue;
-      const int tt = g0 + q;
-      const long long b0 = (long long)tt * KS;
-      const int cw0 = mk_owner(b0, Wt, P), cw1 = mk_owner(b0 + KS - 1, Wt, P);
-      for (int e0 = 0; cw0 + e0 <= cw1; e0 += 4) {  // 4 contributors' loads in flight per round
-        u32x4 part[4];
+      for (int s = 0; s < MK_NSEG; ++s)
+        if (pend >> s & 1)
+          prev[s] = __hip_atomic_fetch_add(a.tickets + 32 * group_of(s), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int cw = min(cw0 + e0 + e, cw1);
-          const int sidx = tt - (int)(mk_lo(cw, Wt, P) / KS);
-          part[e] = __builtin_amdgcn_raw_buffer_load_b128(slr, ((cw * MK_NSEG + sidx) * 64 + lane) * 16, 0, MK_SC1);
+      for (int s = 0; s < MK_NSEG; ++s)
+        if ((pend >> s & 1) && prev[s] == count_of(group_of(s)) - 1) {
+          lastm |= 1 << s;
+          __hip_atomic_store(a.tickets + 32 * group_of(s), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (cw0 + e0 + e <= cw1) sum[q] += __builtin_bit_cast(f32x4, part[e]);
-      }
     }
-    epilogue(g0, sum[0], sum[1]);
+    lastm = __shfl(lastm, 0, 64);
+    for (int s = 0; s < nseg; ++s) {
+      if (!(lastm >> s & 1)) continue;
+      const int g = group_of(s);
+      const int g0 = MODE == MODE_SWIGLU ? 2 * g : g, gn = MODE == MODE_SWIGLU ? 2 : 1;
+      f32x4 sum[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (q >= gn) continue;
+        const int tt = g0 + q;
+        const long long b0 = (long long)tt * KS;
+        const int cw0 = mk_owner(b0, Wt, P), cw1 = mk_owner(b0 + KS - 1, Wt, P);
+        for (int e0 = 0; cw0 + e0 <= cw1; e0 += 12) {  // 12 contributors' loads in flight per round
+          u32x4 part[12];
+#pragma unroll
+          for (int e = 0; e < 12; ++e) {
+            const int cw = min(cw0 + e0 + e, cw1);
+            const int sidx = tt - (int)(mk_lo(cw, Wt, P) / KS);
+            part[e] = __builtin_amdgcn_raw_buffer_load_b128(slr, ((cw * MK_NSEG + sidx) * 64 + lane) * 16, 0, MK_SC1);
+          }
+#pragma unroll
+          for (int e = 0; e < 12; ++e)
+            if (cw0 + e0 + e <= cw1) sum[q] += __builtin_bit_cast(f32x4, part[e]);
+        }
+      }
+      epilogue(g0, sum[0], sum[1]);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this phase's write-through stores have landed
+  mk_mark(a, epoch, 4);
 }
 
 // ---- attention phase: (row, kv head, 64-key split) items; REP query heads share each K / V row
 template <int REP>
-__device__ __attribute__((noinline)) void mk_attn(const MkArgs& a, const MkLayer& ly, unsigned epoch, char* lds,
+__device__ __forceinline__ void mk_attn(const MkArgs& a, const MkLayer& ly, unsigned epoch, char* lds,
                                                   int* flag_s) {
   constexpr int HS = MK_DH + 4, PS = REP * HS;
   float (*sm_m)[REP] = reinterpret_cast<float (*)[REP]>(lds);
   float (*sm_l)[REP] = reinterpret_cast<float (*)[REP]>(lds + MK_NW * REP * 4);
   float (*sm_o)[REP][MK_DH] = reinterpret_cast<float (*)[REP][MK_DH]>(lds + 2 * MK_NW * REP * 4);
-  mk_sync(a.bar, epoch * gridDim.x, a.err, (int)epoch);
+  mk_mark(a, epoch, 0);
+  mk_sync(a.bar, epoch, a.err);
+  mk_mark(a, epoch, 1);
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int slot = a.slot[0];
   const int hi = min(slot + 1, a.T);
-  const int nsp = min((hi + MK_CH - 1) / MK_CH, a.max_splits);
+  const int nsp = min((hi + MK_SPK - 1) / MK_SPK, a.max_splits);
   const int Dq = a.H * MK_DH;
   const int items = a.M * a.Hkv * nsp;
   const __amdgpu_buffer_rsrc_t qr = mk_rsrc(a.q, (long long)a.M * Dq * 2);
@@ -374,7 +443,7 @@ __device__ __attribute__((noinline)) void mk_attn(const MkArgs& a, const MkLayer
     const int split = item % nsp, pair = item / nsp;
     const int kvh = pair % a.Hkv, b = pair / a.Hkv;
     const int lo = a.kv_start[b];
-    const int s_lo = lo / MK_CH, s_hi = hi > lo ? (hi + MK_CH - 1) / MK_CH : s_lo;
+    const int s_lo = lo / MK_SPK, s_hi = hi > lo ? (hi + MK_SPK - 1) / MK_SPK : s_lo;
     const int n_act = s_hi - s_lo;
     const int h0 = kvh * REP;
     auto store_out = [&](int hh, int d, const float* v) {
@@ -391,51 +460,65 @@ __device__ __attribute__((noinline)) void mk_attn(const MkArgs& a, const MkLayer
     }
     if (split < s_lo || split >= s_hi) continue;  // (workgroup-uniform)
 
-    const int c0 = split * MK_CH;
+    const int c0 = split * MK_SPK;
     const long long cache_bytes = (long long)MK_DH * 2 * a.T;
     const size_t head = ((size_t)b * a.Hkv + kvh) * a.T * MK_DH;
     const __amdgpu_buffer_rsrc_t kr_ = mk_rsrc(ly.kc + head, cache_bytes), vr_ = mk_rsrc(ly.vc + head, cache_bytes);
-    u32x4 kr[MK_KPG], vr[MK_KPG], qv[REP];
+    // every K / V row of the split at once (one memory round trip); key of (chunk c, r) for this lane group:
+    // c0 + 64 c + 32 r + 4 w + g (rows past the valid range re-read a valid one and are masked)
+    const int nch = min(MK_ACH, (hi - c0 + MK_CH - 1) / MK_CH);  // chunks of this split holding keys
+    u32x4 kr[MK_ACH][MK_KPG], vr[MK_ACH][MK_KPG], qv[REP];
 #pragma unroll
-    for (int r = 0; r < MK_KPG; ++r) {
-      const int jc = min(max(c0 + 16 * r + 4 * w + g, lo), hi - 1);
-      kr[r] = __builtin_amdgcn_raw_buffer_load_b128(kr_, (jc * MK_DH + 8 * li) * 2, 0, MK_SC1);
-      vr[r] = __builtin_amdgcn_raw_buffer_load_b128(vr_, (jc * MK_DH + 8 * li) * 2, 0, MK_SC1);
-    }
+    for (int c = 0; c < MK_ACH; ++c)
+#pragma unroll
+      for (int r = 0; r < MK_KPG; ++r) {
+        const int jc = min(max(c0 + MK_CH * c + 4 * MK_NW * r + 4 * w + g, lo), hi - 1);
+        if (c < nch) {
+          kr[c][r] = __builtin_amdgcn_raw_buffer_load_b128(kr_, (jc * MK_DH + 8 * li) * 2, 0, MK_SC1);
+          vr[c][r] = __builtin_amdgcn_raw_buffer_load_b128(vr_, (jc * MK_DH + 8 * li) * 2, 0, MK_SC1);
+        }
+      }
 #pragma unroll
     for (int hh = 0; hh < REP; ++hh)
       qv[hh] = __builtin_amdgcn_raw_buffer_load_b128(qr, (b * Dq + (h0 + hh) * MK_DH + 8 * li) * 2, 0, MK_SC1);
 
-    float sc[REP][MK_KPG];
-#pragma unroll
-    for (int r = 0; r < MK_KPG; ++r) {
-      const int j = c0 + 16 * r + 4 * w + g;
-      const bool valid = j >= lo && j < hi;
-#pragma unroll
-      for (int hh = 0; hh < REP; ++hh) {
-        const float d = row16_sum(dot8_bf16(qv[hh], kr[r], 0.f)) * a.scale;
-        sc[hh][r] = valid ? d : -INFINITY;
-      }
-    }
+    // per wave and head: online softmax over the chunks -- the running max wave-uniform, (l, o) lane-partial over the
+    // lane group's keys, summed over the 4 groups once at the end
 #pragma unroll
     for (int hh = 0; hh < REP; ++hh) {
-      float mx = sc[hh][0];
+      float mr = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 1; r < MK_KPG; ++r) mx = fmaxf(mx, sc[hh][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      float l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (mx != -INFINITY) {
+      for (int c = 0; c < MK_ACH; ++c) {
+        if (c >= nch) continue;  // (wave-uniform)
+        float sc[MK_KPG];
+        float mx = -INFINITY;
 #pragma unroll
         for (int r = 0; r < MK_KPG; ++r) {
-          const float p = sc[hh][r] == -INFINITY ? 0.f : __expf(sc[hh][r] - mx);
+          const int j = c0 + MK_CH * c + 4 * MK_NW * r + 4 * w + g;
+          const float d = row16_sum(dot8_bf16(qv[hh], kr[c][r], 0.f)) * a.scale;
+          sc[r] = (j >= lo && j < hi) ? d : -INFINITY;
+          mx = fmaxf(mx, sc[r]);
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        if (mx == -INFINITY) continue;  // no valid key in this chunk (wave-uniform)
+        const float mn = fmaxf(mr, mx);
+        const float al = mr == -INFINITY ? 0.f : __expf(mr - mn);
+        l *= al;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] *= al;
+        mr = mn;
+#pragma unroll
+        for (int r = 0; r < MK_KPG; ++r) {
+          const float p = sc[r] == -INFINITY ? 0.f : __expf(sc[r] - mn);
           l += p;
           float vf[8];
-          unpack8(vr[r], vf);
+          unpack8(vr[c][r], vf);
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] += p * vf[e];
         }
       }
+      const float mx = mr;
       l += __shfl_xor(l, 16, 64);
       l += __shfl_xor(l, 32, 64);
 #pragma unroll
@@ -491,7 +574,7 @@ __device__ __attribute__((noinline)) void mk_attn(const MkArgs& a, const MkLayer
     __syncthreads();  // LDS scores consumed; every storing wave drained
     if (n_act == 1) continue;
     if (threadIdx.x == 0) {
-      int32_t* tk = a.atk + (size_t)b * a.Hkv + kvh;
+      int32_t* tk = a.atk + 32 * ((size_t)b * a.Hkv + kvh);
       const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = prev == n_act - 1;
       if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -532,6 +615,7 @@ __device__ __attribute__((noinline)) void mk_attn(const MkArgs& a, const MkLayer
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mk_mark(a, epoch, 4);
 }
 
 template <int REP>
@@ -587,7 +671,9 @@ static int mk_num_cus() {
 
 int decode_mk_grid() { return mk_num_cus(); }
 size_t decode_mk_slab_floats() { return (size_t)mk_num_cus() * MK_NW * MK_NSEG * 256; }
-int decode_mk_max_splits(int T) { return (T + MK_CH - 1) / MK_CH; }
+int decode_mk_max_splits(int T) { return (T + MK_SPK - 1) / MK_SPK; }
+int decode_mk_bar_words() { return MK_BAR_WORDS; }
+int decode_mk_trace_words() { return MK_TRACE_PH * MK_TRACE_EV * mk_num_cus() * MK_NW; }
 
 // Whether one GEMV phase fits the kernel's plan: <= MK_NSEG tiles per wave run, x rows in the LDS staging area.
 static bool mk_phase_ok(int M, int N, int K, int G) {
@@ -613,12 +699,12 @@ int decode_mk(const void* layers, int L, int M, int D, int H, int Hkv, int F, in
               bf16_t* q, bf16_t* att, bf16_t* act, float* ssq, const float2* rope, int rope_len,
               const int32_t* positions, const int32_t* slot, const int32_t* kv_start, float* slab, size_t slab_floats,
               int32_t* tickets, int n_tickets, unsigned* bar, int32_t* err, float* aws, size_t aws_floats, int32_t* atk,
-              hipStream_t s) {
+              unsigned long long* trace, int prefetch_late, hipStream_t s) {
   if (!decode_mk_supported(M, D, H, Hkv, MK_DH, F)) return -1;
   const int rep = H / Hkv;
   const int max_splits = decode_mk_max_splits(T);
   const int NTmax = max((H + 2 * Hkv) * MK_DH, max(2 * F, D)) >> 4;
-  if (slab_floats < decode_mk_slab_floats() || n_tickets < NTmax ||
+  if (slab_floats < decode_mk_slab_floats() || n_tickets < 32 * NTmax ||
       aws_floats < (size_t)M * Hkv * max_splits * rep * (MK_DH + 4))
     return -3;
   MkArgs a{};
@@ -650,7 +736,9 @@ int decode_mk(const void* layers, int L, int M, int D, int H, int Hkv, int F, in
   a.aws = aws;
   a.atk = atk;
   a.max_splits = max_splits;
-  if (hipMemsetAsync(bar, 0, sizeof(unsigned), s) != hipSuccess) return -2;
+  a.trace = trace;
+  a.prefetch_late = prefetch_late;
+  if (hipMemsetAsync(bar, 0, MK_BAR_WORDS * sizeof(unsigned), s) != hipSuccess) return -2;
   decode_mk_ssq_kernel<<<D / 16, 64, 0, s>>>(hb, ssq, M, D);
   JLA_CHECK_LAUNCH();
   const int G = mk_num_cus();

@@ -138,11 +138,13 @@ int decode_mk_supported(int M, int D, int H, int Hkv, int Dh, int F);
 int decode_mk_grid();
 size_t decode_mk_slab_floats();
 int decode_mk_max_splits(int T);
+int decode_mk_bar_words();    // phase-barrier words (zeroed by decode_mk before each launch)
+int decode_mk_trace_words();  // optional per-phase timestamp buffer (u64)
 int decode_mk(const void* layers, int L, int M, int D, int H, int Hkv, int F, int T, float eps, float* h, bf16_t* hb,
               bf16_t* q, bf16_t* att, bf16_t* act, float* ssq, const float2* rope, int rope_len,
               const int32_t* positions, const int32_t* slot, const int32_t* kv_start, float* slab, size_t slab_floats,
               int32_t* tickets, int n_tickets, unsigned* bar, int32_t* err, float* aws, size_t aws_floats, int32_t* atk,
-              hipStream_t s);  // 1: attn_decode can also write the packed-layout output
+              unsigned long long* trace, int prefetch_late, hipStream_t s);  // 1: attn_decode can also write the packed-layout output
 void attn_prefill_set_impl(int impl);  // 2 = GQA-shared MFMA 32x32 flash kernel (default), 1 = v1
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,

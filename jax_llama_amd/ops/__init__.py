@@ -695,6 +695,8 @@ def topk_sample(logits: torch.Tensor, k: int, temperature: float, top_p: float, 
 # JLA_DECODE_MK=0: the per-layer kernels (A/B).
 DECODE_MK = os.environ.get("JLA_DECODE_MK", "0") != "0"
 DECODE_MK_MAX_M = 4
+DECODE_MK_PREFETCH_LATE = 0  # A/B: next-phase ring loads after the phase barrier instead of before
+DECODE_MK_TRACE = None  # tools: an int64 tensor of ext().decode_mk_trace_words() -> per-phase timestamps of layers 0-1
 
 
 def decode_mk_ok(model, rows: int, seq_len: int, key_mask) -> bool:
@@ -741,15 +743,16 @@ def decode_layers(model, h: torch.Tensor, hb: torch.Tensor, positions: torch.Ten
     table = _decode_mk_table(model, cache)
     slab_floats, splits = e.decode_mk_workspace(T)
     ws = workspace
-    nt = max((H + 2 * Hkv) * dh, 2 * F, c.hidden_size) // 16
+    nt = 32 * max((H + 2 * Hkv) * dh, 2 * F, c.hidden_size) // 16  # one ticket per 128-B line
     e.decode_mk(table, h, hb,
                 ws.get("mk_q", m * H * dh, BF16, dev), ws.get("mk_att", m * H * dh, BF16, dev),
                 ws.get("mk_act", m * F, BF16, dev), ws.get("mk_ssq", c.hidden_size // 16 * 4, torch.float32, dev),
                 model.rope, positions.reshape(-1).to(torch.int32), _slot_tensor(slot0, dev), kv_start, cache.k,
                 ws.get("mk_slab", slab_floats, torch.float32, dev), ws.get_zeroed("mk_tickets", nt, torch.int32, dev),
-                ws.get("mk_bar", 1, torch.int32, dev), ws.get_zeroed("mk_err", 1, torch.int32, dev),
+                ws.get("mk_bar", 32 * 17, torch.int32, dev), ws.get_zeroed("mk_err", 1, torch.int32, dev),
                 ws.get("mk_aws", m * Hkv * splits * (H // Hkv) * (dh + 4), torch.float32, dev),
-                ws.get_zeroed("mk_atk", m * Hkv, torch.int32, dev), H, Hkv, F, float(model.eps))
+                ws.get_zeroed("mk_atk", 32 * m * Hkv, torch.int32, dev), H, Hkv, F, float(model.eps),
+                trace=DECODE_MK_TRACE, prefetch_late=DECODE_MK_PREFETCH_LATE)
 
 
 def decode_mk_error(device) -> int:

@@ -41,6 +41,7 @@ def test_decode_mk_matches_layer_kernels_and_oracle(lens, monkeypatch):
     _, oracle, _, params = build(cfg, seed=21)
     model = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).load_params(params)
     toks, mask = left_padded_batch(lens, 9, cfg.vocab_size, pad=2, seed=22)
+    monkeypatch.setattr(ops, "DECODE_MK", True)
     assert ops.decode_mk_ok(model, len(lens), 1, None)
     lm, hm, km, nxt = _decode_once(model, toks, mask, True, monkeypatch)
     assert ops.decode_mk_error(DEV) == 0
@@ -58,7 +59,8 @@ def test_decode_mk_matches_layer_kernels_and_oracle(lens, monkeypatch):
     assert rel_err(lm, lo) < 5e-2, rel_err(lm, lo)
 
 
-def test_decode_mk_graph_replay_matches_eager():
+def test_decode_mk_graph_replay_matches_eager(monkeypatch):
+    monkeypatch.setattr(ops, "DECODE_MK", True)
     cfg = gpu_config(num_hidden_layers=2)
     _, _, _, params = build(cfg, seed=23)
     model = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).load_params(params)
@@ -91,6 +93,7 @@ def test_decode_mk_llama3_8b_dims(batch, monkeypatch):
     from jax_llama_amd.config import get_preset
     cfg = get_preset("llama3-8b", num_hidden_layers=2, max_seq_len=512)
     model = LLaMAForCausalLM(cfg, device=DEV, _do_init=False).init_random(seed=3)
+    monkeypatch.setattr(ops, "DECODE_MK", True)
     assert ops.decode_mk_ok(model, batch, 1, None)
     g = torch.Generator().manual_seed(5)
     toks = torch.randint(0, cfg.vocab_size, (batch, 200), generator=g, dtype=torch.int32)

@@ -152,27 +152,22 @@ jla::bf16_t* packed_ptr(const c10::optional<Tensor>& t, int64_t m, int64_t cols,
   return bf(*t);
 }
 
-// Decode linear dispatch. variant: 0 = auto (M == 1 -> K-split GEMV, else split-K skinny GEMM),
-// 1/2/3 = K-split GEMV (gemv.hip) with 4/8/16 waves, 4 = split-K skinny GEMM (skinny.hip), 5/6/8-11 = GEMV
-// tile / wave / ring-depth variants (gemv.hip dispatch_nt).
+// Decode linear dispatch (gemv.hip dispatch_nt). variant: 0 / 1 = K-split GEMV (4 waves at M <= 16), 5 / 6 = 4 / 2
+// tiles per workgroup, 10 = 2 tiles with a doubled ring, 20 = 2 tiles x 8 waves, 16 = split-K GEMV, packed-x 12 / 15 /
+// 18 / 21 / 22 / 26 (variant ids of removed forms are not reused: profiles/r4_variant_pruning.md).
 void run_skinny(const Tensor& x, const Tensor& w, int64_t n, int64_t k, void* out, int64_t mode, double rms_eps,
                 bool accumulate, bool out_f32, const jla::QKVArgs* qa, int64_t variant, const Tensor& ws,
                 const Tensor& tickets, const jla::bf16_t* x_packed = nullptr) {
   const int64_t m = x.size(0);
   const bool f32 = x.scalar_type() == torch::kFloat32;
-  if (variant == 0) variant = (m == 1) ? 1 : 4;
+  if (variant == 0) variant = 1;
   const bool xp_variant = jla::gemv_xp_variant((int)variant);
-  check(xp_variant == (x_packed != nullptr), "packed-x variants (12-15, 18, 19, 21-23, 26) need x_packed, the others must not");
+  check(xp_variant == (x_packed != nullptr), "packed-x variants (12, 15, 18, 21, 22, 26) need x_packed, the others must not");
   check(!xp_variant || !f32, "packed-x variants read bf16 activations");
-  check(!(xp_variant && mode == 2 && (variant == 12 || variant == 14)), "SwiGLU packed-x variants: 13 / 15");
-  if (variant == 4) {
-    check_gpu(ws, "ws");
-    check_gpu(tickets, "tickets");
-    check(ws.scalar_type() == torch::kFloat32 && tickets.scalar_type() == torch::kInt32, "ws/tickets dtypes");
-    rc(jla::linear_splitk(x.data_ptr(), f32, w.data_ptr(), out, m, n, k, mode, (float)rms_eps, accumulate, out_f32, qa,
-                          ptr<float>(ws), ws.numel(), ptr<int32_t>(tickets), tickets.numel(), stream()),
-       "linear_splitk");
-  } else {
+  check(!(xp_variant && mode == 2 && variant == 12), "SwiGLU packed-x variants: 15, 18, 21, 22, 26");
+  check(variant == 1 || variant == 5 || variant == 6 || variant == 10 || variant == 16 || variant == 20 || xp_variant,
+        "unknown decode GEMV variant");
+  {
     jla::QKVArgs qs = *qa;
     if (jla::gemv_split_variant((int)variant)) {
       // split-K GEMV: partial slabs + self-resetting tickets (the shared skinny workspace, sized for both)
@@ -208,7 +203,7 @@ void linear_skinny(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t
   // packed copy of the bf16 output (the residual's mirror / the SwiGLU activation): GEMV variants only
   qa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
   check(!qa.pack || (mode == 1 || mode == 2), "pack_out: residual (mirror) or SwiGLU output only");
-  check(!qa.pack || (variant != 0 && variant != 4 && variant != 7), "pack_out: GEMV variants only");
+  check(!qa.pack || (variant != 0 && variant != 7), "pack_out: GEMV variants only");
   check(!qa.pack || mode != 1 || qa.res_bf16, "pack_out of a residual needs the mirror");
   run_skinny(x, w, n, k, out.data_ptr(), mode, rms_eps, accumulate, out.scalar_type() == torch::kFloat32, &qa,
              variant, ws, tickets, packed_ptr(x_packed, m, k, "x_packed"));
@@ -224,7 +219,7 @@ void linear_skinny_argmax(Tensor x, Tensor w, int64_t n, int64_t k, double rms_e
         "x must be fp32/bf16 [M, K]");
   const int64_t m = x.size(0);
   check(m <= SKINNY_MAX_M, "linear_skinny_argmax: M too large");
-  check(variant == 1 || variant == 2 || variant == 3 || (variant >= 5 && variant <= 11 && variant != 7) || variant == 20,
+  check(variant == 1 || variant == 5 || variant == 6 || variant == 10 || variant == 20,
         "argmax: GEMV variants only (row-major x)");
   check_gpu(part, "part");
   check(part.scalar_type() == torch::kFloat32 && part.numel() >= m * (n / 16) * 2, "argmax partials too small");
@@ -240,11 +235,11 @@ void linear_skinny_argmax(Tensor x, Tensor w, int64_t n, int64_t k, double rms_e
   rc(jla::argmax_partials(ptr<float>(part), n / 16, m, ptr<int32_t>(idx), ptr<float>(val), stream()), "argmax_partials");
 }
 
-// the decode workspace shared by the split-K skinny GEMM (variant 4) and the split-K GEMV variants (16-19)
+// the decode workspace of the split-K GEMV variants (16 / 18 / 26): partial slabs + tickets
 py::tuple skinny_workspace(int64_t m, int64_t n, int64_t k, int64_t mode) {
-  return py::make_tuple((int64_t)std::max(jla::skinny_workspace_floats(m, n, k, mode),
-                                          jla::gemv_split_workspace_floats(m, n)),
-                        (int64_t)std::max(jla::skinny_tickets(m, n, k, mode), jla::gemv_split_tickets(n)));
+  (void)k;
+  (void)mode;
+  return py::make_tuple((int64_t)jla::gemv_split_workspace_floats(m, n), (int64_t)jla::gemv_split_tickets(n));
 }
 
 // RoPE + KV-cache epilogue arguments of the fused qkv projection (validated here)
@@ -819,7 +814,7 @@ void linear_tp_residual(int64_t state, Tensor x, Tensor w, int64_t n, int64_t k,
   qa.res_bf16 = bf(hb);
   qa.pack = packed_ptr(hb_pack, m, n, "hb_pack");
   qa.tp = jla::car_device(st);
-  // split-K variants (16-19) take the shared decode workspace: only the last arriver of a column group exchanges
+  // split-K variants (16 / 18 / 26) take the shared decode workspace: only the last arriver of a column group exchanges
   run_skinny(x, w, n, k, h.data_ptr(), MODE_TPRESID_ID, -1.0, true, true, &qa, variant, ws ? *ws : Tensor(),
              tickets ? *tickets : Tensor(), packed_ptr(x_packed, m, k, "x_packed"));
 }
@@ -903,9 +898,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm_argmax", &gemm_argmax, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("ws"),
         py::arg("rms_eps"), py::arg("idx"), py::arg("val"), py::arg("rms_ws") = py::none());
   m.def("gemm_argmax_workspace", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_argmax_workspace_floats(m, n); });
-  m.def("gemm_set_impl", [](int64_t impl) { jla::gemm_set_impl(impl); });
-  m.def("gemm_get_impl", []() { return jla::gemm_get_impl(); });
-  m.def("skinny_set_plan", [](int64_t nt, int64_t ks) { jla::skinny_set_plan((int)nt, (int)ks); });
   m.def("gemm_ksplit", [](int64_t m, int64_t n, int64_t k) { return jla::gemm_ksplit(m, n, k); });
   m.def("rope_kv_write", &rope_kv_write);
   m.def("attn_set_impl", [](int64_t impl, int64_t waves_target) { jla::attn_set_impl(impl, waves_target); },
@@ -925,7 +917,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("bounds_error", [](bool reset) {
     const int r = reset ? 1 : 0;
     return (int64_t)(jla::jla_bounds_norm_embed(r) | jla::jla_bounds_rope_kv(r) | jla::jla_bounds_sample(r) |
-                     jla::jla_bounds_gemm(r) | jla::jla_bounds_gemv(r) | jla::jla_bounds_skinny(r) |
+                     jla::jla_bounds_gemm(r) | jla::jla_bounds_gemv(r) |
                      jla::jla_bounds_attn_decode(r) | jla::jla_bounds_attn_prefill(r));
   }, "OR of the bounds-checked debug build's error words (JLA_BOUNDS_* bits); always 0 in a release build",
         py::arg("reset") = false);

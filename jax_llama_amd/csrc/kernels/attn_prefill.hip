@@ -213,25 +213,25 @@ JLA_DEV u32x2 ld_tr(const char* lds, int off) {
                                        (__attribute__((address_space(3))) s16x4*)(lds + off)));
 }
 
-// QB query blocks of 32 per wave (QB = 2: "v3", 64 queries per wave): every K fragment (ds_read_b128) and V^T
-// fragment (2 x ds_read_b64_tr_b16) read from LDS feeds QB MFMAs instead of one. With QB = 1 four waves x two
-// workgroups re-read each 32-KiB K/V tile per 32 MFMAs per wave -- about the LDS read rate; QB = 2 halves the
-// LDS bytes per MFMA at the price of one workgroup per CU (O^T, S^T, Q^T and P for 64 queries: ~340 registers).
+// One query block of 32 per wave (a 64-query "QB = 2" form halved the LDS bytes per MFMA but needed ~340 registers,
+// one workgroup per CU, and ran 1.4-2x slower: profiles/r2_attn_prefill_qb2_ab.jsonl -- removed).
 //
-// PIPE (QB = 1): the scores of tile i+1 are issued before the softmax of tile i, so one wave's MFMA pipe works
+// PIPE: the scores of tile i+1 are issued before the softmax of tile i, so one wave's MFMA pipe works
 // through S(i+1) while its VALU runs exp / sum / pack of tile i (independent instructions in one basic block).
 // K and V each get a 2-slot LDS ring (64 KiB per workgroup): K(i+1) and V(i) are resident during tile i while
 // the registers stage K(i+2) and V(i+1) into the slots freed by tile i-1, so each tile ends with ONE barrier.
-// LAZY: the running max (and with it the O / l rescale) moves only when a lane's tile max exceeds it by more
-// than 8 (log2 units): exp2 of the rest stays <= 256, exact in fp32 and bf16-representable for P; the 64 O
-// multiplies per tile run only in a wave-uniform branch when some lane needs them (mostly the first tiles).
-template <int NW, int QB, int PIPE = 0, int LAZY = 0>
-__global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
+// Lazy rescale (every launch): the running max (and with it the O / l rescale) moves only when a lane's tile max
+// exceeds it by more than 8 (log2 units): exp2 of the rest stays <= 256, exact in fp32 and bf16-representable for P;
+// the 64 O multiplies per tile run only in a wave-uniform branch when some lane needs them (mostly the first tiles).
+// (The eager-rescale launches, impls 4 / 5 / 6 / 10, were slower everywhere and removed in round 4:
+// profiles/r3_attn_prefill_pipe_ab.jsonl, profiles/r4_variant_pruning.md.)
+template <int NW, int PIPE>
+__global__ void __launch_bounds__(NW * 64, 2)
     attn_prefill_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                            const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
                            const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out, int S, int H,
                            int Hkv, int T, float scale_log2, int npb, int hgroups, int n_qb, int split) {
-  static_assert(!PIPE || QB == 1, "the pipelined loop holds one query block per wave");
+  constexpr int QB = 1;  // query blocks of 32 per wave
   constexpr int NT = NW * 64;
   constexpr int TILE_BYTES = FA_KT * AP_DH * 2;            // 16 KiB
   constexpr int CH_PER_T = FA_KT * 16 / NT;                 // 16-byte chunks per thread per tile (K or V)
@@ -490,21 +490,17 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
             tmax = fmaxf(tmax, v);
           }
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        if constexpr (LAZY) {
-          if (__ballot(tmax > m_run[qq] + 8.f)) {
-            const float m_new = fmaxf(m_run[qq], tmax);
-            const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - (m_new == -INFINITY ? 0.f : m_new));
-            l_run[qq] *= alpha;
-            m_run[qq] = m_new;
+        if (__ballot(tmax > m_run[qq] + 8.f)) {
+          const float m_new = fmaxf(m_run[qq], tmax);
+          const float alpha = __builtin_amdgcn_exp2f(m_run[qq] - (m_new == -INFINITY ? 0.f : m_new));
+          l_run[qq] *= alpha;
+          m_run[qq] = m_new;
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
+          for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-              for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
-          }
+            for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
         }
-        const float m_new = LAZY ? m_run[qq] : fmaxf(m_run[qq], tmax);
-        const float m_use = m_new == -INFINITY ? 0.f : m_new;
-        const float alpha = LAZY ? 1.f : __builtin_amdgcn_exp2f(m_run[qq] - m_use);  // m_run = -inf -> 0
+        const float m_use = m_run[qq] == -INFINITY ? 0.f : m_run[qq];
         float rs = 0.f;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -517,14 +513,7 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
           pf[qq][s] = pack8(e);
         }
         rs += __shfl_xor(rs, 32, 64);
-        l_run[qq] = l_run[qq] * alpha + rs;
-        m_run[qq] = m_new;
-        if constexpr (!LAZY) {
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) o[qq][dt][i] *= alpha;
-        }
+        l_run[qq] += rs;
       }
       // ---- O^T += V^T P^T; A element j of lane half hi = V[key 16 s + 8 (j >> 2) + 4 hi + (j & 3)][d]
 #pragma unroll
@@ -570,12 +559,9 @@ __global__ void __launch_bounds__(NW * 64, QB == 1 ? 2 : 1)
   }  // pass
 }
 
-static int g_attn_prefill_impl = 2;
-void attn_prefill_set_impl(int impl) { g_attn_prefill_impl = impl; }
-
 // v2 launch with NW waves per workgroup: NW / rep position blocks (rep < NW) or NW of the rep q heads (rep >= NW) share
-// each K/V tile the workgroup stages; `paired_only`: always the (heavy, light) pair per workgroup (impl 4 / 6)
-template <int NW, int PIPE = 0, int LAZY = 0>
+// each K/V tile the workgroup stages; `paired_only`: always the (heavy, light) pair per workgroup
+template <int NW, int PIPE>
 static void launch_prefill_v2(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot,
                               const int32_t* kv_start, const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S,
                               int H, int Hkv, int T, int rep, bool paired_only, hipStream_t s) {
@@ -589,14 +575,19 @@ static void launch_prefill_v2(const bf16_t* q, const bf16_t* kc, const bf16_t* v
   // holds two resident workgroups instead of one
   const bool split = !paired_only && pairs < 2 * 256;
   if (split) {
-    attn_prefill_v2_kernel<NW, 1, PIPE, LAZY><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
+    attn_prefill_v2_kernel<NW, PIPE><<<dim3(2 * pairs, 1, 1), NW * 64, 0, s>>>(
         q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H, Hkv, T, sl2, npb, hgroups, n_qb, 1);
   } else {
     dim3 grid2((n_qb + 1) / 2, Hkv * hgroups, B);  // a (heavy, light) pair of query blocks per workgroup
-    attn_prefill_v2_kernel<NW, 1, PIPE, LAZY><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S, H,
-                                                             Hkv, T, sl2, npb, hgroups, n_qb, 0);
+    attn_prefill_v2_kernel<NW, PIPE><<<grid2, NW * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, S,
+                                                                H, Hkv, T, sl2, npb, hgroups, n_qb, 0);
   }
 }
+
+// impl (attn_prefill_set_impl, A/B): 2 = default dispatch; 7 = pipelined 4 waves, 8 = unpipelined 4 waves, 9 =
+// pipelined 8 waves (paired); 1 = the v1 kernel (also the fallback for a non-power-of-two GQA ratio)
+static int g_attn_prefill_impl = 2;
+void attn_prefill_set_impl(int impl) { g_attn_prefill_impl = impl; }
 
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,
@@ -606,12 +597,11 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   const int rep = H / Hkv;
   const bool pow2rep = rep == 1 || rep == 2 || rep == 4 || rep == 8;
   int impl = g_attn_prefill_impl;
-  // default (impl 2): lazy rescale everywhere; the software-pipelined loop from S = 512 (a query block needs a few
-  // tiles to pipeline), with 8 waves per workgroup when that paired grid still fills the CUs (>= 256 workgroups:
-  // twice the queries per staged K/V tile), else 4 waves. Interleaved A/B (profiles/r3_attn_prefill_pipe_ab.jsonl,
-  // TFLOP/s, previous default -> now): 8B B = 1 S = 2048 454 -> 509, B = 16 S = 2048 672 -> 746, S = 8192 854 -> 903,
-  // B = 2048 S = 128 186 -> 198, 70B S = 2048 698 -> 733, 7B (MHA) B = 16 615 -> 651.
-  // impl 10: the previous default dispatch (A/B); 4 / 5 / 6: the unpipelined 4 / 8-wave launches
+  // default (impl 2): the software-pipelined loop from S = 512 (a query block needs a few tiles to pipeline), with 8
+  // waves per workgroup when that paired grid still fills the CUs (>= 256 workgroups: twice the queries per staged
+  // K/V tile), else 4 waves; below S = 512 the unpipelined 4-wave loop. Interleaved A/B
+  // (profiles/r3_attn_prefill_pipe_ab.jsonl, TFLOP/s, previous default -> now): 8B B = 1 S = 2048 454 -> 509,
+  // B = 16 S = 2048 672 -> 746, S = 8192 854 -> 903, B = 2048 S = 128 186 -> 198, 70B S = 2048 698 -> 733.
   if (impl == 2 && pow2rep) {
     if (S <= 256) {
       impl = 8;
@@ -622,28 +612,13 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
       impl = wg8 >= 256 ? 9 : 7;
     }
   }
-  if (impl == 10) impl = 2;
-  // impl 2 here (previous default) / 4 (always paired): 4 waves per workgroup; 5 / 6: the same with 8 waves. The
-  // previous default takes the 8-wave paired launch for long prompts and rep >= 8
-  const bool auto8 = impl == 2 && pow2rep && (S >= 4096 || (rep >= 8 && S >= 1024));
-  const bool eight = impl == 5 || impl == 6 || auto8;
-  const int nw = eight ? 8 : 4;
-  // impl 7 / 9: the software-pipelined loop with lazy rescale (4 / 8 waves), 8: lazy rescale only
   if ((impl == 7 || impl == 8 || impl == 9) && (rep % (impl == 9 ? 8 : 4) == 0 || (impl == 9 ? 8 : 4) % rep == 0)) {
     if (impl == 7)
-      launch_prefill_v2<4, 1, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
+      launch_prefill_v2<4, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
     else if (impl == 8)
-      launch_prefill_v2<4, 0, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
+      launch_prefill_v2<4, 0>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
     else
-      launch_prefill_v2<8, 1, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, true, s);
-    JLA_CHECK_LAUNCH();
-    return 0;
-  }
-  if ((impl == 2 || impl == 4 || eight) && (rep % nw == 0 || nw % rep == 0)) {
-    if (eight)
-      launch_prefill_v2<8>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, impl != 5, s);
-    else
-      launch_prefill_v2<4>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, impl == 4, s);
+      launch_prefill_v2<8, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, true, s);
     JLA_CHECK_LAUNCH();
     return 0;
   }

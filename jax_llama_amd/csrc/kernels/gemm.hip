@@ -22,149 +22,7 @@
 
 namespace jla {
 
-constexpr int GB_M = 128, GB_N = 128;
-constexpr int G_THREADS = 256;
-// fragments per stage: A 8 m-tiles x 2 k-steps, B 8 n-tiles x 2 k-steps (1 KiB each)
-constexpr int G_AFR = 16, G_BFR = 16;
-constexpr int G_STAGE_U4 = (G_AFR + G_BFR) * 64;  // u32x4 per stage (32 KiB); 8 per thread
-constexpr int MODE_PARTIAL = 7;                   // split-K: fp32 partial tile to the workspace
-
-template <int MODE>
-__global__ void __launch_bounds__(G_THREADS)
-    gemm_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc) {
-  __shared__ u32x4 lds[2][G_STAGE_U4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 1, wc = w & 1;
-  const int n0 = blockIdx.x * GB_N, m0 = blockIdx.y * GB_M;
-  const int KS = K >> 5, NTT = N >> 4;
-  const int ks0 = blockIdx.z * kc;                  // this split's k-steps [ks0, ks_end)
-  const int ks_end = min(KS, ks0 + kc);
-  const int KT = (ks_end - ks0 + 1) >> 1;           // stages of 2 k-steps (last may be half)
-
-  // per-thread staging slots: fragment f = tid/64 + 4*j (j = 0..3), lane = tid & 63
-  // A fragments f (mt = f>>1, ks = f&1); B fragments f (nt = f>>1, ks = f&1)
-  const bf16_t* asrc[4];
-  const u32x4* bsrc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int f = w + 4 * j;
-    const int mt = f >> 1, ks = f & 1;
-    const int row = min(m0 + mt * 16 + (lane & 15), M - 1);
-    asrc[j] = x + (size_t)row * K + (size_t)(ks0 + ks) * 32 + 8 * (lane >> 4);
-    const int nt = min((n0 >> 4) + (f >> 1), NTT - 1);
-    bsrc[j] = W + ((size_t)nt * KS + ks0 + ks) * 64 + lane;
-  }
-
-  u32x4 stage[8];
-  auto gload = [&](int kt) {
-    const int kbase = kt * 2;
-    if (ks0 + kbase + 1 < ks_end) {  // uniform branch: only a split's last stage can be half
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        stage[j] = *reinterpret_cast<const u32x4*>(asrc[j] + (size_t)kbase * 32);
-        stage[4 + j] = bsrc[j][(size_t)kbase * 64];
-      }
-    } else {
-      // this thread's fragments all have ks == (w & 1); ks == 1 is past the end -> zeros
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        stage[j] = u32x4{0, 0, 0, 0};
-        stage[4 + j] = u32x4{0, 0, 0, 0};
-      }
-      if ((w & 1) == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          stage[j] = *reinterpret_cast<const u32x4*>(asrc[j] + (size_t)kbase * 32);
-          stage[4 + j] = bsrc[j][(size_t)kbase * 64];
-        }
-      }
-    }
-  };
-  auto swrite = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lds[buf][(w + 4 * j) * 64 + lane] = stage[j];
-      lds[buf][(G_AFR + w + 4 * j) * 64 + lane] = stage[4 + j];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < KT) gload(kt + 1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      u32x4 a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = lds[buf][((wr * 4 + i) * 2 + ks) * 64 + lane];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = lds[buf][(G_AFR + (wc * 4 + j) * 2 + ks) * 64 + lane];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
-    }
-    if (kt + 1 < KT) swrite(buf ^ 1);
-    __syncthreads();
-  }
-
-  // epilogue: lane holds C[4*(lane>>4) + r][lane & 15] of each 16x16 tile
-  const int c = lane & 15;
-  if constexpr (MODE == MODE_SWIGLU) {
-    const int F = N >> 1;
-    bf16_t* o = static_cast<bf16_t*>(out);
-#pragma unroll
-    for (int j = 0; j < 4; j += 2) {
-      const int gtile = (n0 >> 4) + wc * 4 + j;  // even
-      if (gtile >= NTT) continue;
-      const int col = (gtile >> 1) * 16 + c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + (wr * 4 + i) * 16 + 4 * (lane >> 4) + r;
-          if (row < M) o[(size_t)row * F + col] = f2bf(silu(acc[i][j][r]) * acc[i][j + 1][r]);
-        }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int tile = (n0 >> 4) + wc * 4 + j;
-      if (tile >= NTT) continue;
-      const int col = tile * 16 + c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + (wr * 4 + i) * 16 + 4 * (lane >> 4) + r;
-          if (row >= M) continue;
-          const size_t idx = (size_t)row * N + col;
-          const float v = acc[i][j][r];
-          if constexpr (MODE == MODE_PARTIAL) {
-            static_cast<float*>(out)[(size_t)blockIdx.z * M * N + idx] = v;
-          } else if constexpr (MODE == MODE_RESIDUAL) {
-            float* o = static_cast<float*>(out);
-            const float nv = accumulate ? o[idx] + v : v;
-            o[idx] = nv;
-            if (mirror) mirror[idx] = f2bf(nv);
-          } else if (out_f32) {
-            static_cast<float*>(out)[idx] = v;
-          } else {
-            static_cast<bf16_t*>(out)[idx] = f2bf(v);
-          }
-        }
-    }
-  }
-}
+constexpr int MODE_PARTIAL = 7;  // split-K: fp32 partial tile to the workspace
 
 // ---------------------------------------------------------------------------------------------
 // gemm2: BM x 256 tile (BM = 128 * WM), 4 * WM waves as WM(M) x 4(N), each wave a 128 x 64 sub-tile
@@ -1732,24 +1590,11 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Which tiled kernel gemm() launches: 2 = gemm2 (default), 1 = the 128x128 register-staged kernel
-// (kept for A/B measurements: tools/bench_gemm.py --impl 1).
-static int g_gemm_impl = 2;
-// gemm2 pipeline variant (A/B): 0 = 4 LDS buffers, wait before the reads; 1 = 4 buffers, wait after
-// the reads; 2 = 5 buffers (all 160 KiB of LDS at WM = 2, one more tile in flight), wait after;
-// 3 = SUB = 2 half phases; 5 = full-line x staging (FA, the default: 6-21 % faster than 1 at M = 2048/4096
-// on every Llama-3-8B projection, bit-identical -- profiles/r1_gemm2_fullline_x_ab.jsonl)
-static int g_g2_var = 5;
-void gemm_set_impl(int impl) {
-  g_gemm_impl = impl == 1 ? 1 : 2;
-  // 2/8 = default (FA), 4 = fragment-shaped x (late wait), 3 = early wait, 5 = 5 buffers,
-  // 6 = two half phases per K-tile (SUB = 2)
-  // The default FA issues each K-tile's 2 weight loads from the M phase, between the MFMAs (FAM = 2); 9 = FA with all 4 issued at the head of the L phase (FAM = 0). FAM = 2 was
-  // 1-8 % faster than FAM = 0 on 15 of 20 Llama-3-8B projection shapes, FAM = 3 / 4 slower
-  // (profiles/r1_gemm2_fam_ab.jsonl).
-  if (impl >= 2) g_g2_var = impl == 3 ? 0 : (impl == 4 ? 1 : (impl == 5 ? 2 : (impl == 6 ? 3 : (impl == 9 ? 6 : 5))));
-}
-int gemm_get_impl() { return g_gemm_impl; }
+// The 256 x 256 gemm2 runs the full-line x staging pipeline (FA) with each K-tile's weight loads issued between the
+// MFMAs (FAM = 2): 6-21 % faster than fragment-shaped x and 1-8 % faster than issuing the loads up front on the
+// Llama-3-8B projections (profiles/r1_gemm2_fullline_x_ab.jsonl, r1_gemm2_fam_ab.jsonl). The other pipeline forms
+// (early / late waits, 5 LDS buffers, two half phases, loads up front) and the 128 x 128 register-staged v1 kernel were
+// never picked and were removed in round 4 (profiles/r4_variant_pruning.md).
 
 static int g2_wm(int M) { return M <= 128 ? 1 : 2; }  // default tile rows / 128
 
@@ -1757,12 +1602,6 @@ static int g2_wm(int M) { return M <= 128 ? 1 : 2; }  // default tile rows / 128
 // target ~256 WGs) / >= 8 k-steps (gemm v1: ~512 WGs) per split.
 int gemm_ksplit(int M, int N, int K) {
   const int KS = K >> 5;
-  if (g_gemm_impl == 1) {
-    const int tiles = ((N + GB_N - 1) / GB_N) * ((M + GB_M - 1) / GB_M);
-    int ks = 1;
-    while (tiles * ks < 512 && KS / (ks * 2) >= 8 && ks < 16) ks *= 2;
-    return ks;
-  }
   const int bm = 128 * g2_wm(M);
   const int tiles = ((N + G2_BN - 1) / G2_BN) * ((M + bm - 1) / bm);
   // one WG per CU, and the fp32 partial slabs (ks * M * N * 8 bytes written + read) kept within
@@ -1805,7 +1644,7 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
 static bool use_g4(int tile, int M, int K);
 int gemm_qkv_direct_ok(int M, int tile, int K) {
-  return (g_gemm_impl == 2 && g_g2_var == 5 && (tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
+  return ((tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
          use_g4(tile, M, K);
 }
 
@@ -1818,7 +1657,7 @@ void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
 static bool g_g4_ring = false;  // gemm4 main loop: the deeper LDS ring (gemm4w.h g4_mainloop_ring)
 void gemm_set_g4_ring(int on) { g_g4_ring = on != 0; }
 static bool use_g4(int tile, int M, int K) {
-  return g_gemm_impl == 2 && (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
+  return (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
 }
 
 template <int MODE>
@@ -1912,14 +1751,8 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
         JLA_G2(1, 4, false, true, 8, 4);
       else if (cfg == 3)
         JLA_G2(2, 4, true, true, 4, 2);
-      else if (g_g2_var == 3)
-        JLA_G2S(2, 4, true, true, 8, 4, 2);
-      else if (g_g2_var == 5)
-        JLA_G2FA(true, 2);
-      else if (g_g2_var == 6)
-        JLA_G2FA(true, 0);
       else
-        JLA_G2(2, 4, true, true, 8, 4);
+        JLA_G2FA(true, 2);
       return;
     }
   }
@@ -1927,18 +1760,8 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     JLA_G2(1, 4, false, false, 8, 4);
   else if (cfg == 3)
     JLA_G2(2, 4, true, false, 4, 2);
-  else if (g_g2_var == 1)
-    JLA_G2(2, 4, true, false, 8, 4);
-  else if (g_g2_var == 2)
-    JLA_G2(2, 5, true, false, 8, 4);
-  else if (g_g2_var == 3)
-    JLA_G2S(2, 4, true, false, 8, 4, 2);
-  else if (g_g2_var == 5)
-    JLA_G2FA(false, 2);
-  else if (g_g2_var == 6)
-    JLA_G2FA(false, 0);
   else
-    JLA_G2(2, 4, false, false, 8, 4);
+    JLA_G2FA(false, 2);
   }
 #undef JLA_G2FA
 #undef JLA_G2
@@ -1949,14 +1772,8 @@ template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
                          int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile,
                          hipStream_t s, float* rms_ws = nullptr) {
-
-  if (g_gemm_impl == 2) {
-    launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s, 0, G2Fix{},
-                    QKVArgs{}, rms_ws);
-  } else {
-    dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, ksplit);
-    gemm_kernel<MODE><<<grid, G_THREADS, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc);
-  }
+  launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s, 0, G2Fix{},
+                  QKVArgs{}, rms_ws);
 }
 
 // ---- stream-K tail plan (tile config 4): whole waves of 256x256 tiles data-parallel, the rest dealt
@@ -2056,7 +1873,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
          float rms_eps, int tile, int32_t* tickets, int n_tickets, float* rms_ws, size_t rms_ws_floats) {
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
   if (tile == G4_SK_TILE) {  // gemm4 stream-K over every (tile, K-tile) iteration: one persistent workgroup per CU
-    if (g_gemm_impl != 2 || ksplit > 1) return -1;
+    if (ksplit > 1) return -1;
     if ((N & 15) || (K & 31)) return -1;
     if (mode == MODE_QKV && !qkv) return -1;
     const u32x4* wp = static_cast<const u32x4*>(W);
@@ -2082,9 +1899,9 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   const bool rms = rms_eps >= 0.f;
-  if (rms && (g_gemm_impl == 1 || mode == MODE_RESIDUAL)) return -5;  // caller pre-scales x instead
+  if (rms && mode == MODE_RESIDUAL) return -5;  // caller pre-scales x instead
   if (tile == 6) {  // whole waves of 256x256 tiles data-parallel + the last partial wave split 2-way (fixup)
-    if (g_gemm_impl != 2 || mode == MODE_QKV || tickets == nullptr || !(g_g2_var == 5 || g_g2_var == 6)) return -1;
+    if (mode == MODE_QKV || tickets == nullptr) return -1;
     const int P = num_cus();
     const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
     const int dp = (tiles / P) * P, tail = tiles - dp;
@@ -2108,7 +1925,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
     return 0;
   }
   if (tile == 4) {  // stream-K tail (256x256 ping-pong tiles; no K split)
-    if (g_gemm_impl != 2 || ksplit > 1) return -1;
+    if (ksplit > 1) return -1;
     if (mode == MODE_QKV && !qkv) return -1;
     if (g2sk_plan(M, N, K).sk > 0)
       return gemm_sk(x, static_cast<const u32x4*>(W), out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ws,
@@ -2148,8 +1965,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   }
   // in-kernel split-K fixup (G2Fix): the default FA pipeline on 256 x 256 tiles, a tickets array from the
   // caller and slabs of gemm_fix_workspace_floats(); otherwise the partial slabs + reduce kernel below
-  if (g_gemm_fixup && tickets != nullptr && mode != MODE_QKV && g_gemm_impl == 2 && tile_cfg(tile, M) == 1 &&
-      (g_g2_var == 5 || g_g2_var == 6) && (tile < 4)) {
+  if (g_gemm_fixup && tickets != nullptr && mode != MODE_QKV && tile_cfg(tile, M) == 1 && (tile < 4)) {
     const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
     if (n_tickets < tiles || ws == nullptr || ws_floats < (size_t)tiles * ksplit * G2FIX_SLAB_FLOATS) return -3;
     const G2Fix fix{ws, tickets, ksplit, 0, 0, 0};
@@ -2283,7 +2099,6 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
-  if (g_gemm_impl != 2) return -1;
   if (ws == nullptr || ws_floats < gemm_argmax_workspace_floats(M, N)) return -3;
   const int tm = (M + 255) / 256, tn = (N + G2_BN - 1) / G2_BN;
   const u32x4* w = static_cast<const u32x4*>(W);

@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(NW * 64)
   constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
   // hand-counted ring (see asm_load_nt) where the assembly check passes: every bf16-activation
   // variant (the decode path: the residual stream's bf16 mirror) up to 8 waves, single or doubled ring,
-  // and fp32 at MT = 1 (the 16-wave variant 8 uses compiler-counted loads: its ring fails the check)
+  // and fp32 at MT = 1
   constexpr int U_BASE = ((NT == 1 ? 8 : 4) / MT) < 2 ? 2 : ((NT == 1 ? 8 : 4) / MT);
   constexpr bool ASM = (MT == 1 || sizeof(XT) == 2) && NW <= 8 && U <= 2 * U_BASE;
   auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
@@ -409,26 +409,14 @@ static int launch_skinny(const void* x, const void* W, void* out, int M, int N, 
   return 0;
 }
 
-// waves per workgroup: more waves when there are few workgroups (small N) so every CU keeps
-// enough weight bytes in flight; variant (1: 4, 2: 8, 3: 16 waves) overrides for tuning.
-static int pick_nw(int ngroups, int variant) {
-  if (variant == 1) return 4;
-  if (variant == 2) return 8;
-  if (variant == 3) return 16;
-  return 4;  // measured best on MI355X for every Llama-3-8B projection at M = 1 and 16
-}
-
+// waves per workgroup: 4 at M <= 16 (measured best on MI355X for every Llama-3-8B projection at M = 1 and 16), 8
+// above. (The 8 / 16-wave forms of the one-m-tile GEMV, variants 2 / 3, were never picked at a bench or latency
+// shape -- 8B, 70B MP 1, the TP8 rank proxy -- and were removed in round 4: profiles/r4_variant_pruning.md.)
 template <typename XT, int MT, int NT, int MODE>
 static int dispatch_nw(const void* x, const void* W, void* out, int M, int N, int K, float eps, int use_rms,
-                       int accumulate, int out_f32, const QKVArgs& qa, int variant, hipStream_t s) {
-  const int ngroups = ((N >> 4) + NT - 1) / NT;
-  if constexpr (MT == 1) {
-    switch (pick_nw(ngroups, variant)) {
-      case 4: return launch_skinny<XT, MT, NT, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-      case 16: return launch_skinny<XT, MT, NT, MODE, 16>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-      default: break;
-    }
-  }
+                       int accumulate, int out_f32, const QKVArgs& qa, hipStream_t s) {
+  if constexpr (MT == 1)
+    return launch_skinny<XT, MT, NT, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
   return launch_skinny<XT, MT, NT, MODE, 8>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
 }
 
@@ -444,24 +432,15 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       return launch_skinny<XT, MT, 4, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
     if (variant == 6)
       return launch_skinny<XT, MT, 2, MODE, 4>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-    // variants 8 / 9 / 11 (bf16 activations, M > 16): 1 tile per workgroup, 16 waves / 8 waves with a doubled
-    // ring / 4 waves with a doubled ring -- more weight + activation bytes in flight per wave for the
-    // latency-bound projections; variant 10: 2 tiles per workgroup (as 6) with a doubled ring
+    // variant 10 (bf16 activations, M > 16): 2 tiles per workgroup (as 6) with a doubled ring -- more weight +
+    // activation bytes in flight per wave for the latency-bound projections
     if constexpr (MT > 1 && sizeof(XT) == 2) {
-      if constexpr (MODE != MODE_SWIGLU) {
-        if (variant == 8)
-          return launch_skinny<XT, MT, 1, MODE, 16>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-        if (variant == 9)
-          return launch_skinny<XT, MT, 1, MODE, 8, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-        if (variant == 11)
-          return launch_skinny<XT, MT, 1, MODE, 4, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
-      }
       if (variant == 10)
         return launch_skinny<XT, MT, 2, MODE, 4, 1>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
     }
-    // split-K variants (bf16 activations): K cut over 2 (16, 18) or 4 (17, 19) workgroups per column group, the last
+    // split-K variants (bf16 activations): K cut over 2 workgroups per column group (16; 18 on packed x), the last
     // arriver sums the splits and runs the epilogue -- for projections with few column groups (tensor-parallel qkv
-    // shards, N = 1280 at Llama-3-70B MP 8: 80 one-tile workgroups leave most CUs idle); 18 / 19 read packed x.
+    // shards, N = 1280 at Llama-3-70B MP 8: 80 one-tile workgroups leave most CUs idle).
     // 1 tile per workgroup (SwiGLU: the gate/up pair), 4 waves at M <= 16, 8 above.
     if constexpr (sizeof(XT) == 2 && MODE != MODE_ARGMAX) {
       // 26: 4 tiles x 8 waves per workgroup on packed x with K over 4 workgroups -- the 4-tile x re-read ratio of 22/23
@@ -474,8 +453,8 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       }
       if (gemv_split_variant(variant)) {
         constexpr int SNT = MODE == MODE_SWIGLU ? 2 : 1, SNW = MT == 1 ? 4 : 8;
-        const int ks = (variant == 16 || variant == 18) ? 2 : 4;
-        if (variant >= 18)
+        const int ks = 2;
+        if (variant == 18)
           return launch_skinny<XT, MT, SNT, MODE, SNW, 0, true, true>(x, W, out, M, N, K, eps, use_rms, accumulate,
                                                                       out_f32, qa, s, ks);
         return launch_skinny<XT, MT, SNT, MODE, SNW, 0, false, true>(x, W, out, M, N, K, eps, use_rms, accumulate,
@@ -491,35 +470,28 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
         return launch_skinny<XT, MT, 2, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
       // 4 tiles x 4 waves reading packed x (22): half the activation bytes per weight byte of the 2-tile variants,
       // for wide projections at M = 17..64 (w1|w3: 1792 column tiles at Llama-3-8B)
-      if (variant == 22 || variant == 23) {  // (x is the packed copy: never fall through to a row-major variant)
+      if (variant == 22) {  // (x is the packed copy: never fall through to a row-major variant)
         if (N & 63) return -1;
-        if (variant == 23)  // the same with 8 waves
-          return launch_skinny<XT, MT, 4, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa,
-                                                            s);
         return launch_skinny<XT, MT, 4, MODE, 4, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
       }
     }
     // packed-x variants (x is the packed copy, common.h pack_off, padded to MT * 16 rows): 12 = 1 tile x 8 waves,
-    // 13 = 2 tiles x 4 waves, 14 / 15 = the same with a doubled ring
+    // 15 = 2 tiles x 4 waves with a doubled ring (also the SwiGLU form)
     if constexpr (sizeof(XT) == 2) {
-      if (variant == 13)
-        return launch_skinny<XT, MT, 2, MODE, 4, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
       if (variant == 15)
         return launch_skinny<XT, MT, 2, MODE, 4, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
       if constexpr (MODE != MODE_SWIGLU) {
-        if (variant == 14)
-          return launch_skinny<XT, MT, 1, MODE, 8, 1, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
         if (variant == 12)
           return launch_skinny<XT, MT, 1, MODE, 8, 0, true>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
       }
     }
   }
   if constexpr (MODE == MODE_SWIGLU) {
-    return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+    return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
   } else {
     if (MODE != MODE_QKV && (N >> 4) >= 2048)
-      return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
-    return dispatch_nw<XT, MT, 1, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, variant, s);
+      return dispatch_nw<XT, MT, 2, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
+    return dispatch_nw<XT, MT, 1, MODE>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, s);
   }
 }
 
@@ -546,7 +518,7 @@ size_t gemv_split_workspace_floats(int M, int N) {
   const int groups = N >> 4;  // upper bound: 1 tile per column group
   if (groups > GEMV_SPLIT_MAX_GROUPS || M < 1 || M > SKINNY_MAX_M) return 0;
   const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  return (size_t)groups * 4 * (mt * 256 + mt * 16);
+  return (size_t)groups * 2 * (mt * 256 + mt * 16);
 }
 int gemv_split_tickets(int N) { return (N >> 4) > GEMV_SPLIT_MAX_GROUPS ? 0 : (N >> 4); }
 

@@ -33,7 +33,7 @@ struct QKVArgs {
   bf16_t* pack;               // optional packed-layout copy (common.h pack_off) of the bf16 output: RESIDUAL -> the
                               // mirror, SWIGLU -> the activation (GEMV only; the next projection's packed-x input)
   const void* tp;             // MODE_TPRESID: the TP group's CarDevice (car.h) the partials are all-reduced through
-  float* sk_ws;               // split-K GEMV variants (gemv.hip, 16-19): per-(group, split) partial slabs
+  float* sk_ws;               // split-K GEMV variants (gemv.hip, 16 / 18 / 26): per-(group, split) partial slabs
   int32_t* sk_tk;             //   and per-group tickets (zero-initialised once, reset by each group's last arriver)
   int sk_ws_floats;           //   slab buffer size (buffer-descriptor range)
 };
@@ -43,21 +43,13 @@ constexpr long long TPRES_REGION = 64 * 64 * 4;  // up to 64 rows x 64 columns x
 
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
-// split-K GEMV variants 16-19 (K over gridDim.y workgroups per column group, last arriver sums + epilogue): their slab
+// split-K GEMV variants 16 / 18 / 26 (K over gridDim.y workgroups per column group, last arriver sums + epilogue): their slab
 // floats / tickets (0 when N has too many column groups for them)
 constexpr int GEMV_SPLIT_MAX_GROUPS = 1024;
 size_t gemv_split_workspace_floats(int M, int N);
 int gemv_split_tickets(int N);
-inline bool gemv_split_variant(int v) { return (v >= 16 && v <= 19) || v == 26; }
-inline bool gemv_xp_variant(int v) { return (v >= 12 && v <= 15) || v == 18 || v == 19 || (v >= 21 && v <= 23) || v == 26; }
-// split-K skinny GEMM (skinny.hip): waves split N and share an LDS copy of x; ws/tickets sized by
-// skinny_workspace_floats / skinny_tickets (tickets zero-initialised once, self-resetting)
-size_t skinny_workspace_floats(int M, int N, int K, int mode);
-int skinny_tickets(int M, int N, int K, int mode);
-void skinny_set_plan(int nt, int ksplit);  // split-K skinny GEMM plan override (0, 0 = heuristic)
-int linear_splitk(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode, float rms_eps,
-                  int accumulate, int out_f32, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
-                  int n_tickets, hipStream_t s);
+inline bool gemv_split_variant(int v) { return v == 16 || v == 18 || v == 26; }
+inline bool gemv_xp_variant(int v) { return v == 12 || v == 15 || v == 18 || v == 21 || v == 22 || v == 26; }
 // 128x128-tile MFMA GEMM (gemm.hip). ksplit > 1 splits K over gridDim.z into fp32 partials
 // (ws >= gemm_workspace_floats) reduced in fixed order by an epilogue kernel; MODE_QKV needs ksplit > 1.
 int gemm_ksplit(int M, int N, int K);
@@ -70,8 +62,6 @@ void gemm_set_g4_ring(int on);
 // zero-initialised once (self-resetting); the fused norm needs rms_ws; every mode incl. MODE_QKV
 size_t gemm4_sk_workspace_floats();
 int gemm4_sk_tickets(int M, int N);  // gemm4 main loop on the 160 KiB LDS ring (3 x pairs + 4 W stages in flight)
-void gemm_set_impl(int impl);  // 2 = gemm2 (default, full-line x), 4 = gemm2 fragment-shaped x, 1 = 128x128 v1 (A/B)
-int gemm_get_impl();
 size_t gemm_workspace_floats(int M, int N, int K);
 // rms_eps >= 0: x is the UNscaled activation and each output row is scaled by rsqrt(mean(x^2) + eps)
 // (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
@@ -123,7 +113,6 @@ unsigned jla_bounds_rope_kv(int reset);
 unsigned jla_bounds_sample(int reset);
 unsigned jla_bounds_gemm(int reset);
 unsigned jla_bounds_gemv(int reset);
-unsigned jla_bounds_skinny(int reset);
 unsigned jla_bounds_attn_decode(int reset);
 unsigned jla_bounds_attn_prefill(int reset);
 int attn_decode_splits(int B, int Hkv, int T, int rep);

@@ -236,9 +236,9 @@ PACKED_X_MIN_M = int(os.environ.get("JLA_PACKED_X_MIN_M", "9"))
 PACKED_X_MAX_M = int(os.environ.get("JLA_PACKED_X_MAX_M", "64"))
 PACKED_ATT_MAX_M = int(os.environ.get("JLA_PACKED_ATT_MAX_M", "64"))  # attention output only, up to here
 SKINNY_M = 64  # decode GEMV rows (csrc: SKINNY_MAX_M): packed copies exist only on that path
-XP_VARIANTS = (12, 13, 14, 15, 18, 19, 21, 22, 23, 26)  # packed-x GEMV variants (18 / 19 / 26 split-K; 21-23: 2x8 / 4x4 / 4x8;
-#   26: 4 tiles x 8 waves, K over 4)
-SPLIT_VARIANTS = (16, 17, 18, 19, 26)  # split-K GEMV variants (the shared skinny workspace holds their slabs)
+XP_VARIANTS = (12, 15, 18, 21, 22, 26)  # packed-x GEMV variants (18 / 26 split-K; 21 / 22: 2x8 / 4x4; 26: 4 tiles x 8
+#   waves, K over 4)
+SPLIT_VARIANTS = (16, 18, 26)  # split-K GEMV variants (the shared decode workspace holds their slabs)
 
 
 def packed_rows(m: int) -> int:
@@ -283,7 +283,7 @@ def linear_tp_residual(x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, st
     assert x.dtype == BF16 and x.is_contiguous() and m <= e.SKINNY_MAX_M, (x.dtype, x.shape)
     # the exchange lives in the GEMV epilogue: tune among the GEMV variants (``pack_out`` excludes split-K / tiled)
     v = _variant(e, x, w, MODE_RESIDUAL, x_packed, pack_out=True)
-    if v in (4, TILED):
+    if v == TILED:
         v = 1
     ws = tk = None
     if v in SPLIT_VARIANTS:
@@ -300,9 +300,9 @@ QKV_DIRECT = os.environ.get("JLA_QKV_DIRECT", "1") != "0"
 
 
 def _fused_rms(e, mode, rms_eps) -> bool:
-    """The tiled GEMM applies RMSNorm itself (statistics from its own A-fragment reads, row scale in
-    the epilogue) except in residual mode and on the legacy 128x128 kernel."""
-    return rms_eps is not None and mode != MODE_RESIDUAL and e.gemm_get_impl() != 1
+    """The tiled GEMM applies RMSNorm itself (statistics from its own A-fragment reads or a precomputed per-row
+    statistic, row scale in the epilogue) except in residual mode."""
+    return rms_eps is not None and mode != MODE_RESIDUAL
 
 
 def _tiled_input(x, rms_eps, fused=False):
@@ -410,13 +410,13 @@ def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int
     xp_in, p_out = x_packed is not None, pack_out is not None
     if GEMV_VARIANT:
         v = GEMV_VARIANT
-        if (v in XP_VARIANTS and not xp_in) or (p_out and v == 4) or (p_out and v == TILED and not _tiled_packs(
+        if (v in XP_VARIANTS and not xp_in) or (p_out and v == TILED and not _tiled_packs(
                 e, x.shape[0], w.n, w.k, x.device, mode, None if mode == MODE_RESIDUAL else 1e-5)) or (
                 v in SPLIT_VARIANTS and (
                 no_split or x.dtype != BF16 or w.n // 16 > autotune.SPLIT_MAX_GROUPS)):
             v = 1
-        if v in (12, 14) and mode == MODE_SWIGLU:
-            v += 1
+        if v == 12 and mode == MODE_SWIGLU:
+            v = 15
         return v
     m = x.shape[0]
     pmode = MODE_STORE if mode == MODE_QKV else mode  # QKV epilogue has side effects: tune as STORE
@@ -448,7 +448,7 @@ _SK_SIZES = {}
 
 
 def _skinny_ws(e, m, n, k, mode, device):
-    """Split-K partial slabs + self-resetting tickets of the skinny GEMM (shared, stream-ordered;
+    """Split-K partial slabs + self-resetting tickets of the split-K GEMV variants (shared, stream-ordered;
     sized during the eager warm-up step so nothing is allocated under hipGraph capture)."""
     key = (m, n, k, mode)
     sz = _SK_SIZES.get(key)
@@ -625,8 +625,6 @@ def linear_argmax(x: torch.Tensor, w, rms_eps: Optional[float] = None):
     if m < ARGMAX_FUSED_MIN_M:
         return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
     e = ext()
-    if e.gemm_get_impl() != 2:
-        return argmax(linear(x, w, rms_eps, out_dtype=torch.float32))
     assert x.is_contiguous() and x.shape[1] == w.k, (x.shape, w.k)
     xb = x if x.dtype == BF16 else x.to(BF16)
     ws = workspace.get("gemm_argmax", e.gemm_argmax_workspace(m, w.n), torch.float32, x.device)

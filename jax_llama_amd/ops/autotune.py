@@ -1,17 +1,17 @@
 """Per-shape selection among the decode linear kernels, measured on the device at first use.
 
-Two decode GEMM designs ship (``csrc/kernels/gemv.hip`` K-split-across-waves GEMV with 1/2/4
-tiles per workgroup; ``csrc/kernels/skinny.hip`` split-K GEMM sharing x through LDS); which one
-streams the weights fastest depends on (M, N, K) in ways that are cheaper to measure than to
-model (rocprof studies: profiles/README.md). The first eager call of a shape times every
+The decode GEMV (``csrc/kernels/gemv.hip``: K split across the waves of a workgroup, 1/2/4 tiles per workgroup, optional
+K split across workgroups, row-major or packed activations) and the tiled MFMA GEMM compete; which one streams the
+weights fastest depends on (M, N, K) in ways that are cheaper to measure than to model (rocprof studies:
+profiles/README.md). Variants never picked at a bench or latency shape were removed in round 4
+(profiles/r4_variant_pruning.md). The first eager call of a shape times every
 candidate on a rotating set of scratch weights (> Infinity Cache, so each call streams from HBM,
 as in a real decode step) and caches the winner. Never runs under hipGraph capture; shapes first
 seen during capture fall back to the static heuristic.
 
-Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG, 8 / 9 = 1-tile GEMV
-with 16 waves / a doubled register ring (M > 16, bf16 activations),
-4 = split-K skinny GEMM, 7 = tiled MFMA GEMM with split-K (gemm.hip; a candidate for M > 16, always used
-for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
+Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 tiles/WG, 10 = 2 tiles with a doubled
+register ring (M > 16, bf16 activations), 20 = 2 tiles x 8 waves, 16 = K over 2 workgroups, packed-x 12 / 15 / 18 / 21 /
+22 / 26, 7 = tiled MFMA GEMM with split-K (gemm.hip; a candidate for M > 16, always used for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
 
 Tensor parallelism: inside ``tp_scope(comm)`` (the model's forward under TP) a decision is collective -- rank 0
 of the TP group measures and broadcasts its choice, so every rank runs the same plans (a rank on a slower plan
@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 5  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K), so older persisted picks are re-measured
+TUNE_VERSION = 6  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -131,7 +131,7 @@ def heuristic(m: int, n: int, k: int, mode: int) -> int:
     """Static choice from MI355X measurements (Llama-3-8B projections, profiles/README.md)."""
     ntt = n // 16
     if m > 16:
-        return 4 if n * k >= 20_000_000 else 1
+        return 6 if n % 32 == 0 else 1
     if m <= 4:
         return 1
     if ntt // 4 >= 384 and n % 64 == 0:
@@ -145,38 +145,31 @@ def candidates(m: int, n: int, swiglu: bool = False, bf16_x: bool = True) -> Tup
     # M > 16: two or four activation m-tiles per weight fragment, so the 2/4-tile GEMV workgroups
     # (fewer activation re-reads) and the tiled MFMA GEMM win on some shapes (M=24..64 sweep,
     # profiles/r1_decode_m32_variants.jsonl: qkv -> 6, gate_up -> 5, down/lm_head -> 7 at M=32)
-    c = [1, 6, 4]
+    c = [1, 6]
     if n % 64 == 0:
         c.insert(1, 5)
-    if n // 16 < 512:
-        # few n-tiles (tensor-parallel qkv / o shards, e.g. Llama-3-70B at MP 8: qkv N = 1280 -> 80 workgroups): 8 or
-        # 16 waves per workgroup keep more weight bytes in flight per CU (gemv.hip pick_nw variants 2 / 3)
-        c.extend([2, 3])
     if m > 16:
         c.append(TILED_VARIANT)
         if bf16_x:
-            # doubled hand-counted rings (8 / 4 waves, 1 tile; 4 waves, 2 tiles): at M > 16 the single ring
-            # keeps only 4 (or 2) k-steps in flight per wave (profiles/r2_decode_m32_asm_ring.jsonl)
-            c.extend([9, 11, 10])
-        # (variant 8 -- 16 waves -- measured no faster than 1/4/6/7 at M = 32:
-        # profiles/r2_decode_m32_variants_8_9.jsonl; kept as an explicit choice, not tuned)
+            # doubled hand-counted ring (4 waves, 2 tiles): at M > 16 the single ring keeps only 2 k-steps in flight
+            # per wave (profiles/r2_decode_m32_asm_ring.jsonl)
+            c.append(10)
     if n // 32 < 512:
         c.append(20)  # 2 tiles x 8 waves: few column groups (w1|w3 shards)
     if bf16_x and n // 16 <= SPLIT_MAX_GROUPS:
-        # split-K GEMV (K over 2 / 4 workgroups per column group, in-kernel last-arriver sum): few column groups
-        c.extend([16, 17])
+        # split-K GEMV (K over 2 workgroups per column group, in-kernel last-arriver sum): few column groups
+        c.append(16)
     return tuple(c)
 
 
 SPLIT_MAX_GROUPS = 1024  # csrc GEMV_SPLIT_MAX_GROUPS
-SPLIT_GEMV = (16, 17, 18, 19, 26)  # split-K GEMV variants (gemv.hip gemv_split_variant)
+SPLIT_GEMV = (16, 18, 26)  # split-K GEMV variants (gemv.hip gemv_split_variant)
 
 
 TILED_VARIANT = 7
 
 
-XP_CANDIDATES = (12, 13, 14, 15, 18, 19, 21, 22, 23, 26)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 19 / 26
-#   split-K)
+XP_CANDIDATES = (12, 15, 18, 21, 22, 26)  # packed-x GEMV variants (gemv.hip dispatch_nt; 18 / 26 split-K)
 
 
 def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out: bool = False,
@@ -184,7 +177,7 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
     """``run(variant, x, weight_tensor)`` launches the op once. ``xp_in``: a packed copy of x exists, so the
     packed-x variants compete too; ``pack_out``: the epilogue must also write a packed copy of its output,
     which the GEMV variants do, and the tiled GEMM when ``tiled_packs`` (its split-K plan); ``no_split``: without the split-K GEMV
-    variants (16-19; the fused-argmax lm_head GEMV has no split form)."""
+    variants (16 / 18 / 26; the fused-argmax lm_head GEMV has no split form)."""
     m = x.shape[0]
     # (TP-scoped decisions are cached apart: every rank of the group must take the same collective path)
     key = (m_bucket(m), w.n, w.k, mode, x.dtype, xp_in, pack_out, no_split, tiled_packs, _SCOPE["comm"] is not None)
@@ -193,11 +186,11 @@ def choose(e, x: torch.Tensor, w, mode: int, run, xp_in: bool = False, pack_out:
         return v
     cands = list(candidates(m, w.n, swiglu=(mode == 2), bf16_x=(x.dtype == torch.bfloat16)))
     if pack_out:  # the tiled GEMM qualifies when its split-K reduce epilogue writes the copy (``tiled_packs``)
-        cands = [c for c in cands if c != 4 and (c != TILED_VARIANT or tiled_packs)]
+        cands = [c for c in cands if c != TILED_VARIANT or tiled_packs]
     if xp_in and x.dtype == torch.bfloat16:
-        cands += [c for c in XP_CANDIDATES if (mode != 2 or c in (13, 15, 18, 19, 21, 22, 23, 26)) and
-                  (c not in (18, 19) or w.n // 16 <= SPLIT_MAX_GROUPS) and (c != 21 or w.n // 32 < 512) and
-                  (c not in (22, 23) or (w.n % 64 == 0 and w.n // 64 >= 64)) and
+        cands += [c for c in XP_CANDIDATES if (mode != 2 or c != 12) and
+                  (c != 18 or w.n // 16 <= SPLIT_MAX_GROUPS) and (c != 21 or w.n // 32 < 512) and
+                  (c != 22 or (w.n % 64 == 0 and w.n // 64 >= 64)) and
                   # 4-tile split-K: narrow outputs only (few 64-column groups), M > 16
                   (c != 26 or (m > 16 and w.n % 64 == 0 and w.n // 64 < 256))]
     if no_split:

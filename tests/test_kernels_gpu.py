@@ -257,7 +257,7 @@ def _attn_ref_gpu(q, kc, vc, slot0, kv_start, key_mask=None, chunk=512):
     return out.reshape(b * s, h * dh)
 
 
-@pytest.mark.parametrize("impl", [4, 2, 1, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("impl", [2, 1, 7, 8, 9])
 @pytest.mark.parametrize("rep", [1, 4, 8])
 @pytest.mark.parametrize("s,slot0,masked", [(7, 0, False), (130, 10, False), (512, 0, False), (300, 0, True),
                                             (2048, 0, False)])
@@ -327,7 +327,7 @@ def test_attention_decode_8k(rep):
 
 
 @pytest.mark.parametrize("m", [1, 5, 17, 40, 64])
-@pytest.mark.parametrize("variant", [1, 5, 6, 9, 10, 11, 20])
+@pytest.mark.parametrize("variant", [1, 5, 6, 10, 20])
 def test_linear_skinny_argmax(m, variant):
     """Decode lm_head with the argmax in the GEMV epilogue == stored fp32 logits + first-max argmax,
     bit for bit (same accumulation order), including an exact tie across two 16-column tiles."""
@@ -388,10 +388,10 @@ def test_linear_qkv_rope_fused(m, s, k, xdt):
     _close(vg, vc, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("variant", [16, 17])
+@pytest.mark.parametrize("variant", [16])
 @pytest.mark.parametrize("m,s,k", [(1, 1, 8192), (16, 1, 4096), (32, 1, 8192), (64, 1, 1024), (6, 3, 256)])
 def test_split_gemv_qkv_rope(m, s, k, variant):
-    """Split-K GEMV (K over 2 / 4 workgroups per column group, last arriver sums + runs the epilogue): the fused
+    """Split-K GEMV (K over 2 workgroups per column group, last arriver sums + runs the epilogue): the fused
     qkv projection (RMS statistics summed over the splits, RoPE, KV-cache write) at tensor-parallel shard widths
     (10 heads = 80 column tiles, as Llama-3-70B at MP 8) against the fp32 oracle, and repeatable bit for bit (the
     tickets reset themselves)."""
@@ -428,7 +428,7 @@ def test_gemv_variants_agree():
     x = torch.randn(16, 2048, device=DEV)
     w = PackedLinear.from_dense((torch.randn(512, 2048) * 0.05).to(BF16), DEV)
     outs = []
-    for v in (1, 2, 3, 4):
+    for v in (1, 5, 6, 16):
         ops.GEMV_VARIANT = v
         outs.append(ops.linear(x, w, rms_eps=1e-5, out_dtype=torch.float32))
     ops.GEMV_VARIANT = 0
@@ -437,11 +437,11 @@ def test_gemv_variants_agree():
 
 
 @pytest.mark.parametrize("k", [256, 4096])
-@pytest.mark.parametrize("variant", [1, 4, 6, 9, 10, 11, 16, 17, 20])
+@pytest.mark.parametrize("variant", [1, 5, 6, 10, 16, 20])
 @pytest.mark.parametrize("m", [1, 9, 16, 40, 64])
 def test_decode_linear_paths_all_modes(variant, m, k):
-    """Both decode GEMM designs (and the GEMV's tile / ring-depth variants: at M > 16 the hand-counted
-    doubled rings 9/10/11), every epilogue, real-ish K (multi-split) and the whole-model tests' K = 256."""
+    """The decode GEMV's tile / ring-depth / split variants (at M > 16 the hand-counted doubled ring 10), every
+    epilogue, real-ish K (multi-split) and the whole-model tests' K = 256."""
     ops.GEMV_VARIANT = variant
     try:
         n = 768
@@ -762,10 +762,10 @@ def test_gemm_hybrid_tail(cus, m, n):
 
 @pytest.mark.parametrize("m,k,ks", [(300, 1024, 1), (512, 1056, 1), (256, 992, 3), (700, 4096, 2)])
 def test_gemm_full_line_x(m, k, ks):
-    """gemm2 with x staged in full 128-B lines (the default, impl 2: K-tile pairs, swizzled LDS image) is
-    bit-identical to the fragment-shaped x pipeline (impl 4; same per-accumulator MFMA order) for every epilogue, with and without the
-    fused RMSNorm, including an odd K-tile count (half-used last pair) and split-K ranges that start and
-    end mid-pair; and matches the fp32 reference."""
+    """gemm2 (tile 1) with x staged in full 128-B lines (K-tile pairs, swizzled LDS image): every epilogue, with and
+    without the fused RMSNorm, including an odd K-tile count (half-used last pair) and split-K ranges that start and
+    end mid-pair, against the fp32 reference and reproducible bit for bit. (Its bit-identity with the removed
+    fragment-shaped-x pipeline was checked while both existed; gemm4 == gemm2: tests/test_gemm4_gpu.py.)"""
     e = ops.ext()
     n = 768
     x = torch.randn(m, k).to(BF16)
@@ -788,20 +788,10 @@ def test_gemm_full_line_x(m, k, ks):
         e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, 1)
         return outs + [hg, mir]
 
-    try:
-        e.gemm_set_impl(4)
-        base = run()
-        variants = {}
-        for impl in (2, 9):  # default FA (weight loads issued between the MFMAs); FA with all loads up front
-            e.gemm_set_impl(impl)
-            variants[impl] = run()
-    finally:
-        e.gemm_set_impl(2)
+    got, again = run(), run()
     torch.cuda.synchronize()
-    for impl, got in variants.items():
-        for i, (a, b) in enumerate(zip(base, got)):
-            assert torch.equal(a, b), f"impl {impl}: output {i} differs from the fragment-shaped-x pipeline"
-    got = variants[2]
+    for i, (a, b) in enumerate(zip(got, again)):
+        assert torch.equal(a, b), f"output {i} not reproducible"
     _close(got[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
     _close(got[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
 
@@ -920,7 +910,7 @@ def _qkv_rope_stream_k(e, m, s):
     _close(vg, vc, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("variant", [12, 13, 14, 15, 18, 19, 21, 22, 23, 26, 7])
+@pytest.mark.parametrize("variant", [12, 15, 18, 21, 22, 26, 7])
 @pytest.mark.parametrize("m", [1, 12, 16, 20, 32, 40, 64])
 def test_packed_x_variants_and_packed_epilogues(m, variant):
     """Packed-x GEMV variants read the packed copy (ref.pack_act) and match the fp32 reference; the residual /

@@ -41,8 +41,7 @@ class _W:
 @pytest.mark.parametrize("m", [12, 24, 40])
 def test_autotune_candidates_for_packed_modes(m, monkeypatch):
     """Without measurements (autotune off / under capture) the choice must still respect the packed-mode rules:
-    a required packed output excludes the split-K skinny (4) and tiled (7) kernels; SwiGLU never gets the one-tile
-    packed-x variants (12 / 14)."""
+    a required packed output excludes the tiled (7) kernel; SwiGLU never gets the one-tile packed-x variant (12)."""
     monkeypatch.setattr(autotune, "ENABLED", False)
     autotune._CACHE.clear()
     x = torch.zeros(m, 4096, dtype=torch.bfloat16)
@@ -55,12 +54,11 @@ def test_autotune_candidates_for_packed_modes(m, monkeypatch):
 
 def test_pinned_variant_respects_packed_rules(monkeypatch):
     """ops._variant with a pinned GEMV variant: packed-x variants fall back when no packed x exists, SwiGLU maps
-    12 / 14 to the two-tile 13 / 15, a required packed output never lands on 4 / 7."""
+    12 to the two-tile 15, a required packed output never lands on the tiled GEMM (7)."""
     x = torch.zeros(20, 4096, dtype=torch.bfloat16)
     w = _W(28672, 4096)
-    cases = [(12, None, None, ops.MODE_STORE, 1), (12, x, None, ops.MODE_STORE, 12), (12, x, None, ops.MODE_SWIGLU, 13),
-             (14, x, x, ops.MODE_SWIGLU, 15), (7, None, x, ops.MODE_RESIDUAL, 1), (4, x, x, ops.MODE_STORE, 1),
-             (9, None, None, ops.MODE_STORE, 9)]
+    cases = [(12, None, None, ops.MODE_STORE, 1), (12, x, None, ops.MODE_STORE, 12), (12, x, None, ops.MODE_SWIGLU, 15),
+             (15, x, x, ops.MODE_SWIGLU, 15), (7, None, x, ops.MODE_RESIDUAL, 1), (10, None, None, ops.MODE_STORE, 10)]
     for pinned, xp, po, mode, want in cases:
         monkeypatch.setattr(ops, "GEMV_VARIANT", pinned)
         assert ops._variant(None, x, w, mode, xp, po) == want, (pinned, mode)

@@ -41,7 +41,7 @@ def main():
         slot = torch.zeros(1, dtype=torch.int32, device="cuda")
         flops = 4.0 * b * h * 128 * s * (s + 1) / 2
         ref = None
-        impls = [i for i in (args.impls or (2, 4, 5, 6, 1)) if not (i == 1 and s * s * b * h > 2048 * 2048 * 16 * 32)
+        impls = [i for i in (args.impls or (2, 7, 8, 9, 1)) if not (i == 1 and s * s * b * h > 2048 * 2048 * 16 * 32)
                  and (args.impl is None or i == args.impl)]
         best, diffs = {i: float("inf") for i in impls}, {}
         for impl in impls:  # warm-up + correctness vs the first impl

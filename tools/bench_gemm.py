@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--m", type=int, nargs="+", default=[64, 128, 256, 512, 4096])
     ap.add_argument("--ksplit", type=int, nargs="+", default=[0], help="0 = library heuristic")
     ap.add_argument("--no-blas", action="store_true")
-    ap.add_argument("--impl", type=int, nargs="+", default=[2], help="tiled kernel generation(s) to time")
+    ap.add_argument("--impl", type=int, nargs="+", default=[2], help="label of the round (the tiled kernel is gemm2/gemm4)")
     ap.add_argument("--ops", nargs="+", default=None)
     ap.add_argument("--rounds", type=int, default=1, help="interleaved A/B rounds of the impl list (one process)")
     ap.add_argument("--fixup", type=int, nargs="+", default=[0], help="split-K: 0 partial slabs + reduce kernel, "
@@ -93,7 +93,6 @@ def main():
             ref = None
             first = {}
             for rnd, impl in [(r, i) for r in range(args.rounds) for i in args.impl]:
-                e.gemm_set_impl(impl)
                 for ks in args.ksplit:
                  for ring in args.ring:
                   e.gemm_set_g4_ring(ring)
@@ -151,7 +150,6 @@ def main():
                       if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
                           f0 = first.setdefault((kk, tile), got.clone())
                           assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
-            e.gemm_set_impl(2)
             e.gemm_set_g4_ring(0)
             if not args.no_blas and mode == 0:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)

@@ -45,12 +45,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--m", type=int, nargs="+", default=[1, 16])
-    ap.add_argument("--variants", type=int, nargs="+", default=[1, 4])
+    ap.add_argument("--variants", type=int, nargs="+", default=[1, 6])
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ops", nargs="+", default=None, help="subset of qkv o gate_up down lm_head attn")
     ap.add_argument("--attn-impls", default="1:0,2:4096", help="impl:waves_target pairs for attn A/B")
-    ap.add_argument("--sk-plans", nargs="*", default=None,
-                    help="variant 4 (split-K skinny GEMM) plan overrides nt:ksplit, e.g. 1:16 2:8")
     ap.add_argument("--attn-shapes", nargs="*", default=None, help="BxT decode attention shapes (default: a sweep)")
     ap.add_argument("--v3-kpg", type=int, nargs="*", default=[0],
                     help="small-batch decode attention (v3) chunk-depth multipliers to sweep (0: by size, the default)")
@@ -75,14 +73,10 @@ def main():
         ws = [PackedLinear.random(n, k, DEV) for _ in range(copies_for(nbytes))]
         for m in args.m:
             x = torch.randn(m, k, device=DEV).to(xdt)
-            runs = [(v, None) for v in args.variants]
-            if args.sk_plans:
-                runs += [(4, tuple(int(t) for t in p.split(":"))) for p in args.sk_plans]
-            for var, plan in runs:
+            for var in args.variants:
                 ops.GEMV_VARIANT = var
-                # packed-x variants (12-15) read a real packed copy of x (ref.pack_act), as in the model
+                # packed-x variants read a real packed copy of x (ref.pack_act), as in the model
                 xpk = ref.pack_act(x, ops.packed_rows(m)) if var in ops.XP_VARIANTS else None
-                e.skinny_set_plan(*(plan or (0, 0)))
                 ops._SK_SIZES.clear()
                 if mode == ops.MODE_QKV:
                     table = torch.randn(4096, hd // 2, 2, device=DEV)
@@ -108,9 +102,8 @@ def main():
                     def fn(i, x=x, xpk=xpk, out32=out32):
                         ops._gpu_linear(x, ws[i % len(ws)], out32, ops.MODE_STORE, 1e-5, True, None, xpk)
                 us = timeit(fn)
-                e.skinny_set_plan(0, 0)
                 ops._SK_SIZES.clear()
-                print(json.dumps({"op": name, "n": n, "k": k, "m": m, "variant": var, "sk_plan": plan, "us": round(us, 2),
+                print(json.dumps({"op": name, "n": n, "k": k, "m": m, "variant": var, "us": round(us, 2),
                                   "TBps": round(nbytes / us / 1e6, 3)}), flush=True)
         del ws
         torch.cuda.empty_cache()

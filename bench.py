@@ -33,7 +33,7 @@ Extra keys (outside the timed region, reported alongside the headline):
 from __future__ import annotations
 
 import argparse
-import gc
+import gc as _gc
 import json
 import os
 import sys
@@ -235,7 +235,7 @@ def main():
         # the grow-only op workspaces sized by the B = 2048 prefill's split-K slabs)
         eng_mod._ENGINES.clear()
         ops.workspace.clear()
-        gc.collect()
+        _gc.collect()
         torch.cuda.empty_cache()
         extra("mp1_point", lambda: res.__setitem__("mp1_point", _mp1_point(args)))
     if not args.no_calibration:  # last: the GEMM / copy probes of this box, next to the numbers above

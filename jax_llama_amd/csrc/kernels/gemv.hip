@@ -518,7 +518,7 @@ size_t gemv_split_workspace_floats(int M, int N) {
   const int groups = N >> 4;  // upper bound: 1 tile per column group
   if (groups > GEMV_SPLIT_MAX_GROUPS || M < 1 || M > SKINNY_MAX_M) return 0;
   const int mt = M <= 16 ? 1 : (M <= 32 ? 2 : 4);
-  return (size_t)groups * 2 * (mt * 256 + mt * 16);
+  return (size_t)groups * 4 * (mt * 256 + mt * 16);  // (variant 26: 4 tiles per group, K over 4)
 }
 int gemv_split_tickets(int N) { return (N >> 4) > GEMV_SPLIT_MAX_GROUPS ? 0 : (N >> 4); }
 

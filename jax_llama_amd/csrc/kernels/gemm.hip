@@ -798,10 +798,13 @@ struct G4Epi {
   float* ssq_ws;
   const float* rms_inv;
 };
-template <int MODE, int RMSM, typename Acc>
+template <int MODE, int RMSM, typename Acc, int NJ = 8>
 JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int m0, int n0, int split,
                          const G4Epi& ep, const QKVArgs& qa) {
   constexpr bool RMS = RMSM == 1;
+  static_assert(NJ == 8 || (RMSM != 1 && MODE != MODE_ARGMAX && MODE != MODE_QKV),
+                "the 256 x 128 tile: precomputed norm statistic; store / residual / SwiGLU / partial epilogues");
+  constexpr int WN = 16 * NJ;  // output columns of a wave block
   const int wr = wu >> 1, wc = wu & 1;
   void* const out = ep.out;
   const int M = ep.M, N = ep.N, K = ep.K, accumulate = ep.accumulate, out_f32 = ep.out_f32;
@@ -865,17 +868,17 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
     const int F = N >> 1;
     bf16_t* o = static_cast<bf16_t*>(out);
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
+    for (int j = 0; j < NJ; j += 2) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const f32x4 gv = tile_val(j, i), uv = tile_val(j + 1, i);
         const u32x2 p = {pack2bf(silu(gv[0]) * uv[0], silu(gv[1]) * uv[1]),
                          pack2bf(silu(gv[2]) * uv[2], silu(gv[3]) * uv[3])};
-        g4_stage_put<128>(wl, 16 * i + c, 16 * j + 8 * q, p);
+        g4_stage_put<16 * NJ>(wl, 16 * i + c, 16 * j + 8 * q, p);
       }
     }
-    const int fcol0 = ((n0 >> 4) + wc * 8) * 8;  // first activation column of the wave block
-    g4_stage_rows<128>(wl, lane, [&](int r, int ch, u32x4 v) {
+    const int fcol0 = ((n0 >> 4) + wc * NJ) * 8;  // first activation column of the wave block
+    g4_stage_rows<16 * NJ>(wl, lane, [&](int r, int ch, u32x4 v) {
       const int row = mrow0 + r, col = fcol0 + 8 * ch;
       if (row < M && col < F) *reinterpret_cast<u32x4*>(o + (size_t)row * F + col) = v;
     });
@@ -963,8 +966,8 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
   } else if constexpr (MODE == MODE_STORE) {
     if (out_f32) {  // fp32 logits (16-byte pieces, direct)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int tile = (n0 >> 4) + wc * 8 + j;
+      for (int j = 0; j < NJ; ++j) {
+        const int tile = (n0 >> 4) + wc * NJ + j;
         if (tile >= NTT) continue;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -975,22 +978,22 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const f32x4 v = tile_val(j, i);
-          g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+          g4_stage_put<32 * NJ>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
         }
       bf16_t* o = static_cast<bf16_t*>(out);
-      g4_stage_rows<256>(wl, lane, [&](int r, int ch, u32x4 v) {
-        const int row = mrow0 + r, col = n0 + wc * 128 + 8 * ch;
+      g4_stage_rows<32 * NJ>(wl, lane, [&](int r, int ch, u32x4 v) {
+        const int row = mrow0 + r, col = n0 + wc * WN + 8 * ch;
         if (row < M && col < N) *reinterpret_cast<u32x4*>(o + (size_t)row * N + col) = v;
       });
     }
   } else {  // PARTIAL / RESIDUAL: fp32, one 16-byte piece per lane per tile
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int tile = (n0 >> 4) + wc * 8 + j;
+    for (int j = 0; j < NJ; ++j) {
+      const int tile = (n0 >> 4) + wc * NJ + j;
       if (tile >= NTT) continue;
       const int col = tile * 16 + 4 * q;
 #pragma unroll
@@ -1012,7 +1015,7 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
   }
 }
 
-template <int MODE, int RMSM, bool RING>
+template <int MODE, int RMSM, bool RING, int NJ = 8>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
@@ -1031,24 +1034,28 @@ __global__ void __launch_bounds__(256, 1)
   const int split = wgid / tiles, pid = wgid - split * tiles;
   int tm, tn;
   g4_tile_coords(pid, tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int m0 = tm * G4_BM, n0 = tn * (32 * NJ);
   const int t0 = split * kc, KT = min(K >> 6, t0 + kc) - t0;
 
-  f32x4 acc[8][8];
+  f32x4 acc[NJ][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float ss[4] = {0.f, 0.f, 0.f, 0.f};
   const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
-  if constexpr (RING) {
+  if constexpr (NJ != 8) {
+    static_assert(!RING && !RMS, "the 256 x 128 tile: slot loop, precomputed statistic");
+    g4n_mainloop<NJ>(g, lds, m0, n0, t0, KT, wu, lane, acc);
+  } else if constexpr (RING) {
     g4_mainloop_ring<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
     wait_vmcnt<0>();  // the ring's clamped tail DMAs land before LDS is reused
   } else {
     g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
   }
-  g4_epilogue<MODE, RMSM>(acc, ss, lds, wu, lane, m0, n0, split,
-                          G4Epi{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, ssq_ws, rms_inv}, qa);
+  g4_epilogue<MODE, RMSM, decltype(acc), NJ>(
+      acc, ss, lds, wu, lane, m0, n0, split,
+      G4Epi{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, ssq_ws, rms_inv}, qa);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1652,6 +1659,9 @@ int gemm_qkv_direct_ok(int M, int tile, int K) {
 // Needs K % 64 == 0; data-parallel or plain split-K (MODE_PARTIAL + reduce kernel) only -- the stream-K tail,
 // hybrid and in-kernel fixup plans stay on gemm2.
 constexpr int G4_TILE = 7;
+// tile config 10: gemm4 on 256 x 128 tiles (g4n_mainloop, 4 n-tiles per wave): store / residual / SwiGLU / split-K
+// partials; a fused norm only with the precomputed statistic (no K split)
+constexpr int G4N_TILE = 10;
 static bool g_g4_default = true;
 void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
 static bool g_g4_ring = false;  // gemm4 main loop: the deeper LDS ring (gemm4w.h g4_mainloop_ring)
@@ -1660,14 +1670,25 @@ static bool use_g4(int tile, int M, int K) {
   return (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
 }
 
-template <int MODE>
+template <int MODE, int NJ = 8>
 static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa,
                       float* rms_ws = nullptr) {
-  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
+  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + 32 * NJ - 1) / (32 * NJ);
   const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   const int grid = tm * tn * ksplit;
+  if constexpr (NJ != 8) {  // 256 x 128 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
+    if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
+      if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
+      gemm4_kernel<MODE, 2, false, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                            rms_eps, ssq, qa, rms_ws);
+    } else if (!rms) {
+      gemm4_kernel<MODE, 0, false, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                            rms_eps, ssq, qa, nullptr);
+    }
+    return;
+  }
 #define JLA_G4(R, INV)                                                                                          \
   do {                                                                                                            \
     if (g_g4_ring)                                                                                                \
@@ -1725,6 +1746,12 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
                       int grid_override = 0, G2Fix fix = G2Fix{}, const QKVArgs& qa = QKVArgs{},
                       float* rms_ws = nullptr) {
+  if constexpr (MODE != MODE_QKV && MODE != MODE_ARGMAX) {
+    if (grid_override == 0 && fix.ksplit <= 1 && fix.tile_count == 0 && tile == G4N_TILE && (K & 63) == 0) {
+      launch_g4<MODE, 4>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
+      return;
+    }
+  }
   if (grid_override == 0 && fix.ksplit <= 1 && fix.tile_count == 0 && use_g4(tile, M, K)) {
     launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
     return;
@@ -1872,6 +1899,9 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps, int tile, int32_t* tickets, int n_tickets, float* rms_ws, size_t rms_ws_floats) {
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
+  if (tile == G4N_TILE && ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
+                           (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
+    return -1;  // the 256 x 128 plan: no QKV / argmax epilogue, the fused norm only precomputed without a K split
   if (tile == G4_SK_TILE) {  // gemm4 stream-K over every (tile, K-tile) iteration: one persistent workgroup per CU
     if (ksplit > 1) return -1;
     if ((N & 15) || (K & 31)) return -1;

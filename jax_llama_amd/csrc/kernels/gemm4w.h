@@ -214,6 +214,112 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
   g4_acc_fence();
 }
 
+// ---------------------------------------------------------------------------------------------
+// g4n_mainloop: the same loop for a 256 (M) x 32 NJ (N) workgroup tile -- each wave a 128 (M) x 16 NJ (N) block,
+// NJ x 8 accumulators (NJ = 4: 256 x 128 tiles, 128 accumulator AGPRs per wave). Twice the tiles of the 256 x 256
+// loop for the outputs whose 256 x 256 grid quantises badly on 256 CUs (Llama-3-8B at M = 2048: o has 128 tiles ->
+// 256 with no K split; w1|w3 896 = 3.5 waves -> 1792 = 7 whole waves), at 1.5x the operand bytes per MFMA. Same LDS
+// images and slot layout (the W half of a slot is half used), same two sub-steps per 64-deep K-tile and one barrier;
+// per sub-step 8 NJ MFMAs with the 8 + NJ fragment reads and 8 + NJ LDS-DMA issues spread over the first slots.
+// No in-loop norm statistic (the caller precomputes it: RMSM 0 / 2 only).
+template <int NJ, typename Acc>
+JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc) {
+  static_assert(NJ == 4 || NJ == 8, "n-tiles per wave");
+  constexpr int ND = NJ;           // W DMAs per wave per K-tile (2 NJ n-tiles x 2 k halves / 4 waves)
+  constexpr int NQ = 8 + NJ;       // fragment reads / DMA issues per sub-step
+  constexpr int MPS = (8 * NJ) / 16;  // MFMAs per slot (16 slots per sub-step)
+  const int wr = wu >> 1, wc = wu & 1;
+  const int K = g.K, KS = K >> 5, NTT = g.N >> 4;
+  const char* const baseA = reinterpret_cast<const char*>(g.x + (size_t)m0 * K + (size_t)t0 * 64);
+  const char* const baseB = reinterpret_cast<const char*>(g.W + ((size_t)(n0 >> 4) * KS + 2 * t0) * 64);
+  unsigned offA[8], offB[ND];
+  const int mlast = g.M - 1 - m0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int P = wu + 4 * j;
+    const int row = min(8 * P + (lane >> 3), mlast);
+    const int chunk = (lane & 7) ^ (4 * (P & 1) + (lane >> 4));
+    offA[j] = (unsigned)row * (unsigned)K * 2u + 16u * (unsigned)chunk;
+  }
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const int f = wu + 4 * j;  // W fragment f: n-tile f >> 1 of the workgroup tile, k half f & 1
+    const int nt = min((n0 >> 4) + (f >> 1), NTT - 1) - (n0 >> 4);
+    offB[j] = ((unsigned)nt * (unsigned)KS + (unsigned)(f & 1)) * 1024u + 16u * (unsigned)lane;
+  }
+  auto dma = [&](int t, int j) {  // the j-th of this wave's NQ DMAs of K-tile t (0..7 x, then W)
+    u32x4* slot = lds + (t & 1) * G4_SLOT_U4;
+    if (j < 8)
+      glds16(baseA + (size_t)t * 128 + offA[j], slot + (wu + 4 * j) * 64);
+    else
+      glds16(baseB + (size_t)t * 2048 + offB[j - 8], slot + G4_A_U4 + (wu + 4 * (j - 8)) * 64);
+  };
+  const int xrd = (wr * 128 + (lane & 15)) * 8;
+  const int xc0 = (0 + (lane >> 4)) ^ ((lane >> 1) & 7), xc1 = (4 + (lane >> 4)) ^ ((lane >> 1) & 7);
+  auto rd = [&](u32x4& dst, int slot, int h, int q) {  // q < NJ: W n-tile q of the wave; else x m-tile q - NJ
+    const u32x4* sp = lds + slot * G4_SLOT_U4;
+    if (q < NJ)
+      dst = sp[G4_A_U4 + ((wc * NJ + q) * 2 + h) * 64 + lane];
+    else
+      dst = sp[xrd + (q - NJ) * 128 + (h ? xc1 : xc0)];
+  };
+  u32x4 w0[NJ], x0[8], w1[NJ], x1[8];
+  auto substep = [&](u32x4 (&wf)[NJ], u32x4 (&xf)[8], u32x4 (&wn)[NJ], u32x4 (&xn)[8], bool do_rd, int rslot, int rh,
+                     bool do_dma, int td) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+#pragma unroll
+      for (int u = 0; u < MPS; ++u) {
+        const int e = MPS * q + u, j = e >> 3, i = e & 7;
+        g4_mfma(acc[j][i], wf[j], xf[i]);
+      }
+      if (q < NQ) {
+        if (do_rd) rd(q < NJ ? wn[q] : xn[q - NJ], rslot, rh, q);
+        if (do_dma) dma(td, q);
+      }
+    }
+  };
+  if (KT > 0) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) dma(0, j);
+  }
+  if (KT > 1) {
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) dma(1, j);
+    wait_vmcnt<NQ>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (KT > 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) rd(q < NJ ? w0[q] : x0[q - NJ], 0, 0, q);
+  }
+  auto mid_barrier = [&]() {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  int t = 0;
+  for (; t + 2 < KT; ++t) {
+    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    mid_barrier();
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, true, t + 2);
+  }
+  if (t + 1 < KT) {
+    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    mid_barrier();
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, false, 0);
+    ++t;
+  }
+  if (t < KT) {
+    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    substep(w1, x1, w0, x0, false, 0, 0, false, 0);
+  }
+  g4_acc_fence();
+}
+
 // Staged bf16 epilogue, in two steps on the wave's private 32 KiB of the (now idle) staging array:
 //  g4_stage_put: lane (c, q) puts its 4 bf16 of an output row (8 bytes at logical byte cb of local row r) -- rows of
 //    CB bytes, 8-byte granules XOR-swizzled by (r & 15) so the 16 rows a lane group writes hit distinct banks;
@@ -221,8 +327,10 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 //    them to store(local row, 16-byte chunk index, data) -- full-row global stores instead of 16-row x 32-byte pieces
 //    (the direct form cost 10+ % at prefill sizes: the epilogue runs with the CU's MFMA pipes idle).
 template <int CB>
+JLA_DEV constexpr int g4_swz(int r) { return ((r & 15) << 3) & (CB - 1); }  // (rows narrower than 128 B: fewer banks)
+template <int CB>
 JLA_DEV void g4_stage_put(char* wl, int r, int cb, u32x2 v) {
-  *reinterpret_cast<u32x2*>(wl + r * CB + (cb ^ ((r & 15) << 3))) = v;
+  *reinterpret_cast<u32x2*>(wl + r * CB + (cb ^ g4_swz<CB>(r))) = v;
 }
 template <int CB, typename F>
 JLA_DEV void g4_stage_rows(const char* wl, int lane, F&& store) {
@@ -232,7 +340,7 @@ JLA_DEV void g4_stage_rows(const char* wl, int lane, F&& store) {
 #pragma unroll 4
   for (int s = 0; s < 128 / RPI; ++s) {
     const int r = RPI * s + lane / LPR;
-    const int sw = (r & 15) << 3;
+    const int sw = g4_swz<CB>(r);
     u32x4 v = *reinterpret_cast<const u32x4*>(wl + r * CB + ((16 * ch) ^ (sw & ~15)));
     if (sw & 8) v = u32x4{v[2], v[3], v[0], v[1]};
     store(r, ch, v);

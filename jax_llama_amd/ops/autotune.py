@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 6  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed), so older persisted picks are re-measured
+TUNE_VERSION = 7  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -275,7 +275,8 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3, 7)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg); 7: gemm4;
+TILE_CANDIDATES = (1, 2, 3, 7, 10)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg); 7: gemm4;
+# 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
 # plus (1, SK_TILE) -- 256x256 with a stream-K tail -- for shapes whose tile count is not a multiple of the CUs
 TUNE_MAX_M = 2048
 
@@ -316,6 +317,7 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
 SK_TILE = 4  # 256x256 tiles with a stream-K tail (no K split): csrc/kernels/gemm.hip gemm_sk
 HYBRID_TILE = 6  # whole waves of 256x256 tiles + the partial wave split 2-way with the in-kernel fixup
 G4SK_TILE = 8  # gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration)
+G4N_TILE = 10  # gemm4 on 256 x 128 tiles (csrc/kernels/gemm4w.h g4n_mainloop)
 SK_MARGIN = 0.97
 TUNE_ROUNDS = 3
 
@@ -324,7 +326,8 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     from . import sk_workspace
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
-    cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c]
+    cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
+             if tm != G4N_TILE or (k % 64 == 0 and not (c > 1 and rms and mode != 1))]
     sk_ws, sk_tk = sk_workspace(e, m, n, k, device)
     if sk_ws is not None:
         cands.append((1, SK_TILE))

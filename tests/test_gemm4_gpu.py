@@ -257,3 +257,49 @@ def test_gemm4_stream_k_qkv():
     _close(kg, kc, 2e-2, 2e-2)
     _close(vg, vc, 2e-2, 2e-2)
     assert int(tk.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("m,n,k,ks", [(2048, 4096, 4096, 1), (700, 2560, 4096, 1), (300, 768, 2048, 2),
+                                      (512, 1056, 1024, 1), (1000, 6144, 1536, 3), (256, 512, 128, 1)])
+def test_gemm4_256x128_tiles(m, n, k, ks):
+    """Tile config 10 (gemm4 on 256 x 128 tiles, 4 n-tiles per wave): store (fp32 / bf16), SwiGLU, residual + mirror,
+    split-K partials; the fused norm with its precomputed statistic. The same MFMA chain per output element as the
+    256 x 256 gemm4 (tile 7), so bit-identical to it, and fp32-reference close; N not a multiple of 128 included."""
+    e = ops.ext()
+    torch.manual_seed(m + n + k + 10)
+    x = torch.randn(m, k).to(BF16)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    pg = PackedLinear.from_dense(w, DEV)
+    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+    gp = PackedLinear.from_dense(gu, DEV)
+    xg = x.to(DEV)
+    h0 = torch.randn(m, n).to(DEV)
+    ws = torch.empty(ks * m * (n + 1), dtype=torch.float32, device=DEV) if ks > 1 else None
+    rw = torch.empty(m, device=DEV) if ks == 1 else None
+
+    def run(tile):
+        outs = []
+        for eps in ((-1.0, 1e-5) if ks == 1 else (-1.0,)):
+            r = rw if eps > 0 else None
+            o = torch.empty(m, n, dtype=torch.float32, device=DEV)
+            e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, r)
+            ob = torch.empty(m, n, dtype=BF16, device=DEV)
+            e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, r)
+            o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile, None, None, r)
+            outs += [o, ob, o2]
+        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, tile)
+        torch.cuda.synchronize()
+        return outs + [hg, mir]
+
+    t10, t7 = run(10), run(G4)
+    for i, (a, b) in enumerate(zip(t10, t7)):
+        assert torch.equal(a, b), f"output {i}: differs from the 256 x 256 gemm4"
+    _close(t10[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+    _close(t10[2], ref.linear_swiglu(x, gu, None), 3e-2, 3e-2)
+    _close(t10[-2], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
+    torch.testing.assert_close(t10[-1].cpu(), t10[-2].cpu().to(BF16), rtol=0, atol=0)
+    if ks == 1:
+        _close(t10[3], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
+        _close(t10[5], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)

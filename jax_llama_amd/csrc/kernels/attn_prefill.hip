@@ -225,6 +225,10 @@ JLA_DEV u32x2 ld_tr(const char* lds, int off) {
 // the 64 O multiplies per tile run only in a wave-uniform branch when some lane needs them (mostly the first tiles).
 // (The eager-rescale launches, impls 4 / 5 / 6 / 10, were slower everywhere and removed in round 4:
 // profiles/r3_attn_prefill_pipe_ab.jsonl, profiles/r4_variant_pruning.md.)
+// PIPE 2: the same loop with the K / V DMA as inline asm (glds16_asm: with the builtin, hipcc put a vmcnt(0) before
+// the first V read of every tile, i.e. waited for the DMA of the NEXT tiles it had just issued), and branch-free, with
+// the next tile's 16 scores MFMAs spread over the 4 key steps (4 per step, fenced by sched_barrier) beside the exps and
+// PV MFMAs instead of sunk into one serial read -> wait -> MFMA chain at the end of the tile.
 template <int NW, int PIPE>
 __global__ void __launch_bounds__(NW * 64, 2)
     attn_prefill_v2_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
@@ -338,7 +342,10 @@ __global__ void __launch_bounds__(NW * 64, 2)
       for (int i = 0; i < 16 / NW; ++i) {
         const int bi = w + NW * i, row = 4 * bi + (lane >> 4);
         const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-        glds16(src + (size_t)min(t0 + row, T - 1) * AP_DH + 8 * ch, dst + 1024 * bi);
+        if constexpr (PIPE == 2)
+          glds16_asm(src + (size_t)min(t0 + row, T - 1) * AP_DH + 8 * ch, dst + 1024 * bi);
+        else
+          glds16(src + (size_t)min(t0 + row, T - 1) * AP_DH + 8 * ch, dst + 1024 * bi);
       }
     };
     auto scores = [&](const char* Kt, f32x16 (&s)[2]) {
@@ -362,6 +369,8 @@ __global__ void __launch_bounds__(NW * 64, 2)
     wait_vmcnt<0>();
     __syncthreads();
     if (n_t > 0 && t_begin <= wave_last_slot) scores(Kr(0), st);
+    // the first iteration's DMA of K(2) lands in K(0)'s slot: every wave must be done reading it
+    if (n_t > 2) __syncthreads();
     for (int it = 0; it < n_t; ++it) {
       const int t0 = t_begin + it * FA_KT, cur = it & 1;
       const bool has1 = it + 1 < n_t, has2 = it + 2 < n_t;
@@ -403,11 +412,33 @@ __global__ void __launch_bounds__(NW * 64, 2)
         // O += V(i) P(i); NEXT is a compile-time copy so no branch splits the MFMAs from the VALU work
         auto body = [&](auto NEXT) {
           f32x16 sn[2];
-          if constexpr (decltype(NEXT)::value) scores(Kr(cur ^ 1), sn);
+          if constexpr (decltype(NEXT)::value) {
+            if constexpr (PIPE == 2) {
+#pragma unroll
+              for (int i = 0; i < 16; ++i) sn[0][i] = sn[1][i] = 0.f;
+            } else {
+              scores(Kr(cur ^ 1), sn);
+            }
+          }
           // key step s: 8 exps -> one P fragment -> its 4 PV MFMAs (one fragment live, exp beside the MFMAs)
           float rs = 0.f;
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
+            if constexpr (PIPE == 2) {
+              // PIPE 2: a quarter of the next tile's scores (dk steps 2s, 2s + 1, both key blocks: 4 MFMAs on two
+              // alternating accumulators) in each key step, fenced so the scheduler keeps them beside this step's
+              // exps and PV MFMAs instead of sinking all 16 into a serial read -> wait -> MFMA chain at the end
+              __builtin_amdgcn_sched_barrier(0);
+              if constexpr (decltype(NEXT)::value) {
+                const char* Kt = Kr(cur ^ 1);
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                  for (int kbk = 0; kbk < 2; ++kbk)
+                    sn[kbk] = mfma32(*reinterpret_cast<const u32x4*>(Kt + fa_off(32 * kbk + col, 4 * s + 2 * kk + hi)),
+                                     qf[0][2 * s + kk], sn[kbk]);
+              }
+            }
             float e[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -434,7 +465,9 @@ __global__ void __launch_bounds__(NW * 64, 2)
         };
         // (the branch lets LLVM hoist the shared exp block above the scores MFMAs; a branch-free variant that always
         // runs the NEXT copy interleaves them but measured neutral: profiles/r3_attn_prefill_branchfree_ab.jsonl)
-        if (has1 && t0 + FA_KT <= wave_last_slot)
+        // PIPE 2: branch-free (the next tile's scores always run; past the wave's last tile they read a settled stale
+        // slot and are never used), so the exps stay in the fenced key steps beside the MFMAs
+        if (PIPE == 2 || (has1 && t0 + FA_KT <= wave_last_slot))
           body(std::true_type{});
         else
           body(std::false_type{});
@@ -585,7 +618,8 @@ static void launch_prefill_v2(const bf16_t* q, const bf16_t* kc, const bf16_t* v
 }
 
 // impl (attn_prefill_set_impl, A/B): 2 = default dispatch; 7 = pipelined 4 waves, 8 = unpipelined 4 waves, 9 =
-// pipelined 8 waves (paired); 1 = the v1 kernel (also the fallback for a non-power-of-two GQA ratio)
+// pipelined 8 waves (paired), 13 = the same with asm LDS-DMA and the next tile's scores spread over the key steps
+// (PIPE 2); 1 = the v1 kernel (also the fallback for a non-power-of-two GQA ratio)
 static int g_attn_prefill_impl = 2;
 void attn_prefill_set_impl(int impl) { g_attn_prefill_impl = impl; }
 
@@ -602,6 +636,8 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   // K/V tile), else 4 waves; below S = 512 the unpipelined 4-wave loop. Interleaved A/B
   // (profiles/r3_attn_prefill_pipe_ab.jsonl, TFLOP/s, previous default -> now): 8B B = 1 S = 2048 454 -> 509,
   // B = 16 S = 2048 672 -> 746, S = 8192 854 -> 903, B = 2048 S = 128 186 -> 198, 70B S = 2048 698 -> 733.
+  // The 8-wave launch is PIPE 2 (impl 13) since round 4: bit-identical to impl 9, +1-5 % on the 8-wave shapes
+  // (profiles/r4_attn_prefill_asm_dma_ab.jsonl).
   if (impl == 2 && pow2rep) {
     if (S <= 256) {
       impl = 8;
@@ -609,16 +645,19 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
       const int npb8 = rep >= 8 ? 1 : 8 / rep;
       const int n_qb8 = (S + 32 * npb8 - 1) / (32 * npb8);
       const int wg8 = (n_qb8 + 1) / 2 * Hkv * (rep / (8 / npb8)) * B;
-      impl = wg8 >= 256 ? 9 : 7;
+      impl = wg8 >= 256 ? 13 : 7;
     }
   }
-  if ((impl == 7 || impl == 8 || impl == 9) && (rep % (impl == 9 ? 8 : 4) == 0 || (impl == 9 ? 8 : 4) % rep == 0)) {
+  const int nw_impl = impl == 9 || impl == 13 ? 8 : 4;
+  if ((impl == 7 || impl == 8 || impl == 9 || impl == 13) && (rep % nw_impl == 0 || nw_impl % rep == 0)) {
     if (impl == 7)
       launch_prefill_v2<4, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
     else if (impl == 8)
       launch_prefill_v2<4, 0>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, false, s);
-    else
+    else if (impl == 9)
       launch_prefill_v2<8, 1>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, true, s);
+    else
+      launch_prefill_v2<8, 2>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, S, H, Hkv, T, rep, true, s);
     JLA_CHECK_LAUNCH();
     return 0;
   }

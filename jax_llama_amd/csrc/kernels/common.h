@@ -117,6 +117,18 @@ JLA_DEV void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
+// The same DMA as inline asm: hipcc's waitcnt pass does not see it write LDS, so it adds no vmcnt(0) before LDS
+// reads it cannot prove disjoint from the DMA target (with the builtin, a read of ring slot i waits for the DMA into
+// slot i + 1 issued just before it). The caller owns the wait: s_waitcnt vmcnt before the barrier that publishes
+// the slot. (Loads the compiler counts stay safe: a DMA it does not count only makes its own waits stronger.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: nothing else in these kernels keeps a value in it
+JLA_DEV void glds16_asm(const void* gsrc, void* lds_wave_base) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(m0) : "memory", "m0");
+}
+#pragma clang diagnostic pop
 // s_waitcnt vmcnt(N) only (expcnt/lgkmcnt left at their maxima)
 template <int N>
 JLA_DEV void wait_vmcnt() {

@@ -257,7 +257,7 @@ def _attn_ref_gpu(q, kc, vc, slot0, kv_start, key_mask=None, chunk=512):
     return out.reshape(b * s, h * dh)
 
 
-@pytest.mark.parametrize("impl", [2, 1, 7, 8, 9])
+@pytest.mark.parametrize("impl", [2, 1, 7, 8, 9, 13])
 @pytest.mark.parametrize("rep", [1, 4, 8])
 @pytest.mark.parametrize("s,slot0,masked", [(7, 0, False), (130, 10, False), (512, 0, False), (300, 0, True),
                                             (2048, 0, False)])

@@ -97,10 +97,8 @@ SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20,
               # gemm4 stream-K, bf16/fp32 store: one accumulator tile spilled across the ticket / last-arriver block and
               # one dword in the segment prologue -- outside the main loop (checked in the .s)
               "gemm4_sk_kernelILi0E": 32,
-              # gemm4 stream-K residual: 2 dwords around the double-buffered residual reads of the epilogue
-              "gemm4_sk_kernelILi1E": 16,
-              # gemm4 stream-K QKV: up to 5 dwords around the batched position / cos-sin reads of the epilogue
-              "gemm4_sk_kernelILi3E": 24}
+              # (debug-bounds build) gemm4 stream-K QKV: 2 dwords in the epilogue
+              "gemm4_sk_kernelILi3E": 16}
 
 
 def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):

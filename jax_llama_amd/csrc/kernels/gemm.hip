@@ -919,71 +919,31 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
   } else if constexpr (MODE == MODE_QKV) {
     // RoPE on the two (even, odd) pairs of the lane's 4 columns in fp32, then staged: 16-byte pieces of a row go to
     // q or to the k / v cache row at slot[0] + (position in the sequence); same arithmetic as gemm2's /
-    // gemm_reduce_kernel's QKV epilogue (reference model.py:58-92, :169-199).
-    // The 8 row positions are read once; with Dh = 128 the wave block is one head (RoPE or not: a wave-uniform
-    // branch) and the next n-tile's 8 cos / sin reads are issued before this n-tile's rotations -- the per-piece
-    // position -> table -> rotate chain cost two memory round trips per piece (128 per tile).
-    int pos[8];
+    // gemm_reduce_kernel's QKV epilogue (reference model.py:58-92, :169-199)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      int p = qa.positions[min(rbase + 16 * i, M - 1)];
-      if (p < 0 || p >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
-      pos[i] = p < 0 ? 0 : (p >= qa.table_len ? qa.table_len - 1 : p);
-    }
-    const int gcol0 = n0 + wc * 128;
-    if (qa.Dh == 128) {
-      if (gcol0 / 128 < qa.H + qa.Hkv) {
-        float4 cs[2][8];
-        auto load_cs = [&](int j, float4(&dst)[8]) {
+    for (int j = 0; j < 8; ++j) {
+      const int gcol = n0 + wc * 128 + 16 * j + 4 * q;
+      const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
-            dst[i] = *reinterpret_cast<const float4*>(qa.table + (size_t)pos[i] * 64 + ((16 * j + 4 * q) >> 1));
-        };
-        load_cs(0, cs[0]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (j + 1 < 8) load_cs(j + 1, cs[(j + 1) & 1]);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const f32x4 tv = tile_val(j, i);
-            const float4 t = cs[j & 1][i];
-            const float r0 = tv[0] * t.x - tv[1] * t.y, r1 = tv[0] * t.y + tv[1] * t.x;
-            const float r2 = tv[2] * t.z - tv[3] * t.w, r3 = tv[2] * t.w + tv[3] * t.z;
-            g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(r0, r1), pack2bf(r2, r3)});
-          }
+      for (int i = 0; i < 8; ++i) {
+        const int grow = min(rbase + 16 * i, M - 1);
+        const f32x4 tv = tile_val(j, i);
+        float v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3];
+        if (head < qa.H + qa.Hkv) {
+          int pos = qa.positions[grow];
+          if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
+          pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
+          const float4 cs = *reinterpret_cast<const float4*>(qa.table + (size_t)pos * (qa.Dh >> 1) + (d0 >> 1));
+          const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
+          const float r2 = v2 * cs.z - v3 * cs.w, r3 = v2 * cs.w + v3 * cs.z;
+          v0 = r0;
+          v1 = r1;
+          v2 = r2;
+          v3 = r3;
         }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const f32x4 tv = tile_val(j, i);
-            g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])});
-          }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int gcol = gcol0 + 16 * j + 4 * q;
-        const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const f32x4 tv = tile_val(j, i);
-          float v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3];
-          if (head < qa.H + qa.Hkv) {
-            const float4 cs = *reinterpret_cast<const float4*>(qa.table + (size_t)pos[i] * (qa.Dh >> 1) + (d0 >> 1));
-            const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
-            const float r2 = v2 * cs.z - v3 * cs.w, r3 = v2 * cs.w + v3 * cs.z;
-            v0 = r0;
-            v1 = r1;
-            v2 = r2;
-            v3 = r3;
-          }
-          g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v0, v1), pack2bf(v2, v3)});
-        }
+        g4_stage_put<256>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v0, v1), pack2bf(v2, v3)});
       }
     }
-    const int cslot0 = qa.slot[0];
     g4_stage_rows<256>(wl, lane, [&](int r, int ch, u32x4 v) {
       const int grow = mrow0 + r, gcol = n0 + wc * 128 + 8 * ch;
       if (grow >= M || gcol >= N) return;
@@ -992,7 +952,7 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
         *reinterpret_cast<u32x4*>(qa.q + ((size_t)grow * qa.H + head) * qa.Dh + d0) = v;
       } else {
         const int b = grow / qa.S, sq = grow - b * qa.S;
-        const int cslot = cslot0 + sq;
+        const int cslot = qa.slot[0] + sq;
         if (cslot < qa.T) {
           const bool is_k = head < qa.H + qa.Hkv;
           const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
@@ -1030,54 +990,7 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
         if (row < M && col < N) *reinterpret_cast<u32x4*>(o + (size_t)row * N + col) = v;
       });
     }
-  } else if constexpr (MODE == MODE_RESIDUAL) {
-    // fp32 read-modify-write, one 16-byte piece per lane per tile. One piece at a time (load -> vmcnt(0) -> add ->
-    // store, the order hipcc keeps because a store may alias the next load) paid a memory round trip per piece, ~40 us
-    // per 256 x 256 tile (+40 % on o at M = 32768). Whole, mirrored wave blocks: straight-line, the next n-tile's 8
-    // residual reads issued before this n-tile's adds and stores (one round trip per wave block, hidden behind the
-    // stores); otherwise the guarded piecewise loop.
-    float* const of = static_cast<float*>(out);
-    if (mirror && mrow0 + 128 <= M && (n0 >> 4) + wc * NJ + NJ <= NTT) {
-      f32x4 rv[2][8];
-      auto load_res = [&](int j, f32x4(&r)[8]) {
-        const int col = ((n0 >> 4) + wc * NJ + j) * 16 + 4 * q;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = *reinterpret_cast<const f32x4*>(of + (size_t)(rbase + 16 * i) * N + col);
-      };
-      load_res(0, rv[0]);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if (j + 1 < NJ) load_res(j + 1, rv[(j + 1) & 1]);
-        const int col = ((n0 >> 4) + wc * NJ + j) * 16 + 4 * q;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const size_t idx = (size_t)(rbase + 16 * i) * N + col;
-          const f32x4 v = tile_val(j, i);
-          const f32x4 nv = accumulate ? rv[j & 1][i] + v : v;
-          *reinterpret_cast<f32x4*>(of + idx) = nv;
-          *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int tile = (n0 >> 4) + wc * NJ + j;
-        if (tile >= NTT) continue;
-        const int col = tile * 16 + 4 * q;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int row = rbase + 16 * i;
-          if (row >= M) continue;
-          const size_t idx = (size_t)row * N + col;
-          const f32x4 v = tile_val(j, i);
-          f32x4* o = reinterpret_cast<f32x4*>(of + idx);
-          const f32x4 nv = accumulate ? *o + v : v;
-          *o = nv;
-          if (mirror) *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
-        }
-      }
-    }
-  } else {  // PARTIAL: fp32 slabs, one 16-byte piece per lane per tile
+  } else {  // PARTIAL / RESIDUAL: fp32, one 16-byte piece per lane per tile
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int tile = (n0 >> 4) + wc * NJ + j;
@@ -1088,8 +1001,15 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
         const int row = rbase + 16 * i;
         if (row >= M) continue;
         const size_t idx = (size_t)row * N + col;
-        static_assert(MODE == MODE_PARTIAL, "gemm4 epilogue modes");
-        *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = tile_val(j, i);
+        const f32x4 v = tile_val(j, i);
+        if constexpr (MODE == MODE_PARTIAL) {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = v;
+        } else {
+          f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(out) + idx);
+          const f32x4 nv = accumulate ? *o + v : v;
+          *o = nv;
+          if (mirror) *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
+        }
       }
     }
   }
@@ -1575,17 +1495,8 @@ __global__ void __launch_bounds__(256)
   const size_t total4 = (size_t)M * N / 4;
   if (e4 >= total4) return;
   const size_t idx = e4 * 4;
-  // (32-bit division when the index fits: the 64-bit one is a ~100-instruction software routine per thread)
-  const int m = total4 < (1u << 29) ? (int)((unsigned)idx / (unsigned)N) : (int)(idx / N);
-  const int col = (int)(idx - (size_t)m * N);
-  // every read of this thread in flight at once (the residual row with the partials, the split loop unrolled):
-  // one float4 per thread leaves ~32 KiB in flight per CU, so serial round trips cap the kernel well below HBM rate
-  float4 res = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (MODE == MODE_RESIDUAL) {
-    if (accumulate) res = *reinterpret_cast<const float4*>(static_cast<const float*>(out) + idx);
-  }
+  const int m = (int)(idx / N), col = (int)(idx - (size_t)m * N);
   float4 v = reinterpret_cast<const float4*>(ws)[e4];
-#pragma unroll 4
   for (int s = 1; s < ksplit; ++s) {
     const float4 p = reinterpret_cast<const float4*>(ws + (size_t)s * M * N)[e4];
     v.x += p.x;
@@ -1633,7 +1544,7 @@ __global__ void __launch_bounds__(256)
     }
   } else if constexpr (MODE == MODE_RESIDUAL) {
     float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + idx);
-    float4 r = res;
+    float4 r = *o;
     if (accumulate) {
       r.x += vv[0];
       r.y += vv[1];

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Prefill attention throughput (causal, GQA) at real model shapes: TFLOP/s of impl 2 (GQA-shared
-32x32x16 MFMA flash kernel, 32 queries per wave), impl 4 (always paired launch), impl 5 / 6 (the
-same with 8 waves per workgroup: twice the queries per staged K/V tile) and impl 1 (v1). FLOPs counted for the causal triangle only:
+"""Prefill attention throughput (causal, GQA) at real model shapes: TFLOP/s of impl 2 (the default dispatch of the
+GQA-shared 32x32x16 MFMA flash kernel, 32 queries per wave), 7 / 8 (pipelined / unpipelined, 4 waves), 9 / 13
+(pipelined, 8 waves; 13 with asm LDS-DMA and interleaved next-tile scores) and impl 1 (v1). FLOPs counted for the causal triangle only:
 4 * B * H * Dh * S (S + 1) / 2. Prints one JSON line per (shape, impl)."""
 from __future__ import annotations
 
@@ -26,7 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default=None, help="run only this shape name (profiling)")
     ap.add_argument("--impl", type=int, default=None, help="run only this impl (profiling)")
-    ap.add_argument("--impls", type=int, nargs="*", default=None, help="impls to compare (default 2 4 5 6 1)")
+    ap.add_argument("--impls", type=int, nargs="*", default=None, help="impls to compare (default 2 7 8 9 13 1)")
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     e = ops.ext()
@@ -41,7 +41,7 @@ def main():
         slot = torch.zeros(1, dtype=torch.int32, device="cuda")
         flops = 4.0 * b * h * 128 * s * (s + 1) / 2
         ref = None
-        impls = [i for i in (args.impls or (2, 7, 8, 9, 1)) if not (i == 1 and s * s * b * h > 2048 * 2048 * 16 * 32)
+        impls = [i for i in (args.impls or (2, 7, 8, 9, 13, 1)) if not (i == 1 and s * s * b * h > 2048 * 2048 * 16 * 32)
                  and (args.impl is None or i == args.impl)]
         best, diffs = {i: float("inf") for i in impls}, {}
         for impl in impls:  # warm-up + correctness vs the first impl

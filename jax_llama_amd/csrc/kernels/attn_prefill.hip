@@ -632,8 +632,8 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
   const bool pow2rep = rep == 1 || rep == 2 || rep == 4 || rep == 8;
   int impl = g_attn_prefill_impl;
   // default (impl 2): the software-pipelined loop from S = 512 (a query block needs a few tiles to pipeline), with 8
-  // waves per workgroup when that paired grid still fills the CUs (>= 256 workgroups: twice the queries per staged
-  // K/V tile), else 4 waves; below S = 512 the unpipelined 4-wave loop. Interleaved A/B
+  // waves per workgroup when that paired grid fills the CUs without exceeding ~4 workgroups per CU (256..1023
+  // workgroups: twice the queries per staged K/V tile), else 4 waves; up to S = 256 the unpipelined 4-wave loop. Interleaved A/B
   // (profiles/r3_attn_prefill_pipe_ab.jsonl, TFLOP/s, previous default -> now): 8B B = 1 S = 2048 454 -> 509,
   // B = 16 S = 2048 672 -> 746, S = 8192 854 -> 903, B = 2048 S = 128 186 -> 198, 70B S = 2048 698 -> 733.
   // The 8-wave launch is PIPE 2 (impl 13) since round 4: bit-identical to impl 9, +1-5 % on the 8-wave shapes
@@ -645,7 +645,10 @@ int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int3
       const int npb8 = rep >= 8 ? 1 : 8 / rep;
       const int n_qb8 = (S + 32 * npb8 - 1) / (32 * npb8);
       const int wg8 = (n_qb8 + 1) / 2 * Hkv * (rep / (8 / npb8)) * B;
-      impl = wg8 >= 256 ? 13 : 7;
+      // 8 waves only for mid-sized grids: from 4 paired 8-wave workgroups per CU up, the 4-wave grid (twice the
+      // workgroups, 2 resident per CU) measured faster or tied on 4 of 4 boxes (8B B = 16 S = 2048 747-784 vs 731-762
+      // TFLOP/s, 7B MHA B = 16 661-687 vs 597-675; profiles/r4_attn_prefill_dispatch_ab.jsonl)
+      impl = wg8 >= 256 && wg8 < 1024 ? 13 : 7;
     }
   }
   const int nw_impl = impl == 9 || impl == 13 ? 8 : 4;

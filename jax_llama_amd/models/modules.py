@@ -44,10 +44,12 @@ class LLaMAAttention:
         q4 = q.reshape(b, seq_len, m.n_heads, m.head_dim)
         weights = None
         att_p = None
-        if output_attentions:  # debug path: materialised softmax weights (reference :277-286)
+        if output_attentions:
+            # the layer output still comes from the attention kernel (as without the flag); the softmax weights the
+            # reference returns (:277-286) are materialised beside it by the fp32 oracle, on the tensors' device
             s0 = int(slot0) if not torch.is_tensor(slot0) else int(slot0.item())
-            a, weights = ref.attention(q4, kc, vc, s0, kv_start, key_mask, return_weights=True)
-            a = a.reshape(b * seq_len, -1)
+            _, weights = ref.attention(q4, kc, vc, s0, kv_start, key_mask, return_weights=True)
+            a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask)
         else:
             att_p = pk.att if pk is not None and ops.attention_packs(q4, kc, key_mask) else None
             a = ops.attention(q4, kc, vc, slot0, kv_start, key_mask, out_packed=att_p)

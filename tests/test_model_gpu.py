@@ -180,3 +180,19 @@ def test_packed_activations_decode_rows(rows):
         ops.PACKED_X = saved
     assert rel_err(a, b) < 1e-2
     assert rel_err(a, cpu(toks).logits) < 2e-2
+
+
+def test_output_attentions_gpu_same_logits_and_causal_weights():
+    """output_attentions on the GPU: the layer outputs still come from the attention kernel (logits identical to the
+    run without the flag), and the returned weights are the causal softmax rows (reference model.py:277-286)."""
+    cfg = gpu_config(num_hidden_layers=2)
+    _, gpu, _ = _pair(cfg, seed=4)
+    toks = torch.randint(0, cfg.vocab_size, (2, 9), dtype=torch.int32)
+    plain = gpu(toks).logits.float().cpu()
+    out = gpu(toks, output_attentions=True)
+    assert torch.equal(out.logits.float().cpu(), plain)
+    assert len(out.attentions) == cfg.num_hidden_layers
+    w = out.attentions[0].float().cpu()
+    assert w.shape == (2, cfg.num_attention_heads, 9, 9)
+    assert torch.allclose(w.sum(-1), torch.ones_like(w.sum(-1)), atol=1e-4)
+    assert torch.all(torch.triu(w[0, 0], 1) == 0)

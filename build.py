@@ -128,7 +128,7 @@ def build_C(jobs: int, force: bool, debug_bounds: bool = False) -> Path:
         rebuilt = list(ex.map(lambda so: _compile_hip(so[0], so[1], headers, force, extra), zip(srcs, objs)))
     # the hand-counted load rings must never be read before their waits: check the assembly
     for src, did in zip(srcs, rebuilt):
-        if did and src.stem in ("gemv", "skinny", "attn_decode", "decode_mk"):  # (attn_decode: the v4 ring)
+        if did and src.stem in ("gemv", "attn_decode", "attn_decode_mma"):  # (attn_decode: the v4 ring)
             asm = odir / (src.stem + ".s")
             _run([HIPCC, *HIP_FLAGS, *extra, "--cuda-device-only", "-S", str(src), "-o", str(asm)])
             try:

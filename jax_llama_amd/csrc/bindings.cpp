@@ -542,80 +542,6 @@ void attn_decode(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c
      "attn_decode");
 }
 
-// ---- persistent decode step (csrc/kernels/decode_mk.hip)
-// The per-layer pointer table [L][6] (wqkv, wo, wgu, wdown, k cache, v cache of the layer) as a device int64
-// tensor, every weight's size checked against the model dims here (the kernel trusts the table).
-Tensor decode_mk_table(std::vector<Tensor> wqkv, std::vector<Tensor> wo, std::vector<Tensor> wgu,
-                       std::vector<Tensor> wdown, Tensor kc, Tensor vc, int64_t D, int64_t H, int64_t Hkv,
-                       int64_t F) {
-  const int64_t L = wqkv.size(), dh = 128;
-  check(L > 0 && (int64_t)wo.size() == L && (int64_t)wgu.size() == L && (int64_t)wdown.size() == L,
-        "decode_mk_table: one weight of each kind per layer");
-  check_gpu(kc, "kc");
-  check_gpu(vc, "vc");
-  check(kc.dim() == 5 && kc.size(0) == L && kc.size(2) == Hkv && kc.size(4) == dh && kc.sizes() == vc.sizes() &&
-            kc.scalar_type() == torch::kBFloat16 && vc.scalar_type() == torch::kBFloat16,
-        "decode_mk_table: caches must be bf16 [L, B, Hkv, T, 128]");
-  auto host = torch::empty({L, 6}, torch::dtype(torch::kInt64));
-  int64_t* t = host.data_ptr<int64_t>();
-  const int64_t nq = (H + 2 * Hkv) * dh;
-  for (int64_t l = 0; l < L; ++l) {
-    const Tensor* ws[4] = {&wqkv[l], &wo[l], &wgu[l], &wdown[l]};
-    const int64_t want[4] = {nq * D, D * H * dh, 2 * F * D, D * F};
-    for (int j = 0; j < 4; ++j) {
-      check_gpu(*ws[j], "layer weight");
-      check(ws[j]->scalar_type() == torch::kBFloat16 && ws[j]->numel() == want[j],
-            "decode_mk_table: a packed layer weight does not match the model dims");
-      t[l * 6 + j] = reinterpret_cast<int64_t>(ws[j]->data_ptr());
-    }
-    t[l * 6 + 4] = reinterpret_cast<int64_t>(kc[l].data_ptr());
-    t[l * 6 + 5] = reinterpret_cast<int64_t>(vc[l].data_ptr());
-  }
-  return host.to(kc.device());
-}
-
-void decode_mk(Tensor table, Tensor h, Tensor hb, Tensor q, Tensor att, Tensor act, Tensor ssq, Tensor rope,
-               Tensor positions, Tensor slot, Tensor kv_start, Tensor kc, Tensor slab, Tensor tickets, Tensor bar,
-               Tensor err, Tensor aws, Tensor atk, int64_t H, int64_t Hkv, int64_t F, double eps,
-               c10::optional<Tensor> trace, int64_t prefetch_late) {
-  for (auto* t : {&table, &h, &hb, &q, &att, &act, &ssq, &rope, &positions, &slot, &kv_start, &kc, &slab, &tickets,
-                  &bar, &err, &aws, &atk})
-    check_gpu(*t, "decode_mk operand");
-  const int64_t M = h.size(0), D = h.size(1), L = table.size(0), dh = 128, T = kc.size(3);
-  check(table.scalar_type() == torch::kInt64 && table.dim() == 2 && table.size(1) == 6 && kc.size(0) == L,
-        "decode_mk: table [L, 6] int64 for the cache's layers");
-  check(h.scalar_type() == torch::kFloat32 && h.dim() == 2 && hb.scalar_type() == torch::kBFloat16 &&
-            hb.numel() == M * D,
-        "decode_mk: h fp32 [M, D], hb bf16");
-  check(kc.size(1) == M && kc.size(2) == Hkv && kc.size(4) == dh, "decode_mk: cache rows / heads");
-  check(q.scalar_type() == torch::kBFloat16 && q.numel() >= M * H * dh && att.scalar_type() == torch::kBFloat16 &&
-            att.numel() >= M * H * dh && act.scalar_type() == torch::kBFloat16 && act.numel() >= M * F,
-        "decode_mk: q / att / act buffers");
-  check(ssq.scalar_type() == torch::kFloat32 && ssq.numel() >= D / 16 * 4, "decode_mk: ssq buffer");
-  check(rope.scalar_type() == torch::kFloat32 && rope.dim() == 3 && rope.size(1) == dh / 2 && rope.size(2) == 2,
-        "decode_mk: rope table [len, Dh/2, 2]");
-  check(positions.scalar_type() == torch::kInt32 && positions.numel() == M && kv_start.scalar_type() == torch::kInt32 &&
-            kv_start.numel() == M && slot.scalar_type() == torch::kInt32 && slot.numel() >= 1,
-        "decode_mk: positions / kv_start / slot int32");
-  check(slab.scalar_type() == torch::kFloat32 && tickets.scalar_type() == torch::kInt32 &&
-            bar.scalar_type() == torch::kInt32 && err.scalar_type() == torch::kInt32 &&
-            aws.scalar_type() == torch::kFloat32 && atk.scalar_type() == torch::kInt32 && atk.numel() >= 32 * M * Hkv &&
-            bar.numel() >= jla::decode_mk_bar_words(),
-        "decode_mk: workspace dtypes / sizes");
-  unsigned long long* tr = nullptr;
-  if (trace.has_value()) {
-    check_gpu(*trace, "trace");
-    check(trace->scalar_type() == torch::kInt64 && trace->numel() >= jla::decode_mk_trace_words(), "decode_mk: trace");
-    tr = reinterpret_cast<unsigned long long*>(trace->data_ptr());
-  }
-  rc(jla::decode_mk(table.data_ptr(), L, M, D, H, Hkv, F, T, (float)eps, ptr<float>(h), bf(hb), bf(q), bf(att),
-                    bf(act), ptr<float>(ssq), reinterpret_cast<const float2*>(rope.data_ptr()), rope.size(0),
-                    ptr<int32_t>(positions), ptr<int32_t>(slot), ptr<int32_t>(kv_start), ptr<float>(slab),
-                    slab.numel(), ptr<int32_t>(tickets), tickets.numel(), reinterpret_cast<unsigned*>(bar.data_ptr()),
-                    ptr<int32_t>(err), ptr<float>(aws), aws.numel(), ptr<int32_t>(atk), tr, (int)prefetch_late, stream()),
-     "decode_mk");
-}
-
 void attn_prefill(Tensor q, Tensor kc, Tensor vc, Tensor slot, Tensor kv_start, c10::optional<Tensor> key_mask,
                   Tensor out) {
   check_attn(q, kc, vc, slot, kv_start, key_mask, out);
@@ -872,7 +798,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
     return jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k) != 0;
   });
   m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
-  m.def("gemm_set_g4_ring", [](int64_t on) { jla::gemm_set_g4_ring((int)on); });
   m.def("gemm4_sk_workspace", [](int64_t m, int64_t n) {
     return py::make_tuple((int64_t)jla::gemm4_sk_workspace_floats(), (int64_t)jla::gemm4_sk_tickets(m, n));
   });
@@ -931,23 +856,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_set_v3_max_pairs", [](int64_t n) { jla::attn_set_v3_max_pairs((int)n); });
   m.def("attn_set_v5_max_pairs", [](int64_t n) { jla::attn_set_v5_max_pairs((int)n); });
   m.def("attn_set_v5_fold", [](int64_t n) { jla::attn_set_v5_fold((int)n); });
+  m.def("attn_set_v6", [](int64_t mode) { jla::attn_set_v6((int)mode); });
+  m.def("attn_set_v6_wpp", [](int64_t wpp) { jla::attn_set_v6_wpp((int)wpp); });
+  m.def("attn_v6_wpp", [](int64_t pairs) { return jla::attn_v6_wpp((int)pairs); });
   m.def("attn_set_v1_min_wgs", [](int64_t n) { jla::attn_set_v1_min_wgs((int)n); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
         py::arg("nsplit"), py::arg("out_pack") = py::none());
-  m.def("decode_mk_table", &decode_mk_table);
-  m.def("decode_mk", &decode_mk, py::arg("table"), py::arg("h"), py::arg("hb"), py::arg("q"), py::arg("att"),
-        py::arg("act"), py::arg("ssq"), py::arg("rope"), py::arg("positions"), py::arg("slot"), py::arg("kv_start"),
-        py::arg("kc"), py::arg("slab"), py::arg("tickets"), py::arg("bar"), py::arg("err"), py::arg("aws"),
-        py::arg("atk"), py::arg("H"), py::arg("Hkv"), py::arg("F"), py::arg("eps"), py::arg("trace") = py::none(),
-        py::arg("prefetch_late") = 0);
-  m.def("decode_mk_trace_words", []() { return jla::decode_mk_trace_words(); });
-  m.def("decode_mk_supported", [](int64_t m, int64_t d, int64_t h, int64_t hkv, int64_t dh, int64_t f) {
-    return jla::decode_mk_supported(m, d, h, hkv, dh, f) != 0;
-  });
-  m.def("decode_mk_workspace", [](int64_t T) {  // (slab floats, attention splits per (row, kv head))
-    return py::make_tuple((int64_t)jla::decode_mk_slab_floats(), (int64_t)jla::decode_mk_max_splits(T));
-  });
   m.def("attn_prefill", &attn_prefill, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"));
   m.def("attn_prefill_set_impl", [](int64_t impl) { jla::attn_prefill_set_impl((int)impl); });

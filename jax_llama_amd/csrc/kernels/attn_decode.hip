@@ -1125,18 +1125,29 @@ static bool use_v5(int B, int Hkv, int rep) {
   return g_attn_impl == 2 && rep <= 16 && (rep & (rep - 1)) == 0 &&
          (pairs <= g_attn_v5_max_pairs || (rep >= 8 && pairs <= 4 * g_attn_v5_max_pairs));
 }
-// the kernels that also write the packed output copy: v5, v3, and v4 at decode rows <= 64 (mid-batch)
+// v6 (attn_decode_mma.hip: scores and P.V on the matrix cores, one workgroup per pair, no workspace): 0 off,
+// 1 where it wins (by shape), 2 every decode shape it supports (A/B, tests)
+static int g_attn_v6 = 0;
+void attn_set_v6(int mode) { g_attn_v6 = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
+static bool use_v6(int B, int Hkv, int rep) {
+  if (g_attn_v6 == 0 || g_attn_impl != 2 || rep > 16 || (rep & (rep - 1))) return false;
+  if (g_attn_v6 == 2) return true;
+  return rep >= 8 && B * Hkv >= 128;
+}
+// the kernels that also write the packed output copy: v6, v5, v3, and v4 at decode rows <= 64 (mid-batch)
 int attn_decode_packs(int B, int Hkv, int rep) {
-  return (use_v5(B, Hkv, rep) || use_v3(B, Hkv, rep) || (B <= SKINNY_MAX_M && v4_midbatch(B, Hkv, rep))) ? 1 : 0;
+  return (use_v6(B, Hkv, rep) || use_v5(B, Hkv, rep) || use_v3(B, Hkv, rep) || (B <= SKINNY_MAX_M && v4_midbatch(B, Hkv, rep))) ? 1 : 0;
 }
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep) {
+  if (use_v6(B, Hkv, rep)) return T;
   if (use_v5(B, Hkv, rep)) return 16 * kpg5(rep);
   if (use_v3(B, Hkv, rep)) return T;
   return use_v2(B, Hkv, rep) ? 4 * kpg_v2(rep, B * Hkv) : 16 * kpg_v1(rep, B, Hkv, T);
 }
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
+  if (use_v6(B, Hkv, rep)) return 1;
   if (use_v5(B, Hkv, rep)) return (T + 16 * kpg5(rep) - 1) / (16 * kpg5(rep));
   if (use_v3(B, Hkv, rep)) return 1;
   if (!use_v2(B, Hkv, rep)) {
@@ -1157,10 +1168,13 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
   if (B <= 0) return 0;
   if (out_pack && !attn_decode_packs(B, Hkv, H / Hkv)) return -3;  // only the small-batch kernels write the packed copy
   // (a key mask sends the mid-batch rows to v2, which does not write it)
-  if (out_pack && key_mask && !use_v5(B, Hkv, H / Hkv) && !use_v3(B, Hkv, H / Hkv)) return -3;
+  if (out_pack && key_mask && !use_v6(B, Hkv, H / Hkv) && !use_v5(B, Hkv, H / Hkv) && !use_v3(B, Hkv, H / Hkv))
+    return -3;
   if (Dh != AD_DH || H % Hkv) return -1;
   const int rep = H / Hkv;
   if (attn_decode_splits(B, Hkv, t_cap, rep) != nsplit) return -2;
+  if (use_v6(B, Hkv, rep))
+    return attn_decode_v6(q, kc, vc, slot, kv_start, key_mask, mask_len, out, B, H, Hkv, T, t_cap, s, out_pack);
   const float scale = 1.f / sqrtf((float)Dh);
   if (use_v5(B, Hkv, rep)) {
     dim3 grid5(nsplit, Hkv, B);

@@ -785,8 +785,6 @@ __global__ void __launch_bounds__(256 * WM)
 // [split][M][N] (+ the fused-RMS partial sums [split][M]) summed by gemm_reduce_kernel, as gemm2's.
 // RMSM (fused RMSNorm statistic): 0 none; 1 summed inside the main loop from the x fragments (split-K partial
 // slabs: per-split sums to ssq_ws); 2 read from rms_inv[M], computed ahead of the GEMM by rms_rowinv_kernel.
-// RING: the main loop of g4_mainloop_ring (3-slot x ring + 4-slot W ring, all 160 KiB of LDS) instead of the
-// two 64 KiB K-tile slots of g4_mainloop.
 // The epilogue of one gemm4 output tile (every mode; see gemm4_kernel), shared by the data-parallel and the
 // stream-K launches. acc: this wave's finished C^T accumulators; ss: the in-loop RMS partial sums (RMSM 1).
 struct G4Epi {
@@ -1015,14 +1013,14 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
   }
 }
 
-template <int MODE, int RMSM, bool RING, int NJ = 8>
+template <int MODE, int RMSM, int NJ = 8>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
                  float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv) {
   constexpr bool RMS = RMSM == 1;
-  // the K-tile slots / rings; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
-  __shared__ u32x4 lds[RING ? G4R_LDS_U4 : 2 * G4_SLOT_U4 + 64];
+  // the two K-tile slots; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
+  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wu >> 1, wc = wu & 1;
@@ -1045,11 +1043,8 @@ __global__ void __launch_bounds__(256, 1)
   float ss[4] = {0.f, 0.f, 0.f, 0.f};
   const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
   if constexpr (NJ != 8) {
-    static_assert(!RING && !RMS, "the 256 x 128 tile: slot loop, precomputed statistic");
+    static_assert(!RMS, "the 256 x 128 tile: precomputed statistic");
     g4n_mainloop<NJ>(g, lds, m0, n0, t0, KT, wu, lane, acc);
-  } else if constexpr (RING) {
-    g4_mainloop_ring<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
-    wait_vmcnt<0>();  // the ring's clamped tail DMAs land before LDS is reused
   } else {
     g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
   }
@@ -1664,8 +1659,6 @@ constexpr int G4_TILE = 7;
 constexpr int G4N_TILE = 10;
 static bool g_g4_default = true;
 void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
-static bool g_g4_ring = false;  // gemm4 main loop: the deeper LDS ring (gemm4w.h g4_mainloop_ring)
-void gemm_set_g4_ring(int on) { g_g4_ring = on != 0; }
 static bool use_g4(int tile, int M, int K) {
   return (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
 }
@@ -1681,23 +1674,17 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   if constexpr (NJ != 8) {  // 256 x 128 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
     if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
       if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
-      gemm4_kernel<MODE, 2, false, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+      gemm4_kernel<MODE, 2, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
                                                             rms_eps, ssq, qa, rms_ws);
     } else if (!rms) {
-      gemm4_kernel<MODE, 0, false, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+      gemm4_kernel<MODE, 0, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
                                                             rms_eps, ssq, qa, nullptr);
     }
     return;
   }
 #define JLA_G4(R, INV)                                                                                          \
-  do {                                                                                                            \
-    if (g_g4_ring)                                                                                                \
-      gemm4_kernel<MODE, R, true><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, \
-                                                       rms_eps, ssq, qa, INV);                                   \
-    else                                                                                                          \
-      gemm4_kernel<MODE, R, false><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,    \
-                                                        tn, rms_eps, ssq, qa, INV);                              \
-  } while (0)
+  gemm4_kernel<MODE, R><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, \
+                                             ssq, qa, INV)
   if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
     if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;  // (K % 8 == 0 always holds here)
     JLA_G4(2, rms_ws);

@@ -69,13 +69,7 @@ struct G4Args {
 // RMS: also accumulate the row sums of squares of x (the fused RMSNorm statistic, reference model.py:42-48) from
 // the x fragments already in registers: wave (wr, wc) takes m-tiles 4wc..4wc+3 of its row block, ss[i] holds lane
 // (row lane & 15, k-chunk lane >> 4)'s partial of m-tile 4wc + i, k32 step after k32 step in K order.
-// RMSV: how the fused-RMS sums of squares are formed (1: v_dot2_f32_bf16 x 4 per fragment; 2: unpack + 8 fp32 FMAs).
-// RDF / DMF (schedule variants, A/B in tools/debug/gemm4w_probe.hip): put a sub-step's 16 fragment reads / 16 DMA
-// issues in its first half (2 per 4 MFMAs) instead of spreading them over all of it (1 per 4 MFMAs), so the next
-// sub-step's lgkmcnt(0) / the next barrier's vmcnt(0) find them done.
-// ABL (diagnostic ablations, tools/debug/gemm4w_probe.hip only; wrong results): bit 0 drops the steady-state DMAs,
-// bit 1 the steady-state fragment reads, bit 2 the mid-tile barrier.
-template <bool RMS = false, bool RDF = false, bool DMF = false, int RMSV = 2, int ABL = 0, typename Acc>
+template <bool RMS = false, typename Acc>
 JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc,
                          float* ss = nullptr) {
   const int wr = wu >> 1, wc = wu & 1;
@@ -131,39 +125,17 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
         const int e = 4 * q + u, j = e >> 3, i = e & 7;
         g4_mfma(acc[j][i], wf[j], xf[i]);
       }
-      if (do_rd && !(ABL & 2)) {
-        if constexpr (RDF) {
-          if (q < 8) {
-            rd(2 * q < 8 ? wn[2 * q] : xn[2 * q - 8], rslot, rh, 2 * q);
-            rd(2 * q + 1 < 8 ? wn[2 * q + 1] : xn[2 * q + 1 - 8], rslot, rh, 2 * q + 1);
-          }
-        } else {
-          rd(q < 8 ? wn[q] : xn[q - 8], rslot, rh, q);
-        }
-      }
-      if (do_dma && !(ABL & 1)) {
-        if constexpr (DMF) {
-          if (q < 8) {
-            dma(td, 2 * q);
-            dma(td, 2 * q + 1);
-          }
-        } else {
-          dma(td, q);
-        }
-      }
+      if (do_rd) rd(q < 8 ? wn[q] : xn[q - 8], rslot, rh, q);
+      if (do_dma) dma(td, q);
       if constexpr (RMS) {
         if (q < 4) {  // m-tile 4wc + q: the runtime wc selects between two named fragments (no indexed array)
           const u32x4 f = wc ? xf[4 + q] : xf[q];
-          if constexpr (RMSV == 1) {
-            ss[q] = dot8_bf16(f, f, ss[q]);
-          } else {
-            // plain fp32 FMAs on the unpacked halves: v_dot2 beside the MFMAs costs ~10 cycles each (15 % of the loop)
+          // plain fp32 FMAs on the unpacked halves: v_dot2 beside the MFMAs costs ~10 cycles each (15 % of the loop)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float lo = __uint_as_float(f[e] << 16), hi = __uint_as_float(f[e] & 0xffff0000u);
-              ss[q] = fmaf(lo, lo, ss[q]);
-              ss[q] = fmaf(hi, hi, ss[q]);
-            }
+          for (int e = 0; e < 4; ++e) {
+            const float lo = __uint_as_float(f[e] << 16), hi = __uint_as_float(f[e] & 0xffff0000u);
+            ss[q] = fmaf(lo, lo, ss[q]);
+            ss[q] = fmaf(hi, hi, ss[q]);
           }
         }
       }
@@ -191,7 +163,7 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 
   auto mid_barrier = [&]() {
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0), visible to hipcc's own wait bookkeeping
-    if constexpr (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
@@ -380,256 +352,5 @@ JLA_DEV void g4_store_bf16(Acc& acc, u32x4* lds, bf16_t* out, int M, int N, int 
   }
 }
 
-
-// ---------------------------------------------------------------------------------------------
-// g4_mainloop_ring: the same waves / accumulators / sub-steps, with a deeper LDS ring so more bytes are in flight
-// per CU (the loop above keeps one 64 KiB K-tile in flight; an L2 -> LDS stream of ~1 us latency then caps a CU at
-// ~64 GB/s, which is what the 256 x 256 tile needs at full MFMA rate -- the DMA ablation costs 12 %):
-//   x : 3 pair slots x 32 KiB (a pair = the 64-deep k range of two sub-steps, 8-row x 128-B pieces as above),
-//   W : 4 stage slots x 16 KiB (one 32-deep k step of the 16 n-tiles: 16 packed fragments),
-// = all 160 KiB of LDS. Sub-step u (32 k) reads its fragments during sub-step u - 1; during sub-step u a wave
-// issues W stage u + 3 (4 DMAs) and half of x pair (u >> 1) + 2 (4 DMAs), so every DMA has two sub-steps to land;
-// one barrier per sub-step, behind vmcnt(8) (= everything but this sub-step's own 8 DMAs has landed) and
-// lgkmcnt(0). Past the end the DMA sources are clamped to the last stage / pair (re-loads into slots nobody reads),
-// which keeps one uniform loop body; the caller must drain vmcnt before reusing LDS.
-constexpr int G4R_X_U4 = 3 * 2048, G4R_W_U4 = 4 * 1024, G4R_LDS_U4 = G4R_X_U4 + G4R_W_U4;  // 160 KiB
-
-template <bool RMS = false, typename Acc>
-JLA_DEV void g4_mainloop_ring(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane,
-                              Acc& acc, float* ss = nullptr) {
-  const int wr = wu >> 1, wc = wu & 1;
-  const int K = g.K, KS = K >> 5, NTT = g.N >> 4;
-  const int U = 2 * KT, P = KT;  // 32-deep sub-steps, 64-deep x pairs of this split
-  const char* const baseA = reinterpret_cast<const char*>(g.x + (size_t)m0 * K + (size_t)t0 * 64);
-  const char* const baseB = reinterpret_cast<const char*>(g.W + ((size_t)(n0 >> 4) * KS + 2 * t0) * 64);
-  unsigned offA[8], offB[4];  // x: [half][j] -> piece 16 half + wu + 4j; W: n-tile wu + 4j
-  const int mlast = g.M - 1 - m0;
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int Pc = 16 * hh + wu + 4 * j;
-      const int row = min(8 * Pc + (lane >> 3), mlast);
-      const int chunk = (lane & 7) ^ (4 * (Pc & 1) + (lane >> 4));
-      offA[4 * hh + j] = (unsigned)row * (unsigned)K * 2u + 16u * (unsigned)chunk;
-    }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nt = min((n0 >> 4) + wu + 4 * j, NTT - 1) - (n0 >> 4);
-    offB[j] = (unsigned)nt * (unsigned)KS * 1024u + 16u * (unsigned)lane;
-  }
-  u32x4* const xring = lds;
-  u32x4* const wring = lds + G4R_X_U4;
-  // the j-th (0..7) DMA of sub-step u: j < 4 -> W stage u + 3; j >= 4 -> half (u & 1) of x pair (u >> 1) + 2
-  auto dma = [&](int u, int j) {
-    if (j < 4) {
-      const int st = min(u + 3, U - 1);
-      glds16(baseB + (size_t)st * 1024 + offB[j], wring + ((u + 3) & 3) * 1024 + (wu + 4 * j) * 64);
-    } else {
-      const int pr = min((u >> 1) + 2, P - 1), hh = u & 1, jj = j - 4;
-      glds16(baseA + (size_t)pr * 128 + offA[4 * hh + jj],
-             xring + (((u >> 1) + 2) % 3) * 2048 + (16 * hh + wu + 4 * jj) * 64);
-    }
-  };
-  const int xrd = (wr * 128 + (lane & 15)) * 8;
-  const int xc0 = (0 + (lane >> 4)) ^ ((lane >> 1) & 7), xc1 = (4 + (lane >> 4)) ^ ((lane >> 1) & 7);
-  auto rd = [&](u32x4& dst, int u, int q) {  // fragment q of sub-step u (0..7: W n-tile q; 8..15: x m-tile q - 8)
-    if (q < 8)
-      dst = wring[(u & 3) * 1024 + (wc * 8 + q) * 64 + lane];
-    else
-      dst = xring[((u >> 1) % 3) * 2048 + xrd + (q - 8) * 128 + ((u & 1) ? xc1 : xc0)];
-  };
-  u32x4 w0[8], x0[8], w1[8], x1[8];
-  auto substep = [&](u32x4 (&wf)[8], u32x4 (&xf)[8], u32x4 (&wn)[8], u32x4 (&xn)[8], int u) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int e = 4 * q + v, j = e >> 3, i = e & 7;
-        g4_mfma(acc[j][i], wf[j], xf[i]);
-      }
-      rd(q < 8 ? wn[q] : xn[q - 8], u + 1, q);
-      if ((q & 1) == 0) dma(u, q >> 1);
-      if constexpr (RMS) {
-        if (q < 4) {
-          const u32x4 f = wc ? xf[4 + q] : xf[q];
-          ss[q] = dot8_bf16(f, f, ss[q]);
-        }
-      }
-    }
-  };
-  // prologue: x pairs 0, 1 and W stages 0, 1, 2 in flight; pair 0 + stage 0 landed; set 0 <- sub-step 0
-  auto dma_pre_x = [&](int pr) {
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        glds16(baseA + (size_t)min(pr, P - 1) * 128 + offA[4 * hh + jj], xring + pr * 2048 + (16 * hh + wu + 4 * jj) * 64);
-  };
-  auto dma_pre_w = [&](int st) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      glds16(baseB + (size_t)min(st, U - 1) * 1024 + offB[j], wring + st * 1024 + (wu + 4 * j) * 64);
-  };
-  dma_pre_x(0);
-  dma_pre_w(0);
-  dma_pre_w(1);
-  dma_pre_x(1);
-  dma_pre_w(2);
-  wait_vmcnt<16>();  // pair 0 and stage 0
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-#pragma unroll
-  for (int q = 0; q < 16; ++q) rd(q < 8 ? w0[q] : x0[q - 8], 0, q);
-  auto barrier = [&]() {
-    // this wave's DMAs up to the previous sub-step have landed (vmcnt 8: only the current sub-step's remain) and its
-    // fragment reads are done; then everyone's
-    __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  for (int u = 0; u < U; u += 2) {
-    substep(w0, x0, w1, x1, u);
-    barrier();
-    substep(w1, x1, w0, x0, u + 1);
-    barrier();
-  }
-  g4_acc_fence();
-}
-
-// ---------------------------------------------------------------------------------------------
-// The same main loop on v_mfma_f32_32x32x16_bf16 (4 x 4 accumulator blocks of 32 x 32 per wave, 16 AGPRs each):
-// half as many MFMA instructions per K-tile, each holding the SIMD's issue for 8 of its 32 cycles instead of 8 of
-// 16, so the fragment reads and DMA issues of the loop find twice the free issue slots. Same LDS images and DMA
-// schedule as g4_mainloop. Fragments (lane l, r = l & 31, h = l >> 5):
-//   A = W: n-block jb = n-tiles 2jb (rows 0-15), 2jb + 1 (rows 16-31) of the wave block; k16 half kk of the k32
-//          sub-step -> packed-fragment slot (r & 15) + 16 (2kk + h) of fragment (n-tile, k32 step);
-//   B = x: m-block ib, row wr*128 + 32ib + r, 16-byte k-chunk 4 hs + 2kk + h (hs = k32 sub-step of the 64-k tile).
-// D (32 x 32, C^T): lane l holds output row 32ib + r at the 4 consecutive columns 32jb + 8g + 4h + 0..3 in registers
-// 4g..4g+3.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-JLA_DEV void g4_mfma32(f32x16& acc, const u32x4& a, const u32x4& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-JLA_DEV f32x16 g4_take32(f32x16& a) {
-  asm volatile("" : "+a"(a));
-  return a;
-}
-
-template <int ABL = 0, typename Acc>
-JLA_DEV void g4_mainloop32(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc) {
-  const int wr = wu >> 1, wc = wu & 1;
-  const int K = g.K, KS = K >> 5, NTT = g.N >> 4;
-  const char* const baseA = reinterpret_cast<const char*>(g.x + (size_t)m0 * K + (size_t)t0 * 64);
-  const char* const baseB = reinterpret_cast<const char*>(g.W + ((size_t)(n0 >> 4) * KS + 2 * t0) * 64);
-  unsigned offA[8], offB[8];
-  const int mlast = g.M - 1 - m0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int P = wu + 4 * j;
-    const int row = min(8 * P + (lane >> 3), mlast);
-    const int chunk = (lane & 7) ^ (4 * (P & 1) + (lane >> 4));
-    offA[j] = (unsigned)row * (unsigned)K * 2u + 16u * (unsigned)chunk;
-    const int f = wu + 4 * j;
-    const int nt = min((n0 >> 4) + (f >> 1), NTT - 1) - (n0 >> 4);
-    offB[j] = ((unsigned)nt * (unsigned)KS + (unsigned)(f & 1)) * 1024u + 16u * (unsigned)lane;
-  }
-  auto dma = [&](int t, int j) {
-    u32x4* slot = lds + (t & 1) * G4_SLOT_U4;
-    if (j < 8)
-      glds16(baseA + (size_t)t * 128 + offA[j], slot + (wu + 4 * j) * 64);
-    else
-      glds16(baseB + (size_t)t * 2048 + offB[j - 8], slot + G4_A_U4 + (wu + 4 * (j - 8)) * 64);
-  };
-  const int r = lane & 31, h = lane >> 5;
-  // W: u32x4 index in the slot = G4_A_U4 + ((wc*8 + 2jb + (r >> 4)) * 2 + hs) * 64 + (r & 15) + 16 (2kk + h)
-  const int wrd = G4_A_U4 + (wc * 8 + (r >> 4)) * 128 + (r & 15) + 16 * h;
-  // x: row wr*128 + 32ib + r -> (row * 8 + (chunk ^ ((row & 15) >> 1))), chunk = 4hs + 2kk + h
-  const int xrow = wr * 128 + r, xsw = (r & 15) >> 1;
-  auto rd = [&](u32x4& dst, int slot, int hs, int q) {  // q 0..7: W (kk = q >> 2, jb = q & 3); 8..15: x (kk, ib)
-    const u32x4* s = lds + slot * G4_SLOT_U4;
-    const int kk = (q & 7) >> 2, bb = q & 3;
-    if (q < 8)
-      dst = s[wrd + bb * 256 + hs * 64 + 32 * kk];
-    else
-      dst = s[(xrow + 32 * bb) * 8 + ((4 * hs + 2 * kk + h) ^ xsw)];
-  };
-  u32x4 w0[8], x0[8], w1[8], x1[8];
-  auto substep = [&](u32x4 (&wf)[8], u32x4 (&xf)[8], u32x4 (&wn)[8], u32x4 (&xn)[8], bool do_rd, int rslot, int rh,
-                     bool do_dma, int td) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int e = 2 * q + u, kk = e >> 4, jb = (e >> 2) & 3, ib = e & 3;
-        g4_mfma32(acc[jb][ib], wf[4 * kk + jb], xf[4 * kk + ib]);
-      }
-      if (do_rd && !(ABL & 2)) rd(q < 8 ? wn[q] : xn[q - 8], rslot, rh, q);
-      if (do_dma && !(ABL & 1)) dma(td, q);
-    }
-  };
-  if (KT > 0) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) dma(0, j);
-  }
-  if (KT > 1) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) dma(1, j);
-    wait_vmcnt<16>();
-  } else {
-    wait_vmcnt<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (KT > 0) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) rd(q < 8 ? w0[q] : x0[q - 8], 0, 0, q);
-  }
-  auto mid_barrier = [&]() {
-    __builtin_amdgcn_s_waitcnt(0x0070);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  int t = 0;
-  for (; t + 2 < KT; ++t) {
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
-    mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, true, t + 2);
-  }
-  if (t + 1 < KT) {
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
-    mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, false, 0);
-    ++t;
-  }
-  if (t < KT) {
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
-    substep(w1, x1, w0, x0, false, 0, 0, false, 0);
-  }
-  g4_acc_fence();
-}
-
-// staged bf16 store of a 32x32-layout wave block (see g4_mainloop32)
-template <typename Acc>
-JLA_DEV void g4_store32_bf16(Acc& acc, u32x4* lds, bf16_t* out, int M, int N, int m0, int n0, int wu, int lane) {
-  const int wr = wu >> 1, wc = wu & 1;
-  char* const wl = reinterpret_cast<char*>(lds) + wu * 32768;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-    for (int ib = 0; ib < 4; ++ib) {
-      const f32x16 v = g4_take32(acc[jb][ib]);
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg)
-        g4_stage_put<256>(wl, 32 * ib + r, 64 * jb + 16 * gg + 8 * h,
-                          u32x2{pack2bf(v[4 * gg], v[4 * gg + 1]), pack2bf(v[4 * gg + 2], v[4 * gg + 3])});
-    }
-  const int gcol0 = n0 + wc * 128;
-  g4_stage_rows<256>(wl, lane, [&](int rr, int ch, u32x4 v) {
-    const int row = m0 + wr * 128 + rr, col = gcol0 + 8 * ch;
-    if (row < M && col < N) *reinterpret_cast<u32x4*>(out + (size_t)row * N + col) = v;
-  });
-}
 
 }  // namespace jla

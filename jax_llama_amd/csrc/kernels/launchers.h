@@ -56,7 +56,6 @@ int gemm_ksplit(int M, int N, int K);
 int gemm_qkv_direct_ok(int M, int tile, int K);  // qkv without a K split: the direct RoPE / KV-write GEMM epilogue applies
 // gemm4 (the 4-wave 256 x 256 kernel, tile config 7) as the tile-0 default for M > 128, K % 64 == 0 (on by default)
 void gemm_set_g4_default(int on);
-void gemm_set_g4_ring(int on);
 // tile config 8: gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration; partial tiles
 // summed by the last arriver): ws >= gemm4_sk_workspace_floats(), tickets >= gemm4_sk_tickets(M, N) int32
 // zero-initialised once (self-resetting); the fused norm needs rms_ws; every mode incl. MODE_QKV
@@ -121,19 +120,13 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
                 const uint8_t* key_mask, int mask_len, bf16_t* out, float* ws, int32_t* tickets, int B, int H,
                 int Hkv, int Dh, int T, int t_cap, int nsplit, hipStream_t s, bf16_t* out_pack = nullptr);
 int attn_decode_packs(int B, int Hkv, int rep);
-// persistent decode step (decode_mk.hip): every layer of one decode token for M <= 4 rows in one launch; `layers` is
-// a device array of L MkLayer records (6 pointers: wqkv, wo, wgu, wdown, k cache, v cache of the layer)
-int decode_mk_supported(int M, int D, int H, int Hkv, int Dh, int F);
-int decode_mk_grid();
-size_t decode_mk_slab_floats();
-int decode_mk_max_splits(int T);
-int decode_mk_bar_words();    // phase-barrier words (zeroed by decode_mk before each launch)
-int decode_mk_trace_words();  // optional per-phase timestamp buffer (u64)
-int decode_mk(const void* layers, int L, int M, int D, int H, int Hkv, int F, int T, float eps, float* h, bf16_t* hb,
-              bf16_t* q, bf16_t* att, bf16_t* act, float* ssq, const float2* rope, int rope_len,
-              const int32_t* positions, const int32_t* slot, const int32_t* kv_start, float* slab, size_t slab_floats,
-              int32_t* tickets, int n_tickets, unsigned* bar, int32_t* err, float* aws, size_t aws_floats, int32_t* atk,
-              unsigned long long* trace, int prefetch_late, hipStream_t s);  // 1: attn_decode can also write the packed-layout output
+// decode attention on the matrix cores (attn_decode_mma.hip); dispatched by attn_decode (attn_set_v6 mode)
+int attn_decode_v6(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
+                   const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int H, int Hkv, int T, int t_cap,
+                   hipStream_t s, bf16_t* out_pack);
+void attn_set_v6(int mode);
+void attn_set_v6_wpp(int wpp);
+int attn_v6_wpp(int pairs);
 void attn_prefill_set_impl(int impl);  // 2 = GQA-shared MFMA 32x32 flash kernel (default), 1 = v1
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
                  const uint8_t* key_mask, int mask_len, bf16_t* out, int B, int S, int H, int Hkv, int Dh, int T,

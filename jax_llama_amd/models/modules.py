@@ -121,11 +121,6 @@ class LLaMABlockCollection:
         hidden, attns = [], []
         b = hb.shape[0] // seq_len
         rows = hb.shape[0]
-        if (not output_hidden_states and not output_attentions and hb.is_cuda
-                and ops.decode_mk_ok(self.model, rows, seq_len, key_mask)):
-            # batch <= 4 decode: every layer in one persistent launch (csrc/kernels/decode_mk.hip)
-            ops.decode_layers(self.model, h, hb, positions, cache, slot0, kv_start)
-            return hidden, attns
         pk = None
         if (ops.PACKED_X and hb.is_cuda and ops.PACKED_X_MIN_M <= rows <= min(ops.PACKED_ATT_MAX_M, ops.SKINNY_M)
                 and self.model.comm.packs_residual(rows * self.model.config.hidden_size * 4)):

@@ -685,74 +685,3 @@ def topk_sample(logits: torch.Tensor, k: int, temperature: float, top_p: float, 
     e.topk_merge(cv, ci, k, 1, nxt=nxt, temperature=float(temperature),
                  top_p=1.0 if top_p is None else float(top_p), seed=int(seed) & ((1 << 63) - 1), step=step)
     return nxt
-
-
-# ----------------------------------------------------------------------------------
-# persistent decode step (csrc/kernels/decode_mk.hip): every layer of one decode token for M <= 4 rows in ONE launch
-# (phase barriers on the device; each wave's first weight loads of the next phase issued before the barrier).
-# JLA_DECODE_MK=0: the per-layer kernels (A/B).
-DECODE_MK = os.environ.get("JLA_DECODE_MK", "0") != "0"
-DECODE_MK_MAX_M = 4
-DECODE_MK_PREFETCH_LATE = 0  # A/B: next-phase ring loads after the phase barrier instead of before
-DECODE_MK_TRACE = None  # tools: an int64 tensor of ext().decode_mk_trace_words() -> per-phase timestamps of layers 0-1
-
-
-def decode_mk_ok(model, rows: int, seq_len: int, key_mask) -> bool:
-    """Whether ``decode_layers`` runs this step: GPU, one token per row, <= 4 rows, no key mask, TP = 1, and the
-    model's dims inside the kernel's plan (csrc decode_mk_supported)."""
-    if not DECODE_MK or seq_len != 1 or key_mask is not None or rows > DECODE_MK_MAX_M:
-        return False
-    if model.comm.size != 1 or model.device.type != "cuda" or model.precision == "highest":
-        return False
-    c = model.config
-    return bool(ext().decode_mk_supported(rows, c.hidden_size, model.n_heads, model.n_kv_heads, model.head_dim,
-                                          model.ffn))
-
-
-def _decode_mk_table(model, cache):
-    """Device [L, 6] pointer table of the layers' packed weights and KV-cache slices, cached on the model per cache
-    buffer (built outside graph capture: the engine runs eager steps first)."""
-    key = (cache.k.data_ptr(), cache.v.data_ptr(), tuple(lw.qkv.weight.data_ptr() for lw in model.layers[:1]),
-           model.layers[-1].down.weight.data_ptr())
-    tabs = model.__dict__.setdefault("_mk_tables", {})
-    t = tabs.get(key)
-    if t is None:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("decode_layers: the layer table must be built before graph capture")
-        tabs.clear()
-        c = model.config
-        t = ext().decode_mk_table([lw.qkv.weight for lw in model.layers], [lw.o.weight for lw in model.layers],
-                                  [lw.gu.weight for lw in model.layers], [lw.down.weight for lw in model.layers],
-                                  cache.k, cache.v, c.hidden_size, model.n_heads, model.n_kv_heads, model.ffn)
-        tabs[key] = t
-    return t
-
-
-def decode_layers(model, h: torch.Tensor, hb: torch.Tensor, positions: torch.Tensor, cache, slot0,
-                  kv_start: torch.Tensor) -> None:
-    """All decoder layers of one decode token (``h`` fp32 [M, D] and its bf16 mirror ``hb`` updated in place; the
-    per-layer KV rows written at ``slot0``): reference ``FlaxLLaMABlockCollection`` (model.py:579-595) for S = 1."""
-    e = ext()
-    dev = h.device
-    m = h.shape[0]
-    c = model.config
-    H, Hkv, F, dh = model.n_heads, model.n_kv_heads, model.ffn, model.head_dim
-    T = cache.k.shape[3]
-    table = _decode_mk_table(model, cache)
-    slab_floats, splits = e.decode_mk_workspace(T)
-    ws = workspace
-    nt = 32 * max((H + 2 * Hkv) * dh, 2 * F, c.hidden_size) // 16  # one ticket per 128-B line
-    e.decode_mk(table, h, hb,
-                ws.get("mk_q", m * H * dh, BF16, dev), ws.get("mk_att", m * H * dh, BF16, dev),
-                ws.get("mk_act", m * F, BF16, dev), ws.get("mk_ssq", c.hidden_size // 16 * 4, torch.float32, dev),
-                model.rope, positions.reshape(-1).to(torch.int32), _slot_tensor(slot0, dev), kv_start, cache.k,
-                ws.get("mk_slab", slab_floats, torch.float32, dev), ws.get_zeroed("mk_tickets", nt, torch.int32, dev),
-                ws.get("mk_bar", 32 * 17, torch.int32, dev), ws.get_zeroed("mk_err", 1, torch.int32, dev),
-                ws.get("mk_aws", m * Hkv * splits * (H // Hkv) * (dh + 4), torch.float32, dev),
-                ws.get_zeroed("mk_atk", 32 * m * Hkv, torch.int32, dev), H, Hkv, F, float(model.eps),
-                trace=DECODE_MK_TRACE, prefetch_late=DECODE_MK_PREFETCH_LATE)
-
-
-def decode_mk_error(device) -> int:
-    """The persistent decode step's error word (a phase-barrier timeout records its phase; 0 = none)."""
-    return int(workspace.get_zeroed("mk_err", 1, torch.int32, torch.device(device)).item())

@@ -43,19 +43,10 @@ def _run_all(e, xg, pg, gp, h0, n, k, ks, ws, tile, rms_ws=None):
     return outs + [hg, mir]
 
 
-@pytest.fixture(params=[0, 1], ids=["slots", "ring"])
-def g4_ring(request):
-    """Both gemm4 main loops: the two 64 KiB K-tile slots, and the 160 KiB LDS ring (gemm4w.h g4_mainloop_ring)."""
-    e = ops.ext()
-    e.gemm_set_g4_ring(request.param)
-    yield request.param
-    e.gemm_set_g4_ring(0)
-
-
 @pytest.mark.parametrize("m,n,k,ks", [(200, 768, 1024, 1), (512, 1056, 1024, 1), (700, 2560, 4096, 1),
                                       (300, 768, 2048, 3), (2048, 4096, 4096, 2), (1000, 6144, 1536, 1),
                                       (256, 512, 128, 1), (300, 768, 192, 3)])
-def test_gemm4_every_epilogue(m, n, k, ks, g4_ring):
+def test_gemm4_every_epilogue(m, n, k, ks):
     e = ops.ext()
     torch.manual_seed(m + n + k)
     x = torch.randn(m, k).to(BF16)
@@ -95,7 +86,7 @@ def test_gemm4_every_epilogue(m, n, k, ks, g4_ring):
 
 
 @pytest.mark.parametrize("m,s,n_heads", [(512, 512, 8), (256, 1, 32), (300, 3, 8)])
-def test_gemm4_qkv_rope_epilogue(m, s, n_heads, g4_ring):
+def test_gemm4_qkv_rope_epilogue(m, s, n_heads):
     """The RoPE / KV-cache write in gemm4's epilogue (rotation in fp32 on the lane's two column pairs) against the
     fp32 oracle and gemm2's LDS-staged epilogue."""
     e = ops.ext()

@@ -1026,3 +1026,45 @@ def test_attention_decode_small_batch_kernels(kernel, rep, t, slot, masked):
     if not masked:
         assert got[2].float().abs().max().item() == 0.0
     assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())
+
+
+@pytest.mark.parametrize("wpp", [1, 2, 4, 8])
+@pytest.mark.parametrize("rep", [1, 4, 8, 16])
+@pytest.mark.parametrize("t,slot", [(40, 17), (384, 200), (1030, 1029)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_decode_mfma_v6(wpp, rep, t, slot, masked):
+    """Decode attention on the matrix cores (attn_decode_mma.hip, v6) forced at every waves-per-pair geometry against
+    the fp32 reference: left padding that starts inside a 32-key step, a row with no valid key (zeros), the general key
+    mask, rep 1..16 (the heads of a pair are the MFMA columns); the packed output copy equals the row-major one and a
+    second call is identical (no state between calls)."""
+    e = ops.ext()
+    b, hkv, dh = 3, 2, 128
+    h = hkv * rep
+    kc, vc = _cache(b, hkv, t, dh)
+    q = torch.randn(b, 1, h, dh).to(BF16)
+    kv_start = torch.tensor([0, 37, slot + 1], dtype=torch.int32)
+    mask = None
+    if masked:
+        mask = (torch.rand(b, t) > 0.3).to(torch.uint8)
+        mask[:, slot] = 1
+        kv_start[1] = 0
+    expect = ref.attention(q, kc, vc, slot, kv_start, mask).reshape(b, h * dh)
+    try:
+        e.attn_set_v6(2)
+        e.attn_set_v6_wpp(wpp)
+        qd, kd, vd = q.to(DEV), kc.to(DEV), vc.to(DEV)
+        sl = torch.tensor([slot], dtype=torch.int32, device=DEV)
+        md = None if mask is None else mask.to(DEV)
+        assert e.attn_decode_splits(b, hkv, t, rep) == 1 and e.attn_decode_packs(b, hkv, rep)
+        packed = ops.packed_empty(b, h * dh, DEV)
+        got = ops.attention(qd, kd, vd, sl, kv_start.to(DEV), md, out_packed=packed)
+        again = ops.attention(qd, kd, vd, sl, kv_start.to(DEV), md)
+        torch.cuda.synchronize()
+    finally:
+        e.attn_set_v6(0)
+        e.attn_set_v6_wpp(0)
+    _close(got, expect, 2e-2, 2e-2)
+    assert torch.equal(got, again)
+    if not masked:
+        assert got[2].float().abs().max().item() == 0.0
+    assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())

@@ -7,7 +7,8 @@ evicts L2 and the Infinity Cache, as the weight stream of a real step does). Tim
 
 impl (ext.attn_set_impl / attn_set_v3_max_pairs): 2 = default dispatch; 1 = the split v1 kernel (v3 off);
 5 = split small-batch kernel (v5) where it applies; 6 = v5 with the first merge (4 splits per load round);
-7 = v4 (register ring, one split) forced; 9 = v2 (LDS-DMA ring) forced. Prints one JSON line per (shape, impl).
+7 = v4 (register ring, one split) forced; 9 = v2 (LDS-DMA ring) forced; 60 = v6 (matrix cores), 61 / 62 / 64 / 68 = v6
+with 1 / 2 / 4 / 8 waves per (row, kv head) pair. Prints one JSON line per (shape, impl).
 """
 from __future__ import annotations
 
@@ -26,6 +27,9 @@ from jax_llama_amd.config import get_preset  # noqa: E402
 
 def set_impl(e, impl):
     e.attn_set_impl(2, 4096)
+    # 60: the MFMA kernel (v6) with its default waves per pair; 61 / 62 / 64 / 68: v6 with 1 / 2 / 4 / 8 waves per pair
+    e.attn_set_v6(2 if 60 <= impl <= 68 else 0)
+    e.attn_set_v6_wpp(impl - 60 if 61 <= impl <= 68 else 0)
     e.attn_set_v3_max_pairs(0 if impl == 1 else 4096)
     if impl in (7, 9):
         # the streaming kernels at any pair count, one split: 7 = v4 register ring, 9 = v2 (LDS-DMA ring)

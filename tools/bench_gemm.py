@@ -53,8 +53,8 @@ def main():
     ap.add_argument("--mode", default="store", choices=["store", "swiglu", "residual"],
                     help="epilogue (the model's: qkv/lm_head store, gate_up swiglu, o/down residual)")
     ap.add_argument("--rms", action="store_true", help="fused RMSNorm statistic (store / swiglu)")
-    ap.add_argument("--ring", type=int, nargs="+", default=[0], help="gemm4 main loop: 0 two K-tile slots, 1 the "
-                    "160 KiB ring (gemm_set_g4_ring); only for tile 7 / tile-0 gemm4 plans")
+    ap.add_argument("--tp", type=int, default=1, help="per-rank shapes of that TP degree (qkv / gate_up column-parallel, "
+                    "o / down row-parallel, lm_head vocab-parallel; parallel/partition.py)")
     ap.add_argument("--data", default="normal", choices=["normal", "uniform"],
                     help="operand distribution (uniform: as tools/debug/gemm4w_probe.hip)")
     args = ap.parse_args()
@@ -63,8 +63,9 @@ def main():
     cfg = get_preset(args.model)
     d, f, hd = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
     h, hkv = cfg.num_attention_heads, cfg.num_key_value_heads
-    shapes = {"qkv": ((h + 2 * hkv) * hd, d), "o": (d, h * hd), "gate_up": (2 * f, d), "down": (d, f),
-              "lm_head": (cfg.vocab_size, d)}
+    tp = args.tp
+    shapes = {"qkv": ((h + 2 * hkv) * hd // tp, d), "o": (d, h * hd // tp), "gate_up": (2 * f // tp, d),
+              "down": (d, f // tp), "lm_head": (cfg.vocab_size // tp // 16 * 16, d)}
     e = ops.ext()
     for name, (n, k) in shapes.items():
         if args.ops and name not in args.ops:
@@ -94,12 +95,13 @@ def main():
             first = {}
             for rnd, impl in [(r, i) for r in range(args.rounds) for i in args.impl]:
                 for ks in args.ksplit:
-                 for ring in args.ring:
-                  e.gemm_set_g4_ring(ring)
+                 for ring in (0,):
                   for tile in args.tile:
-                    if ring and tile not in (0, 7):
-                        continue
                     kk = ks or e.gemm_ksplit(m, n, k)
+                    if tile == 10 and kk > 1 and eps > 0:
+                        continue  # (gemm4 256 x 128: no K split under the fused norm)
+                    if kk > 1 and (k // 32) // kk < 4:
+                        continue
                     tk = None
                     for fx in args.fixup:
                       tk = None
@@ -125,7 +127,7 @@ def main():
                           ws = torch.empty(max(floats, kk * m * n), device=DEV, dtype=torch.float32)
                           tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
                       else:
-                          ws = torch.empty(max(1, kk * m * n), device=DEV, dtype=torch.float32)
+                          ws = torch.empty(max(1, kk * m * (n + 1)), device=DEV, dtype=torch.float32)
 
                       tcfg = tile
 
@@ -134,7 +136,7 @@ def main():
                       def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
                           e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
                                  ws if (kk > 1 or tile in (4, 6, 8)) else None, eps, tile, tk, None, rws)
-                      res[f"v{impl}_ks{kk}_t{tile}" + ("_ring" if ring else "") + ("_fix" if fx and kk > 1 else "") +
+                      res[f"v{impl}_ks{kk}_t{tile}"  + ("_fix" if fx and kk > 1 else "") +
                           (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                       run(0)
                       if mode != 0:  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
@@ -150,7 +152,6 @@ def main():
                       if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
                           f0 = first.setdefault((kk, tile), got.clone())
                           assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
-            e.gemm_set_g4_ring(0)
             if not args.no_blas and mode == 0:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)
             for impl, us in res.items():

@@ -98,7 +98,7 @@ def scan(body, seed):
             for a in args:
                 if a:
                     touched |= regs(a.split()[0])
-            if op.startswith(_VMEM) and in_asm:
+            if op.startswith(_VMEM) and in_asm and "_lds" not in op:
                 touched -= regs(args[0])  # the asm load's own destination (tied operand)
         pend = set()
         for r_, asm in queue:
@@ -108,7 +108,8 @@ def scan(body, seed):
         if hit:
             hazards.append((i, s, sorted(hit)[0]))
         if op.startswith(_VMEM):
-            is_load = "load" in op
+            # global_load_lds_*: the first operand is the address (the data goes to LDS, no VGPR destination)
+            is_load = "load" in op and "_lds" not in op
             queue.append((regs(args[0]) if (in_asm and is_load) else set(), in_asm and is_load))
     return hazards, back
 

@@ -300,6 +300,14 @@ void check_gemm_ws(const c10::optional<Tensor>& ws, int64_t ksplit, int64_t m, i
         "gemm ws too small");
 }
 
+// gemm5 (tiles 11 / 12) slab workspace: [ks][M][N] (+ [ks][M] norm partials) for its effective split over 64-deep stages
+void check_g5_ws(const c10::optional<Tensor>& ws, int64_t k, int64_t ksplit, int64_t m, int64_t n, bool rms) {
+  check(ws.has_value(), "gemm tile 11 / 12: the slab workspace is required (any split)");
+  check_gpu(*ws, "gemm ws");
+  const int64_t eks = jla::gemm5_ksplit((int)k, (int)ksplit);
+  check(ws->scalar_type() == torch::kFloat32 && ws->numel() >= eks * m * (n + (rms ? 1 : 0)), "gemm ws too small");
+}
+
 // stream-K tail (tile 4) workspace: slabs (float) + self-resetting tickets (int32, zeroed once)
 struct SkWs {
   float* ws = nullptr;
@@ -372,9 +380,18 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   if (pack_out.has_value()) {
     check(m <= SKINNY_MAX_M && (mode == 1 || mode == 2) && (mode != 1 || mir), "gemm pack_out: decode M, residual "
           "(with its mirror) or SwiGLU");
-    check(ksplit > 1 && tile != 4 && tile != 6 && !(tickets.has_value() && jla::gemm_fixup_enabled()),
+    check((ksplit > 1 || tile == 11 || tile == 12) && tile != 4 && tile != 6 &&
+              !(tickets.has_value() && jla::gemm_fixup_enabled()),
           "gemm pack_out: the split-K reduce-kernel path only");
     pqa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
+  }
+  if (tile == 11 || tile == 12) {  // gemm5 (weight-streaming) partial slabs + the reduce kernel's epilogue, any split
+    check_g5_ws(ws, k, ksplit, m, n, rms_eps >= 0);
+    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
+                 out.scalar_type() == torch::kFloat32, mir, pqa.pack ? &pqa : nullptr, ptr<float>(*ws), ws->numel(),
+                 ksplit, stream(), (float)rms_eps, (int)tile, nullptr, 0, nullptr, 0),
+       "gemm");
+    return;
   }
   if (tile == 8) {
     check(ksplit <= 1, "gemm tile 8: no K split");
@@ -463,6 +480,13 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
     check(sk.ws != nullptr, "gemm_qkv tile 4: this shape has no stream-K tail");
     rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, sk.ws, sk.ws_floats, 1,
                  stream(), (float)rms_eps, 4, sk.tk, sk.n_tk),
+       "gemm_qkv");
+    return;
+  }
+  if (tile == 11 || tile == 12) {  // gemm5 partial slabs, RoPE / KV write in the reduce kernel
+    check_g5_ws(ws, k, ksplit, m, n, rms_eps >= 0);
+    rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(*ws), ws->numel(),
+                 ksplit, stream(), (float)rms_eps, (int)tile, nullptr, 0, nullptr, 0),
        "gemm_qkv");
     return;
   }
@@ -856,6 +880,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_set_v3_max_pairs", [](int64_t n) { jla::attn_set_v3_max_pairs((int)n); });
   m.def("attn_set_v5_max_pairs", [](int64_t n) { jla::attn_set_v5_max_pairs((int)n); });
   m.def("attn_set_v5_fold", [](int64_t n) { jla::attn_set_v5_fold((int)n); });
+  m.def("clock_probe", [](int64_t iters, int64_t grid, Tensor out) {
+    check(out.is_cuda() && out.scalar_type() == torch::kInt64 && out.numel() >= 3, "clock_probe: int64[3] on the GPU");
+    rc(jla::clock_probe((int)iters, (int)grid, reinterpret_cast<unsigned long long*>(out.data_ptr()), stream()),
+       "clock_probe");
+  });
+  m.def("gemm5_set_diag", [](int64_t d) { jla::gemm5_set_diag((int)d); });
+  m.def("gemm5_ksplit", [](int64_t k, int64_t ks) { return jla::gemm5_ksplit((int)k, (int)ks); });
   m.def("attn_set_v6", [](int64_t mode) { jla::attn_set_v6((int)mode); });
   m.def("attn_set_v6_wpp", [](int64_t wpp) { jla::attn_set_v6_wpp((int)wpp); });
   m.def("attn_v6_wpp", [](int64_t pairs) { return jla::attn_v6_wpp((int)pairs); });

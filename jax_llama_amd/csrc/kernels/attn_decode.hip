@@ -1127,12 +1127,16 @@ static bool use_v5(int B, int Hkv, int rep) {
 }
 // v6 (attn_decode_mma.hip: scores and P.V on the matrix cores, one workgroup per pair, no workspace): 0 off,
 // 1 where it wins (by shape), 2 every decode shape it supports (A/B, tests)
-static int g_attn_v6 = 0;
+// By shape (graph-timed with cold K/V, profiles/r5_attn_decode_v6_ab.jsonl): at rep 8 from 8 up to (not including)
+// 2048 (row, kv head) pairs -- Llama-3-70B at MP 8, B = 32 / 256: 12.9 / 28.8 -> 10.2 / 14.1 us; MP 1, B = 32: 39.0 ->
+// 18.7 -- the VALU kernels there are compute-bound on the 8 q heads of a pair; v4 keeps rep 8 from 2048 pairs (MP 1,
+// B = 256: 80 vs 94 us) and every rep <= 4 shape (v4 / v3 / v5 stream those faster).
+static int g_attn_v6 = 1;
 void attn_set_v6(int mode) { g_attn_v6 = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
 static bool use_v6(int B, int Hkv, int rep) {
   if (g_attn_v6 == 0 || g_attn_impl != 2 || rep > 16 || (rep & (rep - 1))) return false;
   if (g_attn_v6 == 2) return true;
-  return rep >= 8 && B * Hkv >= 128;
+  return rep >= 8 && B * Hkv >= 8 && B * Hkv < 2048;
 }
 // the kernels that also write the packed output copy: v6, v5, v3, and v4 at decode rows <= 64 (mid-batch)
 int attn_decode_packs(int B, int Hkv, int rep) {

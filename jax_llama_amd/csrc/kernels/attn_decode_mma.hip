@@ -283,7 +283,7 @@ static int g_v6_wpp = 0;
 void attn_set_v6_wpp(int wpp) { g_v6_wpp = (wpp == 1 || wpp == 2 || wpp == 4 || wpp == 8) ? wpp : 0; }
 int attn_v6_wpp(int pairs) {
   if (g_v6_wpp) return g_v6_wpp;
-  return pairs >= 4096 ? 1 : (pairs >= 1024 ? 2 : (pairs >= 128 ? 4 : 8));
+  return pairs >= 4096 ? 1 : 2;  // 2 waves were best or tied from 1 to 256 pairs (r5_attn_decode_v6_ab.jsonl)
 }
 
 int attn_decode_v6(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,

@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "gemm4w.h"
+#include "gemm5ws.h"
 #include "launchers.h"
 
 namespace jla {
@@ -1882,9 +1883,85 @@ static int gemm_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int
   return 0;
 }
 
+// the split-K reduce + epilogue launch over [ksplit][M][N] partial slabs (+ [ksplit][M] sums of squares, fused norm)
+static int launch_reduce(const float* ws, int ksplit, void* out, int M, int N, int K, int mode, int accumulate,
+                         int out_f32, bf16_t* mirror, const QKVArgs* qkv, const float* ssq, float rms_eps,
+                         hipStream_t s) {
+  const size_t total4 = (size_t)M * N / 4;
+  const int rgrid = (int)((total4 + 255) / 256);
+  QKVArgs qa{};
+  if (qkv) qa = *qkv;
+  const float eps = ssq ? rms_eps : 0.f;
+  switch (mode) {
+    case MODE_STORE:
+      gemm_reduce_kernel<MODE_STORE><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, out_f32, nullptr, qa,
+                                                           ssq, K, eps);
+      break;
+    case MODE_RESIDUAL:
+      gemm_reduce_kernel<MODE_RESIDUAL><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 1, mirror, qa,
+                                                              nullptr, K, eps);
+      break;
+    case MODE_SWIGLU:
+      gemm_reduce_kernel<MODE_SWIGLU><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq,
+                                                            K, eps);
+      break;
+    case MODE_QKV:
+      gemm_reduce_kernel<MODE_QKV><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq, K,
+                                                         eps);
+      break;
+    default: return -1;
+  }
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
+// gemm5 (tile 11: 4 n-tiles per wave, 256-column workgroups; tile 12: 2 n-tiles, 128 columns): the weight-streaming
+// split-K main loop (gemm5ws.h), then the reduce kernel runs the epilogue (even without a K split)
+static int g_g5_diag = 0;  // tools only (gemm5ws.h diag bits: ablations with wrong results)
+void gemm5_set_diag(int d) { g_g5_diag = d; }
+int gemm5_ksplit(int K, int ksplit) {  // the effective split count over 64-deep K-stages
+  const int KS64 = K >> 6;
+  if (ksplit < 1) ksplit = 1;
+  const int kc = (KS64 + ksplit - 1) / ksplit;
+  return (KS64 + kc - 1) / kc;
+}
+static int launch_g5(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int mode, int accumulate,
+                     int out_f32, bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit,
+                     float rms_eps, int tile, hipStream_t s) {
+  if ((K & 63) || (N & 15) || M <= 0) return -1;
+  if (mode == MODE_SWIGLU && (N & 31)) return -1;
+  if (mode == MODE_QKV && !qkv) return -1;
+  const bool rms = rms_eps >= 0.f && mode != MODE_RESIDUAL;
+  const int KS64 = K >> 6;
+  ksplit = gemm5_ksplit(K, ksplit);
+  const int kc = (KS64 + ksplit - 1) / ksplit;
+  const size_t need = (size_t)ksplit * M * N + (rms ? (size_t)ksplit * M : 0);
+  if (ws == nullptr || ws_floats < need) return -3;
+  float* ssq = rms ? ws + (size_t)ksplit * M * N : nullptr;
+  const int mt = M <= 128 ? 8 : 16, rows = 16 * mt;
+  const int ntw = tile == G5_TILE ? 4 : 2;
+  const int tiles_m = (M + rows - 1) / rows, tiles_n = (N + 64 * ntw - 1) / (64 * ntw);
+  const int grid = tiles_m * tiles_n * ksplit;
+  if (mt == 8 && ntw == 4)
+    gemm5_partial_kernel<8, 4><<<grid, 256, 0, s>>>(x, w, ws, M, N, K, kc, tiles_m, tiles_n, ssq, g_g5_diag);
+  else if (mt == 8)
+    gemm5_partial_kernel<8, 2><<<grid, 256, 0, s>>>(x, w, ws, M, N, K, kc, tiles_m, tiles_n, ssq, g_g5_diag);
+  else if (ntw == 4)
+    gemm5_partial_kernel<16, 4><<<grid, 256, 0, s>>>(x, w, ws, M, N, K, kc, tiles_m, tiles_n, ssq, g_g5_diag);
+  else
+    gemm5_partial_kernel<16, 2><<<grid, 256, 0, s>>>(x, w, ws, M, N, K, kc, tiles_m, tiles_n, ssq, g_g5_diag);
+  JLA_CHECK_LAUNCH();
+  return launch_reduce(ws, ksplit, out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ssq, rms_eps, s);
+}
+
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps, int tile, int32_t* tickets, int n_tickets, float* rms_ws, size_t rms_ws_floats) {
+  if (tile == G5_TILE || tile == G5_TILE + 1) {
+    if (mode == MODE_ARGMAX || (rms_eps >= 0.f && mode == MODE_RESIDUAL)) return -1;
+    return launch_g5(x, static_cast<const u32x4*>(W), out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ws,
+                     ws_floats, ksplit, rms_eps, tile, s);
+  }
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
   if (tile == G4N_TILE && ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
                            (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
@@ -2010,32 +2087,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   float* ssq = rms ? ws + (size_t)ksplit * M * N : nullptr;
   launch_tiled<MODE_PARTIAL>(x, w, ws, M, N, K, 0, 1, nullptr, kc, ksplit, rms_eps, ssq, tile, s);
   JLA_CHECK_LAUNCH();
-  const size_t total4 = (size_t)M * N / 4;
-  const int rgrid = (int)((total4 + 255) / 256);
-  QKVArgs qa{};
-  if (qkv) qa = *qkv;
-  const float eps = rms ? rms_eps : 0.f;
-  switch (mode) {
-    case MODE_STORE:
-      gemm_reduce_kernel<MODE_STORE><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, out_f32, nullptr, qa,
-                                                           ssq, K, eps);
-      break;
-    case MODE_RESIDUAL:
-      gemm_reduce_kernel<MODE_RESIDUAL><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 1, mirror, qa,
-                                                              nullptr, K, eps);
-      break;
-    case MODE_SWIGLU:
-      gemm_reduce_kernel<MODE_SWIGLU><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq,
-                                                            K, eps);
-      break;
-    case MODE_QKV:
-      gemm_reduce_kernel<MODE_QKV><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq, K,
-                                                         eps);
-      break;
-    default: return -1;
-  }
-  JLA_CHECK_LAUNCH();
-  return 0;
+  return launch_reduce(ws, ksplit, out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ssq, rms_eps, s);
 }
 
 // ---- greedy lm_head: GEMM with the argmax in its epilogue (no fp32 logits round trip through HBM:

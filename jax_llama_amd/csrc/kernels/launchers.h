@@ -56,6 +56,9 @@ int gemm_ksplit(int M, int N, int K);
 int gemm_qkv_direct_ok(int M, int tile, int K);  // qkv without a K split: the direct RoPE / KV-write GEMM epilogue applies
 // gemm4 (the 4-wave 256 x 256 kernel, tile config 7) as the tile-0 default for M > 128, K % 64 == 0 (on by default)
 void gemm_set_g4_default(int on);
+int gemm5_ksplit(int K, int ksplit);
+int clock_probe(int iters, int grid, unsigned long long* out, hipStream_t s);  // [cycles, 100 MHz ticks]
+void gemm5_set_diag(int d);  // tools only: gemm5 ablations (wrong results)  // gemm5 (tiles 11 / 12): the effective split over 64-deep K-stages
 // tile config 8: gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration; partial tiles
 // summed by the last arriver): ws >= gemm4_sk_workspace_floats(), tickets >= gemm4_sk_tickets(M, N) int32
 // zero-initialised once (self-resetting); the fused norm needs rms_ws; every mode incl. MODE_QKV

@@ -214,6 +214,37 @@ int prefetch(const void* p, long long nbytes, int grid, unsigned* sink, hipStrea
   return 0;
 }
 
+// Shader-clock probe (runtime/benchmark.py calibration): every workgroup keeps its SIMDs' matrix pipes busy with
+// dependent MFMA chains for `iters` rounds, the first lane of workgroup 0 reads the shader cycle counter (s_memtime)
+// and the constant 100 MHz counter (s_memrealtime) before and after: cycles / real time = the clock the chip runs at
+// under a full matrix load (sysfs pp_dpm_sclk shows a DPM request level, not the running clock).
+__global__ void __launch_bounds__(256) clock_probe_kernel(int iters, unsigned long long* __restrict__ out) {
+  const bool rec = blockIdx.x == 0 && threadIdx.x == 0;
+  unsigned long long c0 = 0, r0 = 0;
+  if (rec) {
+    c0 = __builtin_readcyclecounter();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  f32x4 acc[4] = {};
+  const u32x4 a = {threadIdx.x, 1u, 2u, 3u}, b = {blockIdx.x, 5u, 6u, 7u};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = mfma16x16x32(a, b, acc[j]);
+  }
+  if (rec) {
+    const unsigned long long c1 = __builtin_readcyclecounter(), r1 = __builtin_amdgcn_s_memrealtime();
+    out[0] = c1 - c0;
+    out[1] = r1 - r0;
+  }
+  if (acc[0][0] == 1.2345f && acc[3][1] == 6.789f) out[2] = 1;  // keep the chain alive
+}
+
+int clock_probe(int iters, int grid, unsigned long long* out, hipStream_t s) {
+  clock_probe_kernel<<<grid, 256, 0, s>>>(iters, out);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 JLA_BOUNDS_ACCESSOR(norm_embed)
 
 }  // namespace jla

@@ -340,6 +340,7 @@ def fix_workspace(e, m, n, ks, device):
 
 
 G4SK_TILE = 8  # gemm4 stream-K plan (csrc/kernels/gemm.hip gemm4_sk_kernel)
+G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h): 256- / 128-column workgroups
 
 
 def g4sk_workspace(e, m, n, device):
@@ -355,6 +356,9 @@ def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
     A split plan gets fixup tickets (the GEMM sums its splits itself) except for the QKV epilogue, whose
     RoPE + cache write lives in the reduce kernel."""
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, rms)
+    if tm in G5_TILES:  # weight-streaming split-K (any split, slabs always): partial slabs + the reduce kernel
+        eks = e.gemm5_ksplit(k, ks)
+        return ks, tm, workspace.get("gemm_ws", eks * m * (n + 1), torch.float32, device), None
     if tm == G4SK_TILE:
         ws, tk = g4sk_workspace(e, m, n, device)
         return 1, tm, ws, tk
@@ -400,6 +404,8 @@ def _tiled_packs(e, m, n, k, device, mode, rms_eps) -> bool:
     if e is None or m > SKINNY_M or mode not in (MODE_RESIDUAL, MODE_SWIGLU):
         return False
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, _fused_rms(e, mode, rms_eps))
+    if tm in G5_TILES:
+        return True
     return ks > 1 and tm not in (SK_TILE, autotune.HYBRID_TILE, G4SK_TILE) and not e.gemm_fixup_enabled()
 
 

@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 7  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles), so older persisted picks are re-measured
+TUNE_VERSION = 8  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -275,8 +275,9 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3, 7, 10)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg); 7: gemm4;
-# 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
+TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
+# 7: gemm4; 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
+# 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
 # plus (1, SK_TILE) -- 256x256 with a stream-K tail -- for shapes whose tile count is not a multiple of the CUs
 TUNE_MAX_M = 2048
 
@@ -318,6 +319,7 @@ SK_TILE = 4  # 256x256 tiles with a stream-K tail (no K split): csrc/kernels/gem
 HYBRID_TILE = 6  # whole waves of 256x256 tiles + the partial wave split 2-way with the in-kernel fixup
 G4SK_TILE = 8  # gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration)
 G4N_TILE = 10  # gemm4 on 256 x 128 tiles (csrc/kernels/gemm4w.h g4n_mainloop)
+G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h)
 SK_MARGIN = 0.97
 TUNE_ROUNDS = 3
 
@@ -327,7 +329,10 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
-             if tm != G4N_TILE or (k % 64 == 0 and not (c > 1 and rms and mode != 1))]
+             if (tm != G4N_TILE or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
+             and (tm not in G5_TILES or (k % 64 == 0 and m <= 512))]
+    if k % 64 == 0 and m <= 512:  # gemm5 also at the deeper splits its 64-deep stages allow (narrow shards, long K)
+        cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c]
     sk_ws, sk_tk = sk_workspace(e, m, n, k, device)
     if sk_ws is not None:
         cands.append((1, SK_TILE))
@@ -355,7 +360,8 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     eps = 1e-5 if (rms and mode != 1) else -1.0
     # split plans run the way the model runs them: with the in-kernel fixup (tickets) where it applies
     fix = e.gemm_fixup_enabled()
-    need = max(max(ks_c) * m * (n + 1), max(e.gemm_fix_workspace(m, n, c)[0] for c in ks_c), hyb_floats)
+    need = max(max(c for c, _ in cands) * m * (n + 1), max(e.gemm_fix_workspace(m, n, c)[0] for c in ks_c),
+               hyb_floats)
     ws = torch.empty(need, dtype=torch.float32, device=device)
     fix_tk = torch.zeros(max(e.gemm_fix_workspace(m, n, 2)[1], 1), dtype=torch.int32, device=device) if fix else None
     if fix_tk is None and hyb_floats:
@@ -371,6 +377,8 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, sk_ws, eps, tm, sk_tk)
         elif tm == HYBRID_TILE:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, ws, eps, tm, fix_tk)
+        elif tm in G5_TILES:
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws, eps, tm)
         else:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm,
                    fix_tk if c > 1 else None, None, rms_ws if c == 1 and eps > 0 else None)

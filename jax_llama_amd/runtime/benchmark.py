@@ -111,12 +111,30 @@ def generate_tokens_per_sec(model, batch: int, prompt_len: int, gen_len: int, gc
     return {"batch": batch, "ms_per_generate": round(1000 * dt, 2), "tokens_per_sec": round(batch * gen_len / dt, 2)}
 
 
-def calibration(device) -> Dict[str, object]:
-    """Fixed-work probes that tell a slower box from a kernel regression (bench.py ``calibration``): bf16 GEMM
-    TFLOP/s of one fixed 8192^3 shape on this framework's tiled GEMM and on the vendor library (torch.mm ->
-    hipBLASLt), HBM copy TB/s (read + write bytes), and the current shader clock level if sysfs exposes it."""
+def _sclk_levels():
+    """(current level line, max level line) of the shader clock from sysfs (pp_dpm_sclk), or (None, None)."""
     import glob
+    try:
+        for f in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
+            lines = [ln.strip() for ln in open(f) if ln.strip()]
+            if lines:
+                cur = next((ln for ln in lines if ln.endswith("*")), None)
+                return cur, lines[-1]
+    except OSError:
+        pass
+    return None, None
 
+
+def calibration(device) -> Dict[str, object]:
+    """Fixed-work probes that tell a slower box from a kernel regression (bench.py ``calibration``):
+      * bf16 GEMM TFLOP/s of one fixed 8192^3 shape on this framework's tiled GEMM and on the vendor library
+        (torch.mm -> hipBLASLt);
+      * ``stream_read_tbps``: a 2 GiB read-only stream through the repo's own streaming-read kernel (norm_embed.hip
+        prefetch_kernel, 16 loads in flight per lane, 4 workgroups per CU) -- the same kind of traffic as a decode
+        weight stream, so it and the rooflines (weight bytes / 6.29e12) compare like with like; ``copy_tbps`` (a torch
+        copy, read + write bytes) is kept beside it;
+      * ``sclk_mhz_under_mfma_load``: the shader clock measured in-kernel under a full matrix load (cycle counter over
+        the constant 100 MHz counter), and ``sclk_max_level`` from sysfs."""
     from .. import ops
     from ..models.weights import PackedLinear
     out: Dict[str, object] = {}
@@ -140,24 +158,39 @@ def calibration(device) -> Dict[str, object]:
         torch.cuda.synchronize(device)
         return ev0.elapsed_time(ev1) / iters
 
+    def gemm():
+        e.gemm(x, pw.weight, n, n, y, ops.MODE_STORE, False, None, 1, None, -1.0, 0)
+
     flop = 2.0 * n * n * n
-    ms = timed(lambda: e.gemm(x, pw.weight, n, n, y, ops.MODE_STORE, False, None, 1, None, -1.0, 0), 10)
+    ms = timed(gemm, 10)
     out["gemm_8192_tflops"] = round(flop / ms / 1e9, 1)
+    # the clock under a full matrix load, measured in-kernel (shader cycles / 100 MHz real-time ticks over ~50 ms of
+    # dependent MFMA chains on every CU; norm_embed.hip clock_probe_kernel) -- sysfs shows only the DPM request level
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    ticks = torch.zeros(3, dtype=torch.int64, device=device)
+    e.clock_probe(200, 4 * cus, ticks)  # warm
+    e.clock_probe(1000000, 4 * cus, ticks)
+    torch.cuda.synchronize(device)
+    cyc, rt = (int(v) for v in ticks[:2].tolist())
+    if rt > 0:
+        out["sclk_mhz_under_mfma_load"] = round(cyc / rt * 100.0, 1)
+    cur, top = _sclk_levels()
+    if top is not None:
+        out["sclk_max_level"] = top
     ms = timed(lambda: torch.mm(x, w.t(), out=y), 10)
     out["hipblaslt_8192_tflops"] = round(flop / ms / 1e9, 1)
     del x, w, pw, y
     src = torch.empty(1 << 29, dtype=torch.float32, device=device).fill_(1.0)  # 2 GiB
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    ms = timed(lambda: ext_prefetch(e, src, 4 * cus), 5)  # (cus: set above)
+    out["stream_read_tbps"] = round(src.numel() * 4 / ms / 1e9, 2)
     dst = torch.empty_like(src)
     ms = timed(lambda: dst.copy_(src), 5)
     out["copy_tbps"] = round(2 * src.numel() * 4 / ms / 1e9, 2)
     del src, dst
     torch.cuda.empty_cache()
-    try:
-        for f in sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk")):
-            cur = [ln.strip() for ln in open(f) if ln.strip().endswith("*")]
-            if cur:
-                out["sclk"] = cur[0]
-                break
-    except OSError:
-        pass
     return out
+
+
+def ext_prefetch(e, t: torch.Tensor, grid: int) -> None:
+    e.prefetch(t, int(grid))

@@ -226,17 +226,14 @@ def test_tp_decode_matches_single_process(world, kind, rows):
         assert r0["fused_used"]
     assert r0["err_fp32"] < 2e-2, r0["err_fp32"]
     assert r0["err_bf16"] < 2e-2, r0["err_bf16"]
-    # every token the TP decode chose is TP1's argmax up to rounding (exact equality of whole sequences is
-    # not a property of a K-split sum: a near-tie can break the other way and the sequences then differ)
-    # (the TP1 decode and its teacher-forced prefill round the logits at different points: near-ties within
-    # bf16 rounding of the logits, ~1e-3 of their scale at V = 32000, can break either way)
-    # per kind: the V = 32000 MHA configs (13b / 65b) carry near-ties up to ~1e-3 of the logit scale; the small and
-    # 70b configs keep the tight bound
-    # (1e-2 for those: the prefill GEMM applies the fused norm's precomputed statistic in its epilogue, the decode
-    # GEMV in-loop, so the two TP1 paths round the logits at different points; measured 6.7e-3 at 65b dims)
-    # one bound for every kind: a near-tie within the bf16 rounding of the logits themselves (2^-8 ~ 3.9e-3 of their
-    # scale) can break either way; measured 1.7e-3 at 70b dims, 6.7e-3 at 65b dims
-    assert r0["tp1_argmax_gap"] < 1e-2, r0["tp1_argmax_gap"]
+    # every token the TP decode chose is TP1's argmax up to rounding (exact equality of whole sequences is not a
+    # property of a K-split sum: a near-tie can break the other way and the sequences then differ). The TP1 decode and
+    # its teacher-forced prefill round the logits at different points (the prefill GEMM applies the fused norm's
+    # precomputed statistic in its epilogue, the decode GEMV sums it in-loop), so the bound is per kind: the V = 32000
+    # MHA configs (13b / 65b) carry near-ties up to the bf16 rounding of their logits (2^-8 ~ 3.9e-3 of the scale;
+    # measured 6.7e-3 at 65b dims), the GQA small / 70b configs stay tight (measured 1.7e-3 at 70b dims)
+    gap_bound = 1e-2 if kind in ("13b", "65b") else 5e-3
+    assert r0["tp1_argmax_gap"] < gap_bound, (kind, r0["tp1_argmax_gap"])
     # (a near-tie broken the other way costs at most the logits' rounding error: err_fp32 above is < 2e-2)
     assert r0["tp_argmax_gap"] < 1e-2, (r0["tp_argmax_gap"], r0["greedy_eq_tp1"])
     assert r0["greedy_bf16_first_eq"]

@@ -292,6 +292,32 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
 }
 
 
+// fused small-batch qkv projection + decode attention (gemv.hip qkv_attn_kernel): q [M, H, Dh] (scratch the
+// attention workgroups read), the attention output out [M, H * Dh] (+ its packed copy); splits from qkv_attn_splits
+void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions,
+                     Tensor kc, Tensor vc, Tensor slot, int64_t h, int64_t hkv, int64_t dh, Tensor q, Tensor kv_start,
+                     Tensor out, c10::optional<Tensor> out_pack, Tensor ws, Tensor tickets, Tensor sync, int64_t t_cap,
+                     int64_t splits, c10::optional<Tensor> x_packed) {
+  check_gpu(x, "x");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "linear_qkv_attn: x bf16 [M, K]");
+  const int64_t m = x.size(0);
+  check(m <= 32, "linear_qkv_attn: M <= 32");
+  jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, 1, h, hkv, dh, q);
+  for (auto* t : {&kv_start, &out, &ws, &tickets, &sync}) check_gpu(*t, "linear_qkv_attn arg");
+  check(kv_start.scalar_type() == torch::kInt32 && kv_start.numel() == m, "kv_start int32 [B]");
+  check(out.scalar_type() == torch::kBFloat16 && out.numel() == m * h * dh, "out bf16 [B, H * Dh]");
+  check(ws.scalar_type() == torch::kFloat32 && ws.numel() >= m * hkv * splits * (h / hkv) * (dh + 4), "ws too small");
+  check(tickets.scalar_type() == torch::kInt32 && tickets.numel() >= m * hkv, "tickets int32 [pairs]");
+  check(sync.scalar_type() == torch::kInt32 && sync.numel() >= 3, "sync int32 [3]");
+  check(t_cap <= kc.size(2), "t_cap <= cache length");
+  const jla::bf16_t* xp = packed_ptr(x_packed, m, k, "x_packed");
+  rc(jla::linear_qkv_attn(xp ? xp : cbf(x), w.data_ptr(), m, n, k, (float)rms_eps, qa, xp != nullptr, bf(out),
+                          packed_ptr(out_pack, m, h * dh, "out_pack"), ptr<int32_t>(kv_start), ptr<float>(ws),
+                          ptr<int32_t>(tickets), ptr<int32_t>(sync), (int)t_cap, (int)splits, stream()),
+     "linear_qkv_attn");
+}
+
 void check_gemm_ws(const c10::optional<Tensor>& ws, int64_t ksplit, int64_t m, int64_t n, bool rms = false) {
   if (ksplit <= 1) return;
   check(ws.has_value(), "gemm: split-K needs a workspace");
@@ -857,6 +883,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("table"), py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"),
         py::arg("h"), py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("variant"), py::arg("ws"), py::arg("tickets"),
         py::arg("x_packed") = py::none());
+  m.def("linear_qkv_attn", &linear_qkv_attn, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"),
+        py::arg("rms_eps"), py::arg("table"), py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
+        py::arg("h"), py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("kv_start"), py::arg("out"),
+        py::arg("out_pack"), py::arg("ws"), py::arg("tickets"), py::arg("sync"), py::arg("t_cap"), py::arg("splits"),
+        py::arg("x_packed") = py::none());
+  m.def("qkv_attn_splits", [](int64_t m, int64_t b, int64_t hkv, int64_t rep, int64_t t_cap, int64_t n, int64_t cus) {
+    return jla::qkv_attn_splits((int)m, (int)b, (int)hkv, (int)rep, (int)t_cap, (int)n, (int)cus);
+  });
+  m.def("qkv_attn_occupancy", [](int64_t m, int64_t rep) { return jla::qkv_attn_occupancy((int)m, (int)rep); });
   m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);

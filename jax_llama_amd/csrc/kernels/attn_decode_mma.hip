@@ -20,43 +20,12 @@
 // and its own K register ring: V by LDS-DMA, K by plain loads, both issued one step ahead as inline asm with
 // hand-counted waits so the next step's 16 loads stay in flight while this one computes). The WPP waves merge
 // (m, l, O) once through LDS at the end. Rows with no valid key output 0.
+#include "attn_mma.h"
 #include "common.h"
 #include "launchers.h"
 #include "ring.h"
 
 namespace jla {
-
-constexpr int AD6_DH = 128;
-constexpr int AD6_STEP = 32;                        // keys per step
-constexpr int AD6_SLOT_BYTES = AD6_STEP * AD6_DH * 2;  // 8 KiB of V per step
-constexpr int AD6_WAVE_LDS = 2 * AD6_SLOT_BYTES;        // two V slots per wave
-
-typedef short s16x4_6 __attribute__((ext_vector_type(4)));
-
-// byte offset of 16-byte chunk ch (0..15) of row `row` in a [rows][128 bf16] image: conflict-free for both the
-// DMA's lane-linear writes and ds_read_b64_tr_b16's 4-row x 16-column reads (the flash prefill's image)
-JLA_DEV int ad6_off(int row, int ch) { return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))); }
-
-// The O^T accumulators are pinned to AGPRs through inline-asm MFMAs (with the intrinsic, hipcc kept them in VGPRs
-// across the loop and copied all 32 in from AGPRs every step). hipcc's hazard recognizer does not look inside the
-// asm, so the wait states are explicit: before the PV group (the VALU-written P operand and, after a rescale, the
-// v_accvgpr_write of the accumulators) and between the last MFMA and a read of its result (ad6_take).
-JLA_DEV void ad6_mfma_acc(f32x4& acc, const u32x4& a, const u32x4& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-JLA_DEV f32x4 ad6_take(f32x4& a) {  // an AGPR accumulator at this point in program order (MFMA -> read: s_nop pad)
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(a));
-  return a;
-}
-JLA_DEV void ad6_put(f32x4& a, const f32x4 v) {
-  a = v;
-  asm volatile("" : "+a"(a));
-}
-
-JLA_DEV u32x2 ad6_tr(const char* lds, int off) {
-  return __builtin_bit_cast(u32x2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                                       (__attribute__((address_space(3))) s16x4_6*)(lds + off)));
-}
 
 template <int REP, int WPP>
 __global__ void __launch_bounds__(WPP * 64)
@@ -82,112 +51,24 @@ __global__ void __launch_bounds__(WPP * 64)
   const bf16_t* const kb = kc + head_off;
   const bf16_t* const vb = vc + head_off;
 
-  // Q^T fragments: lane (c, j) holds head h0 + j, dims 32jj + 8c .. +7 for dk step jj (zero columns past REP)
+  // Q^T fragments (attn_mma.h); a wait hipcc sees: otherwise it places a vmcnt(0) for these loads inside the loop,
+  // behind the hand-counted ring
   u32x4 qf[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    qf[jj] = u32x4{0u, 0u, 0u, 0u};
-    if (j < REP) qf[jj] = *reinterpret_cast<const u32x4*>(q + ((size_t)b * H + h0 + j) * AD6_DH + 32 * jj + 8 * c);
-  }
-  // a wait hipcc sees: otherwise it places a vmcnt(0) for these loads inside the loop, behind the hand-counted ring
+  ad6_load_q<REP, false>(qf, q + ((size_t)b * H + h0) * AD6_DH, lane);
   ::wait_vmcnt<0>();
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) pin(qf[jj]);
+  ad6_q_ready<REP>(qf, lane);
 
   const int s_begin = lo >= 0 ? lo / AD6_STEP : 0;
   const int n_steps = lo < hi ? (hi - 1) / AD6_STEP - s_begin + 1 : 0;
   const int my_steps = n_steps > w ? (n_steps - w + WPP - 1) / WPP : 0;
-
-  // per-lane load addresses of one step (relative to the step's first key row)
-  //   K: key (l & 15) of block kb (kb = 0, 1), bytes 64jj + 16c (jj = 0..3)
-  //   V DMA: 1 KiB block bi (rows 4bi .. 4bi+3), lane L -> row 4bi + L / 16, slot L % 16 <- source chunk slot ^ swz(row)
   auto issue = [&](int step, u32x4 (&kr)[8], char* vslot) {
-    const int key0 = (s_begin + step) * AD6_STEP;
-#pragma unroll
-    for (int bi = 0; bi < 8; ++bi) {
-      const int row = 4 * bi + (lane >> 4);
-      const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-      const int key = min(key0 + row, T - 1);
-      glds16_asm(vb + (size_t)key * AD6_DH + 8 * ch, vslot + 1024 * bi);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int key = min(key0 + 16 * kk + j, T - 1);
-      const bf16_t* p = kb + (size_t)key * AD6_DH + 8 * c;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) asm_load<true>(kr[4 * kk + jj], p + 32 * jj);
-    }
+    ad6_issue<false>((s_begin + step) * AD6_STEP, kr, vslot, kb, vb, T, lane);
   };
-
-  float m_run = -INFINITY, l_run = 0.f;
-  f32x4 o[8];  // O^T accumulators, pinned to AGPRs (ad6_mfma_acc): touched by the VALU only in the rescale branch
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
+  Ad6Acc st;
+  ad6_init(st);
   // valid = false: a ring slot loaded past the wave's last step (clamped addresses, fully masked, adds nothing)
   auto compute = [&](int step, bool valid, u32x4 (&kr)[8], const char* vslot) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) pin(kr[i]);
-    const int key0 = (s_begin + step) * AD6_STEP;
-    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      s0 = mfma16x16x32(kr[jj], qf[jj], s0);
-      s1 = mfma16x16x32(kr[4 + jj], qf[jj], s1);
-    }
-    // lane (c, j): s0[r] = score of key key0 + 4c + r, s1[r] = key key0 + 16 + 4c + r, head h0 + j
-    float sc[8];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sc[r] = s0[r] * scale_log2;
-      sc[4 + r] = s1[r] * scale_log2;
-    }
-    if (!(valid && key0 >= lo && key0 + AD6_STEP <= hi && !mrow)) {  // wave-uniform: only the edge steps mask
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int key = key0 + (e < 4 ? 4 * c + e : 16 + 4 * c + e - 4);
-        bool ok = valid && key >= lo && key < hi;
-        if (mrow) ok = ok && key < mask_len && mrow[key] != 0;
-        sc[e] = ok ? sc[e] : -INFINITY;
-      }
-    }
-    float tmax = sc[0];
-#pragma unroll
-    for (int e = 1; e < 8; ++e) tmax = fmaxf(tmax, sc[e]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    // lazy rescale (as the flash prefill): move the running max only when it grows by more than 8 (log2 units)
-    if (__ballot(tmax > m_run + 8.f)) {
-      const float m_new = fmaxf(m_run, tmax);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - (m_new == -INFINITY ? 0.f : m_new));
-      l_run *= alpha;
-      m_run = m_new;
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) {
-        f32x4 t = ad6_take(o[dt]);
-        t *= alpha;
-        ad6_put(o[dt], t);
-      }
-    }
-    const float m_use = m_run == -INFINITY ? 0.f : m_run;
-    float p[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      p[e] = __builtin_amdgcn_exp2f(sc[e] - m_use);
-      l_run += p[e];
-    }
-    u32x4 pf = pack8(p);
-    asm volatile("s_nop 4" : "+v"(pf));  // VALU write of the P operand (and any accumulator write above) -> MFMA read
-    // V^T fragments: lane 4q + pp of group c reads row 4c + q (and 16 + 4c + q), columns 16dt + 4pp .. +3
-    const int q4 = (lane & 15) >> 2, pp = lane & 3;
-    const int r0 = 4 * c + q4;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      const int ch = 2 * dt + (pp >> 1);
-      const u32x2 a = ad6_tr(vslot, ad6_off(r0, ch) + 8 * (pp & 1));
-      const u32x2 bb = ad6_tr(vslot, ad6_off(r0 + 16, ch) + 8 * (pp & 1));
-      ad6_mfma_acc(o[dt], u32x4{a[0], a[1], bb[0], bb[1]}, pf);
-    }
+    ad6_compute<REP>(st, kr, qf, vslot, (s_begin + step) * AD6_STEP, valid, lo, hi, mrow, mask_len, scale_log2, lane);
   };
 
   // Two-slot ring, branch-free around the loads (a branch there makes hipcc merge in-flight ring registers with
@@ -215,11 +96,9 @@ __global__ void __launch_bounds__(WPP * 64)
     wait_vmcnt<0>();  // the last refill of slot A: drained before the LDS is reused or the wave ends
   }
 
-  // per wave: the row sum over the 4 lane groups (the running max is already shared by them)
-#pragma unroll
-  for (int dt = 0; dt < 8; ++dt) o[dt] = ad6_take(o[dt]);
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
+  ad6_finish(st);
+  const float m_run = st.m, l_run = st.l;
+  f32x4 (&o)[8] = st.o;
   // lane (c, j) holds O[head j][dims 16dt + 4c + r]
   if constexpr (WPP == 1) {
     if (j < REP) {

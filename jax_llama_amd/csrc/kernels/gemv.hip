@@ -23,6 +23,7 @@
 //     interleaved [w1;w3] weight, or (QKV mode) rotates q/k pairs with RoPE and writes q plus the
 //     k/v cache rows at the device-side cache slot.
 // No atomics: results are deterministic and the residual add happens exactly once.
+#include "attn_mma.h"
 #include "car.h"
 #include "common.h"
 #include "launchers.h"
@@ -32,10 +33,19 @@ namespace jla {
 
 __device__ u32x4 g_zero_frag[64];  // 1 KiB of zeros (static storage is zero-initialised)
 
-template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false>
-__global__ void __launch_bounds__(NW * 64)
-    linear_skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out,
-                         int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa) {
+// 2-byte agent-coherent (sc1, write-through) store: outputs another workgroup of the SAME launch reads (the qkv
+// epilogue of the fused qkv + attention launch)
+JLA_DEV void st_sc1_b16(bf16_t* p, bf16_t v) {
+  asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"((unsigned)v) : "memory");
+}
+
+// The GEMV body of one workgroup (bx: column group, by / gy: K split index / count), shared by linear_skinny_kernel
+// and the fused qkv + attention launch. SC1: the QKV epilogue's q / cache stores are write-through (sc1), for the
+// attention workgroups of the same launch.
+template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false, bool SC1 = false>
+JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                         int K, float eps, int use_rms, int accumulate, int out_f32, const QKVArgs& qa, int bx, int by,
+                         int gy) {
   extern __shared__ float smem[];
   float* red = smem;                              // [NW][MT][NT][64][4]
   float* red_ss = red + NW * MT * NT * 256;       // [NW][MT][16]
@@ -45,12 +55,12 @@ __global__ void __launch_bounds__(NW * 64)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
   const int KS = K >> 5;
   const int NTT = N >> 4;
-  const int nt0 = blockIdx.x * NT;
-  // SPLIT: K is cut over gridDim.y workgroups per column group; this one streams k-steps [kb, kb + kn)
+  const int nt0 = bx * NT;
+  // SPLIT: K is cut over gy workgroups per column group; this one streams k-steps [kb, kb + kn)
   int kb = 0, kn = KS;
   if constexpr (SPLIT) {
-    kb = (int)((long long)KS * blockIdx.y / gridDim.y);
-    kn = (int)((long long)KS * (blockIdx.y + 1) / gridDim.y) - kb;
+    kb = (int)((long long)KS * by / gy);
+    kn = (int)((long long)KS * (by + 1) / gy) - kb;
   }
 
   const u32x4* wt[NT];
@@ -71,7 +81,7 @@ __global__ void __launch_bounds__(NW * 64)
   int tp_calls = 0;
   if constexpr (MODE == MODE_TPRESID) {
     if (threadIdx.x == 0)
-      tp_calls = __hip_atomic_load(static_cast<const CarDevice*>(qa.tp)->wg_ctr + blockIdx.x, __ATOMIC_RELAXED,
+      tp_calls = __hip_atomic_load(static_cast<const CarDevice*>(qa.tp)->wg_ctr + bx, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
   }
 
@@ -166,9 +176,9 @@ __global__ void __launch_bounds__(NW * 64)
   constexpr int NWR = SPLIT ? 1 : NW;  // wave slots of `red` / `red_ss` the epilogue sums
   if constexpr (SPLIT) {
     constexpr int E = MT * NT * 256, SLAB = E + MT * 16;
-    const int ns = gridDim.y, grp = blockIdx.x;
+    const int ns = gy, grp = bx;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(qa.sk_ws, 0, qa.sk_ws_floats * 4, 0x00020000);
-    const int mine = (grp * ns + blockIdx.y) * SLAB * 4;
+    const int mine = (grp * ns + by) * SLAB * 4;
     for (int e = threadIdx.x; e < E; e += NW * 64) {
       float v = 0.f;
 #pragma unroll
@@ -244,7 +254,7 @@ __global__ void __launch_bounds__(NW * 64)
     }
   } else if constexpr (MODE == MODE_TPRESID) {
     // ---- row-parallel partial all-reduced in the epilogue (no separate collective launch): every rank's workgroup
-    // blockIdx.x computes the same (rows, columns) of its own K shard. Each even-column lane packs its value and its
+    // bx computes the same (rows, columns) of its own K shard. Each even-column lane packs its value and its
     // neighbour's (RNE to bf16, as the unfused partial) into one 8-byte granule {2 x bf16, tag} and stores it into
     // slot [parity][rank] of every peer (this workgroup's fixed TPRES_REGION), then polls the same granule of every
     // rank's slot in its own buffer until it carries this call's tag, sums in rank order in fp32 and applies the
@@ -254,7 +264,7 @@ __global__ void __launch_bounds__(NW * 64)
     const CarDevice& d = *static_cast<const CarDevice*>(qa.tp);
     const int calls = reinterpret_cast<const int*>(inv_rms + MT * 16)[0];
     const unsigned tag = gran_tag_fused(calls);
-    const long long wg_base = (long long)blockIdx.x * TPRES_REGION;
+    const long long wg_base = (long long)bx * TPRES_REGION;
     const long long par_base = (long long)(calls & 1) * d.world * d.max_bytes;
     const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
     float* h = static_cast<float*>(out);
@@ -305,7 +315,7 @@ __global__ void __launch_bounds__(NW * 64)
       if (qa.pack) *reinterpret_cast<uint32_t*>(qa.pack + pack_off(m, col, N)) = pk;
     }
     if (threadIdx.x == 0)
-      __hip_atomic_store(d.wg_ctr + blockIdx.x, calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.wg_ctr + bx, calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
       const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
@@ -347,14 +357,20 @@ __global__ void __launch_bounds__(NW * 64)
           r = (d & 1) ? (pv * cs.y + v * cs.x) : (v * cs.x - pv * cs.y);
         }
         if (head < qa.H) {
-          qa.q[((size_t)m * qa.H + head) * qa.Dh + d] = f2bf(r);
+          if constexpr (SC1)
+            st_sc1_b16(qa.q + ((size_t)m * qa.H + head) * qa.Dh + d, f2bf(r));
+          else
+            qa.q[((size_t)m * qa.H + head) * qa.Dh + d] = f2bf(r);
         } else {
           const int slot = qa.slot[0] + s;
           if (slot < qa.T) {
             const bool is_k = head < qa.H + qa.Hkv;
             const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
             bf16_t* cache = is_k ? qa.kc : qa.vc;
-            cache[(((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d] = f2bf(r);
+            if constexpr (SC1)
+              st_sc1_b16(cache + (((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d, f2bf(r));
+            else
+              cache[(((size_t)b * qa.Hkv + kh) * qa.T + slot) * qa.Dh + d] = f2bf(r);
           } else {
             JLA_FLAG(JLA_BOUNDS_KV_SLOT);
           }
@@ -376,6 +392,14 @@ __global__ void __launch_bounds__(NW * 64)
       }
     }
   }
+}
+
+template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false>
+__global__ void __launch_bounds__(NW * 64)
+    linear_skinny_kernel(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out,
+                         int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32, QKVArgs qa) {
+  skinny_body<XT, MT, NT, MODE, NW, U, XP, SPLIT>(x, W, out, M, N, K, eps, use_rms, accumulate, out_f32, qa, blockIdx.x,
+                                                  blockIdx.y, gridDim.y);
 }
 
 template <typename XT, int MT, int NT, int MODE, int NW, int DEEP = 0, bool XP = false, bool SPLIT = false>
@@ -512,6 +536,335 @@ static int dispatch_tp(const void* x, const void* W, void* out, int M, int N, in
   } else {
     return -1;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused small-batch decode launch: the qkv projection (this GEMV, MODE_QKV: fused norm, RoPE, KV-cache write) on
+// workgroups [0, grid_q) and the decode attention (attn_mma.h, the v6 step) on the next pairs x splits workgroups --
+// one launch instead of two (reference model.py:210-291 for S = 1). While the qkv workgroups stream their weights, every
+// attention wave prefetches its 32-key step of K (registers) and V (LDS) from the cache; one lane per attention
+// workgroup then polls the qkv-done counter (every qkv workgroup adds to it once its write-through q / K / V stores
+// have drained), the waves load the pair's q and re-load the one cache row this launch wrote (write-through loads),
+// score their step, merge through LDS, and the pair's splits merge by last arriver (write-through partials + ticket).
+// Co-residency: the host launches this only when every workgroup fits on the CUs at once (grid <= CUs), so the
+// attention workgroups' waits always end; each wait is also bounded (the error word records a timeout).
+constexpr int QA_SPLIT_KEYS = 128;  // keys per attention workgroup (4 waves x one 32-key step)
+constexpr int QA_MAX_SPLITS = 4;    // attention workgroups per (row, kv head) pair: cache length <= 512
+constexpr int QA_PART = AD6_DH + 4; // floats per (split, head) partial: O[128], m, l, pad
+struct FusedAttn {
+  bf16_t* out;              // [B, H * Dh]
+  bf16_t* out_pack;         // optional packed copy (the o projection's packed x)
+  const int32_t* kv_start;  // [B]
+  float* ws;                // [pairs][splits][REP][QA_PART] write-through partials
+  int32_t* tickets;         // [pairs] merge tickets (self-resetting)
+  int32_t* sync;            // [0] qkv-done counter, [1] attention-seen counter (both self-resetting), [2] error word
+  int splits, grid_q, t_cap;
+  float scale_log2;
+};
+
+JLA_DEV void st_sc1_x4(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int MT, int NT, int NW, int U, bool XP, int REP>
+__global__ void __launch_bounds__(256)
+    qkv_attn_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, int M, int N, int K, float eps,
+                    int use_rms, QKVArgs qa, FusedAttn fa) {
+  static_assert(NW == 4, "4-wave workgroups (the attention side uses 4 waves x 32 keys)");
+  if ((int)blockIdx.x < fa.grid_q) {
+    skinny_body<bf16_t, MT, NT, MODE_QKV, NW, U, XP, false, true>(x, W, nullptr, M, N, K, eps, use_rms, 0, 0, qa,
+                                                                  blockIdx.x, 0, 1);
+    // publish (Guideline 16, sc1-store + agent-counter form): every storing wave drains its write-through stores,
+    // the workgroup's barrier, then one agent-scope add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(fa.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  extern __shared__ __attribute__((aligned(16))) char ldsq[];
+  const int a = blockIdx.x - fa.grid_q;
+  const int pair = a / fa.splits, sp = a - pair * fa.splits;
+  const int b = pair / qa.Hkv, kvh = pair - b * qa.Hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int T = qa.T;
+  const int slot = qa.slot[0];
+  const int lo = fa.kv_start[b], hi = min(slot + 1, fa.t_cap);
+  const int k0 = sp * QA_SPLIT_KEYS + AD6_STEP * w;
+  const bool wave_live = k0 < hi && k0 + AD6_STEP > lo;
+  const size_t head_off = ((size_t)b * qa.Hkv + kvh) * (size_t)T * AD6_DH;
+  const bf16_t* const kb = qa.kc + head_off;
+  const bf16_t* const vb = qa.vc + head_off;
+  char* const vslot = ldsq + w * AD6_SLOT_BYTES;
+
+  // 1. prefetch this wave's step (rows clamped into the cache; the row at `slot` is re-loaded after the wait)
+  u32x4 kr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) kr[i] = u32x4{0u, 0u, 0u, 0u};
+  ad6_issue<false>(k0, kr, vslot, kb, vb, T, lane);
+
+  // 2. wait until every qkv workgroup has published (one polling lane, bounded)
+  int* flag = reinterpret_cast<int*>(ldsq + 4 * AD6_SLOT_BYTES + 1008);
+  if (threadIdx.x == 0) {
+    const long long t0 = (long long)wall_clock64();
+    int err = 0;
+    while (__hip_atomic_load(fa.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fa.grid_q) {
+      if ((long long)wall_clock64() - t0 > 20000000LL) {  // 0.2 s at the 100 MHz constant clock
+        __hip_atomic_store(fa.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        err = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    (void)err;
+    // the last attention workgroup past the wait resets both counters for the next launch
+    const int seen = __hip_atomic_fetch_add(fa.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen == (int)gridDim.x - fa.grid_q - 1) {
+      __hip_atomic_store(fa.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(fa.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  // the prefetch landed during the qkv phase: retire it here, before any branch (hipcc must never copy a ring
+  // register that is still in flight)
+  ::wait_vmcnt<0>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pin(kr[i]);
+  const int split_lo = sp * QA_SPLIT_KEYS;
+  const bool split_live = split_lo < hi && split_lo + QA_SPLIT_KEYS > lo;
+  if (!split_live) {
+    if (sp == 0 && lo >= hi && threadIdx.x < REP * 16) {  // a row with no valid key: zeros (as the other kernels)
+      const int col = (kvh * REP + (threadIdx.x >> 4)) * AD6_DH + 8 * (threadIdx.x & 15);
+      *reinterpret_cast<u32x4*>(fa.out + (size_t)b * qa.H * AD6_DH + col) = u32x4{0u, 0u, 0u, 0u};
+      if (fa.out_pack) *reinterpret_cast<u32x4*>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH)) = u32x4{0u, 0u, 0u, 0u};
+    }
+    return;
+  }
+
+  // 3. the pair's q (written by this launch: write-through loads) and the cache row at `slot` (K lanes holding that
+  //    key / V DMA lanes of that row re-load it agent-coherently; each conditional load is drained in its own block,
+  //    so no merge of an in-flight register)
+  u32x4 qf[4];
+  ad6_load_q<REP, true>(qf, qa.q + ((size_t)b * qa.H + kvh * REP) * AD6_DH, lane);
+  ::wait_vmcnt<0>();  // q: nothing in flight before the conditional re-loads
+  ad6_q_ready<REP>(qf, lane);
+  {
+    const int key0 = k0;
+    const int c = lane >> 4, j = lane & 15;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (key0 + 16 * kk + j == slot) {
+        const bf16_t* p = kb + (size_t)slot * AD6_DH + 8 * c;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) asm_load_sc1(kr[4 * kk + jj], p + 32 * jj);
+        ::wait_vmcnt<0>();
+      }
+    }
+    const int vrow = slot - key0;  // 0 .. 31 when the new row is in this wave's step
+    if (vrow >= 0 && vrow < AD6_STEP) {
+      // only the lanes of the DMA block holding that row: block vrow / 4, lanes 16 (vrow % 4) .. +15
+      const int bi = vrow >> 2;
+      if ((lane >> 4) == (vrow & 3)) {
+        const int ch = (lane & 15) ^ (((vrow & 3) << 2) | ((vrow >> 2) & 3));
+        glds16_asm_sc1(vb + (size_t)slot * AD6_DH + 8 * ch, vslot + 1024 * bi);
+      }
+    }
+  }
+  ::wait_vmcnt<0>();
+
+  // 4. this wave's step, then its (m, l, O)
+  Ad6Acc st;
+  ad6_init(st);
+  ad6_compute<REP>(st, kr, qf, vslot, k0, wave_live, lo, hi, nullptr, 0, fa.scale_log2, lane);
+  ad6_finish(st);
+
+  // 5. the 4 waves through LDS (the V slots are free once every wave is past its step)
+  __syncthreads();
+  float* sm_o = reinterpret_cast<float*>(ldsq);  // [4][REP][128]
+  float* sm_ml = sm_o + 4 * REP * AD6_DH;        // [4][REP][2]
+  {
+    const int c = lane >> 4, j = lane & 15;
+    if (j < REP) {
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+        *reinterpret_cast<f32x4*>(sm_o + (w * REP + j) * AD6_DH + 16 * dt + 4 * c) = st.o[dt];
+      if (c == 0) {
+        sm_ml[(w * REP + j) * 2] = st.m;
+        sm_ml[(w * REP + j) * 2 + 1] = st.l;
+      }
+    }
+  }
+  __syncthreads();
+  // this workgroup's (m, l, unnormalised O) per head: thread (h, 8 dims) for REP x 16 chunks
+  const int nlive = min((hi - 1) / QA_SPLIT_KEYS, fa.splits - 1) - max(lo, 0) / QA_SPLIT_KEYS + 1;
+  const int first = max(lo, 0) / QA_SPLIT_KEYS;
+  const int t = threadIdx.x;
+  const bool chunk = t < REP * 16;
+  const int h = t >> 4, d0 = 8 * (t & 15);
+  float Mw = -INFINITY, L = 0.f, num[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (chunk) {
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) Mw = fmaxf(Mw, sm_ml[(ww * REP + h) * 2]);
+    if (Mw != -INFINITY) {
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float mw = sm_ml[(ww * REP + h) * 2];
+        const float f = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - Mw);
+        L += f * sm_ml[(ww * REP + h) * 2 + 1];
+        const float* src = sm_o + (ww * REP + h) * AD6_DH + d0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) num[e] += f * src[e];
+      }
+    }
+  }
+  auto write_out = [&](const float* o8, float den) {
+    const float inv = den > 0.f ? 1.f / den : 0.f;
+    float r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] = o8[e] * inv;
+    const u32x4 v = pack8(r);
+    const int col = (kvh * REP + h) * AD6_DH + d0;
+    *reinterpret_cast<u32x4*>(fa.out + (size_t)b * qa.H * AD6_DH + col) = v;
+    if (fa.out_pack) *reinterpret_cast<u32x4*>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH)) = v;
+  };
+  if (nlive <= 1) {  // the pair's only live split: no merge
+    if (chunk) write_out(num, L);
+    return;
+  }
+  // 6. the pair's splits: write-through partial, ticket, the last arriver merges in split order
+  float* part = fa.ws + ((size_t)pair * fa.splits) * REP * QA_PART;
+  if (chunk) {
+    float* mine = part + ((size_t)sp * REP + h) * QA_PART;
+    st_sc1_x4(mine + d0, u32x4{__float_as_uint(num[0]), __float_as_uint(num[1]), __float_as_uint(num[2]),
+                               __float_as_uint(num[3])});
+    st_sc1_x4(mine + d0 + 4, u32x4{__float_as_uint(num[4]), __float_as_uint(num[5]), __float_as_uint(num[6]),
+                                   __float_as_uint(num[7])});
+    if (d0 == 0) st_sc1_x4(mine + AD6_DH, u32x4{__float_as_uint(Mw), __float_as_uint(L), 0u, 0u});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(fa.tickets + pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == nlive - 1;
+    if (last) __hip_atomic_store(fa.tickets + pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag || !chunk) return;
+  u32x4 po[QA_MAX_SPLITS][2], pml[QA_MAX_SPLITS];
+#pragma unroll
+  for (int s2 = 0; s2 < QA_MAX_SPLITS; ++s2) {  // (all issued, then one wait; splits past the live ones re-read the last)
+    const float* src = part + ((size_t)(first + min(s2, nlive - 1)) * REP + h) * QA_PART;
+    po[s2][0] = po[s2][1] = pml[s2] = u32x4{0u, 0u, 0u, 0u};
+    asm_load_sc1(po[s2][0], src + d0);
+    asm_load_sc1(po[s2][1], src + d0 + 4);
+    asm_load_sc1(pml[s2], src + AD6_DH);
+  }
+  ::wait_vmcnt<0>();
+  float Mx = -INFINITY;
+#pragma unroll
+  for (int s2 = 0; s2 < QA_MAX_SPLITS; ++s2) {
+    pin(po[s2][0]);
+    pin(po[s2][1]);
+    pin(pml[s2]);
+    if (s2 < nlive) Mx = fmaxf(Mx, __uint_as_float(pml[s2][0]));
+  }
+  float o8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, den = 0.f;
+  if (Mx != -INFINITY) {
+#pragma unroll
+    for (int s2 = 0; s2 < QA_MAX_SPLITS; ++s2) {
+      if (s2 >= nlive) break;
+      const float ms = __uint_as_float(pml[s2][0]);
+      const float f = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - Mx);
+      den += f * __uint_as_float(pml[s2][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o8[e] += f * __uint_as_float(po[s2][0][e]);
+        o8[4 + e] += f * __uint_as_float(po[s2][1][e]);
+      }
+    }
+  }
+  write_out(o8, den);
+}
+
+size_t qkv_attn_lds(int mt) {
+  const size_t attn = 4 * AD6_SLOT_BYTES + 1024;  // V slots, the merge's (m, l) and a flag (the merge reuses the slots)
+  const size_t gemv = sizeof(float) * (4 * mt * 1 * 256 + 4 * mt * 16 + mt * 16 + 4);  // NT = 1, NW = 4
+  return attn > gemv ? attn : gemv;
+}
+
+// workgroups of the fused launch that are resident at once per CU (occupancy API, one below its answer as a margin:
+// cdna_hip_programming.md warns it can be one block too high; at least 1)
+// (MT m-tiles: the GEMV ring depth U = 8 / MT, as launch_skinny)
+template <int MT, int REP>
+static int qkv_attn_per_cu() {
+  static int cached = 0;
+  if (cached == 0) {
+    int a = 0, b = 0;
+    const size_t lds = qkv_attn_lds(MT);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, qkv_attn_kernel<MT, 1, 4, 8 / MT, false, REP>, 256, lds) !=
+            hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, qkv_attn_kernel<MT, 1, 4, 8 / MT, true, REP>, 256, lds) !=
+            hipSuccess)
+      a = b = 1;
+    const int n = a < b ? a : b;
+    cached = n > 1 ? n - 1 : 1;
+  }
+  return cached;
+}
+template <int MT>
+static int qkv_attn_per_cu_rep(int rep) {
+  switch (rep) {
+    case 1: return qkv_attn_per_cu<MT, 1>();
+    case 2: return qkv_attn_per_cu<MT, 2>();
+    case 4: return qkv_attn_per_cu<MT, 4>();
+    case 8: return qkv_attn_per_cu<MT, 8>();
+    case 16: return qkv_attn_per_cu<MT, 16>();
+    default: return 0;
+  }
+}
+
+// 0 when the fused launch does not apply (then the caller runs the qkv GEMV and the attention kernel). Every workgroup
+// of the launch must be resident at once (the attention workgroups wait for the qkv ones).
+int qkv_attn_occupancy(int M, int rep) {
+  return M <= 16 ? qkv_attn_per_cu_rep<1>(rep) : qkv_attn_per_cu_rep<2>(rep);
+}
+int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus) {
+  if (M != B || M > 32 || (rep & (rep - 1)) || rep > 16 || t_cap > QA_MAX_SPLITS * QA_SPLIT_KEYS) return 0;
+  const int splits = (t_cap + QA_SPLIT_KEYS - 1) / QA_SPLIT_KEYS;
+  const int grid = (N >> 4) + B * Hkv * splits;
+  return grid <= cus * qkv_attn_occupancy(M, rep) ? splits : 0;
+}
+
+int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
+                    bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
+                    int t_cap, int splits, hipStream_t s) {
+  if (M <= 0) return 0;
+  if (M > 32 || (N & 15) || (K & 31) || qa.Dh != AD6_DH || qa.S != 1 || qa.H % qa.Hkv) return -1;
+  const int rep = qa.H / qa.Hkv;
+  const int grid_q = N >> 4, pairs = M * qa.Hkv;
+  if (splits < 1 || splits > QA_MAX_SPLITS || splits * QA_SPLIT_KEYS < t_cap) return -1;
+  const FusedAttn fa{out, out_pack, kv_start, ws, tickets, sync, splits, grid_q, t_cap,
+                     1.4426950408889634f / sqrtf((float)AD6_DH)};
+  const int use_rms = rms_eps >= 0.f;
+  const float eps = use_rms ? rms_eps : 0.f;
+  const int mt = M <= 16 ? 1 : 2;
+  const size_t lds = qkv_attn_lds(mt);
+  const int grid = grid_q + pairs * splits;
+#define JLA_QA(MTV, R)                                                                                              \
+  if (mt == MTV && rep == R) {                                                                                      \
+    if (xp)                                                                                                         \
+      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, true, R><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M, N, K,   \
+                                                                          eps, use_rms, qa, fa);                    \
+    else                                                                                                            \
+      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, false, R><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M, N, K,  \
+                                                                           eps, use_rms, qa, fa);                   \
+    JLA_CHECK_LAUNCH();                                                                                             \
+    return 0;                                                                                                       \
+  }
+  JLA_QA(1, 1) JLA_QA(1, 2) JLA_QA(1, 4) JLA_QA(1, 8) JLA_QA(1, 16)
+  JLA_QA(2, 1) JLA_QA(2, 2) JLA_QA(2, 4) JLA_QA(2, 8) JLA_QA(2, 16)
+#undef JLA_QA
+  return -1;
 }
 
 size_t gemv_split_workspace_floats(int M, int N) {

@@ -38,6 +38,17 @@ class LLaMAAttention:
                  output_attentions: bool = False, pk: Optional["PackedActs"] = None) -> Optional[torch.Tensor]:
         m, lw = self.model, self.weights
         kc, vc = cache.layer(self.layer_idx)
+        splits = 0 if output_attentions else ops.qkv_attention_splits(hb, lw.qkv, kc, seq_len, m.n_heads,
+                                                                       m.n_kv_heads, key_mask)
+        if splits:  # small-batch decode: qkv projection + attention in one launch
+            att_p = pk.att if pk is not None else None
+            a = ops.linear_qkv_attention(hb, lw.qkv, m.eps, m.rope, positions, kc, vc, slot0, kv_start, m.n_heads,
+                                         m.n_kv_heads, m.head_dim, splits, x_packed=pk.hb_in() if pk else None,
+                                         out_packed=att_p)
+            m._row_parallel(a, lw.o, h, hb, x_packed=att_p, mirror_packed=pk.hb if pk else None)
+            if pk is not None and pk.hb is not None:
+                pk.hb_ok = True
+            return None
         q = ops.linear_qkv_rope(hb, lw.qkv, m.eps, m.rope, positions, kc, vc, slot0, seq_len,
                                 m.n_heads, m.n_kv_heads, m.head_dim, x_packed=pk.hb_in() if pk else None)
         b = hb.shape[0] // seq_len

@@ -542,6 +542,59 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     return q
 
 
+# Fused small-batch decode: the qkv GEMV and the attention in ONE launch (csrc/kernels/gemv.hip qkv_attn_kernel: the
+# attention workgroups prefetch their K / V step while the qkv workgroups stream the weights, then wait on the qkv
+# workgroups' write-through publish). Used where it measured faster (profiles/r5_qkv_attn_fused_ab.jsonl): M <= 4 rows
+# with >= 8 query heads per kv head (the 70B tensor-parallel shard: one kv head per rank) -- 4.92 -> 4.82 ms per token
+# at B = 1; at Llama-3-8B B = 1 (rep 4: 384 qkv workgroups on one 4-wave form) 2.92 -> 3.22 and at the shard's
+# B = 32 6.10 -> 6.58 the tuned standalone GEMVs win. JLA_QKV_ATTN=0: never; =2: wherever the launch fits.
+QKV_ATTN = int(os.environ.get("JLA_QKV_ATTN", "1"))
+_CUS = {}
+
+
+def _num_cus(device) -> int:
+    key = str(device)
+    if key not in _CUS:
+        _CUS[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    return _CUS[key]
+
+
+def qkv_attention_splits(x: torch.Tensor, w, k_cache: torch.Tensor, seq_len: int, n_heads: int, n_kv_heads: int,
+                         key_mask: Optional[torch.Tensor] = None) -> int:
+    """Attention workgroups per (row, kv head) pair of the fused qkv + attention launch for this decode step, or 0
+    when it does not apply (prefill, a key mask, M > 32, a cache longer than 512, or a grid the CUs cannot hold at
+    once)."""
+    if not QKV_ATTN or seq_len != 1 or key_mask is not None or not _is_gpu(x) or x.dtype != BF16:
+        return 0
+    m = x.shape[0]
+    if QKV_ATTN == 1 and (m > 4 or n_heads < 8 * n_kv_heads):
+        return 0
+    return int(ext().qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n,
+                                     _num_cus(x.device)))
+
+
+def linear_qkv_attention(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.Tensor, positions: torch.Tensor,
+                         k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor, n_heads: int,
+                         n_kv_heads: int, head_dim: int, splits: int, x_packed: Optional[torch.Tensor] = None,
+                         out_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One decode token per row: ``linear_qkv_rope`` + ``attention`` in one launch (``qkv_attention_splits`` > 0).
+    Returns the attention output ``[B, H * Dh]`` bf16 (``out_packed``: its packed copy for the o projection)."""
+    e = ext()
+    m = x.shape[0]
+    dev = x.device
+    rep = n_heads // n_kv_heads
+    q = workspace.get("qa_q", m * n_heads * head_dim, BF16, dev).view(m, n_heads, head_dim)
+    out = torch.empty(m, n_heads * head_dim, dtype=BF16, device=dev)
+    ws = workspace.get("qa_ws", m * n_kv_heads * splits * rep * (head_dim + 4), torch.float32, dev)
+    tickets = workspace.get_zeroed("qa_tickets", max(m * n_kv_heads, 64), torch.int32, dev)
+    sync = workspace.get_zeroed("qa_sync", 4, torch.int32, dev)
+    e.linear_qkv_attn(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
+                      positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, dev), n_heads,
+                      n_kv_heads, head_dim, q, kv_start, out, out_packed, ws, tickets, sync, k_cache.shape[2], splits,
+                      x_packed)
+    return out
+
+
 def attention_packs(q: torch.Tensor, k_cache: torch.Tensor, key_mask: Optional[torch.Tensor] = None) -> bool:
     """Whether ``attention(..., out_packed=...)`` can write the packed copy for this decode shape (with a key mask
     only the small-batch kernels, v3 / v5, do: mid-batch rows then go to v2)."""

@@ -1068,3 +1068,59 @@ def test_attention_decode_mfma_v6(wpp, rep, t, slot, masked):
     if not masked:
         assert got[2].float().abs().max().item() == 0.0
     assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())
+
+
+@pytest.mark.parametrize("b,hkv,rep", [(1, 1, 8), (2, 8, 4), (4, 2, 1), (1, 2, 16), (3, 1, 8), (24, 1, 8), (32, 1, 8)])
+@pytest.mark.parametrize("t,slot", [(40, 17), (200, 199), (384, 300), (512, 130)])
+def test_qkv_attention_fused_launch(b, hkv, rep, t, slot):
+    """The fused small-batch decode launch (gemv.hip qkv_attn_kernel: qkv GEMV + RoPE + KV write on one set of
+    workgroups, the attention on another that prefetches its K / V step and waits for the write-through publish)
+    against the fp32 reference of linear_qkv_rope + attention: left padding inside a split, a row with no valid key,
+    the new key at the end of a 32-key step or of a 128-key split; the cache rows it wrote equal the unfused kernel's,
+    the packed output equals the row-major one, and a second launch agrees (the counters reset themselves)."""
+    e = ops.ext()
+    dh, k = 128, 1024
+    h = hkv * rep
+    n = (h + 2 * hkv) * dh
+    torch.manual_seed(b * 100 + t + rep)
+    x = torch.randn(b, k).to(BF16)
+    w = (torch.randn(n, k) * 0.03).to(BF16)
+    table = ref.rope_table(dh, 1024, 500000.0)
+    pos = torch.full((b,), slot, dtype=torch.int32)
+    kc0, vc0 = _cache(b, hkv, t, dh)
+    kv_start = (torch.tensor([0, 37, slot + 1] + [5 * i % 60 for i in range(b - 3)][:max(0, b - 3)], dtype=torch.int32)[:b]
+                if b > 1 else torch.tensor([3], dtype=torch.int32))
+    kcr, vcr = kc0.clone(), vc0.clone()
+    q = ref.linear_qkv_rope(x.float(), w, 1e-5, table, pos, kcr, vcr, slot, 1, h, hkv, dh)
+    expect = ref.attention(q.reshape(b, 1, h, dh), kcr, vcr, slot, kv_start).reshape(b, h * dh)
+    from jax_llama_amd.models.weights import PackedLinear
+    pw = PackedLinear.from_dense(w, DEV)
+    kd, vd = kc0.to(DEV), vc0.to(DEV)
+    xd = x.to(DEV)
+    sl = torch.tensor([slot], dtype=torch.int32, device=DEV)
+    splits = e.qkv_attn_splits(b, b, hkv, rep, t, n, ops._num_cus(xd.device))
+    assert splits == (t + 127) // 128, (splits, e.qkv_attn_occupancy(b, rep))
+    packed = ops.packed_empty(b, h * dh, DEV)
+    got = ops.linear_qkv_attention(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), kd, vd, sl, kv_start.to(DEV), h, hkv, dh,
+                                   splits, out_packed=packed)
+    again = ops.linear_qkv_attention(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), kd, vd, sl, kv_start.to(DEV), h, hkv,
+                                     dh, splits)
+    torch.cuda.synchronize()
+    _close(got, expect, 2e-2, 2e-2)
+    assert torch.equal(got, again)
+    assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())
+    if b > 2:
+        assert got[2].float().abs().max().item() == 0.0  # kv_start = slot + 1: no valid key
+    # the cache rows: as the unfused qkv GEMV of the same geometry (variant 1: one tile x 4 waves) writes them
+    ku, vu = kc0.to(DEV), vc0.to(DEV)
+    try:
+        ops.GEMV_VARIANT = 1
+        ops.linear_qkv_rope(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), ku, vu, sl, 1, h, hkv, dh)
+        torch.cuda.synchronize()
+    finally:
+        ops.GEMV_VARIANT = 0
+    if b <= 16:
+        assert torch.equal(ku.cpu(), kd.cpu()) and torch.equal(vu.cpu(), vd.cpu())
+    else:  # (M > 16: the unfused GEMV cuts K over 8 waves, the fused launch over 4 -- another summation order)
+        _close(kd, ku, 1e-2, 1e-2)
+        _close(vd, vu, 1e-2, 1e-2)

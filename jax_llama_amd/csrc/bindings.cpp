@@ -848,6 +848,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
     return jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k) != 0;
   });
   m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
+  m.def("gemm_set_g4_group", [](int64_t gm) { jla::gemm_set_g4_group((int)gm); });
   m.def("gemm4_sk_workspace", [](int64_t m, int64_t n) {
     return py::make_tuple((int64_t)jla::gemm4_sk_workspace_floats(), (int64_t)jla::gemm4_sk_tickets(m, n));
   });

@@ -1014,11 +1014,12 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
   }
 }
 
-template <int MODE, int RMSM, int NJ = 8>
+template <int MODE, int RMSM, int NJ = 8, int DIAG = 0>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv) {
+                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv,
+                 int group_m) {
   constexpr bool RMS = RMSM == 1;
   // the two K-tile slots; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
   __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];
@@ -1032,7 +1033,7 @@ __global__ void __launch_bounds__(256, 1)
   const int tiles = tiles_m * tiles_n;
   const int split = wgid / tiles, pid = wgid - split * tiles;
   int tm, tn;
-  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn);
+  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn, group_m);
   const int m0 = tm * G4_BM, n0 = tn * (32 * NJ);
   const int t0 = split * kc, KT = min(K >> 6, t0 + kc) - t0;
 
@@ -1047,7 +1048,7 @@ __global__ void __launch_bounds__(256, 1)
     static_assert(!RMS, "the 256 x 128 tile: precomputed statistic");
     g4n_mainloop<NJ>(g, lds, m0, n0, t0, KT, wu, lane, acc);
   } else {
-    g4_mainloop<RMS>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+    g4_mainloop<RMS, decltype(acc), DIAG>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
   }
   g4_epilogue<MODE, RMSM, decltype(acc), NJ>(
       acc, ss, lds, wu, lane, m0, n0, split,
@@ -1664,6 +1665,18 @@ static bool use_g4(int tile, int M, int K) {
   return (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
 }
 
+// Tile rasterisation: the launch order walks groups of gm m-tiles across every n-tile (g4_tile_coords), so the 32
+// workgroups an XCD runs at once cover gm m-tiles x 32 / gm n-tiles. gm = 4 (4 x 8 tiles per XCD) beat 8 (the
+// round-4 order), 1, 2 and 16 on every Llama-3-8B projection at M = 2048 and 32768: qkv -7 / -9 %, o -3 / -8 %,
+// gate_up -5 / 0 %, down -5 / -6 % (profiles/r5_gemm4_group_m.jsonl). gemm_set_g4_group pins another (tools).
+static int g_g4_group = 0;
+void gemm_set_g4_group(int gm) { g_g4_group = gm; }
+static int g4_group_m(int tiles_m, int tiles_n, int K) {
+  (void)tiles_n, (void)K;
+  const int gm = g_g4_group > 0 ? g_g4_group : 4;
+  return gm < tiles_m ? gm : tiles_m;
+}
+static int g_g5_diag = 0;  // tools only (gemm5ws.h diag bits 1-16; gemm4 store ablations 64 / 128: wrong results)
 template <int MODE, int NJ = 8>
 static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa,
@@ -1672,20 +1685,35 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   const int grid = tm * tn * ksplit;
+  const int gm = g4_group_m(tm, tn, K);
   if constexpr (NJ != 8) {  // 256 x 128 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
     if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
       if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
       gemm4_kernel<MODE, 2, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
-                                                            rms_eps, ssq, qa, rms_ws);
+                                                            rms_eps, ssq, qa, rms_ws, gm);
     } else if (!rms) {
       gemm4_kernel<MODE, 0, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
-                                                            rms_eps, ssq, qa, nullptr);
+                                                            rms_eps, ssq, qa, nullptr, gm);
     }
     return;
   }
+  if constexpr (MODE == MODE_STORE) {  // ablation instances (tools only; wrong results)
+    if (!rms && (g_g5_diag & 192)) {
+      if ((g_g5_diag & 192) == 64)
+        gemm4_kernel<MODE, 0, 8, 1><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                        rms_eps, ssq, qa, nullptr, gm);
+      else if ((g_g5_diag & 192) == 128)
+        gemm4_kernel<MODE, 0, 8, 2><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                        rms_eps, ssq, qa, nullptr, gm);
+      else
+        gemm4_kernel<MODE, 0, 8, 3><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                        rms_eps, ssq, qa, nullptr, gm);
+      return;
+    }
+  }
 #define JLA_G4(R, INV)                                                                                          \
   gemm4_kernel<MODE, R><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, \
-                                             ssq, qa, INV)
+                                             ssq, qa, INV, gm)
   if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
     if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;  // (K % 8 == 0 always holds here)
     JLA_G4(2, rms_ws);
@@ -1917,7 +1945,6 @@ static int launch_reduce(const float* ws, int ksplit, void* out, int M, int N, i
 
 // gemm5 (tile 11: 4 n-tiles per wave, 256-column workgroups; tile 12: 2 n-tiles, 128 columns): the weight-streaming
 // split-K main loop (gemm5ws.h), then the reduce kernel runs the epilogue (even without a K split)
-static int g_g5_diag = 0;  // tools only (gemm5ws.h diag bits: ablations with wrong results)
 void gemm5_set_diag(int d) { g_g5_diag = d; }
 int gemm5_ksplit(int K, int ksplit) {  // the effective split count over 64-deep K-stages
   const int KS64 = K >> 6;

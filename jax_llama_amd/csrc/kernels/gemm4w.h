@@ -31,11 +31,11 @@ constexpr int G4_A_U4 = G4_BM * G4_BK * 2 / 16;  // 2048 u32x4 = 32 KiB
 constexpr int G4_B_U4 = G4_BN * G4_BK * 2 / 16;  // 2048 u32x4 = 32 KiB
 constexpr int G4_SLOT_U4 = G4_A_U4 + G4_B_U4;    // 64 KiB
 
-// launch-order tile index -> (m tile, n tile), M-grouped by G4_GROUP_M so consecutive workgroups share W columns
-JLA_DEV void g4_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn) {
-  const int in_group = G4_GROUP_M * tiles_n;
-  const int first_m = (pid / in_group) * G4_GROUP_M;
-  const int gsz = min(tiles_m - first_m, G4_GROUP_M);
+// launch-order tile index -> (m tile, n tile), M-grouped by gm so consecutive workgroups share W columns
+JLA_DEV void g4_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn, int gm = G4_GROUP_M) {
+  const int in_group = gm * tiles_n;
+  const int first_m = (pid / in_group) * gm;
+  const int gsz = min(tiles_m - first_m, gm);
   tm = first_m + (pid % in_group) % gsz;
   tn = (pid % in_group) / gsz;
 }
@@ -69,7 +69,11 @@ struct G4Args {
 // RMS: also accumulate the row sums of squares of x (the fused RMSNorm statistic, reference model.py:42-48) from
 // the x fragments already in registers: wave (wr, wc) takes m-tiles 4wc..4wc+3 of its row block, ss[i] holds lane
 // (row lane & 15, k-chunk lane >> 4)'s partial of m-tile 4wc + i, k32 step after k32 step in K order.
-template <bool RMS = false, typename Acc>
+// DIAG (ablation builds for tools/bench_gemm.py --g5-diag 64 / 128, wrong results): 1 no MFMAs (the fragment reads
+// kept alive), 2 no LDS-DMA past the prologue (every K-tile re-reads the first two tiles' slots). (Moving the
+// sub-step's fragment reads or DMAs into its first 8 slots, two per slot, measured within noise or slower:
+// profiles/r5_gemm4_schedule_ab.jsonl.)
+template <bool RMS = false, typename Acc, int DIAG = 0>
 JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc,
                          float* ss = nullptr) {
   const int wr = wu >> 1, wc = wu & 1;
@@ -123,10 +127,13 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int e = 4 * q + u, j = e >> 3, i = e & 7;
-        g4_mfma(acc[j][i], wf[j], xf[i]);
+        if constexpr (DIAG & 1)
+          asm volatile("" ::"v"(wf[j]), "v"(xf[i]));
+        else
+          g4_mfma(acc[j][i], wf[j], xf[i]);
       }
       if (do_rd) rd(q < 8 ? wn[q] : xn[q - 8], rslot, rh, q);
-      if (do_dma) dma(td, q);
+      if (!(DIAG & 2) && do_dma) dma(td, q);
       if constexpr (RMS) {
         if (q < 4) {  // m-tile 4wc + q: the runtime wc selects between two named fragments (no indexed array)
           const u32x4 f = wc ? xf[4 + q] : xf[q];

@@ -64,6 +64,7 @@ int gemm_ksplit(int M, int N, int K);
 int gemm_qkv_direct_ok(int M, int tile, int K);  // qkv without a K split: the direct RoPE / KV-write GEMM epilogue applies
 // gemm4 (the 4-wave 256 x 256 kernel, tile config 7) as the tile-0 default for M > 128, K % 64 == 0 (on by default)
 void gemm_set_g4_default(int on);
+void gemm_set_g4_group(int gm);
 int gemm5_ksplit(int K, int ksplit);
 int clock_probe(int iters, int grid, unsigned long long* out, hipStream_t s);  // [cycles, 100 MHz ticks]
 void gemm5_set_diag(int d);  // tools only: gemm5 ablations (wrong results)  // gemm5 (tiles 11 / 12): the effective split over 64-deep K-stages

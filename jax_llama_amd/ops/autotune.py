@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 8  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12), so older persisted picks are re-measured
+TUNE_VERSION = 9  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:

@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--rms", action="store_true", help="fused RMSNorm statistic (store / swiglu)")
     ap.add_argument("--g5-diag", type=int, nargs="+", default=[0], help="gemm5 ablation bits (wrong results): 1 no "
                     "MFMAs, 2 weights from a cached zero fragment, 4 x from a cached stage")
+    ap.add_argument("--group", type=int, nargs="+", default=[0], help="gemm4 tile rasterisation: m-tiles per launch "
+                    "group (gemm_set_g4_group; 0 = by shape)")
     ap.add_argument("--tp", type=int, default=1, help="per-rank shapes of that TP degree (qkv / gate_up column-parallel, "
                     "o / down row-parallel, lm_head vocab-parallel; parallel/partition.py)")
     ap.add_argument("--data", default="normal", choices=["normal", "uniform"],
@@ -97,8 +99,9 @@ def main():
             first = {}
             for rnd, impl in [(r, i) for r in range(args.rounds) for i in args.impl]:
                 for ks in args.ksplit:
-                 for diag in args.g5_diag:
+                 for diag, grp in [(d, g) for d in args.g5_diag for g in args.group]:
                   e.gemm5_set_diag(diag)
+                  e.gemm_set_g4_group(grp)
                   for tile in args.tile:
                     kk = ks or e.gemm_ksplit(m, n, k)
                     if tile == 10 and kk > 1 and eps > 0:
@@ -141,10 +144,10 @@ def main():
                       def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
                           e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
                                  ws if (kk > 1 or tile in (4, 6, 8, 11, 12)) else None, eps, tile, tk, None, rws)
-                      res[f"v{impl}_ks{kk}_t{tile}" + (f"_diag{diag}" if diag else "")  + ("_fix" if fx and kk > 1 else "") +
+                      res[f"v{impl}_ks{kk}_t{tile}" + (f"_diag{diag}" if diag else "") + (f"_g{grp}" if grp else "")  + ("_fix" if fx and kk > 1 else "") +
                           (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                       run(0)
-                      if mode != 0 or diag:  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
+                      if mode != 0 or (diag & 255):  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
                           continue
                       got = out.float()
                       if ref is None:
@@ -158,6 +161,7 @@ def main():
                           f0 = first.setdefault((kk, tile), got.clone())
                           assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
             e.gemm5_set_diag(0)
+            e.gemm_set_g4_group(0)
             if not args.no_blas and mode == 0:
                 res["hipblaslt"] = timeit(lambda i: torch.mm(x, dense[i % copies].t(), out=out), iters)
             for impl, us in res.items():

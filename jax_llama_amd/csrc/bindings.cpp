@@ -334,41 +334,25 @@ void check_g5_ws(const c10::optional<Tensor>& ws, int64_t k, int64_t ksplit, int
   check(ws->scalar_type() == torch::kFloat32 && ws->numel() >= eks * m * (n + (rms ? 1 : 0)), "gemm ws too small");
 }
 
-// stream-K tail (tile 4) workspace: slabs (float) + self-resetting tickets (int32, zeroed once)
+// workspace + self-resetting counters of an in-launch hand-off plan (tile 8)
 struct SkWs {
   float* ws = nullptr;
   size_t ws_floats = 0;
   int32_t* tk = nullptr;
   int n_tk = 0;
 };
-SkWs check_sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& tickets, int64_t m, int64_t n,
-                 int64_t k) {
+// gemm4 exchange split-K (tile 8) workspace: partial wave blocks + self-resetting counters (+ the error word)
+SkWs check_g4xk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& tickets, int64_t m, int64_t n,
+                   int64_t ks) {
   SkWs r;
-  if (!jla::gemm_sk_active(m, n, k)) return r;
-  check(ws.has_value() && tickets.has_value(), "gemm tile 4: stream-K needs ws and tickets");
-  check_gpu(*ws, "gemm sk ws");
-  check_gpu(*tickets, "gemm sk tickets");
-  check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm_sk_workspace_floats(),
-        "gemm sk ws too small");
-  check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm_sk_tickets(m, n, k),
-        "gemm sk tickets too small");
-  r.ws = ptr<float>(*ws);
-  r.ws_floats = ws->numel();
-  r.tk = ptr<int32_t>(*tickets);
-  r.n_tk = (int)tickets->numel();
-  return r;
-}
-
-// gemm4 stream-K (tile 8) workspace: slabs + self-resetting tickets
-SkWs check_g4sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& tickets, int64_t m, int64_t n) {
-  SkWs r;
-  check(ws.has_value() && tickets.has_value(), "gemm tile 8: gemm4 stream-K needs ws and tickets");
-  check_gpu(*ws, "gemm4 sk ws");
-  check_gpu(*tickets, "gemm4 sk tickets");
-  check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm4_sk_workspace_floats(),
-        "gemm4 sk ws too small (gemm4_sk_workspace)");
-  check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm4_sk_tickets(m, n),
-        "gemm4 sk tickets too small");
+  check(ws.has_value() && tickets.has_value(), "gemm tile 8: the exchange needs ws and tickets (gemm4_xk_workspace)");
+  check_gpu(*ws, "gemm4 xk ws");
+  check_gpu(*tickets, "gemm4 xk counts");
+  check(ws->scalar_type() == torch::kFloat32 &&
+            (size_t)ws->numel() >= jla::gemm4_xk_workspace_floats((int)m, (int)n, (int)ks),
+        "gemm4 xk ws too small (gemm4_xk_workspace)");
+  check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm4_xk_counts((int)m, (int)n),
+        "gemm4 xk counts too small");
   r.ws = ptr<float>(*ws);
   r.ws_floats = ws->numel();
   r.tk = ptr<int32_t>(*tickets);
@@ -377,7 +361,7 @@ SkWs check_g4sk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>&
 }
 
 // Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel;
-// tile 4 -> data-parallel whole waves + stream-K tail (ws/tickets from gemm_sk_workspace).
+// tile 8 -> gemm4 split-K with the in-launch exchange of partial blocks (ws/tickets from gemm4_xk_workspace).
 // rms_ws: optional fp32 scratch (>= M floats) for the row statistic of the fused norm on gemm4 plans without a K
 // split (computed ahead of the GEMM by rms_rowinv); absent: the statistic is summed inside the main loop.
 static float* rms_ws_ptr(const c10::optional<Tensor>& rws, int64_t m, size_t* floats) {
@@ -406,9 +390,7 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   if (pack_out.has_value()) {
     check(m <= SKINNY_MAX_M && (mode == 1 || mode == 2) && (mode != 1 || mir), "gemm pack_out: decode M, residual "
           "(with its mirror) or SwiGLU");
-    check((ksplit > 1 || tile == 11 || tile == 12) && tile != 4 && tile != 6 &&
-              !(tickets.has_value() && jla::gemm_fixup_enabled()),
-          "gemm pack_out: the split-K reduce-kernel path only");
+    check((ksplit > 1 || tile == 11 || tile == 12) && tile != 8, "gemm pack_out: the split-K reduce-kernel path only");
     pqa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
   }
   if (tile == 11 || tile == 12) {  // gemm5 (weight-streaming) partial slabs + the reduce kernel's epilogue, any split
@@ -419,54 +401,14 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
        "gemm");
     return;
   }
-  if (tile == 8) {
-    check(ksplit <= 1, "gemm tile 8: no K split");
+  if (tile == 8) {  // residual epilogue only: the splits exchange their partial blocks inside the launch
+    check(mode == 1 && rms_eps < 0, "gemm tile 8: residual epilogue, no fused norm");
     check(pqa.pack == nullptr, "gemm tile 8: no packed output copy");
-    const SkWs sk = check_g4sk_ws(ws, tickets, m, n);
-    size_t rfl = 0;
-    float* rws = rms_ws_ptr(rms_ws, m, &rfl);
-    check(rms_eps < 0 || rws != nullptr, "gemm tile 8 with the fused norm needs rms_ws");
-    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-                 out.scalar_type() == torch::kFloat32, mir, nullptr, sk.ws, sk.ws_floats, 1, stream(),
-                 (float)rms_eps, 8, sk.tk, sk.n_tk, rws, rfl),
-       "gemm");
-    return;
-  }
-  if (tile == 4) {
-    check(ksplit <= 1, "gemm tile 4: no K split");
-    const SkWs sk = check_sk_ws(ws, tickets, m, n, k);
-    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-                 out.scalar_type() == torch::kFloat32, mir, nullptr, sk.ws, sk.ws_floats, 1, stream(),
-                 (float)rms_eps, 4, sk.tk, sk.n_tk),
-       "gemm");
-    return;
-  }
-  if (tile == 6) {  // whole waves data-parallel + 2-way split tail with the in-kernel fixup
-    check(ksplit <= 1, "gemm tile 6: no K split of its own");
-    check(ws.has_value() && tickets.has_value(), "gemm tile 6 needs slabs and tickets");
-    check_gpu(*ws, "gemm ws");
-    check_gpu(*tickets, "gemm tickets");
-    check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm_hybrid_workspace_floats(m, n),
-          "gemm tile 6 slabs too small");
-    check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm_fix_tiles(m, n),
-          "gemm tile 6 tickets too small");
-    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-                 out.scalar_type() == torch::kFloat32, mir, nullptr, ptr<float>(*ws), ws->numel(), 1, stream(),
-                 (float)rms_eps, 6, ptr<int32_t>(*tickets), (int)tickets->numel()),
-       "gemm");
-    return;
-  }
-  if (ksplit > 1 && tickets.has_value() && jla::gemm_fixup_enabled()) {  // in-kernel split-K fixup
-    check(ws.has_value(), "gemm: split-K needs a workspace");
-    check_gpu(*ws, "gemm ws");
-    check_gpu(*tickets, "gemm tickets");
-    check(ws->scalar_type() == torch::kFloat32 && (size_t)ws->numel() >= jla::gemm_fix_workspace_floats(m, n, ksplit),
-          "gemm fixup slabs too small (gemm_fix_workspace)");
-    check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm_fix_tiles(m, n),
-          "gemm fixup tickets too small");
-    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
-                 out.scalar_type() == torch::kFloat32, mir, nullptr, ptr<float>(*ws), ws->numel(), ksplit, stream(),
-                 (float)rms_eps, (int)tile, ptr<int32_t>(*tickets), (int)tickets->numel()),
+    check(jla::gemm4_xk_ok((int)m, (int)n, (int)k, (int)ksplit), "gemm tile 8: needs K % 64 == 0, a split of 2+ "
+          "and tiles x split <= CUs (gemm4_xk_ok)");
+    const SkWs sk = check_g4xk_ws(ws, tickets, m, n, ksplit);
+    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate, true, mir, nullptr, sk.ws,
+                 sk.ws_floats, ksplit, stream(), -1.f, 8, sk.tk, sk.n_tk, nullptr, 0),
        "gemm");
     return;
   }
@@ -491,24 +433,8 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
   const int64_t m = x.size(0);
   jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
-  if (tile == 8) {  // gemm4 stream-K: the RoPE + cache-write epilogue runs in the GEMM itself
-    const SkWs sk = check_g4sk_ws(ws, tickets, m, n);
-    size_t rfl = 0;
-    float* rws = rms_ws_ptr(rms_ws, m, &rfl);
-    check(rms_eps < 0 || rws != nullptr, "gemm_qkv tile 8 with the fused norm needs rms_ws");
-    rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, sk.ws, sk.ws_floats, 1,
-                 stream(), (float)rms_eps, 8, sk.tk, sk.n_tk, rws, rfl),
-       "gemm_qkv");
-    return;
-  }
-  if (tile == 4) {  // stream-K: the RoPE + cache-write epilogue runs in the GEMM itself
-    const SkWs sk = check_sk_ws(ws, tickets, m, n, k);
-    check(sk.ws != nullptr, "gemm_qkv tile 4: this shape has no stream-K tail");
-    rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, sk.ws, sk.ws_floats, 1,
-                 stream(), (float)rms_eps, 4, sk.tk, sk.n_tk),
-       "gemm_qkv");
-    return;
-  }
+  check(tile != 8, "gemm_qkv: tile 8 (the exchange split) has the residual epilogue only");
+  (void)tickets;
   if (tile == 11 || tile == 12) {  // gemm5 partial slabs, RoPE / KV write in the reduce kernel
     check_g5_ws(ws, k, ksplit, m, n, rms_eps >= 0);
     rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(*ws), ws->numel(),
@@ -849,24 +775,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   });
   m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
   m.def("gemm_set_g4_group", [](int64_t gm) { jla::gemm_set_g4_group((int)gm); });
-  m.def("gemm4_sk_workspace", [](int64_t m, int64_t n) {
-    return py::make_tuple((int64_t)jla::gemm4_sk_workspace_floats(), (int64_t)jla::gemm4_sk_tickets(m, n));
+  m.def("gemm4_xk_ok", [](int64_t m, int64_t n, int64_t k, int64_t ks) {
+    return jla::gemm4_xk_ok((int)m, (int)n, (int)k, (int)ks) != 0;
   });
-  m.def("gemm_fix_workspace", [](int64_t m, int64_t n, int64_t ksplit) {
-    return py::make_tuple((int64_t)jla::gemm_fix_workspace_floats(m, n, ksplit), (int64_t)jla::gemm_fix_tiles(m, n));
-  }, "(slab floats, tickets) of the in-kernel split-K fixup");
-  m.def("gemm_set_fixup", [](bool on) { jla::gemm_set_fixup(on ? 1 : 0); });
-  m.def("gemm_hybrid_workspace", [](int64_t m, int64_t n) {
-    return py::make_tuple((int64_t)jla::gemm_hybrid_workspace_floats(m, n), (int64_t)jla::gemm_fix_tiles(m, n));
-  }, "(slab floats of the split tail, tickets) of tile config 6; 0 floats: no partial wave");
-  m.def("gemm_fixup_enabled", []() { return jla::gemm_fixup_enabled() != 0; });
-  m.def("gemm_sk_workspace", [](int64_t m, int64_t n, int64_t k) {
-    // (slab floats, tickets) of the stream-K tail of this shape; (0, 0) when it has none
-    if (!jla::gemm_sk_active(m, n, k)) return py::make_tuple((int64_t)0, (int64_t)0);
-    return py::make_tuple((int64_t)jla::gemm_sk_workspace_floats(), (int64_t)jla::gemm_sk_tickets(m, n, k));
+  m.def("gemm4_xk_workspace", [](int64_t m, int64_t n, int64_t ks) {
+    return py::make_tuple((int64_t)jla::gemm4_xk_workspace_floats((int)m, (int)n, (int)ks),
+                          (int64_t)jla::gemm4_xk_counts((int)m, (int)n));
   });
-  m.def("gemm_sk_set_cus", [](int64_t n) { jla::gemm_sk_set_cus((int)n); });
-  m.def("gemm_sk_qkv_ok", [](int64_t m, int64_t n, int64_t k) { return (bool)jla::gemm_sk_qkv_ok(m, n, k); });
   m.def("gemm_qkv", &gemm_qkv, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("table"),
         py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"), py::arg("h"),
         py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("ksplit"), py::arg("ws"), py::arg("rms_eps") = -1.0,

@@ -48,17 +48,6 @@ JLA_DEV u32x2 ad6_tr(const char* lds, int off) {
                                        (__attribute__((address_space(3))) s16x4_6*)(lds + off)));
 }
 
-// LDS-DMA with the agent-coherent (sc1) policy: rows another workgroup of the same launch wrote write-through
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-JLA_DEV void glds16_asm_sc1(const void* gsrc, void* lds_wave_base) {
-  const unsigned m0 = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(gsrc), "s"(m0)
-               : "memory", "m0");
-}
-#pragma clang diagnostic pop
-
 // per-wave online-softmax state of one pair: running max (log2 units), running sum, O^T accumulators (AGPRs)
 struct Ad6Acc {
   float m, l;

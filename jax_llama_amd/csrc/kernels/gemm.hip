@@ -20,6 +20,7 @@
 #include "gemm4w.h"
 #include "gemm5ws.h"
 #include "launchers.h"
+#include "ring.h"
 
 namespace jla {
 
@@ -68,30 +69,12 @@ JLA_DEV void g2_tile_coords(int pid, int tiles_m, int tiles_n, int& tm, int& tn)
 // gfx950 b128 lane groups. x pairs live in a 3-slot ring (96 KiB), weights in the usual 4-slot K-tile
 // ring (64 KiB); pair p is issued in two halves with K-tiles 2p-4 and 2p-3 (4 LDS-DMA per wave per
 // K-tile, as before), so the vmcnt accounting stays "everything issued two K-tiles back has landed".
-// In-kernel split-K fixup (FA pipeline, 256 x 256 tiles): with fix.ksplit > 1 every (tile, K split) workgroup
-// publishes its fp32 accumulators in fragment layout (and the fused-RMS row sums) to its own slab with
-// write-through (sc1) stores, drains them, and takes the tile's agent-scope ticket; the LAST arriver sums the
-// splits in split order (its own from registers) with sc1 loads and runs the mode's normal epilogue. No
-// reduce kernel, no [ksplit][M][N] round trip; deterministic (fixed order); tickets reset themselves
-// (cdna_hip_programming.md Guideline 16, sc1-store + agent ticket + sc1-load form, as the stream-K tail).
-struct G2Fix {
-  float* slabs;       // [tiles of this launch][ksplit][G2FIX_SLAB_FLOATS]
-  int32_t* tickets;   // [tiles], zero-initialised once
-  int ksplit;         // 1 = no fixup (plain tile, or the MODE_PARTIAL + reduce-kernel path)
-  int tile_base;      // tile_count > 0: this launch covers tiles [tile_base, tile_base + tile_count) of the
-  int tile_count;     //   launch order only (the split tail of tile config 6)
-  int pad;
-};
-constexpr int G2FIX_ACC_BYTES = 8 * 8 * 4 * 1024;           // 8 waves x 8 x 4 fragments x 1 KiB
-constexpr int G2FIX_SLAB_BYTES = G2FIX_ACC_BYTES + 256 * 4;  // + 256 row sums of squares
-constexpr int G2FIX_SLAB_FLOATS = G2FIX_SLAB_BYTES / 4;
-
 template <int MODE, int WM, int NBUF = G2_NBUF, bool LATE_WAIT = false, bool RMS = false, int MT = 8, int NTW = 4,
           int SUB = 1, bool FA = false, int FAM = 0>
 __global__ void __launch_bounds__(256 * WM)
     gemm2_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                 float rms_eps, float* __restrict__ ssq_ws, G2Fix fix, QKVArgs qa) {
+                 float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa) {
   // wave tile: MT m-tiles x NTW n-tiles of 16x16 (128 x 64 by default; 64 x 32 for the 128 x 128 tile)
   constexpr int NW = 4 * WM, BM = 16 * MT * WM, BN = 64 * NTW;
   constexpr int RPW = MT / 4;  // RMS: m-tiles whose row statistics each wave accumulates
@@ -113,9 +96,8 @@ __global__ void __launch_bounds__(256 * WM)
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tiles = tiles_m * tiles_n;
-  const int tcount = fix.tile_count > 0 ? fix.tile_count : tiles;  // tiles of this launch
-  const int split = wgid / tcount;
-  const int pid = wgid - split * tcount + (fix.tile_count > 0 ? fix.tile_base : 0);
+  const int split = wgid / tiles;
+  const int pid = wgid - split * tiles;
   int tm, tn;
   g2_tile_coords(pid, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -541,64 +523,6 @@ __global__ void __launch_bounds__(256 * WM)
     ss1 += __shfl_xor(ss1, 16, 64);
     ss1 += __shfl_xor(ss1, 32, 64);
   }
-  if constexpr (FA && MODE != MODE_PARTIAL && MODE != MODE_ARGMAX) {
-    if (fix.ksplit > 1) {
-      // ---- in-kernel split-K fixup (see G2Fix): publish, ticket, last arriver sums in split order
-      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          fix.slabs + (size_t)(pid - (fix.tile_count > 0 ? fix.tile_base : 0)) * fix.ksplit * G2FIX_SLAB_FLOATS, 0,
-          fix.ksplit * G2FIX_SLAB_BYTES, 0x00020000);
-      const int base = split * G2FIX_SLAB_BYTES;
-      const int r0 = (wr * MT + RPW * wc) * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
-                                                 base + ((w * MT + i) * NTW + j) * 1024 + lane * 16, 0, 16);
-      if (RMS && lane < 16) {
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss0), rsrc, base + G2FIX_ACC_BYTES + r0 * 4, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss1), rsrc, base + G2FIX_ACC_BYTES + (r0 + 16) * 4, 0, 16);
-      }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __syncthreads();  // every store of the workgroup drained; every wave is past its last LDS read
-      int* sh_last = reinterpret_cast<int*>(lds);
-      if (threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(fix.tickets + pid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == fix.ksplit - 1;
-        if (last) __hip_atomic_store(fix.tickets + pid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *sh_last = last;
-      }
-      __syncthreads();
-      const int last = *sh_last;
-      __syncthreads();  // the flag is read before the epilogue reuses LDS
-      if (!last) return;
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int off = ((w * MT + i) * NTW + j) * 1024 + lane * 16;
-          f32x4 tsum = f32x4{0.f, 0.f, 0.f, 0.f};
-          for (int q = 0; q < fix.ksplit; ++q)
-            tsum += q == split ? acc[i][j]
-                               : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                               rsrc, q * G2FIX_SLAB_BYTES + off, 0, 16));
-          acc[i][j] = tsum;
-        }
-      if constexpr (RMS) {
-        float t0 = 0.f, t1 = 0.f;
-        for (int q = 0; q < fix.ksplit; ++q) {
-          t0 += q == split ? ss0
-                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                 rsrc, q * G2FIX_SLAB_BYTES + G2FIX_ACC_BYTES + r0 * 4, 0, 16));
-          t1 += q == split ? ss1
-                           : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                 rsrc, q * G2FIX_SLAB_BYTES + G2FIX_ACC_BYTES + (r0 + 16) * 4, 0, 16));
-        }
-        ss0 = t0;
-        ss1 = t1;
-      }
-    }
-  }
   if constexpr (RMS) {
     const int rA = m0 + (wr * MT + RPW * wc) * 16 + (lane & 15), rB = rA + 16;
     if constexpr (MODE == MODE_PARTIAL) {
@@ -613,7 +537,7 @@ __global__ void __launch_bounds__(256 * WM)
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __syncthreads();
       if (lane < 16) {
-        // (t / K exactly as gemm_reduce_kernel: split and unsplit plans and the in-kernel fixup agree bit for bit)
+        // (t / K exactly as gemm_reduce_kernel: split and unsplit plans agree bit for bit)
         const float fk = (float)K;
         rs[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 / fk + rms_eps);
         if constexpr (RPW == 2) rs[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 / fk + rms_eps);
@@ -1056,430 +980,131 @@ __global__ void __launch_bounds__(256, 1)
 }
 
 // ---------------------------------------------------------------------------------------------
-// gemm4 stream-K (tile config 8): one persistent workgroup per CU walks an equal share of ALL the launch's
-// (tile, 64-deep K-tile) iterations -- no partial last wave of tiles (Llama-3-8B at M = 2048: gate_up has 896 256 x 256
-// tiles = 3.5 waves, qkv 192 < 256 CUs). A segment that covers a whole tile runs the epilogue directly; a partial one
-// publishes its fp32 accumulators with write-through (sc1) stores into its own slab slot (slot 0: the segment that
-// opens the workgroup's range, slot 1: the one that closes it), takes the tile's agent-scope ticket, and the LAST
-// arriver sums every contributor in K order (deterministic) and runs the epilogue (cdna_hip_programming.md
-// Guideline 16: sc1 stores + vmcnt(0) + agent ticket + sc1 loads; tickets reset themselves). Nobody waits for
-// anybody. The fused norm needs the precomputed statistic (RMSM 2).
-JLA_DEV int g2sk_owner(long long it, long long iters, int P) {  // workgroup whose range holds iteration it
-  return (int)(((it + 1) * P - 1) / iters);
-}
-JLA_DEV long long g2sk_lo(int w, long long iters, int P) { return iters * w / P; }
-
-struct G4Sk {
-  long long iters;   // tiles * (K / 64)
-  float* slabs;      // [P][2][G4SK_SLAB_FLOATS]
-  int slab_bytes;    // buffer-descriptor range
-  int32_t* tickets;  // [tiles], zero-initialised once
+// gemm4 split-K with an in-kernel exchange (tile config 8): for outputs with too few 256 x 256 tiles to fill the chip
+// (Llama-3-8B at M = 2048: o / down have 128 tiles for 256 CUs) the K range is cut over ks co-resident workgroups per
+// tile, and instead of fp32 slabs + a reduce launch the splits hand their partial wave blocks to each other: wave
+// block b (128 x 128 of the tile, 64 KiB of fp32) is OWNED by split b * ks / 4; every other split's wave b publishes
+// its accumulators with write-through (sc1) stores, drains them (vmcnt(0)) and bumps the block's agent-scope counter,
+// then exits; the owner wave polls the counter (bounded: a missing partner sets the error word instead of hanging),
+// loads the ks - 1 partial blocks with sc1 loads, sums all ks in split order (deterministic, the reduce kernel's
+// order) and runs the ordinary epilogue on its block, then resets the counter (cdna_hip_programming.md Guideline 16).
+// No second launch, no full-size slab re-read, and the residual's read-modify-write is spread over the owners.
+// Needs grid = tiles * ks <= CUs (one 128 KiB-LDS workgroup per CU, all resident at once); the launcher checks it.
+// Epilogues without a workgroup barrier only (residual, fp32 / bf16-direct store): the non-owner waves exit early.
+struct G4Xk {
+  float* ws;         // [tiles][4 blocks][ks][64 KiB]: the partial wave blocks
+  int32_t* counts;   // [tiles * 4] arrivals per block (self-resetting), [tiles * 4]: the error word
+  int ks;
 };
-constexpr int G4SK_SLAB_BYTES = 4 * 64 * 1024;  // 4 waves x 64 accumulator tiles x 1 KiB
-constexpr int G4SK_SLAB_FLOATS = G4SK_SLAB_BYTES / 4;
 
-template <int MODE, int RMSM>
+template <int MODE, int KS>
 __global__ void __launch_bounds__(256, 1)
-    gemm4_sk_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                    int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int tiles_m, int tiles_n,
-                    float rms_eps, G4Sk sk, QKVArgs qa, const float* __restrict__ rms_inv) {
-  static_assert(RMSM != 1, "stream-K: the fused norm's statistic is precomputed");
-  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64 + 1];  // K-tile slots / staging, row scales, last-arriver flag
-  int* const sh_last = reinterpret_cast<int*>(lds + 2 * G4_SLOT_U4 + 64);
-  const int lane0 = threadIdx.x & 63;
+    gemm4_xk_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                    int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
+                    int group_m, G4Xk xk) {
+  static_assert(MODE == MODE_RESIDUAL, "exchange epilogues: residual");
+  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];
+  const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int KT64 = K >> 6;
-  const int P = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = P >> 3, r8 = P & 7;
-  // XCD-aware: the workgroups of one XCD get consecutive iteration ranges (neighbouring tiles share L2)
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const long long lo = g2sk_lo(wg, sk.iters, P), hi = g2sk_lo(wg + 1, sk.iters, P);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(sk.slabs, 0, sk.slab_bytes, 0x00020000);
-  const G4Args g{x, W, out, M, N, K, KT64, tiles_m, tiles_n};
-  const G4Epi ep{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, nullptr, rms_inv};
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int split = wgid / tiles, pid = wgid - split * tiles;
+  int tm, tn;
+  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn, group_m);
+  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+  const int t0 = split * kc, KT = max(0, min(K >> 6, t0 + kc) - t0);
 
-  for (long long it = lo; it < hi;) {
-    const int t = (int)(it / KT64);
-    const int kb = (int)(it - (long long)t * KT64);
-    const int ke = (int)min((long long)KT64, (long long)kb + (hi - it));
-    const int slot = it == lo ? 0 : 1;
-    it += ke - kb;
-    int tm, tn;
-    g4_tile_coords(t, tiles_m, tiles_n, tm, tn);
-    const int m0 = tm * G4_BM, n0 = tn * G4_BN;
-    // the lane index laundered through an opaque move once per segment: the lane-dependent address math of the
-    // main loop and the unrolled epilogue would otherwise be hoisted out of the segment loop and kept live (spills)
-    int lane;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
-    __syncthreads();  // the previous segment's epilogue / slab reads are done with LDS
-    f32x4 acc[8][8];
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
+  g4_mainloop<false>(g, lds, m0, n0, t0, KT, wu, lane, acc);
+
+  if constexpr (KS == 2) __syncthreads();  // every wave is past its last LDS read: the slots take the partner blocks
+  const int owner = (wu * KS) >> 2;
+  const size_t blk = (size_t)pid * 4 + wu;
+  // this block's KS partial slots (64 KiB each); every access write-through / coherent (sc1)
+  u32x4* const slots = reinterpret_cast<u32x4*>(xk.ws + blk * (size_t)KS * 16384);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slots, 0, KS * 65536, 0x00020000);
+  int32_t* const cnt = xk.counts + blk;
+  if (split != owner) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    g4_mainloop<false>(g, lds, m0, n0, kb, ke - kb, wu, lane, acc);
-
-    if (!(kb == 0 && ke == KT64)) {
-      // ---- partial segment: publish (sc1), ticket, the last arriver sums all contributors in K order
-      const int base = (wg * 2 + slot) * G4SK_SLAB_BYTES;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, g4_take(acc[j][i])), rsrc,
-                                                 base + ((wu * 8 + j) * 8 + i) * 1024 + lane * 16, 0, 16);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const long long t_lo = (long long)t * KT64, t_hi = t_lo + KT64;
-      const int w_first = g2sk_owner(t_lo, sk.iters, P), w_last = g2sk_owner(t_hi - 1, sk.iters, P);
-      if (threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(sk.tickets + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == w_last - w_first;
-        if (last) __hip_atomic_store(sk.tickets + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *sh_last = last;
-      }
-      __syncthreads();
-      const int last = *sh_last;
-      if (!last) continue;
-      const int me = wg - w_first;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int off = ((wu * 8 + j) * 8 + i) * 1024 + lane * 16;
-          f32x4 tsum = f32x4{0.f, 0.f, 0.f, 0.f};
-          const f32x4 mine = g4_take(acc[j][i]);
-          for (int cw = w_first; cw <= w_last; ++cw) {
-            const int cb = (cw * 2 + (g2sk_lo(cw, sk.iters, P) >= t_lo ? 0 : 1)) * G4SK_SLAB_BYTES;
-            tsum += cw - w_first == me ? mine
-                                       : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, cb + off, 0, 16));
-          }
-          acc[j][i] = tsum;
-        }
-    }
-    g4_epilogue<MODE, RMSM>(acc, nullptr, lds, wu, lane, m0, n0, 0, ep, qa);
+      for (int i = 0; i < 8; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, g4_take(acc[j][i])), rsrc,
+                                               split * 65536 + (j * 8 + i) * 1024 + lane * 16, 0, 16);  // (16: sc1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
   }
-}
-
-// Stream-K tail of the 256 x 256 ping-pong GEMM (tile config 4). Decode-sized outputs rarely have a
-// multiple of 256 tiles (Llama-3-8B at M = 2048: qkv 192, o/down 128, gate_up 896 tiles), so the
-// last wave of whole tiles leaves CUs idle, and split-K pays a second kernel that re-reads fp32
-// slabs. Here the whole waves run as the ordinary data-parallel launch (gemm2_kernel, tiles
-// [0, dp_tiles)) and the remaining tiles' K-iterations (32-deep K-tiles) are dealt out evenly to one
-// persistent workgroup per CU: workgroup w owns iterations [I*w/P, I*(w+1)/P) of the tail, walking
-// (tile, K-range) segments in tile order. A segment covering a whole tile runs the epilogue directly.
-// A partial segment publishes its fp32 accumulators (and fused-RMS row sums) with write-through
-// (sc1) stores into the workgroup's own slab slot (slot 0: the segment at the start of its range,
-// slot 1: at the end), takes the tile's agent-scope ticket, and the LAST arriver -- whichever that
-// is -- sums every contributor's partial in contributor (= K) order, so results are deterministic,
-// and runs the fused epilogue (store / residual + bf16 mirror / SwiGLU / RoPE + KV-cache write).
-// Nobody waits on anybody (no co-residency assumption); tickets reset themselves
-// (cdna_hip_programming.md Guideline 16, sc1-store + agent ticket + sc1-load form).
-struct G2Sk {
-  int dp_tiles;        // tiles [0, dp_tiles) of the launch order ran in the data-parallel launch
-  int pad;
-  long long iters;     // tail K-iterations = (tiles - dp_tiles) * (K / 32)
-  float* slabs;        // [P][2][G2SK_SLAB_FLOATS]
-  int slab_bytes;      // buffer-descriptor range
-  int32_t* tickets;    // [tiles - dp_tiles]: zero-initialised once, reset by each tile's last arriver
-};
-constexpr int G2SK_ACC_BYTES = 8 * 8 * 4 * 1024;                // 8 waves x 8 x 4 fragments x 1 KiB
-constexpr int G2SK_SLAB_BYTES = G2SK_ACC_BYTES + 256 * 4;       // + 256 row sums of squares
-constexpr int G2SK_SLAB_FLOATS = G2SK_SLAB_BYTES / 4;
-
-
-template <int MODE, bool RMS>
-__global__ void __launch_bounds__(512)
-    gemm2_sk_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                    int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int tiles_m, int tiles_n,
-                    float rms_eps, G2Sk sk, QKVArgs qa) {
-  constexpr int MT = 8, NTW = 4, NBUF = 4, DIST = 3, NW = 8, BM = 256, BN = 256;
-  constexpr int AF = 16, FR = 32, G = 4, RPW = 2;
-  // ONE __shared__ object (tile ring + row scales + last-arriver flag): with a second LDS object hipcc
-  // can no longer tell the LDS-DMA targets apart and drains vmcnt(0) before every ds_read of the ring
-  __shared__ u32x4 lds[NBUF * FR * 64 + BM / 4 + 1];
-  float* rs_sh = reinterpret_cast<float*>(lds + NBUF * FR * 64);  // fused-RMS row scales of the tile
-  int& sh_last = *reinterpret_cast<int*>(lds + NBUF * FR * 64 + BM / 4);
-  const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = w >> 2, wc = w & 3;
-  const int KS = K >> 5, NTT = N >> 4;
-  // XCD-aware (bijective) remap: the workgroups that share an XCD (blockIdx.x = xcd mod 8) get
-  // consecutive iteration ranges, i.e. neighbouring tiles of the M-grouped order, so their A rows and
-  // weight columns are reused in that XCD's L2 (without it the tail streamed ~2x the bytes from HBM)
-  const int P = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = P >> 3, r8 = P & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const long long lo = g2sk_lo(wg, sk.iters, P), hi = g2sk_lo(wg + 1, sk.iters, P);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(sk.slabs, 0, sk.slab_bytes, 0x00020000);
-
-  for (long long it = lo; it < hi;) {
-    const int t = (int)(it / KS);                 // tail tile
-    const int kb = (int)(it - (long long)t * KS);  // this segment's K-tiles [kb, ke)
-    const int ke = (int)min((long long)KS, (long long)kb + (hi - it));
-    const int slot = it == lo ? 0 : 1;
-    it += ke - kb;
-    int tm, tn;
-    g2_tile_coords(sk.dp_tiles + t, tiles_m, tiles_n, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int KT = ke - kb;
-    // lane index laundered through an opaque move once per segment: the lane-dependent address math
-    // of the unrolled epilogue would otherwise be hoisted out of the segment loop and held in
-    // registers across the main loop (spills)
-    int lane;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
-
-    __syncthreads();  // the previous segment's epilogue is done with LDS
-    const char* src[G];
-    int step[G];
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      const int f = w + NW * j;
-      if (f < AF) {
-        const int row = min(m0 + 16 * f + (lane & 15), M - 1);
-        src[j] = reinterpret_cast<const char*>(x + (size_t)row * K + (size_t)kb * 32 + 8 * (lane >> 4));
-        step[j] = 64;
-      } else {
-        const int nt = min((n0 >> 4) + (f - AF), NTT - 1);
-        src[j] = reinterpret_cast<const char*>(W + ((size_t)nt * KS + kb) * 64 + lane);
-        step[j] = 1024;
+  // owner: every partner's block has landed (bounded wait), then the sum in split order
+  {
+    const unsigned long long t_start = wall_clock64();
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < KS - 1) {
+      if (wall_clock64() - t_start > 20000000ull) {  // 200 ms at 100 MHz: a partner never ran
+        if (lane == 0) __hip_atomic_store(xk.counts + (size_t)tiles * 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
       }
-    }
-    auto issue = [&](int tt) {
-      u32x4* buf = lds + (tt % NBUF) * FR * 64;
-#pragma unroll
-      for (int j = 0; j < G; ++j) glds16(src[j] + (size_t)tt * step[j], buf + (w + NW * j) * 64);
-    };
-    f32x4 acc[MT][NTW];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float ss0 = 0.f, ss1 = 0.f;
-#pragma unroll
-    for (int tt = 0; tt < DIST; ++tt)
-      if (tt < KT) issue(tt);
-
-    // ---- the gemm2 ping-pong main loop (see gemm2_kernel for the barrier / vmcnt accounting)
-    wait_vmcnt<0>();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    for (int tt = 0; tt < KT; ++tt) {
-      if (tt + DIST < KT) issue(tt + DIST);
-      const int after = min(KT - 1, tt + DIST) - (tt + 1);
-      const u32x4* buf = lds + (tt % NBUF) * FR * 64;
-      u32x4 a[MT], b[NTW];
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) b[j] = buf[(AF + wc * NTW + j) * 64 + lane];
-#pragma unroll
-      for (int i = 0; i < MT; ++i) a[i] = buf[(wr * MT + i) * 64 + lane];
-      if constexpr (RMS) {
-        const u32x4 f0 = buf[(wr * MT + RPW * wc) * 64 + lane];
-        ss0 = dot8_bf16(f0, f0, ss0);
-        const u32x4 f1 = buf[(wr * MT + RPW * wc + 1) * 64 + lane];
-        ss1 = dot8_bf16(f1, f1, ss1);
-      }
-      if (after >= 3)
-        wait_vmcnt<3 * G>();
-      else if (after == 2)
-        wait_vmcnt<2 * G>();
-      else if (after == 1)
-        wait_vmcnt<G>();
-      else
-        wait_vmcnt<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[i][j] = mfma16x16x32(a[i], b[j], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    if (wr == 0) __builtin_amdgcn_s_barrier();
-    if constexpr (RMS) {  // row sums of this segment's K range (rows (wr*MT + RPW*wc [+1])*16 + lane&15)
-      ss0 += __shfl_xor(ss0, 16, 64);
-      ss0 += __shfl_xor(ss0, 32, 64);
-      ss1 += __shfl_xor(ss1, 16, 64);
-      ss1 += __shfl_xor(ss1, 32, 64);
-    }
-
-    if (!(kb == 0 && ke == KS)) {
-      // ---- partial segment: publish (sc1), ticket, last arriver sums all contributors in K order
-      const int base = (wg * 2 + slot) * G2SK_SLAB_BYTES;
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
-                                                 base + ((w * MT + i) * NTW + j) * 1024 + lane * 16, 0, 16);
-      if (RMS && lane < 16) {
-        const int r0 = (wr * MT + RPW * wc) * 16 + lane;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss0), rsrc, base + G2SK_ACC_BYTES + r0 * 4, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ss1), rsrc, base + G2SK_ACC_BYTES + (r0 + 16) * 4, 0, 16);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const long long t_lo = (long long)t * KS, t_hi = t_lo + KS;
-      const int w_first = g2sk_owner(t_lo, sk.iters, P), w_last = g2sk_owner(t_hi - 1, sk.iters, P);
-      if (threadIdx.x == 0) {
-        const int prev = __hip_atomic_fetch_add(sk.tickets + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == w_last - w_first;
-        if (last) __hip_atomic_store(sk.tickets + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sh_last = last;
-      }
-      __syncthreads();
-      if (!sh_last) continue;
-      // sum the contributors' partials in contributor (= K) order, whoever arrived last: fragment by
-      // fragment, the ones before this workgroup (re-read), then its own (registers), then the rest
-      const int n_c = w_last - w_first + 1, me = wg - w_first;
-      int cb[4];  // slab byte offsets of the contributors (a tail tile never has more than 4: plan)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int cw = min(w_first + q, w_last);
-        cb[q] = (cw * 2 + (g2sk_lo(cw, sk.iters, P) >= t_lo ? 0 : 1)) * G2SK_SLAB_BYTES;
-      }
-#pragma unroll
-      for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int off = ((w * MT + i) * NTW + j) * 1024 + lane * 16;
-          f32x4 tsum = f32x4{0.f, 0.f, 0.f, 0.f};
-          for (int q = 0; q < n_c; ++q)
-            tsum += q == me ? acc[i][j]
-                            : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, cb[q] + off, 0, 16));
-          acc[i][j] = tsum;
-        }
-      if constexpr (RMS) {
-        const int r0 = (wr * MT + RPW * wc) * 16 + (lane & 15);
-        float t0 = 0.f, t1 = 0.f;
-        for (int q = 0; q < n_c; ++q) {
-          t0 += q == me ? ss0 : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, cb[q] + G2SK_ACC_BYTES + r0 * 4, 0, 16));
-          t1 += q == me ? ss1 : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, cb[q] + G2SK_ACC_BYTES + (r0 + 16) * 4, 0, 16));
-        }
-        ss0 = t0;
-        ss1 = t1;
-      }
-    }
-
-    // ---- epilogue of a finished tile, staged through LDS one wave row (128 x 256 fp32) at a time so
-    // every output row is written by one wave with 16-byte-per-lane coalesced stores (columns swizzled
-    // by row group: the 4 row groups of an accumulator write land on distinct banks)
-    float* ep = reinterpret_cast<float*>(lds);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave is past its last read of the tile buffers
-    if constexpr (RMS) {
-      if (lane < 16) {
-        const float fk = (float)K;
-        rs_sh[(wr * MT + RPW * wc) * 16 + lane] = 1.f / sqrtf(ss0 / fk + rms_eps);
-        rs_sh[(wr * MT + RPW * wc + 1) * 16 + lane] = 1.f / sqrtf(ss1 / fk + rms_eps);
-      }
-    }
-#pragma unroll 1
-    for (int half = 0; half < 2; ++half) {
-      if (wr == half) {
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-#pragma unroll
-          for (int j = 0; j < NTW; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int row = i * 16 + 4 * (lane >> 4) + r;
-              const int col = ((wc * NTW + j) * 16 + (lane & 15)) ^ (((row >> 2) & 3) << 4);
-              ep[row * BN + col] = acc[i][j][r];
-            }
-      }
-      __syncthreads();
-#pragma unroll 2
-      for (int q = 0; q < 16; ++q) {
-        const int e = threadIdx.x + 512 * q;
-        const int row = e >> 6, c4 = (e & 63) * 4;
-        const int grow = m0 + half * 128 + row, gcol = n0 + c4;
-        float4 v = *reinterpret_cast<const float4*>(ep + row * BN + (c4 ^ (((row >> 2) & 3) << 4)));
-        if (grow >= M || gcol >= N) continue;
-        if constexpr (RMS) {
-          const float sc = rs_sh[half * 128 + row];
-          v.x *= sc;
-          v.y *= sc;
-          v.z *= sc;
-          v.w *= sc;
-        }
-        const size_t idx = (size_t)grow * N + gcol;
-        if constexpr (MODE == MODE_SWIGLU) {
-          if (((gcol >> 4) & 1) == 0) {  // gate tile; its up tile is the next 16 columns
-            const int uc = c4 + 16;
-            float4 u = *reinterpret_cast<const float4*>(ep + row * BN + (uc ^ (((row >> 2) & 3) << 4)));
-            if constexpr (RMS) {
-              const float sc = rs_sh[half * 128 + row];
-              u.x *= sc;
-              u.y *= sc;
-              u.z *= sc;
-              u.w *= sc;
-            }
-            bf16_t* o = static_cast<bf16_t*>(out) + (size_t)grow * (N >> 1) + (gcol >> 5) * 16 + (gcol & 15);
-            *reinterpret_cast<uint2*>(o) = make_uint2(pack2bf(silu(v.x) * u.x, silu(v.y) * u.y),
-                                                      pack2bf(silu(v.z) * u.z, silu(v.w) * u.w));
-          }
-        } else if constexpr (MODE == MODE_QKV) {
-          float vv[4] = {v.x, v.y, v.z, v.w};
-          const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
-          const int b = grow / qa.S, sq = grow - b * qa.S;
-          if (head < qa.H + qa.Hkv) {
-            int pos = qa.positions[grow];
-            if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
-            pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
-#pragma unroll
-            for (int p2 = 0; p2 < 2; ++p2) {
-              const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d0 >> 1) + p2];
-              const float xr = vv[2 * p2], xi = vv[2 * p2 + 1];
-              vv[2 * p2] = xr * cs.x - xi * cs.y;
-              vv[2 * p2 + 1] = xr * cs.y + xi * cs.x;
-            }
-          }
-          const uint2 packed = make_uint2(pack2bf(vv[0], vv[1]), pack2bf(vv[2], vv[3]));
-          if (head < qa.H) {
-            *reinterpret_cast<uint2*>(qa.q + ((size_t)grow * qa.H + head) * qa.Dh + d0) = packed;
-          } else {
-            const int cslot = qa.slot[0] + sq;
-            if (cslot < qa.T) {
-              const bool is_k = head < qa.H + qa.Hkv;
-              const int kh = is_k ? head - qa.H : head - qa.H - qa.Hkv;
-              bf16_t* cache = is_k ? qa.kc : qa.vc;
-              *reinterpret_cast<uint2*>(cache + (((size_t)b * qa.Hkv + kh) * qa.T + cslot) * qa.Dh + d0) = packed;
-            } else {
-              JLA_FLAG(JLA_BOUNDS_KV_SLOT);
-            }
-          }
-        } else if constexpr (MODE == MODE_RESIDUAL) {
-          float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + idx);
-          float4 r4 = v;
-          if (accumulate) {
-            const float4 old = *o;
-            r4.x += old.x;
-            r4.y += old.y;
-            r4.z += old.z;
-            r4.w += old.w;
-          }
-          *o = r4;
-          if (mirror)
-            *reinterpret_cast<uint2*>(mirror + idx) = make_uint2(pack2bf(r4.x, r4.y), pack2bf(r4.z, r4.w));
-        } else {
-          if (out_f32)
-            *reinterpret_cast<float4*>(static_cast<float*>(out) + idx) = v;
-          else
-            *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + idx) =
-                make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
-        }
-      }
-      __syncthreads();  // the half-tile is consumed before the other wave row overwrites it
+      __builtin_amdgcn_s_sleep(2);
     }
   }
+  if constexpr (KS == 2) {
+    // the partner's whole 64 KiB block lands in this wave's half of the (idle) K-tile slots by LDS-DMA: 64 loads in
+    // flight, one wait, then the sum from LDS (p0 + p1: the reduce kernel's order either way round)
+    char* const wl = reinterpret_cast<char*>(lds) + (wu & 1) * 65536;
+    const u32x4* const src = slots + (split ^ 1) * 4096 + lane;
+#pragma unroll
+    for (int f = 0; f < 64; ++f) glds16_asm_sc1(src + f * 64, wl + f * 1024);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(wl + (j * 8 + i) * 1024 + lane * 16);
+        const f32x4 tsum = g4_take(acc[j][i]) + p;
+        asm volatile("" : "=a"(acc[j][i]) : "0"(tsum));
+      }
+  } else {
+  // UI accumulator tiles per batch: (KS - 1) * UI partial loads in flight, branch-free (the loads are hand-counted
+  // asm: no control flow may separate them from their wait) with static register indices. The sum starts at the
+  // owner's own split and walks the others cyclically -- a fixed order per block, so the result is reproducible
+  // (at KS = 2 it equals the reduce kernel's p0 + p1 bit for bit).
+  constexpr int UI = KS == 2 ? 8 : (KS <= 4 ? 4 : 2);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i0 = 0; i0 < 8; i0 += UI) {
+      u32x4 raw[UI][KS - 1];
+#pragma unroll
+      for (int u = 0; u < UI; ++u)
+#pragma unroll
+        for (int d = 1; d < KS; ++d) {
+          const int q = (split + d) & (KS - 1);
+          asm_load_sc1(raw[u][d - 1], slots + q * 4096 + (j * 8 + i0 + u) * 64 + lane);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < UI; ++u) {
+        f32x4 tsum = g4_take(acc[j][i0 + u]);
+#pragma unroll
+        for (int d = 0; d < KS - 1; ++d) {
+          pin(raw[u][d]);
+          tsum += __builtin_bit_cast(f32x4, raw[u][d]);
+        }
+        asm volatile("" : "=a"(acc[j][i0 + u]) : "0"(tsum));  // back into its AGPRs (a VGPR copy of all 64 spills)
+      }
+    }
+  }
+  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  g4_epilogue<MODE, 0>(acc, nullptr, lds, wu, lane, m0, n0, 0,
+                       G4Epi{out, M, N, K, accumulate, out_f32, mirror, tiles_n, -1.f, nullptr, nullptr}, QKVArgs{});
 }
+
 
 // Sum the split-K partials (fixed order) and apply the epilogue. One thread = 4 consecutive
 // columns of one row (two RoPE pairs; a 16-column tile never straddles a float4).
@@ -1618,24 +1243,6 @@ int gemm_ksplit(int M, int N, int K) {
 }
 
 static int num_cus();
-// Off by default: measured slower than partial slabs + the reduce kernel on MI355X (the sc1 write-through
-// publish + vmcnt(0) round trip + one workgroup re-reading 256 KiB per split costs more than the separate pass:
-// o / down / qkv / gate_up at M = 512 / 2048, profiles/r2_gemm_splitk_fixup_ab.jsonl); kept as an option.
-static bool g_gemm_fixup = false;
-void gemm_set_fixup(int on) { g_gemm_fixup = on != 0; }
-int gemm_fixup_enabled() { return g_gemm_fixup ? 1 : 0; }
-// slabs of the in-kernel split-K fixup: [tiles of 256 x 256][ksplit][acc + row sums]
-size_t gemm_fix_workspace_floats(int M, int N, int ksplit) {
-  const size_t tiles = (size_t)((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
-  return tiles * ksplit * G2FIX_SLAB_FLOATS;
-}
-int gemm_fix_tiles(int M, int N) { return ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN); }
-// tile config 6 (whole waves data-parallel + 2-way split tail): slab floats of the tail (0: no tail)
-size_t gemm_hybrid_workspace_floats(int M, int N) {
-  const int tiles = gemm_fix_tiles(M, N), P = num_cus();
-  return (size_t)(tiles - (tiles / P) * P) * 2 * G2FIX_SLAB_FLOATS;
-}
-
 size_t gemm_workspace_floats(int M, int N, int K) {
   const int ks = gemm_ksplit(M, N, K);
   return ks > 1 ? (size_t)ks * M * (N + 1) : 0;  // slabs + fused-RMS partial sums
@@ -1725,65 +1332,63 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
 #undef JLA_G4
 }
 
-// gemm4 stream-K (tile config 8): slabs + tickets of the plan
-constexpr int G4_SK_TILE = 8;
+// gemm4 split-K with the in-kernel exchange (tile config 8): partial wave blocks + self-resetting counters
+constexpr int G4_XK_TILE = 8;
 static int num_cus();
-size_t gemm4_sk_workspace_floats() { return (size_t)num_cus() * 2 * G4SK_SLAB_FLOATS; }
-int gemm4_sk_tickets(int M, int N) { return ((M + G4_BM - 1) / G4_BM) * ((N + G4_BN - 1) / G4_BN); }
+static int g4_xk_tiles(int M, int N) { return ((M + G4_BM - 1) / G4_BM) * ((N + G4_BN - 1) / G4_BN); }
+size_t gemm4_xk_workspace_floats(int M, int N, int ks) { return (size_t)g4_xk_tiles(M, N) * 4 * ks * 16384; }
+int gemm4_xk_counts(int M, int N) { return g4_xk_tiles(M, N) * 4 + 1; }
+// the plan applies: a real split, every workgroup resident at once (one per CU)
+int gemm4_xk_ok(int M, int N, int K, int ks) {
+  return (K & 63) == 0 && (ks == 2 || ks == 4 || ks == 8) && (K >> 6) >= ks && g4_xk_tiles(M, N) * ks <= num_cus();
+}
 
-template <int MODE>
-static int launch_g4_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                        bf16_t* mirror, float rms_eps, const QKVArgs& qa, float* ws, size_t ws_floats,
-                        int32_t* tickets, int n_tickets, float* rms_ws, hipStream_t s) {
-  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
-  const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
-  if ((K & 63) || ws == nullptr || ws_floats < gemm4_sk_workspace_floats() || tickets == nullptr ||
-      n_tickets < tm * tn || (rms && rms_ws == nullptr))
+static int launch_g4_xk(const bf16_t* x, const u32x4* w, float* out, int M, int N, int K, int accumulate,
+                        bf16_t* mirror, int ks, float* ws, size_t ws_floats, int32_t* counts, int n_counts,
+                        hipStream_t s) {
+  if (!gemm4_xk_ok(M, N, K, ks) || ws == nullptr || ws_floats < gemm4_xk_workspace_floats(M, N, ks) ||
+      counts == nullptr || n_counts < gemm4_xk_counts(M, N))
     return -3;
-  // one workgroup per CU, never more than there are iterations: an empty range inside a tile's contributor span
-  // would never take its ticket
-  const long long iters = (long long)tm * tn * (K >> 6);
-  const int P = (int)min((long long)num_cus(), iters);
-  const G4Sk sk{iters, ws, (int)(gemm4_sk_workspace_floats() * 4), tickets};
-  if (rms) {
-    if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return -1;
-    gemm4_sk_kernel<MODE, 2><<<P, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, sk,
-                                                 qa, rms_ws);
-  } else {
-    gemm4_sk_kernel<MODE, 0><<<P, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, sk,
-                                                 qa, nullptr);
+  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
+  const int KS64 = K >> 6, kc = (KS64 + ks - 1) / ks;
+  const int gm = g4_group_m(tm, tn, K);
+#define JLA_XK(KSV)                                                                                               \
+  if (ks == KSV) {                                                                                                \
+    gemm4_xk_kernel<MODE_RESIDUAL, KSV><<<tm * tn * ks, 256, 0, s>>>(x, w, out, M, N, K, accumulate, 1, mirror, kc, \
+                                                                     tm, tn, gm, G4Xk{ws, counts, ks});           \
+    JLA_CHECK_LAUNCH();                                                                                           \
+    return 0;                                                                                                     \
   }
-  JLA_CHECK_LAUNCH();
-  return 0;
+  JLA_XK(2) JLA_XK(4) JLA_XK(8)
+#undef JLA_XK
+  return -1;
 }
 
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
-                      int grid_override = 0, G2Fix fix = G2Fix{}, const QKVArgs& qa = QKVArgs{},
-                      float* rms_ws = nullptr) {
+                      const QKVArgs& qa = QKVArgs{}, float* rms_ws = nullptr) {
   if constexpr (MODE != MODE_QKV && MODE != MODE_ARGMAX) {
-    if (grid_override == 0 && fix.ksplit <= 1 && fix.tile_count == 0 && tile == G4N_TILE && (K & 63) == 0) {
+    if (tile == G4N_TILE && (K & 63) == 0) {
       launch_g4<MODE, 4>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
       return;
     }
   }
-  if (grid_override == 0 && fix.ksplit <= 1 && fix.tile_count == 0 && use_g4(tile, M, K)) {
+  if (use_g4(tile, M, K)) {
     launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
     return;
   }
   const int cfg = tile_cfg(tile, M);
   const int bm = cfg == 1 ? 256 : 128, bn = cfg == 3 ? 128 : 256;
   const int tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn;
-  // grid_override: only the first grid_override tiles of the launch order (stream-K's data-parallel part)
-  const int grid = grid_override > 0 ? grid_override : (fix.tile_count > 0 ? fix.tile_count : tm * tn) * ksplit;
+  const int grid = tm * tn * ksplit;
 #define JLA_G2S(WMV, NB, LATE, R, MTV, NTV, SB)                                                             \
   gemm2_kernel<MODE, WMV, NB, LATE, R, MTV, NTV, SB><<<grid, 256 * WMV, 0, s>>>(                            \
-      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix, qa)
+      x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, ssq, qa)
 #define JLA_G2(WMV, NB, LATE, R, MTV, NTV) JLA_G2S(WMV, NB, LATE, R, MTV, NTV, 1)
 #define JLA_G2FA(R, FM)                                                                                      \
   gemm2_kernel<MODE, 2, 4, true, R, 8, 4, 1, true, FM><<<grid, 512, 0, s>>>(x, w, out, M, N, K, accumulate,     \
-                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq, fix, qa)
+                                                                           out_f32, mirror, kc, tm, tn, rms_eps, ssq, qa)
   if constexpr (MODE == MODE_QKV) {  // the direct RoPE / KV-write epilogue: the default 256 x 256 FA pipeline only
     JLA_G2FA(true, 2);
   } else {
@@ -1815,12 +1420,10 @@ template <int MODE>
 static void launch_tiled(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate,
                          int out_f32, bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile,
                          hipStream_t s, float* rms_ws = nullptr) {
-  launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s, 0, G2Fix{},
-                  QKVArgs{}, rms_ws);
+  launch_g2<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, ksplit, rms_eps, ssq, tile, s, QKVArgs{},
+                  rms_ws);
 }
 
-// ---- stream-K tail plan (tile config 4): whole waves of 256x256 tiles data-parallel, the rest dealt
-// out as K-iterations to one workgroup per CU
 static int g_num_cus = 0;
 static int num_cus() {
   if (g_num_cus == 0) {
@@ -1831,84 +1434,6 @@ static int num_cus() {
     if (g_num_cus <= 0) g_num_cus = 256;
   }
   return g_num_cus;
-}
-
-struct G2SkPlan {
-  int dp, sk;        // data-parallel tiles, stream-K tail tiles (sk == 0: no tail, plain launch)
-  long long iters;   // tail K-iterations
-};
-static G2SkPlan g2sk_plan(int M, int N, int K) {
-  const int P = num_cus(), KS = K >> 5;
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  G2SkPlan p{tiles, 0, 0};
-  const int rem = tiles % P;
-  if (rem == 0) return p;
-  int sk = rem;
-  // a thin tail would split every tile over many contributors (each one a 256 KiB partial to publish
-  // and re-read): give the tail one more whole wave, and never let a tile have more than 4
-  // contributors (>= KS/3 K-tiles per workgroup), which the fixup's fixed-size table assumes
-  if ((long long)sk * KS < (long long)P * ((KS + 2) / 3) && tiles >= sk + P) sk += P;
-  if ((long long)sk * KS < (long long)P * ((KS + 2) / 3)) return p;  // leave it data-parallel
-  p.dp = tiles - sk;
-  p.sk = sk;
-  p.iters = (long long)sk * KS;
-  return p;
-}
-// test hook: pretend the device has n CUs (0 = query it) so small shapes get a data-parallel part + tail
-void gemm_sk_set_cus(int n) { g_num_cus = n > 0 ? n : 0; }
-size_t gemm_sk_workspace_floats() { return (size_t)num_cus() * 2 * G2SK_SLAB_FLOATS; }
-int gemm_sk_tickets(int M, int N, int K) { return max(1, g2sk_plan(M, N, K).sk); }
-int gemm_sk_active(int M, int N, int K) { return g2sk_plan(M, N, K).sk > 0; }
-int gemm_sk_qkv_ok(int M, int N, int K) {  // every tile in the tail: the RoPE/KV epilogue can run in-kernel
-  const G2SkPlan p = g2sk_plan(M, N, K);
-  return p.sk > 0 && p.dp == 0;
-}
-
-template <int MODE>
-static void launch_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
-                      bf16_t* mirror, float rms_eps, const G2Sk& sk, const QKVArgs& qa, hipStream_t s) {
-  const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-  if (MODE != MODE_RESIDUAL && rms_eps >= 0.f)
-    gemm2_sk_kernel<MODE, true><<<num_cus(), 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn,
-                                                          rms_eps, sk, qa);
-  else
-    gemm2_sk_kernel<MODE, false><<<num_cus(), 512, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn,
-                                                           rms_eps, sk, qa);
-}
-
-static int gemm_sk(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int mode, int accumulate,
-                   int out_f32, bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int32_t* tickets,
-                   int n_tickets, hipStream_t s, float rms_eps) {
-  const G2SkPlan p = g2sk_plan(M, N, K);
-  if (ws == nullptr || ws_floats < gemm_sk_workspace_floats() || tickets == nullptr || n_tickets < p.sk) return -3;
-  if (p.dp > 0) {
-    if (mode == MODE_QKV) return -1;  // the data-parallel kernel has no RoPE epilogue
-    switch (mode) {
-      case MODE_STORE:
-        launch_g2<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, K >> 5, 1, rms_eps, nullptr, 1, s, p.dp);
-        break;
-      case MODE_RESIDUAL:
-        launch_g2<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, K >> 5, 1, -1.f, nullptr, 1, s, p.dp);
-        break;
-      case MODE_SWIGLU:
-        launch_g2<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, K >> 5, 1, rms_eps, nullptr, 1, s, p.dp);
-        break;
-      default: return -1;
-    }
-    JLA_CHECK_LAUNCH();
-  }
-  G2Sk sk{p.dp, 0, p.iters, ws, (int)(gemm_sk_workspace_floats() * 4), tickets};
-  QKVArgs qa{};
-  if (qkv) qa = *qkv;
-  switch (mode) {
-    case MODE_STORE: launch_sk<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, rms_eps, sk, qa, s); break;
-    case MODE_RESIDUAL: launch_sk<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, -1.f, sk, qa, s); break;
-    case MODE_SWIGLU: launch_sk<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, rms_eps, sk, qa, s); break;
-    case MODE_QKV: launch_sk<MODE_QKV>(x, w, out, M, N, K, 0, 0, nullptr, rms_eps, sk, qa, s); break;
-    default: return -1;
-  }
-  JLA_CHECK_LAUNCH();
-  return 0;
 }
 
 // the split-K reduce + epilogue launch over [ksplit][M][N] partial slabs (+ [ksplit][M] sums of squares, fused norm)
@@ -1993,67 +1518,16 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (tile == G4N_TILE && ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
                            (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
     return -1;  // the 256 x 128 plan: no QKV / argmax epilogue, the fused norm only precomputed without a K split
-  if (tile == G4_SK_TILE) {  // gemm4 stream-K over every (tile, K-tile) iteration: one persistent workgroup per CU
-    if (ksplit > 1) return -1;
-    if ((N & 15) || (K & 31)) return -1;
-    if (mode == MODE_QKV && !qkv) return -1;
-    const u32x4* wp = static_cast<const u32x4*>(W);
-    QKVArgs qa{};
-    if (qkv) qa = *qkv;
-    switch (mode) {
-      case MODE_STORE:
-        return launch_g4_sk<MODE_STORE>(x, wp, out, M, N, K, accumulate, out_f32, nullptr, rms_eps, qa, ws, ws_floats,
-                                        tickets, n_tickets, rms_ws, s);
-      case MODE_RESIDUAL:
-        return launch_g4_sk<MODE_RESIDUAL>(x, wp, out, M, N, K, accumulate, 1, mirror, -1.f, qa, ws, ws_floats,
-                                           tickets, n_tickets, nullptr, s);
-      case MODE_SWIGLU:
-        return launch_g4_sk<MODE_SWIGLU>(x, wp, out, M, N, K, accumulate, 0, nullptr, rms_eps, qa, ws, ws_floats,
-                                         tickets, n_tickets, rms_ws, s);
-      case MODE_QKV:
-        return launch_g4_sk<MODE_QKV>(x, wp, nullptr, M, N, K, 0, 0, nullptr, rms_eps, qa, ws, ws_floats, tickets,
-                                      n_tickets, rms_ws, s);
-      default: return -1;
-    }
+  if (tile == G4_XK_TILE) {  // gemm4 split-K, the splits exchange their partial blocks in-kernel (residual only)
+    if (mode != MODE_RESIDUAL || rms_eps >= 0.f) return -1;
+    return launch_g4_xk(x, static_cast<const u32x4*>(W), static_cast<float*>(out), M, N, K, accumulate, mirror,
+                        ksplit, ws, ws_floats, tickets, n_tickets, s);
   }
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
   const bool rms = rms_eps >= 0.f;
   if (rms && mode == MODE_RESIDUAL) return -5;  // caller pre-scales x instead
-  if (tile == 6) {  // whole waves of 256x256 tiles data-parallel + the last partial wave split 2-way (fixup)
-    if (mode == MODE_QKV || tickets == nullptr) return -1;
-    const int P = num_cus();
-    const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
-    const int dp = (tiles / P) * P, tail = tiles - dp;
-    const u32x4* wp = static_cast<const u32x4*>(W);
-    if (n_tickets < tiles || ws == nullptr || ws_floats < (size_t)tail * 2 * G2FIX_SLAB_FLOATS) return -3;
-    const int KS = K >> 5, kc2 = (KS + 1) / 2;
-    const G2Fix fix{ws, tickets, 2, dp, tail, 0};
-#define JLA_G6(MD, OF32, MIR, EPS)                                                                                \
-  {                                                                                                              \
-    if (dp > 0) launch_g2<MD>(x, wp, out, M, N, K, accumulate, OF32, MIR, KS, 1, EPS, nullptr, 1, s, dp);        \
-    if (tail > 0) launch_g2<MD>(x, wp, out, M, N, K, accumulate, OF32, MIR, kc2, 2, EPS, nullptr, 1, s, 0, fix); \
-  }
-    switch (mode) {
-      case MODE_STORE: JLA_G6(MODE_STORE, out_f32, nullptr, rms_eps) break;
-      case MODE_RESIDUAL: JLA_G6(MODE_RESIDUAL, 1, mirror, -1.f) break;
-      case MODE_SWIGLU: JLA_G6(MODE_SWIGLU, 0, nullptr, rms_eps) break;
-      default: return -1;
-    }
-#undef JLA_G6
-    JLA_CHECK_LAUNCH();
-    return 0;
-  }
-  if (tile == 4) {  // stream-K tail (256x256 ping-pong tiles; no K split)
-    if (ksplit > 1) return -1;
-    if (mode == MODE_QKV && !qkv) return -1;
-    if (g2sk_plan(M, N, K).sk > 0)
-      return gemm_sk(x, static_cast<const u32x4*>(W), out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ws,
-                     ws_floats, tickets, n_tickets, s, rms_eps);
-    if (mode == MODE_QKV) return -1;
-    tile = 1;  // whole waves only: the plain data-parallel launch
-  }
   if (mode == MODE_QKV && !qkv) return -1;
   const int KS = K >> 5;
   if (ksplit < 1) ksplit = 1;
@@ -2065,8 +1539,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (ksplit == 1) {
     switch (mode) {
       case MODE_QKV:
-        launch_g2<MODE_QKV>(x, w, nullptr, M, N, K, 0, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s, 0, G2Fix{}, *qkv,
-                            rms_ws);
+        launch_g2<MODE_QKV>(x, w, nullptr, M, N, K, 0, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s, *qkv, rms_ws);
         break;
       case MODE_STORE:
         launch_tiled<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, 1, rms_eps, nullptr, tile, s,
@@ -2078,30 +1551,6 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
       case MODE_SWIGLU:
         launch_tiled<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, 1, rms_eps, nullptr, tile, s,
                                   rms_ws);
-        break;
-      default: return -1;
-    }
-    JLA_CHECK_LAUNCH();
-    return 0;
-  }
-  // in-kernel split-K fixup (G2Fix): the default FA pipeline on 256 x 256 tiles, a tickets array from the
-  // caller and slabs of gemm_fix_workspace_floats(); otherwise the partial slabs + reduce kernel below
-  if (g_gemm_fixup && tickets != nullptr && mode != MODE_QKV && tile_cfg(tile, M) == 1 && (tile < 4)) {
-    const int tiles = ((M + 255) / 256) * ((N + G2_BN - 1) / G2_BN);
-    if (n_tickets < tiles || ws == nullptr || ws_floats < (size_t)tiles * ksplit * G2FIX_SLAB_FLOATS) return -3;
-    const G2Fix fix{ws, tickets, ksplit, 0, 0, 0};
-    switch (mode) {
-      case MODE_STORE:
-        launch_g2<MODE_STORE>(x, w, out, M, N, K, accumulate, out_f32, nullptr, kc, ksplit, rms_eps, nullptr, tile,
-                              s, 0, fix);
-        break;
-      case MODE_RESIDUAL:
-        launch_g2<MODE_RESIDUAL>(x, w, out, M, N, K, accumulate, 1, mirror, kc, ksplit, -1.f, nullptr, tile, s, 0,
-                                 fix);
-        break;
-      case MODE_SWIGLU:
-        launch_g2<MODE_SWIGLU>(x, w, out, M, N, K, accumulate, 0, nullptr, kc, ksplit, rms_eps, nullptr, tile, s, 0,
-                               fix);
         break;
       default: return -1;
     }
@@ -2207,10 +1656,10 @@ int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int
   }
   if (rms_eps >= 0.f)
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, true, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
-        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{}, QKVArgs{});
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, QKVArgs{});
   else
     gemm2_kernel<MODE_ARGMAX, 2, 4, true, false, 8, 4, 1, true, 2><<<tm * tn, 512, 0, s>>>(
-        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, G2Fix{}, QKVArgs{});
+        x, w, ws, M, N, K, 0, 1, nullptr, K >> 5, tm, tn, rms_eps, nullptr, QKVArgs{});
   JLA_CHECK_LAUNCH();
   launch_argmax_partials(reinterpret_cast<const float2*>(ws), tn * 4, M, idx, val, s);
   JLA_CHECK_LAUNCH();

@@ -477,7 +477,7 @@ static int dispatch_nt(const void* x, const void* W, void* out, int M, int N, in
       }
       if (gemv_split_variant(variant)) {
         constexpr int SNT = MODE == MODE_SWIGLU ? 2 : 1, SNW = MT == 1 ? 4 : 8;
-        const int ks = 2;
+        const int ks = 2;  // (K over 4 lost to 2 on the 70B MP 8 qkv shard at M = 1 / 32: profiles/README.md round 5)
         if (variant == 18)
           return launch_skinny<XT, MT, SNT, MODE, SNW, 0, true, true>(x, W, out, M, N, K, eps, use_rms, accumulate,
                                                                       out_f32, qa, s, ks);
@@ -561,10 +561,6 @@ struct FusedAttn {
   int splits, grid_q, t_cap;
   float scale_log2;
 };
-
-JLA_DEV void st_sc1_x4(void* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
 
 template <int MT, int NT, int NW, int U, bool XP, int REP>
 __global__ void __launch_bounds__(256)

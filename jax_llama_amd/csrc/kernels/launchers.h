@@ -68,43 +68,29 @@ void gemm_set_g4_group(int gm);
 int gemm5_ksplit(int K, int ksplit);
 int clock_probe(int iters, int grid, unsigned long long* out, hipStream_t s);  // [cycles, 100 MHz ticks]
 void gemm5_set_diag(int d);  // tools only: gemm5 ablations (wrong results)  // gemm5 (tiles 11 / 12): the effective split over 64-deep K-stages
-// tile config 8: gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration; partial tiles
-// summed by the last arriver): ws >= gemm4_sk_workspace_floats(), tickets >= gemm4_sk_tickets(M, N) int32
-// zero-initialised once (self-resetting); the fused norm needs rms_ws; every mode incl. MODE_QKV
-size_t gemm4_sk_workspace_floats();
-int gemm4_sk_tickets(int M, int N);  // gemm4 main loop on the 160 KiB LDS ring (3 x pairs + 4 W stages in flight)
+// tile config 8: gemm4 split-K whose splits exchange their partial wave blocks inside the launch (residual
+// epilogue): ws >= gemm4_xk_workspace_floats(M, N, ks), tickets >= gemm4_xk_counts(M, N) int32 zero-initialised
+// once (self-resetting; the last one is the error word); only where gemm4_xk_ok (all workgroups resident)
+size_t gemm4_xk_workspace_floats(int M, int N, int ks);
+int gemm4_xk_counts(int M, int N);
+int gemm4_xk_ok(int M, int N, int K, int ks);
 size_t gemm_workspace_floats(int M, int N, int K);
 // rms_eps >= 0: x is the UNscaled activation and each output row is scaled by rsqrt(mean(x^2) + eps)
 // (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
-// tile: gemm2 tile config 1 = 256x256, 2 = 128x256, 3 = 128x128, 0 = by M, 4 = 256x256 with a stream-K tail
-// (ksplit 1; ws >= gemm_sk_workspace_floats(), tickets >= gemm_sk_tickets(M, N, K) int32 zero-initialised
-// once, self-resetting; MODE_QKV supported when every tile is in the tail)
+// tile: gemm2 tile config 1 = 256x256, 2 = 128x256, 3 = 128x128, 0 = by M; 7 / 10 gemm4 (256 x 256 / 256 x 128),
+// 8 gemm4 exchange split (above), 11 / 12 gemm5
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0,
          float* rms_ws = nullptr, size_t rms_ws_floats = 0);
 // rms_ws (>= M floats): with the fused norm, a gemm4 plan without a K split computes the row statistic ahead of
 // the GEMM into it (rms_rowinv) instead of inside its main loop; null: in-loop statistic
-// split-K with tickets (ksplit > 1, tile 0-3, not MODE_QKV): the in-kernel fixup (no reduce kernel) on
-// ws >= gemm_fix_workspace_floats(M, N, ksplit) slabs and >= gemm_fix_tiles(M, N) zero-initialised tickets
-size_t gemm_fix_workspace_floats(int M, int N, int ksplit);
-int gemm_fix_tiles(int M, int N);
-// tile config 6: whole waves of 256x256 tiles data-parallel, the last partial wave split 2-way with the fixup
-// (ws >= gemm_hybrid_workspace_floats(M, N), tickets >= gemm_fix_tiles(M, N))
-size_t gemm_hybrid_workspace_floats(int M, int N);
-void gemm_set_fixup(int on);  // A/B: 0 = partial slabs + reduce kernel even when tickets are given
-int gemm_fixup_enabled();
 // greedy lm_head: GEMM + first-max argmax epilogue (ws >= gemm_argmax_workspace_floats(M, N) floats)
 int gemm_argmax(const bf16_t* x, const void* W, float* ws, size_t ws_floats, int M, int N, int K, float rms_eps,
                 int32_t* idx, float* val, hipStream_t s, float* rms_ws = nullptr, size_t rms_ws_floats = 0);
 size_t gemm_argmax_workspace_floats(int M, int N);
 // first max per row over [M][P] (value, index) float2 partials
 int argmax_partials(const float* part, int P, int M, int32_t* idx, float* val, hipStream_t s);
-size_t gemm_sk_workspace_floats();
-int gemm_sk_tickets(int M, int N, int K);
-int gemm_sk_active(int M, int N, int K);
-int gemm_sk_qkv_ok(int M, int N, int K);
-void gemm_sk_set_cus(int n);
 
 int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const int32_t* positions, bf16_t* kc,
                   bf16_t* vc, const int32_t* slot, int M, int S, int H, int Hkv, int Dh, int T, bf16_t* q_out,

@@ -41,6 +41,23 @@ JLA_DEV void asm_load16(u32x4& r, const void* p) {
 JLA_DEV void asm_load_sc1(u32x4& r, const void* p) {
   asm volatile("global_load_dwordx4 %0, %1, off sc1" : "+v"(r) : "v"(p) : "memory");
 }
+// LDS-DMA with the agent-coherent (sc1) policy: rows another workgroup of the same launch wrote write-through
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+JLA_DEV void glds16_asm_sc1(const void* gsrc, void* lds_wave_base) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(gsrc), "s"(m0)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// write-through (sc1) store: the producer side of the same hand-off. hipcc's hazard recognizer does not see into the
+// asm, and a store of more than 8 bytes reads its upper data dwords after issue: the s_nop is the wait state a VALU
+// write of those registers right behind the store needs (without it lanes' upper dwords came out corrupted).
+JLA_DEV void st_sc1_x4(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
 template <int N>
 JLA_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");

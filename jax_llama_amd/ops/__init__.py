@@ -313,65 +313,27 @@ def _tiled_input(x, rms_eps, fused=False):
     return x if x.dtype == BF16 else x.to(BF16)
 
 
-SK_TILE = 4          # gemm2 "tile config" of the stream-K tail plan (csrc/kernels/gemm.hip)
-SK_MAX_TICKETS = 1024  # >= 2 x CUs: one fixed-size ticket array, so hipGraphs never see a reallocation
-
-
-def sk_workspace(e, m, n, k, device):
-    """Slabs + self-resetting tickets of the stream-K tail (None, None when the shape has no tail)."""
-    floats, tickets = e.gemm_sk_workspace(m, n, k)
-    if floats == 0:
-        return None, None
-    assert tickets <= SK_MAX_TICKETS, tickets
-    return (workspace.get("gemm_sk", floats, torch.float32, device),
-            workspace.get_zeroed("gemm_sk_tickets", SK_MAX_TICKETS, torch.int32, device))
-
-
-FIX_TICKETS = 4096  # tickets of the in-kernel split-K fixup: one fixed-size array (no reallocation under graphs)
-
-
-def fix_workspace(e, m, n, ks, device):
-    """Slabs + self-resetting tickets of the in-kernel split-K fixup (csrc/kernels/gemm.hip G2Fix): sized so
-    the same buffer also serves the partial-slab + reduce-kernel path ([ks][m][n] + [ks][m])."""
-    floats, tiles = e.gemm_fix_workspace(m, n, ks)
-    ws = workspace.get("gemm_ws", max(floats, ks * m * (n + 1)), torch.float32, device)
-    tk = workspace.get_zeroed("gemm_fix_tickets", max(FIX_TICKETS, tiles), torch.int32, device)
-    return ws, tk
-
-
-G4SK_TILE = 8  # gemm4 stream-K plan (csrc/kernels/gemm.hip gemm4_sk_kernel)
+XK_TILE = 8  # gemm4 split-K with the in-launch exchange of partial blocks (csrc/kernels/gemm.hip gemm4_xk_kernel)
+XK_COUNTS = 4096  # counters of the exchange: one fixed-size array (no reallocation under graphs)
 G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h): 256- / 128-column workgroups
 
 
-def g4sk_workspace(e, m, n, device):
-    """Slabs + self-resetting tickets of the gemm4 stream-K plan (sized for the largest M seen; one fixed-size ticket
-    array so captured graphs never see a reallocation)."""
-    floats, tiles = e.gemm4_sk_workspace(m, n)
-    return (workspace.get("gemm4_sk", floats, torch.float32, device),
-            workspace.get_zeroed("gemm4_sk_tickets", max(FIX_TICKETS, tiles), torch.int32, device))
+def xk_workspace(e, m, n, ks, device):
+    """Partial-block buffer + self-resetting counters (and the error word) of the exchange plan."""
+    floats, counts = e.gemm4_xk_workspace(m, n, ks)
+    return (workspace.get("gemm_xk", floats, torch.float32, device),
+            workspace.get_zeroed("gemm_xk_counts", max(XK_COUNTS, counts), torch.int32, device))
 
 
 def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
-    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue.
-    A split plan gets fixup tickets (the GEMM sums its splits itself) except for the QKV epilogue, whose
-    RoPE + cache write lives in the reduce kernel."""
+    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue: partial slabs
+    for a split summed by the reduce kernel, or the exchange plan's block buffer + counters (tile 8)."""
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, rms)
     if tm in G5_TILES:  # weight-streaming split-K (any split, slabs always): partial slabs + the reduce kernel
         eks = e.gemm5_ksplit(k, ks)
         return ks, tm, workspace.get("gemm_ws", eks * m * (n + 1), torch.float32, device), None
-    if tm == G4SK_TILE:
-        ws, tk = g4sk_workspace(e, m, n, device)
-        return 1, tm, ws, tk
-    if tm == SK_TILE:
-        ws, tk = sk_workspace(e, m, n, k, device)
-        return 1, tm, ws, tk
-    if tm == autotune.HYBRID_TILE:
-        floats, tiles = e.gemm_hybrid_workspace(m, n)
-        ws = workspace.get("gemm_ws", max(floats, 1), torch.float32, device)
-        tk = workspace.get_zeroed("gemm_fix_tickets", max(FIX_TICKETS, tiles), torch.int32, device)
-        return 1, tm, ws, tk
-    if ks > 1 and mode != MODE_QKV and e.gemm_fixup_enabled():
-        ws, tk = fix_workspace(e, m, n, ks, device)
+    if tm == XK_TILE:
+        ws, tk = xk_workspace(e, m, n, ks, device)
         return ks, tm, ws, tk
     # split-K slabs [ks][m][n] + the fused-RMS partial sums of squares [ks][m]
     ws = workspace.get("gemm_ws", ks * m * (n + 1), torch.float32, device) if ks > 1 else None
@@ -380,16 +342,15 @@ def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
 
 def _rms_ws(x, fused: bool, ks: int):
     """fp32 [M] scratch for the row statistic of the fused norm, computed ahead of a gemm4 GEMM without a K split
-    (csrc/kernels/norm_embed.hip rms_rowinv; the main loop then carries no sum-of-squares work; the gemm4 stream-K
-    plan requires it)."""
+    (csrc/kernels/norm_embed.hip rms_rowinv; the main loop then carries no sum-of-squares work)."""
     if not fused or ks > 1:
         return None
     return workspace.get("gemm_rms", x.shape[0], torch.float32, x.device)
 
 
 def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None, pack_out=None):
-    """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups, or a stream-K tail,
-    when the output has too few 256x256 tiles to fill the chip (csrc/kernels/gemm.hip). ``pack_out``: the split-K
+    """Tiled MFMA GEMM (prefill, and decode batches > 32): split-K over workgroups when the output has too few
+    256x256 tiles to fill the chip (csrc/kernels/gemm.hip). ``pack_out``: the split-K
     reduce epilogue also writes the packed copy of the bf16 output (plans that ``_tiled_packs``)."""
     fused = _fused_rms(e, mode, rms_eps)
     xb = _tiled_input(x, rms_eps, fused)
@@ -400,13 +361,13 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None, pack
 
 def _tiled_packs(e, m, n, k, device, mode, rms_eps) -> bool:
     """Whether the tiled GEMM's tuned plan for this decode shape can write a packed output copy: the plain split-K
-    path, whose reduce kernel runs the epilogue (not ks = 1, the stream-K / hybrid tiles or the in-kernel fixup)."""
+    path, whose reduce kernel runs the epilogue (not ks = 1 or the exchange plan)."""
     if e is None or m > SKINNY_M or mode not in (MODE_RESIDUAL, MODE_SWIGLU):
         return False
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, _fused_rms(e, mode, rms_eps))
     if tm in G5_TILES:
         return True
-    return ks > 1 and tm not in (SK_TILE, autotune.HYBRID_TILE, G4SK_TILE) and not e.gemm_fixup_enabled()
+    return ks > 1 and tm != XK_TILE
 
 
 def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int:
@@ -501,37 +462,23 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV, x_packed)
     if v == TILED:
         # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
-        ks, tm, ws, tk = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
-        if tm == G4SK_TILE:  # gemm4 stream-K: the RoPE / KV-write epilogue runs in the GEMM itself
-            fused = _fused_rms(e, MODE_QKV, rms_eps)
-            q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
-            e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
-                       k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                       int(head_dim), q, 1, ws, float(rms_eps) if fused else -1.0, tm, tk, _rms_ws(x, fused, 1))
-            return q
-        if tm == autotune.HYBRID_TILE:
-            tm = 1  # (only reached with ks == 1: the plain linear() below runs the hybrid plan itself)
-        if tm != SK_TILE:
-            tk = None  # split QKV: partial slabs + the RoPE / KV-write reduce kernel
-        if tm == SK_TILE and not e.gemm_sk_qkv_ok(m, w.n, w.k):
-            tm = 1  # the stream-K plan has a data-parallel part here: plain GEMM + RoPE kernel
+        ks, tm, ws, _ = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
         fused = _fused_rms(e, MODE_QKV, rms_eps)
-        if ks == 1 and tm != SK_TILE and fused and QKV_DIRECT and e.gemm_qkv_direct_ok(m, tm, w.k):
+        if ks == 1 and fused and QKV_DIRECT and e.gemm_qkv_direct_ok(m, tm, w.k):
             # enough tiles, no K split: the GEMM's own RoPE / KV-write epilogue (no qkv round trip, no rope kernel)
             q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
             e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                        k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
                        int(head_dim), q, 1, None, float(rms_eps), tm, None, _rms_ws(x, fused, 1))
             return q
-        if ks == 1 and tm != SK_TILE:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
+        if ks == 1:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
             qkv = linear(x, w, rms_eps=rms_eps)
             return rope_kv_write(qkv, table, positions, k_cache, v_cache, slot0, seq_len, n_heads, n_kv_heads,
                                  head_dim)
         q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
-        fused = _fused_rms(e, MODE_QKV, rms_eps)
         e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                    k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm, tk)
+                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm, None)
         return q
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)

@@ -25,8 +25,6 @@ def _load():
         name = "_C_dbg" if os.environ.get("JLA_DEBUG_BOUNDS", "0") == "1" else "_C"
         _EXT = importlib.import_module("jax_llama_amd." + name)
         # A/B knobs for tools: JLA_ATTN_IMPL=<impl>[:<waves_target>] (csrc/kernels/attn_decode.hip attn_set_impl)
-        if os.environ.get("JLA_GEMM_FIXUP") == "1":  # split-K summed in the GEMM (default: reduce kernel)
-            _EXT.gemm_set_fixup(True)
         if os.environ.get("JLA_ATTN_IMPL"):
             impl, _, tgt = os.environ["JLA_ATTN_IMPL"].partition(":")
             _EXT.attn_set_impl(int(impl), int(tgt or 0))

@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 9  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles), so older persisted picks are re-measured
+TUNE_VERSION = 10  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -278,7 +278,8 @@ KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
 TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
 # 7: gemm4; 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
 # 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
-# plus (1, SK_TILE) -- 256x256 with a stream-K tail -- for shapes whose tile count is not a multiple of the CUs
+# plus (ks, XK_TILE) -- gemm4 split-K whose splits exchange their partial blocks in-launch -- for the residual epilogue
+# where tiles x split fit the CUs
 TUNE_MAX_M = 2048
 
 
@@ -315,17 +316,13 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
     return choose_gemm_plan(e, m, n, k, device)[0]
 
 
-SK_TILE = 4  # 256x256 tiles with a stream-K tail (no K split): csrc/kernels/gemm.hip gemm_sk
-HYBRID_TILE = 6  # whole waves of 256x256 tiles + the partial wave split 2-way with the in-kernel fixup
-G4SK_TILE = 8  # gemm4 stream-K (one persistent workgroup per CU over every (tile, K-tile) iteration)
+XK_TILE = 8  # gemm4 split-K with the in-launch exchange of partial wave blocks (residual epilogue)
 G4N_TILE = 10  # gemm4 on 256 x 128 tiles (csrc/kernels/gemm4w.h g4n_mainloop)
 G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h)
-SK_MARGIN = 0.97
 TUNE_ROUNDS = 3
 
 
 def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int]:
-    from . import sk_workspace
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
@@ -333,18 +330,14 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
              and (tm not in G5_TILES or (k % 64 == 0 and m <= 512))]
     if k % 64 == 0 and m <= 512:  # gemm5 also at the deeper splits its 64-deep stages allow (narrow shards, long K)
         cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c]
-    sk_ws, sk_tk = sk_workspace(e, m, n, k, device)
-    if sk_ws is not None:
-        cands.append((1, SK_TILE))
-    g4sk = None
-    if k % 64 == 0:  # gemm4 stream-K over every (tile, K-tile) iteration
-        cands.append((1, G4SK_TILE))
-        fl, tiles = e.gemm4_sk_workspace(m, n)
-        g4sk = (torch.empty(fl, dtype=torch.float32, device=device), torch.zeros(tiles, dtype=torch.int32,
-                                                                                  device=device))
-    hyb_floats = e.gemm_hybrid_workspace(m, n)[0] if e.gemm_fixup_enabled() else 0
-    if hyb_floats > 0:  # whole waves data-parallel + the partial wave split 2-way (in-kernel fixup)
-        cands.append((1, HYBRID_TILE))
+    xk = None
+    if mode == 1:  # the exchange split: every split count whose workgroups all fit the CUs at once
+        xks = [c for c in (2, 3, 4, 6, 8) if e.gemm4_xk_ok(m, n, k, c)]
+        cands += [(c, XK_TILE) for c in xks]
+        if xks:
+            fl, counts = e.gemm4_xk_workspace(m, n, max(xks))
+            xk = (torch.empty(fl, dtype=torch.float32, device=device),
+                  torch.zeros(counts, dtype=torch.int32, device=device))
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
@@ -358,30 +351,19 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     else:
         out = torch.empty(m, n // 2 if mode == 2 else n, dtype=torch.bfloat16, device=device)
     eps = 1e-5 if (rms and mode != 1) else -1.0
-    # split plans run the way the model runs them: with the in-kernel fixup (tickets) where it applies
-    fix = e.gemm_fixup_enabled()
-    need = max(max(c for c, _ in cands) * m * (n + 1), max(e.gemm_fix_workspace(m, n, c)[0] for c in ks_c),
-               hyb_floats)
+    need = max(c for c, _ in cands) * m * (n + 1)
     ws = torch.empty(need, dtype=torch.float32, device=device)
-    fix_tk = torch.zeros(max(e.gemm_fix_workspace(m, n, 2)[1], 1), dtype=torch.int32, device=device) if fix else None
-    if fix_tk is None and hyb_floats:
-        fix_tk = torch.zeros(e.gemm_fix_workspace(m, n, 2)[1], dtype=torch.int32, device=device)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     rms_ws = torch.empty(m, dtype=torch.float32, device=device)  # as ops._rms_ws: the statistic ahead of gemm4
 
     def run(c, tm, i):
-        if tm == G4SK_TILE:
-            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, g4sk[0], eps, tm, g4sk[1], None,
-                   rms_ws if eps > 0 else None)
-        elif tm == SK_TILE:
-            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, sk_ws, eps, tm, sk_tk)
-        elif tm == HYBRID_TILE:
-            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, 1, ws, eps, tm, fix_tk)
+        if tm == XK_TILE:
+            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, xk[0], eps, tm, xk[1])
         elif tm in G5_TILES:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws, eps, tm)
         else:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm,
-                   fix_tk if c > 1 else None, None, rms_ws if c == 1 and eps > 0 else None)
+                   None, None, rms_ws if c == 1 and eps > 0 else None)
 
     for c, tm in cands:  # warm every variant (code objects, caches) before any timing
         for i in range(2):
@@ -398,11 +380,8 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
             ev1.record()
             ev1.synchronize()
             times[(c, tm)] = min(times[(c, tm)], ev0.elapsed_time(ev1) / iters)
-    best = min((cand for cand in cands if cand[1] != SK_TILE), key=times.get)
-    # the stream-K tail publishes fp32 partials in-kernel: keep it only when it clearly wins
-    if (1, SK_TILE) in times and times[(1, SK_TILE)] < SK_MARGIN * times[best]:
-        best = (1, SK_TILE)
-    del ws_w, ws, g4sk
+    best = min(cands, key=times.get)
+    del ws_w, ws, xk
     return best
 
 

@@ -658,108 +658,6 @@ def test_gemm_tile_configs(tile, ks, m):
     torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("m,k,ks", [(256, 1024, 2), (700, 4096, 3), (2048, 4096, 2), (300, 992, 4)])
-def test_gemm_splitk_fixup(m, k, ks):
-    """In-kernel split-K fixup (G2Fix: sc1-published fragment slabs, agent ticket, last arriver sums in split
-    order + runs the epilogue) against the partial-slab + reduce-kernel path: bit-identical (same summation
-    order, same row-scale formula) for every epilogue with and without the fused RMSNorm; tickets reset
-    themselves (three back-to-back runs, one under a hipGraph); and the fp32 reference."""
-    e = ops.ext()
-    n = 768
-    x = torch.randn(m, k).to(BF16)
-    w, pg, _ = _mk_linear(n, k)
-    xg = x.to(DEV)
-    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
-    gp = PackedLinear.from_dense(gu, DEV)
-    h0 = torch.randn(m, n).to(DEV)
-    floats, tiles = e.gemm_fix_workspace(m, n, ks)
-    ws = torch.empty(max(floats, ks * m * (n + 1)), dtype=torch.float32, device=DEV)
-    tk = torch.zeros(tiles, dtype=torch.int32, device=DEV)
-
-    def run(tickets):
-        outs = []
-        for eps in (-1.0, 1e-5):
-            o = torch.empty(m, n, dtype=torch.float32, device=DEV)
-            e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, 1, tickets)
-            o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
-            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, 1, tickets)
-            outs += [o, o2]
-        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, 1, tickets)
-        return outs + [hg, mir]
-
-    base = run(None)       # partial slabs + reduce kernel
-    e.gemm_set_fixup(True)  # (off by default: slower than the reduce kernel on MI355X)
-    try:
-        fixed = run(tk)        # in-kernel fixup
-        again = run(tk)        # tickets were reset by the last arrivers
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            graphed = run(tk)
-        g.replay()
-        torch.cuda.synchronize()
-    finally:
-        e.gemm_set_fixup(False)
-    assert int(tk.abs().sum()) == 0
-    for i, (a, b, c, d) in enumerate(zip(base, fixed, again, graphed)):
-        assert torch.equal(b, c) and torch.equal(b, d), f"output {i}: fixup not reproducible"
-        assert torch.equal(a, b), f"output {i}: fixup differs from the reduce path"
-    _close(fixed[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
-    _close(fixed[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
-    _close(fixed[3], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
-    _close(fixed[4], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
-
-
-@pytest.mark.parametrize("cus,m,n", [(4, 512, 768), (8, 700, 1536), (0, 2048, 28672)])
-def test_gemm_hybrid_tail(cus, m, n):
-    """Tile config 6: whole waves of 256x256 tiles data-parallel + the last partial wave split 2-way with the
-    in-kernel fixup (two launches); every epilogue with / without the fused RMSNorm vs the fp32 reference and
-    vs the plain tile-1 plan; tickets reset (two runs identical); cus > 0 pretends a smaller chip so small
-    shapes have a tail."""
-    e = ops.ext()
-    k = 1024
-    x = torch.randn(m, k).to(BF16)
-    w, pg, _ = _mk_linear(n, k)
-    xg = x.to(DEV)
-    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
-    gp = PackedLinear.from_dense(gu, DEV)
-    h0 = torch.randn(m, n).to(DEV)
-    try:
-        e.gemm_sk_set_cus(cus)
-        floats, tiles = e.gemm_hybrid_workspace(m, n)
-        assert floats > 0, "shape must have a partial wave"
-        ws = torch.empty(floats, dtype=torch.float32, device=DEV)
-        tk = torch.zeros(tiles, dtype=torch.int32, device=DEV)
-
-        def run(tile, tickets, wsp):
-            outs = []
-            for eps in (-1.0, 1e-5):
-                o = torch.empty(m, n, dtype=torch.float32, device=DEV)
-                e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, 1, wsp, eps, tile, tickets)
-                o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
-                e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, wsp, eps, tile, tickets)
-                outs += [o, o2]
-            hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
-            e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, wsp, -1.0, tile, tickets)
-            return outs + [hg, mir]
-
-        hyb, hyb2 = run(6, tk, ws), run(6, tk, ws)
-        plain = run(1, None, None)
-        torch.cuda.synchronize()
-    finally:
-        e.gemm_sk_set_cus(0)
-    assert int(tk.abs().sum()) == 0
-    for i, (a, b) in enumerate(zip(hyb, hyb2)):
-        assert torch.equal(a, b), f"output {i}: not reproducible"
-    for i, (a, b) in enumerate(zip(hyb, plain)):
-        _close(a, b, 2e-2, 2e-2)
-    _close(hyb[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
-    _close(hyb[2], ref.linear(x, w, 1e-5, torch.float32), 1e-2, 2e-3)
-    _close(hyb[3], ref.linear_swiglu(x, gu, 1e-5), 3e-2, 3e-2)
-    _close(hyb[4], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
-    torch.testing.assert_close(hyb[5].cpu(), hyb[4].cpu().to(BF16), rtol=0, atol=0)
-
-
 @pytest.mark.parametrize("m,k,ks", [(300, 1024, 1), (512, 1056, 1), (256, 992, 3), (700, 4096, 2)])
 def test_gemm_full_line_x(m, k, ks):
     """gemm2 (tile 1) with x staged in full 128-B lines (K-tile pairs, swizzled LDS image): every epilogue, with and
@@ -832,82 +730,6 @@ def test_gemm_argmax_fused(m, n, k):
     # the op-level API picks the fused path from ARGMAX_FUSED_MIN_M rows on
     idx, val = ops.linear_argmax(xg, pg, 1e-5)
     assert torch.equal(idx.cpu(), i1.cpu()) and torch.equal(val.cpu(), v1.cpu())
-
-
-@pytest.mark.parametrize("cus,m", [(0, 768), (0, 1000), (16, 200), (16, 512)])
-def test_gemm_stream_k_tail(cus, m):
-    """256x256 tiles with a stream-K tail (tile config 4): every epilogue, with and without the fused
-    RMSNorm, against the fp32 reference; bit-identical on a re-run (fixed contributor order, tickets
-    reset themselves). cus=16 pretends a 16-CU device so the small shape gets a data-parallel part
-    (16 / 64 whole tiles) plus a tail split across workgroups; cus=0 uses the real CU count (all tail)."""
-    e = ops.ext()
-    e.gemm_sk_set_cus(cus)
-    try:
-        k, n = 1024, 256 * 37
-        assert e.gemm_sk_workspace(m, n, k)[0] > 0
-        x = torch.randn(m, k).to(BF16)
-        w, pg, _ = _mk_linear(n, k)
-        xg = x.to(DEV)
-        ws, tk = ops.sk_workspace(e, m, n, k, DEV)
-        for eps in (-1.0, 1e-5):
-            r = None if eps < 0 else eps
-            out = torch.empty(m, n, dtype=torch.float32, device=DEV)
-            e.gemm(xg, pg.weight, n, k, out, ops.MODE_STORE, True, None, 1, ws, eps, 4, tk)
-            _close(out, ref.linear(x, w, r, torch.float32), 1e-2, 2e-3)
-            again = torch.empty_like(out)
-            e.gemm(xg, pg.weight, n, k, again, ops.MODE_STORE, True, None, 1, ws, eps, 4, tk)
-            assert torch.equal(out, again)
-            ob = torch.empty(m, n, dtype=BF16, device=DEV)
-            e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, ws, eps, 4, tk)
-            torch.testing.assert_close(ob, out.to(BF16), rtol=0, atol=0)
-            gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
-            gp = PackedLinear.from_dense(gu, DEV)
-            o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
-            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, ws, eps, 4, tk)
-            _close(o2, ref.linear_swiglu(x, gu, r), 3e-2, 3e-2)
-        h = torch.randn(m, n)
-        hg, mir = h.to(DEV), torch.empty(m, n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, ws, -1.0, 4, tk)
-        _close(hg, ref.linear_residual(x, w, h.clone()), 1e-2, 1e-3)
-        torch.testing.assert_close(mir.cpu(), hg.cpu().to(BF16), rtol=0, atol=0)
-        assert int(tk.abs().sum()) == 0  # every tail tile's last arriver reset its ticket
-    finally:
-        e.gemm_sk_set_cus(0)
-
-
-@pytest.mark.parametrize("m,s", [(512, 1), (384, 2)])
-def test_qkv_rope_stream_k(m, s):
-    """Fused qkv projection on the stream-K plan: RoPE + KV-cache write in the GEMM epilogue (a 16-CU
-    plan so this small projection has a tail)."""
-    e = ops.ext()
-    e.gemm_sk_set_cus(16)
-    try:
-        _qkv_rope_stream_k(e, m, s)
-    finally:
-        e.gemm_sk_set_cus(0)
-
-
-def _qkv_rope_stream_k(e, m, s):
-    h, hkv, dh, k, t = 8, 2, 128, 4096, 80
-    b = m // s
-    n = (h + 2 * hkv) * dh
-    assert e.gemm_sk_qkv_ok(m, n, k)
-    w = (torch.randn(n, k) * 0.05).to(BF16)
-    x = torch.randn(m, k).to(BF16)
-    table = ref.rope_table(dh, 256, 500000.0)
-    pos = torch.randint(0, 200, (m,), dtype=torch.int32)
-    kc = torch.zeros(b, hkv, t, dh, dtype=BF16)
-    vc = torch.zeros_like(kc)
-    q = ref.linear_qkv_rope(x, w, 1e-5, table, pos, kc, vc, 11, s, h, hkv, dh)
-    kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
-    pg = PackedLinear.from_dense(w, DEV)
-    ws, tk = ops.sk_workspace(e, m, n, k, DEV)
-    qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
-    e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
-               torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, ws, 1e-5, 4, tk)
-    _close(qg, q, 2e-2, 2e-2)
-    _close(kg, kc, 2e-2, 2e-2)
-    _close(vg, vc, 2e-2, 2e-2)
 
 
 @pytest.mark.parametrize("variant", [12, 15, 18, 21, 22, 26, 7])

@@ -46,8 +46,6 @@ def main():
     ap.add_argument("--impl", type=int, nargs="+", default=[2], help="label of the round (the tiled kernel is gemm2/gemm4)")
     ap.add_argument("--ops", nargs="+", default=None)
     ap.add_argument("--rounds", type=int, default=1, help="interleaved A/B rounds of the impl list (one process)")
-    ap.add_argument("--fixup", type=int, nargs="+", default=[0], help="split-K: 0 partial slabs + reduce kernel, "
-                    "1 in-kernel fixup (tickets); tile 6 always uses the fixup")
     ap.add_argument("--tile", type=int, nargs="+", default=[0], help="gemm2 tile config(s): 0 auto, 1 256x256, "
                     "2 128x256, 3 128x128")
     ap.add_argument("--mode", default="store", choices=["store", "swiglu", "residual"],
@@ -111,29 +109,14 @@ def main():
                     if tile in (11, 12) and (k % 64 or (k // 64) // kk < 1):
                         continue
                     tk = None
-                    for fx in args.fixup:
+                    for fx in (0,):
                       tk = None
-                      if tile == 4:  # stream-K tail plan (no K split)
-                          kk = 1
-                          ws, tk = ops.sk_workspace(e, m, n, k, DEV)
-                          if ws is None:
+                      if tile == 8:  # gemm4 exchange split (residual epilogue only)
+                          if mode != 1 or not e.gemm4_xk_ok(m, n, k, kk):
                               continue
-                      elif tile == 8:  # gemm4 stream-K (persistent, every iteration)
-                          kk = 1
-                          floats, tiles = e.gemm4_sk_workspace(m, n)
+                          floats, counts = e.gemm4_xk_workspace(m, n, kk)
                           ws = torch.empty(floats, device=DEV, dtype=torch.float32)
-                          tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
-                      elif tile == 6:  # whole waves + 2-way split tail (fixup)
-                          kk = 1
-                          floats, tiles = e.gemm_hybrid_workspace(m, n)
-                          if floats == 0:
-                              continue
-                          ws = torch.empty(floats, device=DEV, dtype=torch.float32)
-                          tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
-                      elif fx and kk > 1:
-                          floats, tiles = e.gemm_fix_workspace(m, n, kk)
-                          ws = torch.empty(max(floats, kk * m * n), device=DEV, dtype=torch.float32)
-                          tk = torch.zeros(tiles, device=DEV, dtype=torch.int32)
+                          tk = torch.zeros(counts, device=DEV, dtype=torch.int32)
                       else:
                           ws = torch.empty(max(1, kk * m * (n + 1)), device=DEV, dtype=torch.float32)
 
@@ -143,8 +126,8 @@ def main():
 
                       def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
                           e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
-                                 ws if (kk > 1 or tile in (4, 6, 8, 11, 12)) else None, eps, tile, tk, None, rws)
-                      res[f"v{impl}_ks{kk}_t{tile}" + (f"_diag{diag}" if diag else "") + (f"_g{grp}" if grp else "")  + ("_fix" if fx and kk > 1 else "") +
+                                 ws if (kk > 1 or tile in (11, 12)) else None, eps, tile, tk, None, rws)
+                      res[f"v{impl}_ks{kk}_t{tile}" + (f"_diag{diag}" if diag else "") + (f"_g{grp}" if grp else "")  + "" +
                           (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
                       run(0)
                       if mode != 0 or (diag & 255):  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)

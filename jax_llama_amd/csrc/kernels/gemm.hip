@@ -986,8 +986,9 @@ __global__ void __launch_bounds__(256, 1)
 // block b (128 x 128 of the tile, 64 KiB of fp32) is OWNED by split b * ks / 4; every other split's wave b publishes
 // its accumulators with write-through (sc1) stores, drains them (vmcnt(0)) and bumps the block's agent-scope counter,
 // then exits; the owner wave polls the counter (bounded: a missing partner sets the error word instead of hanging),
-// loads the ks - 1 partial blocks with sc1 loads, sums all ks in split order (deterministic, the reduce kernel's
-// order) and runs the ordinary epilogue on its block, then resets the counter (cdna_hip_programming.md Guideline 16).
+// lands the ks - 1 partner blocks in its idle K-tile slots by sc1 LDS-DMA, sums them onto its own in a fixed order
+// (at ks = 2 the reduce kernel's p0 + p1) and runs the ordinary epilogue on its block, then resets the counter
+// (cdna_hip_programming.md Guideline 16).
 // No second launch, no full-size slab re-read, and the residual's read-modify-write is spread over the owners.
 // Needs grid = tiles * ks <= CUs (one 128 KiB-LDS workgroup per CU, all resident at once); the launcher checks it.
 // Epilogues without a workgroup barrier only (residual, fp32 / bf16-direct store): the non-owner waves exit early.
@@ -1024,7 +1025,7 @@ __global__ void __launch_bounds__(256, 1)
   const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
   g4_mainloop<false>(g, lds, m0, n0, t0, KT, wu, lane, acc);
 
-  if constexpr (KS == 2) __syncthreads();  // every wave is past its last LDS read: the slots take the partner blocks
+  __syncthreads();  // every wave is past its last LDS read: the K-tile slots take the partner blocks
   const int owner = (wu * KS) >> 2;
   const size_t blk = (size_t)pid * 4 + wu;
   // this block's KS partial slots (64 KiB each); every access write-through / coherent (sc1)
@@ -1070,34 +1071,28 @@ __global__ void __launch_bounds__(256, 1)
         asm volatile("" : "=a"(acc[j][i]) : "0"(tsum));
       }
   } else {
-  // UI accumulator tiles per batch: (KS - 1) * UI partial loads in flight, branch-free (the loads are hand-counted
-  // asm: no control flow may separate them from their wait) with static register indices. The sum starts at the
-  // owner's own split and walks the others cyclically -- a fixed order per block, so the result is reproducible
-  // (at KS = 2 it equals the reduce kernel's p0 + p1 bit for bit).
-  constexpr int UI = KS == 2 ? 8 : (KS <= 4 ? 4 : 2);
+    // one owner wave per workgroup: the KS - 1 partner blocks land two at a time in the two (idle) 64 KiB K-tile slots
+    // (128 DMAs in flight per round), summed from the owner's own split cyclically -- a fixed order per block
+    char* const wl = reinterpret_cast<char*>(lds);
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+    for (int d0 = 1; d0 < KS; d0 += 2) {
+      const int nb = d0 + 1 < KS ? 2 : 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous round's reads are done with the slots
 #pragma unroll
-    for (int i0 = 0; i0 < 8; i0 += UI) {
-      u32x4 raw[UI][KS - 1];
+      for (int b = 0; b < nb; ++b) {
+        const u32x4* const src = slots + ((split + d0 + b) & (KS - 1)) * 4096 + lane;
 #pragma unroll
-      for (int u = 0; u < UI; ++u)
-#pragma unroll
-        for (int d = 1; d < KS; ++d) {
-          const int q = (split + d) & (KS - 1);
-          asm_load_sc1(raw[u][d - 1], slots + q * 4096 + (j * 8 + i0 + u) * 64 + lane);
-        }
+        for (int f = 0; f < 64; ++f) glds16_asm_sc1(src + f * 64, wl + b * 65536 + f * 1024);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int u = 0; u < UI; ++u) {
-        f32x4 tsum = g4_take(acc[j][i0 + u]);
+      for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int d = 0; d < KS - 1; ++d) {
-          pin(raw[u][d]);
-          tsum += __builtin_bit_cast(f32x4, raw[u][d]);
+        for (int i = 0; i < 8; ++i) {
+          f32x4 tsum = g4_take(acc[j][i]) + *reinterpret_cast<const f32x4*>(wl + (j * 8 + i) * 1024 + lane * 16);
+          if (nb == 2) tsum += *reinterpret_cast<const f32x4*>(wl + 65536 + (j * 8 + i) * 1024 + lane * 16);
+          asm volatile("" : "=a"(acc[j][i]) : "0"(tsum));
         }
-        asm volatile("" : "=a"(acc[j][i0 + u]) : "0"(tsum));  // back into its AGPRs (a VGPR copy of all 64 spills)
-      }
     }
   }
   if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -297,7 +297,8 @@ void linear_qkv(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor
 void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, Tensor table, Tensor positions,
                      Tensor kc, Tensor vc, Tensor slot, int64_t h, int64_t hkv, int64_t dh, Tensor q, Tensor kv_start,
                      Tensor out, c10::optional<Tensor> out_pack, Tensor ws, Tensor tickets, Tensor sync, int64_t t_cap,
-                     int64_t splits, c10::optional<Tensor> x_packed) {
+                     int64_t splits, c10::optional<Tensor> x_packed, int64_t spl, c10::optional<Tensor> sk_ws,
+                     c10::optional<Tensor> sk_tk) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "linear_qkv_attn: x bf16 [M, K]");
@@ -312,9 +313,21 @@ void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, T
   check(sync.scalar_type() == torch::kInt32 && sync.numel() >= 3, "sync int32 [3]");
   check(t_cap <= kc.size(2), "t_cap <= cache length");
   const jla::bf16_t* xp = packed_ptr(x_packed, m, k, "x_packed");
+  check(spl == 1 || spl == 2, "linear_qkv_attn: spl 1 or 2");
+  if (spl > 1) {  // the split qkv GEMV's slabs + tickets (skinny_workspace)
+    check(sk_ws.has_value() && sk_tk.has_value(), "linear_qkv_attn spl 2: sk_ws and sk_tk (skinny_workspace)");
+    check_gpu(*sk_ws, "sk_ws");
+    check_gpu(*sk_tk, "sk_tk");
+    check(sk_ws->scalar_type() == torch::kFloat32 && sk_tk->scalar_type() == torch::kInt32 &&
+              sk_tk->numel() >= n / 16,
+          "linear_qkv_attn: sk_ws fp32, sk_tk int32 [N / 16]");
+    qa.sk_ws = ptr<float>(*sk_ws);
+    qa.sk_tk = ptr<int32_t>(*sk_tk);
+    qa.sk_ws_floats = (int)sk_ws->numel();
+  }
   rc(jla::linear_qkv_attn(xp ? xp : cbf(x), w.data_ptr(), m, n, k, (float)rms_eps, qa, xp != nullptr, bf(out),
                           packed_ptr(out_pack, m, h * dh, "out_pack"), ptr<int32_t>(kv_start), ptr<float>(ws),
-                          ptr<int32_t>(tickets), ptr<int32_t>(sync), (int)t_cap, (int)splits, stream()),
+                          ptr<int32_t>(tickets), ptr<int32_t>(sync), (int)t_cap, (int)splits, (int)spl, stream()),
      "linear_qkv_attn");
 }
 
@@ -803,11 +816,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("rms_eps"), py::arg("table"), py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("h"), py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("kv_start"), py::arg("out"),
         py::arg("out_pack"), py::arg("ws"), py::arg("tickets"), py::arg("sync"), py::arg("t_cap"), py::arg("splits"),
-        py::arg("x_packed") = py::none());
-  m.def("qkv_attn_splits", [](int64_t m, int64_t b, int64_t hkv, int64_t rep, int64_t t_cap, int64_t n, int64_t cus) {
-    return jla::qkv_attn_splits((int)m, (int)b, (int)hkv, (int)rep, (int)t_cap, (int)n, (int)cus);
-  });
-  m.def("qkv_attn_occupancy", [](int64_t m, int64_t rep) { return jla::qkv_attn_occupancy((int)m, (int)rep); });
+        py::arg("x_packed") = py::none(), py::arg("spl") = 1, py::arg("sk_ws") = py::none(),
+        py::arg("sk_tk") = py::none());
+  m.def("qkv_attn_splits", [](int64_t m, int64_t b, int64_t hkv, int64_t rep, int64_t t_cap, int64_t n, int64_t cus,
+                              int64_t spl) {
+    return jla::qkv_attn_splits((int)m, (int)b, (int)hkv, (int)rep, (int)t_cap, (int)n, (int)cus, (int)spl);
+  }, py::arg("m"), py::arg("b"), py::arg("hkv"), py::arg("rep"), py::arg("t_cap"), py::arg("n"), py::arg("cus"),
+     py::arg("spl") = 1);
+  m.def("qkv_attn_occupancy", [](int64_t m, int64_t rep, int64_t spl) {
+    return jla::qkv_attn_occupancy((int)m, (int)rep, (int)spl);
+  }, py::arg("m"), py::arg("rep"), py::arg("spl") = 1);
   m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);

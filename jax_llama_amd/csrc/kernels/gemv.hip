@@ -562,14 +562,17 @@ struct FusedAttn {
   float scale_log2;
 };
 
-template <int MT, int NT, int NW, int U, bool XP, int REP>
+// SPL: K of the qkv GEMV cut over SPL workgroups per column group (the split GEMV's last-arriver sum; only that
+// workgroup writes q / the cache rows, but every qkv workgroup counts itself in the publish below)
+template <int MT, int NT, int NW, int U, bool XP, int REP, int SPL>
 __global__ void __launch_bounds__(256)
     qkv_attn_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, int M, int N, int K, float eps,
                     int use_rms, QKVArgs qa, FusedAttn fa) {
   static_assert(NW == 4, "4-wave workgroups (the attention side uses 4 waves x 32 keys)");
   if ((int)blockIdx.x < fa.grid_q) {
-    skinny_body<bf16_t, MT, NT, MODE_QKV, NW, U, XP, false, true>(x, W, nullptr, M, N, K, eps, use_rms, 0, 0, qa,
-                                                                  blockIdx.x, 0, 1);
+    skinny_body<bf16_t, MT, NT, MODE_QKV, NW, U, XP, (SPL > 1), true>(x, W, nullptr, M, N, K, eps, use_rms, 0, 0, qa,
+                                                                      (int)blockIdx.x / SPL, (int)blockIdx.x % SPL,
+                                                                      SPL);
     // publish (Guideline 16, sc1-store + agent-counter form): every storing wave drains its write-through stores,
     // the workgroup's barrier, then one agent-scope add
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -791,53 +794,62 @@ size_t qkv_attn_lds(int mt) {
 // workgroups of the fused launch that are resident at once per CU (occupancy API, one below its answer as a margin:
 // cdna_hip_programming.md warns it can be one block too high; at least 1)
 // (MT m-tiles: the GEMV ring depth U = 8 / MT, as launch_skinny)
-template <int MT, int REP>
+template <int MT, int REP, int SPL>
 static int qkv_attn_per_cu() {
   static int cached = 0;
   if (cached == 0) {
     int a = 0, b = 0;
     const size_t lds = qkv_attn_lds(MT);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, qkv_attn_kernel<MT, 1, 4, 8 / MT, false, REP>, 256, lds) !=
-            hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, qkv_attn_kernel<MT, 1, 4, 8 / MT, true, REP>, 256, lds) !=
-            hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, qkv_attn_kernel<MT, 1, 4, 8 / MT, false, REP, SPL>, 256,
+                                                     lds) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, qkv_attn_kernel<MT, 1, 4, 8 / MT, true, REP, SPL>, 256,
+                                                     lds) != hipSuccess)
       a = b = 1;
     const int n = a < b ? a : b;
     cached = n > 1 ? n - 1 : 1;
   }
   return cached;
 }
-template <int MT>
+template <int MT, int SPL>
 static int qkv_attn_per_cu_rep(int rep) {
   switch (rep) {
-    case 1: return qkv_attn_per_cu<MT, 1>();
-    case 2: return qkv_attn_per_cu<MT, 2>();
-    case 4: return qkv_attn_per_cu<MT, 4>();
-    case 8: return qkv_attn_per_cu<MT, 8>();
-    case 16: return qkv_attn_per_cu<MT, 16>();
+    case 1: return qkv_attn_per_cu<MT, 1, SPL>();
+    case 2: return qkv_attn_per_cu<MT, 2, SPL>();
+    case 4: return qkv_attn_per_cu<MT, 4, SPL>();
+    case 8: return qkv_attn_per_cu<MT, 8, SPL>();
+    case 16: return qkv_attn_per_cu<MT, 16, SPL>();
     default: return 0;
   }
 }
 
 // 0 when the fused launch does not apply (then the caller runs the qkv GEMV and the attention kernel). Every workgroup
 // of the launch must be resident at once (the attention workgroups wait for the qkv ones).
-int qkv_attn_occupancy(int M, int rep) {
-  return M <= 16 ? qkv_attn_per_cu_rep<1>(rep) : qkv_attn_per_cu_rep<2>(rep);
+int qkv_attn_occupancy(int M, int rep, int spl) {
+  if (spl == 2) return M <= 16 ? qkv_attn_per_cu_rep<1, 2>(rep) : qkv_attn_per_cu_rep<2, 2>(rep);
+  return M <= 16 ? qkv_attn_per_cu_rep<1, 1>(rep) : qkv_attn_per_cu_rep<2, 1>(rep);
 }
-int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus) {
+int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl) {
   if (M != B || M > 32 || (rep & (rep - 1)) || rep > 16 || t_cap > QA_MAX_SPLITS * QA_SPLIT_KEYS) return 0;
+  if ((spl != 1 && spl != 2) || (spl > 1 && (N >> 4) > GEMV_SPLIT_MAX_GROUPS)) return 0;
   const int splits = (t_cap + QA_SPLIT_KEYS - 1) / QA_SPLIT_KEYS;
-  const int grid = (N >> 4) + B * Hkv * splits;
-  return grid <= cus * qkv_attn_occupancy(M, rep) ? splits : 0;
+  const int grid = (N >> 4) * spl + B * Hkv * splits;
+  return grid <= cus * qkv_attn_occupancy(M, rep, spl) ? splits : 0;
 }
 
 int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
                     bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
-                    int t_cap, int splits, hipStream_t s) {
+                    int t_cap, int splits, int spl, hipStream_t s) {
   if (M <= 0) return 0;
   if (M > 32 || (N & 15) || (K & 31) || qa.Dh != AD6_DH || qa.S != 1 || qa.H % qa.Hkv) return -1;
   const int rep = qa.H / qa.Hkv;
-  const int grid_q = N >> 4, pairs = M * qa.Hkv;
+  const int grid_q = (N >> 4) * spl, pairs = M * qa.Hkv;
+  if (spl != 1 && spl != 2) return -1;
+  if (spl > 1) {  // the split GEMV's slabs and tickets (as launch_skinny checks them)
+    const int mt0 = M <= 16 ? 1 : 2;
+    if ((N >> 4) > GEMV_SPLIT_MAX_GROUPS || !qa.sk_ws || !qa.sk_tk || (K >> 5) < spl ||
+        (size_t)qa.sk_ws_floats < (size_t)(N >> 4) * spl * (mt0 * 256 + mt0 * 16))
+      return -3;
+  }
   if (splits < 1 || splits > QA_MAX_SPLITS || splits * QA_SPLIT_KEYS < t_cap) return -1;
   const FusedAttn fa{out, out_pack, kv_start, ws, tickets, sync, splits, grid_q, t_cap,
                      1.4426950408889634f / sqrtf((float)AD6_DH)};
@@ -846,20 +858,22 @@ int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float r
   const int mt = M <= 16 ? 1 : 2;
   const size_t lds = qkv_attn_lds(mt);
   const int grid = grid_q + pairs * splits;
-#define JLA_QA(MTV, R)                                                                                              \
-  if (mt == MTV && rep == R) {                                                                                      \
+#define JLA_QA_S(MTV, R, SP)                                                                                        \
+  if (mt == MTV && rep == R && spl == SP) {                                                                         \
     if (xp)                                                                                                         \
-      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, true, R><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M, N, K,   \
-                                                                          eps, use_rms, qa, fa);                    \
+      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, true, R, SP><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M, N, \
+                                                                              K, eps, use_rms, qa, fa);             \
     else                                                                                                            \
-      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, false, R><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M, N, K,  \
-                                                                           eps, use_rms, qa, fa);                   \
+      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, false, R, SP><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M,  \
+                                                                               N, K, eps, use_rms, qa, fa);         \
     JLA_CHECK_LAUNCH();                                                                                             \
     return 0;                                                                                                       \
   }
+#define JLA_QA(MTV, R) JLA_QA_S(MTV, R, 1) JLA_QA_S(MTV, R, 2)
   JLA_QA(1, 1) JLA_QA(1, 2) JLA_QA(1, 4) JLA_QA(1, 8) JLA_QA(1, 16)
   JLA_QA(2, 1) JLA_QA(2, 2) JLA_QA(2, 4) JLA_QA(2, 8) JLA_QA(2, 16)
 #undef JLA_QA
+#undef JLA_QA_S
   return -1;
 }
 

@@ -44,11 +44,11 @@ constexpr long long TPRES_REGION = 64 * 64 * 4;  // up to 64 rows x 64 columns x
 // fused small-batch qkv projection + decode attention (gemv.hip qkv_attn_kernel): one launch; splits from
 // qkv_attn_splits (0 = not applicable: run the two kernels); ws >= pairs * splits * rep * 132 floats, tickets >= pairs,
 // sync >= 3 int32 (zeroed once, self-resetting)
-int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus);
-int qkv_attn_occupancy(int M, int rep);  // resident workgroups per CU the fused launch counts on
+int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl = 1);
+int qkv_attn_occupancy(int M, int rep, int spl = 1);  // resident workgroups per CU the fused launch counts on
 int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
                     bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
-                    int t_cap, int splits, hipStream_t s);
+                    int t_cap, int splits, int spl, hipStream_t s);  // spl 2: K of the qkv GEMV over 2 (qa.sk_ws/sk_tk)
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
 // split-K GEMV variants 16 / 18 / 26 (K over gridDim.y workgroups per column group, last arriver sums + epilogue): their slab

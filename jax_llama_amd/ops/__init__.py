@@ -491,11 +491,15 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
 
 # Fused small-batch decode: the qkv GEMV and the attention in ONE launch (csrc/kernels/gemv.hip qkv_attn_kernel: the
 # attention workgroups prefetch their K / V step while the qkv workgroups stream the weights, then wait on the qkv
-# workgroups' write-through publish). Used where it measured faster (profiles/r5_qkv_attn_fused_ab.jsonl): M <= 4 rows
-# with >= 8 query heads per kv head (the 70B tensor-parallel shard: one kv head per rank) -- 4.92 -> 4.82 ms per token
-# at B = 1; at Llama-3-8B B = 1 (rep 4: 384 qkv workgroups on one 4-wave form) 2.92 -> 3.22 and at the shard's
-# B = 32 6.10 -> 6.58 the tuned standalone GEMVs win. JLA_QKV_ATTN=0: never; =2: wherever the launch fits.
+# workgroups' write-through publish). Used where it measured faster (profiles/r5_qkv_attn_fused_ab.jsonl,
+# r5_qkv_attn_fused_split_ab.jsonl): M <= 4 rows with >= 8 query heads per kv head (the 70B tensor-parallel shard: one
+# kv head per rank) -- 4.88 -> 4.77 ms per token at B = 1 with the split qkv part; at Llama-3-8B B = 1 (rep 4: 384 qkv
+# workgroups) 2.93 -> 3.24 and at the shard's B = 8 / 32 the tuned standalone GEMVs win. JLA_QKV_ATTN=0: never;
+# =2: wherever the launch fits.
 QKV_ATTN = int(os.environ.get("JLA_QKV_ATTN", "1"))
+# K of the fused launch's qkv GEMV over 2 workgroups per column group (the split GEMV's last-arriver sum) when the grid
+# still fits the CUs; JLA_QKV_ATTN_SPL=1: one workgroup per column group (A/B)
+QKV_ATTN_SPL = int(os.environ.get("JLA_QKV_ATTN_SPL", "2"))
 _CUS = {}
 
 
@@ -517,15 +521,23 @@ def qkv_attention_splits(x: torch.Tensor, w, k_cache: torch.Tensor, seq_len: int
     if QKV_ATTN == 1 and (m > 4 or n_heads < 8 * n_kv_heads):
         return 0
     return int(ext().qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n,
-                                     _num_cus(x.device)))
+                                     _num_cus(x.device), 1))
+
+
+def _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, device) -> int:
+    if QKV_ATTN_SPL > 1 and e.qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n,
+                                               _num_cus(device), 2) > 0:
+        return 2
+    return 1
 
 
 def linear_qkv_attention(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.Tensor, positions: torch.Tensor,
                          k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor, n_heads: int,
                          n_kv_heads: int, head_dim: int, splits: int, x_packed: Optional[torch.Tensor] = None,
-                         out_packed: Optional[torch.Tensor] = None) -> torch.Tensor:
+                         out_packed: Optional[torch.Tensor] = None, spl: Optional[int] = None) -> torch.Tensor:
     """One decode token per row: ``linear_qkv_rope`` + ``attention`` in one launch (``qkv_attention_splits`` > 0).
-    Returns the attention output ``[B, H * Dh]`` bf16 (``out_packed``: its packed copy for the o projection)."""
+    Returns the attention output ``[B, H * Dh]`` bf16 (``out_packed``: its packed copy for the o projection).
+    ``spl``: K of the qkv GEMV over 1 or 2 workgroups per column group (default: 2 where the grid fits)."""
     e = ext()
     m = x.shape[0]
     dev = x.device
@@ -535,10 +547,14 @@ def linear_qkv_attention(x: torch.Tensor, w, rms_eps: Optional[float], table: to
     ws = workspace.get("qa_ws", m * n_kv_heads * splits * rep * (head_dim + 4), torch.float32, dev)
     tickets = workspace.get_zeroed("qa_tickets", max(m * n_kv_heads, 64), torch.int32, dev)
     sync = workspace.get_zeroed("qa_sync", 4, torch.int32, dev)
+    spl = _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, dev) if spl is None else int(spl)
+    sk_ws = sk_tk = None
+    if spl > 1:
+        sk_ws, sk_tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, dev)
     e.linear_qkv_attn(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
                       positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, dev), n_heads,
                       n_kv_heads, head_dim, q, kv_start, out, out_packed, ws, tickets, sync, k_cache.shape[2], splits,
-                      x_packed)
+                      x_packed, spl, sk_ws, sk_tk)
     return out
 
 

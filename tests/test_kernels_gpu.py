@@ -892,14 +892,16 @@ def test_attention_decode_mfma_v6(wpp, rep, t, slot, masked):
     assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())
 
 
+@pytest.mark.parametrize("spl", [1, 2])
 @pytest.mark.parametrize("b,hkv,rep", [(1, 1, 8), (2, 8, 4), (4, 2, 1), (1, 2, 16), (3, 1, 8), (24, 1, 8), (32, 1, 8)])
 @pytest.mark.parametrize("t,slot", [(40, 17), (200, 199), (384, 300), (512, 130)])
-def test_qkv_attention_fused_launch(b, hkv, rep, t, slot):
+def test_qkv_attention_fused_launch(b, hkv, rep, t, slot, spl):
     """The fused small-batch decode launch (gemv.hip qkv_attn_kernel: qkv GEMV + RoPE + KV write on one set of
     workgroups, the attention on another that prefetches its K / V step and waits for the write-through publish)
     against the fp32 reference of linear_qkv_rope + attention: left padding inside a split, a row with no valid key,
     the new key at the end of a 32-key step or of a 128-key split; the cache rows it wrote equal the unfused kernel's,
-    the packed output equals the row-major one, and a second launch agrees (the counters reset themselves)."""
+    the packed output equals the row-major one, and a second launch agrees (the counters reset themselves); with the
+    qkv GEMV's K over one or two workgroups per column group (spl)."""
     e = ops.ext()
     dh, k = 128, 1024
     h = hkv * rep
@@ -920,23 +922,27 @@ def test_qkv_attention_fused_launch(b, hkv, rep, t, slot):
     kd, vd = kc0.to(DEV), vc0.to(DEV)
     xd = x.to(DEV)
     sl = torch.tensor([slot], dtype=torch.int32, device=DEV)
-    splits = e.qkv_attn_splits(b, b, hkv, rep, t, n, ops._num_cus(xd.device))
-    assert splits == (t + 127) // 128, (splits, e.qkv_attn_occupancy(b, rep))
+    splits = e.qkv_attn_splits(b, b, hkv, rep, t, n, ops._num_cus(xd.device), spl)
+    if spl == 2 and splits == 0:  # (twice the qkv workgroups: this grid no longer fits the CUs at once)
+        assert e.qkv_attn_splits(b, b, hkv, rep, t, n, ops._num_cus(xd.device), 1) > 0
+        pytest.skip("the split qkv grid does not fit the CUs")
+    assert splits == (t + 127) // 128, (splits, e.qkv_attn_occupancy(b, rep, spl))
     packed = ops.packed_empty(b, h * dh, DEV)
     got = ops.linear_qkv_attention(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), kd, vd, sl, kv_start.to(DEV), h, hkv, dh,
-                                   splits, out_packed=packed)
+                                   splits, out_packed=packed, spl=spl)
     again = ops.linear_qkv_attention(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), kd, vd, sl, kv_start.to(DEV), h, hkv,
-                                     dh, splits)
+                                     dh, splits, spl=spl)
     torch.cuda.synchronize()
     _close(got, expect, 2e-2, 2e-2)
     assert torch.equal(got, again)
     assert torch.equal(ref.unpack_act(packed.cpu(), b), got.cpu())
     if b > 2:
         assert got[2].float().abs().max().item() == 0.0  # kv_start = slot + 1: no valid key
-    # the cache rows: as the unfused qkv GEMV of the same geometry (variant 1: one tile x 4 waves) writes them
+    # the cache rows: as the unfused qkv GEMV of the same geometry (variant 1: one tile x 4 waves; spl 2: variant 16,
+    # the same with K over 2 workgroups) writes them
     ku, vu = kc0.to(DEV), vc0.to(DEV)
     try:
-        ops.GEMV_VARIANT = 1
+        ops.GEMV_VARIANT = 1 if spl == 1 else 16
         ops.linear_qkv_rope(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), ku, vu, sl, 1, h, hkv, dh)
         torch.cuda.synchronize()
     finally:

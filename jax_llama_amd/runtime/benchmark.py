@@ -133,8 +133,10 @@ def calibration(device) -> Dict[str, object]:
         prefetch_kernel, 16 loads in flight per lane, 4 workgroups per CU) -- the same kind of traffic as a decode
         weight stream, so it and the rooflines (weight bytes / 6.29e12) compare like with like; ``copy_tbps`` (a torch
         copy, read + write bytes) is kept beside it;
-      * ``sclk_mhz_under_mfma_load``: the shader clock measured in-kernel under a full matrix load (cycle counter over
-        the constant 100 MHz counter), and ``sclk_max_level`` from sysfs."""
+      * ``sclk_mhz_mfma_probe``: the shader clock measured in-kernel (cycle counter over the constant 100 MHz counter)
+        under a dependent-MFMA loop on constant, low-entropy operands -- an upper bound: a GEMM on random data draws
+        more power and the chip gives clock back (gate_up at M = 8192 ran at ~1.65 GHz effective under the profiler,
+        profiles/r5_pmc_gemm4_vs_hipblaslt_gateup8192.txt); ``sclk_max_level`` from sysfs."""
     from .. import ops
     from ..models.weights import PackedLinear
     out: Dict[str, object] = {}
@@ -173,7 +175,7 @@ def calibration(device) -> Dict[str, object]:
     torch.cuda.synchronize(device)
     cyc, rt = (int(v) for v in ticks[:2].tolist())
     if rt > 0:
-        out["sclk_mhz_under_mfma_load"] = round(cyc / rt * 100.0, 1)
+        out["sclk_mhz_mfma_probe"] = round(cyc / rt * 100.0, 1)
     cur, top = _sclk_levels()
     if top is not None:
         out["sclk_max_level"] = top

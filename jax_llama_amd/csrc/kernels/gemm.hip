@@ -979,6 +979,44 @@ __global__ void __launch_bounds__(256, 1)
       G4Epi{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, ssq_ws, rms_inv}, qa);
 }
 
+// Persistent gemm4 (tile config 13): one workgroup per CU walks the launch order round by round (tile wg, wg + CUs,
+// ...), so a CU's next tile starts without a workgroup teardown and relaunch, and the CUs drift apart over the rounds:
+// their epilogues (the residual's fp32 read-modify-write above all) stop arriving at HBM as one chip-wide burst.
+template <int MODE, int RMSM>
+__global__ void __launch_bounds__(256, 1)
+    gemm4p_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int tiles_m, int tiles_n,
+                  float rms_eps, QKVArgs qa, const float* __restrict__ rms_inv, int group_m) {
+  constexpr bool RMS = RMSM == 1;
+  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];
+  const int lane0 = threadIdx.x & 63;
+  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const G4Args g{x, W, out, M, N, K, K >> 6, tiles_m, tiles_n};
+  const G4Epi ep{out, M, N, K, accumulate, out_f32, mirror, tiles_n, rms_eps, nullptr, rms_inv};
+  for (int pid = wg; pid < tiles; pid += nwg) {
+    int tm, tn;
+    g4_tile_coords(pid, tiles_m, tiles_n, tm, tn, group_m);
+    const int m0 = tm * G4_BM, n0 = tn * G4_BN;
+    // the lane index laundered once per tile: the lane-dependent address math of the main loop and the unrolled
+    // epilogue would otherwise be hoisted out of the tile loop and kept live (spills)
+    int lane;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane0));
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss[4] = {0.f, 0.f, 0.f, 0.f};
+    g4_mainloop<RMS>(g, lds, m0, n0, 0, K >> 6, wu, lane, acc, ss);
+    g4_epilogue<MODE, RMSM>(acc, ss, lds, wu, lane, m0, n0, 0, ep, qa);
+    __syncthreads();  // the epilogue's staging / row scales are done with LDS before the next tile's DMA
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // gemm4 split-K with an in-kernel exchange (tile config 8): for outputs with too few 256 x 256 tiles to fill the chip
 // (Llama-3-8B at M = 2048: o / down have 128 tiles for 256 CUs) the K range is cut over ks co-resident workgroups per
@@ -1263,8 +1301,9 @@ constexpr int G4_TILE = 7;
 constexpr int G4N_TILE = 10;
 static bool g_g4_default = true;
 void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
+constexpr int G4P_TILE = 13;  // persistent gemm4 (gemm4p_kernel)
 static bool use_g4(int tile, int M, int K) {
-  return (K & 63) == 0 && (tile == G4_TILE || (tile == 0 && g_g4_default && M > 128));
+  return (K & 63) == 0 && (tile == G4_TILE || tile == G4P_TILE || (tile == 0 && g_g4_default && M > 128));
 }
 
 // Tile rasterisation: the launch order walks groups of gm m-tiles across every n-tile (g4_tile_coords), so the 32
@@ -1282,12 +1321,29 @@ static int g_g5_diag = 0;  // tools only (gemm5ws.h diag bits 1-16; gemm4 store 
 template <int MODE, int NJ = 8>
 static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa,
-                      float* rms_ws = nullptr) {
+                      float* rms_ws = nullptr, bool persistent = false) {
   const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + 32 * NJ - 1) / (32 * NJ);
   const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
   const int grid = tm * tn * ksplit;
   const int gm = g4_group_m(tm, tn, K);
+  if constexpr (NJ == 8 && MODE != MODE_PARTIAL && MODE != MODE_ARGMAX) {
+    if (persistent && ksplit == 1) {  // tile config 13: one workgroup per CU over every tile
+      const int pg = min(grid, num_cus());
+      if (rms && rms_ws != nullptr) {
+        if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
+        gemm4p_kernel<MODE, 2><<<pg, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, qa,
+                                                  rms_ws, gm);
+      } else if (rms) {
+        gemm4p_kernel<MODE, 1><<<pg, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, qa,
+                                                  nullptr, gm);
+      } else {
+        gemm4p_kernel<MODE, 0><<<pg, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, tm, tn, rms_eps, qa,
+                                                  nullptr, gm);
+      }
+      return;
+    }
+  }
   if constexpr (NJ != 8) {  // 256 x 128 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
     if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
       if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
@@ -1370,7 +1426,11 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     }
   }
   if (use_g4(tile, M, K)) {
-    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
+    // persistent for the residual epilogue at prefill sizes: o / down at M = 32768 3.5 / 2.4 % faster (the CUs'
+    // fp32 read-modify-write bursts desynchronise); the store / SwiGLU / QKV epilogues lose 1.5-3.6 % that way
+    // (profiles/r5_gemm4_persistent_ab.jsonl)
+    const bool persist = tile == G4P_TILE || (MODE == MODE_RESIDUAL && tile == 0 && ksplit == 1 && M >= 4096);
+    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, persist);
     return;
   }
   const int cfg = tile_cfg(tile, M);

@@ -217,6 +217,42 @@ def test_gemm4_exchange_split(m, n, k, ks):
     torch.testing.assert_close(a1[1].cpu(), a1[0].cpu().to(BF16), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("m,n,k", [(2048, 4096, 1024), (700, 2560, 512), (4352, 1536, 256)])
+def test_gemm4_persistent_identical(m, n, k):
+    """Tile config 13 (persistent gemm4: one workgroup per CU over every tile) runs the same per-tile MFMA chain and
+    epilogues as tile 7: store (fp32 / bf16), SwiGLU with the fused norm (precomputed / in-loop statistic) and the
+    residual + mirror are bit-identical; ragged M / N and more tiles than CUs included."""
+    e = ops.ext()
+    torch.manual_seed(m + n + k + 13)
+    x = torch.randn(m, k).to(BF16)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    pg = PackedLinear.from_dense(w, DEV)
+    gu = ref.interleave_gate_up(w[: n // 2], w[n // 2:])
+    gp = PackedLinear.from_dense(gu, DEV)
+    xg = x.to(DEV)
+    h0 = torch.randn(m, n).to(DEV)
+    rw = torch.empty(m, device=DEV)
+
+    def run(tile):
+        o = torch.empty(m, n, dtype=torch.float32, device=DEV)
+        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, 1, None, -1.0, tile)
+        ob = torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, None, 1e-5, tile, None, None, rw)
+        o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile, None, None, rw)
+        o3 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+        e.gemm(xg, gp.weight, n, k, o3, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile)
+        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, None, -1.0, tile)
+        torch.cuda.synchronize()
+        return [o, ob, o2, o3, hg, mir]
+
+    a, b = run(13), run(G4)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), f"output {i}: persistent differs from tile 7"
+    _close(a[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+
+
 def test_gemm4_exchange_split_guards():
     """The exchange plan needs every workgroup resident (tiles x split <= CUs) and a real split."""
     e = ops.ext()

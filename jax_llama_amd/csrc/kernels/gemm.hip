@@ -1139,26 +1139,48 @@ __global__ void __launch_bounds__(256, 1)
 }
 
 
-// Sum the split-K partials (fixed order) and apply the epilogue. One thread = 4 consecutive
-// columns of one row (two RoPE pairs; a 16-column tile never straddles a float4).
+// Sum of the ksplit fp32 slabs at float4 e4 in split order: the loads of up to 8 splits are issued before the first
+// add (the round-4 loop waited on each split in turn: 12 dependent L2/HBM round trips for the 70B shard's qkv at M =
+// 256, 9 us for 1.3 MB of output). Same addition order as before, so bit for bit the same sums.
+__device__ __forceinline__ float4 sum_splits(const float* __restrict__ ws, int ksplit, size_t slab4, size_t e4) {
+  const float4* p = reinterpret_cast<const float4*>(ws) + e4;
+  float4 v = p[0];
+  for (int s0 = 1; s0 < ksplit; s0 += 8) {
+    float4 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s0 + j < ksplit) q[j] = p[(size_t)(s0 + j) * slab4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s0 + j < ksplit) {
+        v.x += q[j].x;
+        v.y += q[j].y;
+        v.z += q[j].z;
+        v.w += q[j].w;
+      }
+  }
+  return v;
+}
+
+// Sum the split-K partials (fixed order) and apply the epilogue. One thread = 4 consecutive columns of one row (two
+// RoPE pairs; a 16-column tile never straddles a float4); SwiGLU: 4 consecutive output columns, i.e. the gate float4
+// and the up float4 16 columns to its right (the launch covers M * N / 8 threads there).
 template <int MODE>
 __global__ void __launch_bounds__(256)
     gemm_reduce_kernel(const float* __restrict__ ws, int ksplit, void* __restrict__ out, int M, int N,
                        int accumulate, int out_f32, bf16_t* __restrict__ mirror, QKVArgs qa,
                        const float* __restrict__ ssq, int K, float rms_eps) {
-  const size_t e4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total4 = (size_t)M * N / 4;
-  if (e4 >= total4) return;
+  const size_t t4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t slab4 = (size_t)M * N / 4;
+  if (t4 >= (MODE == MODE_SWIGLU ? slab4 >> 1 : slab4)) return;
+  size_t e4 = t4;
+  if constexpr (MODE == MODE_SWIGLU) {  // output float4 t4 -> the gate float4 of its 32-column (gate, up) tile pair
+    const size_t oq = (size_t)N >> 3, mo = t4 / oq, c = (t4 - mo * oq) * 4;
+    e4 = (mo * N + (c >> 4) * 32 + (c & 15)) >> 2;
+  }
   const size_t idx = e4 * 4;
   const int m = (int)(idx / N), col = (int)(idx - (size_t)m * N);
-  float4 v = reinterpret_cast<const float4*>(ws)[e4];
-  for (int s = 1; s < ksplit; ++s) {
-    const float4 p = reinterpret_cast<const float4*>(ws + (size_t)s * M * N)[e4];
-    v.x += p.x;
-    v.y += p.y;
-    v.z += p.z;
-    v.w += p.w;
-  }
+  float4 v = sum_splits(ws, ksplit, slab4, e4);
   float rs = 1.f;  // fused RMSNorm: the splits' partial sums of squares of row m (fixed order)
   if (ssq) {
     float t = 0.f;
@@ -1172,31 +1194,19 @@ __global__ void __launch_bounds__(256)
   float vv[4] = {v.x, v.y, v.z, v.w};
   if constexpr (MODE == MODE_SWIGLU) {
     // gate tile t = 2p holds columns [32p, 32p+16), the up tile the next 16: pair the two halves
-    const int tile = col >> 4, c0 = col & 15;
-    if ((tile & 1) == 0) {
-      const float4 u = [&] {
-        float4 a = reinterpret_cast<const float4*>(ws)[e4 + 4];
-        for (int s = 1; s < ksplit; ++s) {
-          const float4 p = reinterpret_cast<const float4*>(ws + (size_t)s * M * N)[e4 + 4];
-          a.x += p.x;
-          a.y += p.y;
-          a.z += p.z;
-          a.w += p.w;
-        }
-        a.x *= rs;
-        a.y *= rs;
-        a.z *= rs;
-        a.w *= rs;
-        return a;
-      }();
-      const float uu[4] = {u.x, u.y, u.z, u.w};
-      bf16_t* o = static_cast<bf16_t*>(out) + (size_t)m * (N >> 1) + (tile >> 1) * 16 + c0;
-      const uint2 pk = make_uint2(pack2bf(silu(vv[0]) * uu[0], silu(vv[1]) * uu[1]),
-                                  pack2bf(silu(vv[2]) * uu[2], silu(vv[3]) * uu[3]));
-      *reinterpret_cast<uint2*>(o) = pk;
-      // decode M: also the packed copy (common.h pack_off) the next projection's packed-x GEMV reads
-      if (qa.pack) *reinterpret_cast<uint2*>(qa.pack + pack_off(m, (tile >> 1) * 16 + c0, N >> 1)) = pk;
-    }
+    const int tile = col >> 4, c0 = col & 15;  // tile is even: the gate half of the pair
+    float4 u = sum_splits(ws, ksplit, slab4, e4 + 4);
+    u.x *= rs;
+    u.y *= rs;
+    u.z *= rs;
+    u.w *= rs;
+    const float uu[4] = {u.x, u.y, u.z, u.w};
+    bf16_t* o = static_cast<bf16_t*>(out) + (size_t)m * (N >> 1) + (tile >> 1) * 16 + c0;
+    const uint2 pk = make_uint2(pack2bf(silu(vv[0]) * uu[0], silu(vv[1]) * uu[1]),
+                                pack2bf(silu(vv[2]) * uu[2], silu(vv[3]) * uu[3]));
+    *reinterpret_cast<uint2*>(o) = pk;
+    // decode M: also the packed copy (common.h pack_off) the next projection's packed-x GEMV reads
+    if (qa.pack) *reinterpret_cast<uint2*>(qa.pack + pack_off(m, (tile >> 1) * 16 + c0, N >> 1)) = pk;
   } else if constexpr (MODE == MODE_RESIDUAL) {
     float4* o = reinterpret_cast<float4*>(static_cast<float*>(out) + idx);
     float4 r = *o;
@@ -1495,7 +1505,7 @@ static int num_cus() {
 static int launch_reduce(const float* ws, int ksplit, void* out, int M, int N, int K, int mode, int accumulate,
                          int out_f32, bf16_t* mirror, const QKVArgs* qkv, const float* ssq, float rms_eps,
                          hipStream_t s) {
-  const size_t total4 = (size_t)M * N / 4;
+  const size_t total4 = (size_t)M * N / (mode == MODE_SWIGLU ? 8 : 4);
   const int rgrid = (int)((total4 + 255) / 256);
   QKVArgs qa{};
   if (qkv) qa = *qkv;

@@ -333,16 +333,17 @@ class LLaMAForCausalLM:
         ``h`` and writes its bf16 mirror ``hb`` (the A operand of the next projection). TP>1: the GEMM
         writes only this rank's partial (``comm.reduce_dtype``, bf16 by default). Decode-sized partials: one
         custom collective kernel (or the GEMV itself, ``comm.FUSED``) sums them in fp32 in rank order, adds them to
-        ``h`` and rewrites ``hb``. Prefill-sized partials: RCCL sums them upcast to fp32 (RCCL's order; bf16 on the
-        wire only with ``JLA_TP_RCCL_BF16=1``), then one kernel adds into ``h`` (``comm.all_reduce_residual_``;
+        ``h`` and rewrites ``hb``. Prefill-sized partials: the GEMM writes them in fp32 (``comm.partial_dtype``) and RCCL
+        sums them (RCCL's order; bf16 on the wire only with ``JLA_TP_RCCL_BF16=1``), then one kernel adds into ``h`` (``comm.all_reduce_residual_``;
         reference ``partition.py:67,70``)."""
         if self.comm.size == 1:
             ops.linear_residual(x, w, h, mirror=hb, x_packed=x_packed, mirror_packed=mirror_packed)
         elif self.comm.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=mirror_packed):
             pass  # decode: the GEMV exchanged its partials itself (one kernel; comm.FUSED)
         else:
-            part = ops.linear(x, w, out_dtype=self.comm.reduce_dtype, x_packed=x_packed)
-            self.comm.all_reduce_residual_(part, h, hb, hb_pack=mirror_packed)
+            dt = self.comm.partial_dtype(x.numel() // x.shape[-1] * w.n, x.is_cuda)
+            part = ops.linear(x, w, out_dtype=dt, x_packed=x_packed)
+            self.comm.all_reduce_residual_(part, h, hb, hb_pack=mirror_packed, owned=True)
 
     def forward_tokens(self, ids: torch.Tensor, positions: torch.Tensor, cache: KVCache, slot0,
                        kv_start: torch.Tensor, key_mask: Optional[torch.Tensor] = None,

@@ -99,10 +99,24 @@ class TPComm:
         dist.all_reduce(t, group=self.group)
         return t
 
+    def partial_dtype(self, numel: int, is_cuda: bool) -> torch.dtype:
+        """The dtype a row-parallel GEMM should write its ``numel``-element partial in: ``reduce_dtype`` when the
+        custom kernels take it (they sum bf16 partials in fp32 themselves), else fp32 whenever
+        ``all_reduce_residual_`` would upcast a bf16 partial anyway -- the GEMM's fp32 store replaces the bf16
+        rounding, the upcast copy and its allocation (the bytes on the wire are the same)."""
+        dt = self.reduce_dtype
+        if dt != torch.bfloat16 or self.size == 1:
+            return dt
+        c = self.custom
+        if c is not None and is_cuda and 0 < numel * 2 <= c.max_bytes and (numel * 2) % 16 == 0:
+            return dt
+        return dt if (RCCL_BF16 and is_cuda and dist.get_backend(self.group) != "gloo") else torch.float32
+
     def all_reduce_residual_(self, partial: torch.Tensor, h: torch.Tensor, hb: Optional[torch.Tensor],
-                             hb_pack: Optional[torch.Tensor] = None):
+                             hb_pack: Optional[torch.Tensor] = None, owned: bool = False):
         """``h (fp32) += sum over ranks of partial``; ``hb = bf16(h)`` when given; ``hb_pack``: a packed-layout
-        copy of hb too (custom path only -- callers ask ``packs_residual`` first)."""
+        copy of hb too (custom path only -- callers ask ``packs_residual`` first). ``owned``: the caller's partial
+        is scratch and may be reduced in place."""
         if self.size > 1 and self.custom is not None and hb is not None and self.custom.can_handle(partial):
             self.custom.all_reduce_residual_(partial, h, hb, hb_pack=hb_pack)
             return h
@@ -116,7 +130,7 @@ class TPComm:
             p = partial if partial.is_contiguous() else partial.contiguous()
             if p.dtype == torch.bfloat16 and not (RCCL_BF16 and p.is_cuda and not self._host_staged(p)):
                 p = p.float()
-            elif p.data_ptr() == partial.data_ptr():
+            elif p.data_ptr() == partial.data_ptr() and not owned:
                 p = p.clone()  # never reduce the caller's buffer in place
             self.all_reduce_(p)
         else:

@@ -938,15 +938,16 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
   }
 }
 
-template <int MODE, int RMSM, int NJ = 8, int DIAG = 0>
+template <int MODE, int RMSM, int NJ = 8, int DIAG = 0, bool W3 = false>
 __global__ void __launch_bounds__(256, 1)
     gemm4_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
                  int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
                  float rms_eps, float* __restrict__ ssq_ws, QKVArgs qa, const float* __restrict__ rms_inv,
                  int group_m) {
   constexpr bool RMS = RMSM == 1;
-  // the two K-tile slots; after the loop: the epilogue's staging (128 KiB) + 1 KiB of row scales
-  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];
+  // the two K-tile slots (W3: two x + three W slots, all 160 KiB); after the loop: the epilogue's staging (128 KiB)
+  // + 1 KiB of row scales
+  __shared__ u32x4 lds[W3 ? 2 * G4_A_U4 + 3 * G4_B_U4 : 2 * G4_SLOT_U4 + 64];
   const int lane = threadIdx.x & 63;
   const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wu >> 1, wc = wu & 1;
@@ -972,7 +973,7 @@ __global__ void __launch_bounds__(256, 1)
     static_assert(!RMS, "the 256 x 128 tile: precomputed statistic");
     g4n_mainloop<NJ>(g, lds, m0, n0, t0, KT, wu, lane, acc);
   } else {
-    g4_mainloop<RMS, decltype(acc), DIAG>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
+    g4_mainloop<RMS, decltype(acc), DIAG, W3>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
   }
   g4_epilogue<MODE, RMSM, decltype(acc), NJ>(
       acc, ss, lds, wu, lane, m0, n0, split,
@@ -1312,8 +1313,12 @@ constexpr int G4N_TILE = 10;
 static bool g_g4_default = true;
 void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
 constexpr int G4P_TILE = 13;  // persistent gemm4 (gemm4p_kernel)
+// tile config 14: gemm4 with the weight operand three K-tiles deep (g4_mainloop W3, 160 KiB of LDS) -- for the small-M
+// plans whose weights stream from HBM with few tiles sharing them
+constexpr int G4D_TILE = 14;
 static bool use_g4(int tile, int M, int K) {
-  return (K & 63) == 0 && (tile == G4_TILE || tile == G4P_TILE || (tile == 0 && g_g4_default && M > 128));
+  return (K & 63) == 0 &&
+         (tile == G4_TILE || tile == G4P_TILE || tile == G4D_TILE || (tile == 0 && g_g4_default && M > 128));
 }
 
 // Tile rasterisation: the launch order walks groups of gm m-tiles across every n-tile (g4_tile_coords), so the 32
@@ -1331,7 +1336,7 @@ static int g_g5_diag = 0;  // tools only (gemm5ws.h diag bits 1-16; gemm4 store 
 template <int MODE, int NJ = 8>
 static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int ksplit, float rms_eps, float* ssq, hipStream_t s, const QKVArgs& qa,
-                      float* rms_ws = nullptr, bool persistent = false) {
+                      float* rms_ws = nullptr, bool persistent = false, bool deep = false) {
   const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + 32 * NJ - 1) / (32 * NJ);
   const int KS64 = K >> 6, kc = (KS64 + ksplit - 1) / ksplit;  // splits past the end run no K-tile (zero slabs)
   const bool rms = MODE != MODE_RESIDUAL && rms_eps >= 0.f;
@@ -1379,9 +1384,13 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
       return;
     }
   }
-#define JLA_G4(R, INV)                                                                                          \
-  gemm4_kernel<MODE, R><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, \
-                                             ssq, qa, INV, gm)
+#define JLA_G4(R, INV)                                                                                             \
+  if (deep)                                                                                                         \
+    gemm4_kernel<MODE, R, 8, 0, true><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, \
+                                                           tn, rms_eps, ssq, qa, INV, gm);                          \
+  else                                                                                                              \
+    gemm4_kernel<MODE, R><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn, rms_eps, \
+                                               ssq, qa, INV, gm)
   if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
     if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;  // (K % 8 == 0 always holds here)
     JLA_G4(2, rms_ws);
@@ -1440,7 +1449,8 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     // fp32 read-modify-write bursts desynchronise); the store / SwiGLU / QKV epilogues lose 1.5-3.6 % that way
     // (profiles/r5_gemm4_persistent_ab.jsonl)
     const bool persist = tile == G4P_TILE || (MODE == MODE_RESIDUAL && tile == 0 && ksplit == 1 && M >= 4096);
-    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, persist);
+    launch_g4<MODE>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, persist,
+                    tile == G4D_TILE);
     return;
   }
   const int cfg = tile_cfg(tile, M);

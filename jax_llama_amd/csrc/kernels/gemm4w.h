@@ -73,7 +73,7 @@ struct G4Args {
 // kept alive), 2 no LDS-DMA past the prologue (every K-tile re-reads the first two tiles' slots). (Moving the
 // sub-step's fragment reads or DMAs into its first 8 slots, two per slot, measured within noise or slower:
 // profiles/r5_gemm4_schedule_ab.jsonl.)
-template <bool RMS = false, typename Acc, int DIAG = 0>
+template <bool RMS = false, typename Acc, int DIAG = 0, bool W3 = false>
 JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc,
                          float* ss = nullptr) {
   const int wr = wu >> 1, wc = wu & 1;
@@ -96,12 +96,15 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
     const int nt = min((n0 >> 4) + (f >> 1), NTT - 1) - (n0 >> 4);
     offB[j] = ((unsigned)nt * (unsigned)KS + (unsigned)(f & 1)) * 1024u + 16u * (unsigned)lane;
   }
-  auto dma = [&](int t, int j) {  // the j-th of this wave's 16 DMAs of K-tile t (0..7 x, 8..15 W)
-    u32x4* slot = lds + (t & 1) * G4_SLOT_U4;
+  // slot images: two x + two W halves of 64 KiB slots, or (W3) x slots [0, 2) then three W slots
+  auto xslot = [&](int sl) -> u32x4* { return lds + sl * (W3 ? G4_A_U4 : G4_SLOT_U4); };
+  auto wslot = [&](int sl) -> u32x4* { return W3 ? lds + 2 * G4_A_U4 + sl * G4_B_U4 : lds + sl * G4_SLOT_U4 + G4_A_U4; };
+  // the j-th of this wave's 16 DMAs of K-tile t (0..7 x into x slot t & 1, 8..15 W into W slot wsl)
+  auto dma = [&](int t, int j, int wsl) {
     if (j < 8) {
-      glds16(baseA + (size_t)t * 128 + offA[j], slot + (wu + 4 * j) * 64);
+      glds16(baseA + (size_t)t * 128 + offA[j], xslot(t & 1) + (wu + 4 * j) * 64);
     } else {
-      glds16(baseB + (size_t)t * 2048 + offB[j - 8], slot + G4_A_U4 + (wu + 4 * (j - 8)) * 64);
+      glds16(baseB + (size_t)t * 2048 + offB[j - 8], wslot(wsl) + (wu + 4 * (j - 8)) * 64);
     }
   };
 
@@ -109,19 +112,19 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
   // x: row r = wr*128 + 16i + (lane & 15), k-chunk 4h + (lane >> 4), stored at cell chunk ^ ((r & 15) >> 1)
   const int xrd = (wr * 128 + (lane & 15)) * 8;
   const int xc0 = (0 + (lane >> 4)) ^ ((lane >> 1) & 7), xc1 = (4 + (lane >> 4)) ^ ((lane >> 1) & 7);
-  auto rd = [&](u32x4& dst, int slot, int h, int q) {  // q 0..7: W n-tile q; 8..15: x m-tile q - 8
-    const u32x4* s = lds + slot * G4_SLOT_U4;
+  auto rd = [&](u32x4& dst, int xs, int wsl, int h, int q) {  // q 0..7: W n-tile q; 8..15: x m-tile q - 8
     if (q < 8)
-      dst = s[G4_A_U4 + ((wc * 8 + q) * 2 + h) * 64 + lane];
+      dst = wslot(wsl)[((wc * 8 + q) * 2 + h) * 64 + lane];
     else
-      dst = s[xrd + (q - 8) * 128 + (h ? xc1 : xc0)];
+      dst = xslot(xs)[xrd + (q - 8) * 128 + (h ? xc1 : xc0)];
   };
 
   u32x4 w0[8], x0[8], w1[8], x1[8];
 
-  // one 64-MFMA sub-step on (wf, xf), interleaved with up to 16 fragment reads into (wn, xn) and 16 DMAs of tile td
-  auto substep = [&](u32x4 (&wf)[8], u32x4 (&xf)[8], u32x4 (&wn)[8], u32x4 (&xn)[8], bool do_rd, int rslot, int rh,
-                     bool do_dma, int td) {
+  // one 64-MFMA sub-step on (wf, xf), interleaved with up to 16 fragment reads into (wn, xn) from x slot rslot / W slot
+  // rw, the 8 x DMAs of tile td (do_dma) and the 8 W DMAs of tile tw into W slot tws (do_wdma)
+  auto substep = [&](u32x4 (&wf)[8], u32x4 (&xf)[8], u32x4 (&wn)[8], u32x4 (&xn)[8], bool do_rd, int rslot, int rw,
+                     int rh, bool do_dma, int td, bool do_wdma, int tw, int tws) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #pragma unroll
@@ -132,8 +135,8 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
         else
           g4_mfma(acc[j][i], wf[j], xf[i]);
       }
-      if (do_rd) rd(q < 8 ? wn[q] : xn[q - 8], rslot, rh, q);
-      if (!(DIAG & 2) && do_dma) dma(td, q);
+      if (do_rd) rd(q < 8 ? wn[q] : xn[q - 8], rslot, rw, rh, q);
+      if (!(DIAG & 2) && (q < 8 ? do_dma : do_wdma)) dma(q < 8 ? td : tw, q, tws);
       if constexpr (RMS) {
         if (q < 4) {  // m-tile 4wc + q: the runtime wc selects between two named fragments (no indexed array)
           const u32x4 f = wc ? xf[4 + q] : xf[q];
@@ -149,14 +152,89 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
     }
   };
 
+  auto mid_barrier = [&]() {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0), visible to hipcc's own wait bookkeeping
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  if constexpr (W3) {
+    // W three K-tiles deep (x stays two): tile t's W DMA is issued one K-tile before its x DMA, so the weight
+    // stream -- the operand that comes from HBM when few tiles share it (small M) -- has ~3 sub-steps to land
+    // instead of ~1.5. Issue order per sub-step: x DMAs then W DMAs; vmcnt retires in order, so "tile t+1 landed"
+    // is vmcnt(8) while the next tile's W (the youngest 8) may stay in flight across the barrier.
+    if (KT > 0) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dma(0, j, 0);
+    }
+    if (KT > 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dma(1, j, 1);
+    }
+    if (KT > 2) {
+#pragma unroll
+      for (int j = 8; j < 16; ++j) dma(2, j, 2);
+      wait_vmcnt<24>();
+    } else if (KT > 1) {
+      wait_vmcnt<16>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (KT > 0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rd(q < 8 ? w0[q] : x0[q - 8], 0, 0, 0, q);
+    }
+    // straight-line phases with constant DMA / wait choices (as the two-slot loop below): a single loop with
+    // run-time tails merged the register sets and spilled
+    auto vm8_barrier = [&]() {
+      __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0): all but the youngest 8 (W of tile t+2)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    int t = 0, wt = 0;  // wt = t % 3: tile t's W slot
+    for (; t + 3 < KT; ++t) {
+      const int wn1 = wt == 2 ? 0 : wt + 1;
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      vm8_barrier();
+      // x of tile t+2 into tile t's x slot, W of tile t+3 into tile t's W slot (both read out before the barrier)
+      substep(w1, x1, w0, x0, true, (t + 1) & 1, wn1, 0, true, t + 2, true, t + 3, wt);
+      wt = wn1;
+    }
+    if (t + 2 < KT) {  // third to last: the last x DMA, no W left to issue
+      const int wn1 = wt == 2 ? 0 : wt + 1;
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      vm8_barrier();
+      substep(w1, x1, w0, x0, true, (t + 1) & 1, wn1, 0, true, t + 2, false, 0, 0);
+      wt = wn1;
+      ++t;
+    }
+    if (t + 1 < KT) {  // second to last: nothing left to DMA
+      const int wn1 = wt == 2 ? 0 : wt + 1;
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      mid_barrier();
+      substep(w1, x1, w0, x0, true, (t + 1) & 1, wn1, 0, false, 0, false, 0, 0);
+      wt = wn1;
+      ++t;
+    }
+    if (t < KT) {  // last K-tile
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      substep(w1, x1, w0, x0, false, 0, 0, 0, false, 0, false, 0, 0);
+    }
+    wait_vmcnt<0>();
+    g4_acc_fence();
+    return;
+  }
+
   // prologue: tiles 0 and 1 in flight, tile 0 landed, set 0 <- tile 0 k 0..31
   if (KT > 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) dma(0, j);
+    for (int j = 0; j < 16; ++j) dma(0, j, 0);
   }
   if (KT > 1) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) dma(1, j);
+    for (int j = 0; j < 16; ++j) dma(1, j, 1);
     wait_vmcnt<16>();
   } else {
     wait_vmcnt<0>();
@@ -165,30 +243,24 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
   asm volatile("" ::: "memory");
   if (KT > 0) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) rd(q < 8 ? w0[q] : x0[q - 8], 0, 0, q);
+    for (int q = 0; q < 16; ++q) rd(q < 8 ? w0[q] : x0[q - 8], 0, 0, 0, q);
   }
-
-  auto mid_barrier = [&]() {
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0), visible to hipcc's own wait bookkeeping
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
 
   int t = 0;
   for (; t + 2 < KT; ++t) {  // steady state: reads of tile t+1 and DMA of tile t+2 in every K-tile
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
     mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, true, t + 2);
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, (t + 1) & 1, 0, true, t + 2, true, t + 2, t & 1);
   }
   if (t + 1 < KT) {  // second to last: nothing left to DMA
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
     mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, false, 0);
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, (t + 1) & 1, 0, false, 0, false, 0, 0);
     ++t;
   }
   if (t < KT) {  // last K-tile
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
-    substep(w1, x1, w0, x0, false, 0, 0, false, 0);
+    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
+    substep(w1, x1, w0, x0, false, 0, 0, 0, false, 0, false, 0, 0);
   }
   g4_acc_fence();
 }

@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 10  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split), so older persisted picks are re-measured
+TUNE_VERSION = 11  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split; 11: gemm4 with the weights three K-tiles deep), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -275,11 +275,13 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
-# 7: gemm4; 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
+TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
+# 7: gemm4; 14: gemm4 with the weights three K-tiles deep (160 KiB of LDS); 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
 # 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
 # plus (ks, XK_TILE) -- gemm4 split-K whose splits exchange their partial blocks in-launch -- for the residual epilogue
 # where tiles x split fit the CUs
+if os.environ.get("JLA_TUNE_TILES"):  # A/B tooling: restrict the tile candidates, e.g. JLA_TUNE_TILES=1,2,3,7,10,11,12
+    TILE_CANDIDATES = tuple(int(v) for v in os.environ["JLA_TUNE_TILES"].split(","))
 TUNE_MAX_M = 2048
 
 

@@ -217,11 +217,14 @@ def test_gemm4_exchange_split(m, n, k, ks):
     torch.testing.assert_close(a1[1].cpu(), a1[0].cpu().to(BF16), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("m,n,k", [(2048, 4096, 1024), (700, 2560, 512), (4352, 1536, 256)])
-def test_gemm4_persistent_identical(m, n, k):
-    """Tile config 13 (persistent gemm4: one workgroup per CU over every tile) runs the same per-tile MFMA chain and
-    epilogues as tile 7: store (fp32 / bf16), SwiGLU with the fused norm (precomputed / in-loop statistic) and the
-    residual + mirror are bit-identical; ragged M / N and more tiles than CUs included."""
+@pytest.mark.parametrize("tile", [13, 14])
+@pytest.mark.parametrize("m,n,k", [(2048, 4096, 1024), (700, 2560, 512), (4352, 1536, 256), (256, 1280, 192),
+                                   (256, 2048, 128), (300, 1024, 64)])
+def test_gemm4_persistent_identical(m, n, k, tile):
+    """Tile configs 13 (persistent gemm4: one workgroup per CU over every tile) and 14 (the weight operand three
+    K-tiles deep) run the same per-tile MFMA chain and epilogues as tile 7: store (fp32 / bf16), SwiGLU with the fused
+    norm (precomputed / in-loop statistic) and the residual + mirror are bit-identical; ragged M / N, more tiles than
+    CUs and every K-tile count of the deep ring's prologue / tail phases (1..4, 16) included."""
     e = ops.ext()
     torch.manual_seed(m + n + k + 13)
     x = torch.randn(m, k).to(BF16)
@@ -247,10 +250,41 @@ def test_gemm4_persistent_identical(m, n, k):
         torch.cuda.synchronize()
         return [o, ob, o2, o3, hg, mir]
 
-    a, b = run(13), run(G4)
+    a, b = run(tile), run(G4)
     for i, (u, v) in enumerate(zip(a, b)):
-        assert torch.equal(u, v), f"output {i}: persistent differs from tile 7"
+        assert torch.equal(u, v), f"output {i}: tile {tile} differs from tile 7"
     _close(a[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+
+
+@pytest.mark.parametrize("m,n,k,ks", [(256, 1280, 8192, 12), (256, 7168, 8192, 4), (512, 2048, 1024, 2),
+                                      (256, 1024, 768, 3)])
+def test_gemm4_deep_split_identical(m, n, k, ks):
+    """The deep-W gemm4 (tile 14) under a K split (fp32 partial slabs + the reduce kernel, fused norm in-loop):
+    bit-identical to tile 7 for the store and SwiGLU epilogues, and the residual epilogue, at the 70B shard's shapes."""
+    e = ops.ext()
+    torch.manual_seed(m + n + k + ks)
+    x = torch.randn(m, k).to(BF16)
+    w = (torch.randn(n, k) * 0.02).to(BF16)
+    pg = PackedLinear.from_dense(w, DEV)
+    xg = x.to(DEV)
+    ws = torch.empty(ks * m * (n + 1), device=DEV)
+    h0 = torch.randn(m, n).to(DEV)
+
+    def run(tile):
+        o = torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, 1e-5, tile)
+        o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, 1e-5, tile)
+        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, tile)
+        torch.cuda.synchronize()
+        return [o, o2, hg, mir]
+
+    a, b = run(14), run(G4)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), f"output {i}: tile 14 differs from tile 7"
+    xs = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    _close(a[0].float().cpu(), xs @ w.float().t(), 2e-2, 2e-2)
 
 
 def test_gemm4_exchange_split_guards():

@@ -725,9 +725,10 @@ template <int MODE, int RMSM, typename Acc, int NJ = 8>
 JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int m0, int n0, int split,
                          const G4Epi& ep, const QKVArgs& qa) {
   constexpr bool RMS = RMSM == 1;
-  static_assert(NJ == 8 || (RMSM != 1 && MODE != MODE_ARGMAX && MODE != MODE_QKV),
-                "the 256 x 128 tile: precomputed norm statistic; store / residual / SwiGLU / partial epilogues");
+  static_assert(NJ == 8 || (RMSM != 1 && MODE != MODE_ARGMAX),
+                "the 256 x 128 / 192 tiles: precomputed norm statistic; no argmax epilogue");
   constexpr int WN = 16 * NJ;  // output columns of a wave block
+  constexpr int PJ = NJ == 6 ? 8 : NJ;  // staged row width in n-tiles (a power of two; NJ = 6 leaves the rest unused)
   const int wr = wu >> 1, wc = wu & 1;
   void* const out = ep.out;
   const int M = ep.M, N = ep.N, K = ep.K, accumulate = ep.accumulate, out_f32 = ep.out_f32;
@@ -797,13 +798,13 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
         const f32x4 gv = tile_val(j, i), uv = tile_val(j + 1, i);
         const u32x2 p = {pack2bf(silu(gv[0]) * uv[0], silu(gv[1]) * uv[1]),
                          pack2bf(silu(gv[2]) * uv[2], silu(gv[3]) * uv[3])};
-        g4_stage_put<16 * NJ>(wl, 16 * i + c, 16 * j + 8 * q, p);
+        g4_stage_put<16 * PJ>(wl, 16 * i + c, 16 * j + 8 * q, p);
       }
     }
     const int fcol0 = ((n0 >> 4) + wc * NJ) * 8;  // first activation column of the wave block
-    g4_stage_rows<16 * NJ>(wl, lane, [&](int r, int ch, u32x4 v) {
+    g4_stage_rows<16 * PJ>(wl, lane, [&](int r, int ch, u32x4 v) {
       const int row = mrow0 + r, col = fcol0 + 8 * ch;
-      if (row < M && col < F) *reinterpret_cast<u32x4*>(o + (size_t)row * F + col) = v;
+      if (row < M && col < F && ch < NJ) *reinterpret_cast<u32x4*>(o + (size_t)row * F + col) = v;
     });
   } else if constexpr (MODE == MODE_ARGMAX) {
     // per row: the first maximum over this wave's 128 columns -> one (value, index) partial at
@@ -844,8 +845,8 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
     // q or to the k / v cache row at slot[0] + (position in the sequence); same arithmetic as gemm2's /
     // gemm_reduce_kernel's QKV epilogue (reference model.py:58-92, :169-199)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int gcol = n0 + wc * 128 + 16 * j + 4 * q;
+    for (int j = 0; j < NJ; ++j) {
+      const int gcol = n0 + wc * WN + 16 * j + 4 * q;
       const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -868,8 +869,8 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
       }
     }
     g4_stage_rows<256>(wl, lane, [&](int r, int ch, u32x4 v) {
-      const int grow = mrow0 + r, gcol = n0 + wc * 128 + 8 * ch;
-      if (grow >= M || gcol >= N) return;
+      const int grow = mrow0 + r, gcol = n0 + wc * WN + 8 * ch;
+      if (grow >= M || gcol >= N || 8 * ch >= WN) return;
       const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
       if (head < qa.H) {
         *reinterpret_cast<u32x4*>(qa.q + ((size_t)grow * qa.H + head) * qa.Dh + d0) = v;
@@ -905,12 +906,12 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const f32x4 v = tile_val(j, i);
-          g4_stage_put<32 * NJ>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+          g4_stage_put<32 * PJ>(wl, 16 * i + c, 32 * j + 8 * q, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
         }
       bf16_t* o = static_cast<bf16_t*>(out);
-      g4_stage_rows<32 * NJ>(wl, lane, [&](int r, int ch, u32x4 v) {
+      g4_stage_rows<32 * PJ>(wl, lane, [&](int r, int ch, u32x4 v) {
         const int row = mrow0 + r, col = n0 + wc * WN + 8 * ch;
-        if (row < M && col < N) *reinterpret_cast<u32x4*>(o + (size_t)row * N + col) = v;
+        if (row < M && col < N && 8 * ch < WN) *reinterpret_cast<u32x4*>(o + (size_t)row * N + col) = v;
       });
     }
   } else {  // PARTIAL / RESIDUAL: fp32, one 16-byte piece per lane per tile
@@ -1298,9 +1299,10 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 //      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
 static bool use_g4(int tile, int M, int K);
+constexpr int G4N6_TILE = 15;  // gemm4 on 256 x 192 tiles (g4n_mainloop<6>)
 int gemm_qkv_direct_ok(int M, int tile, int K) {
   return ((tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
-         use_g4(tile, M, K);
+         use_g4(tile, M, K) || (tile == G4N6_TILE && (K & 63) == 0);
 }
 
 // gemm4 (tile config 7; the default for tile 0 once g_g4_default is set): the 4-wave 256 x 256 kernel of gemm4w.h.
@@ -1441,6 +1443,14 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   if constexpr (MODE != MODE_QKV && MODE != MODE_ARGMAX) {
     if (tile == G4N_TILE && (K & 63) == 0) {
       launch_g4<MODE, 4>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
+      return;
+    }
+  }
+  // tile config 15: 256 x 192 tiles -- Llama-3-8B qkv (N = 6144) at M = 2048 is 8 x 32 = 256 tiles, one per CU, where
+  // the 256 x 256 grid has 192 (0.75 of a wave); the QKV epilogue included
+  if constexpr (MODE != MODE_ARGMAX) {
+    if (tile == G4N6_TILE && (K & 63) == 0) {
+      launch_g4<MODE, 6>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
       return;
     }
   }

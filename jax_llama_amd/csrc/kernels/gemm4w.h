@@ -267,7 +267,7 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 
 // ---------------------------------------------------------------------------------------------
 // g4n_mainloop: the same loop for a 256 (M) x 32 NJ (N) workgroup tile -- each wave a 128 (M) x 16 NJ (N) block,
-// NJ x 8 accumulators (NJ = 4: 256 x 128 tiles, 128 accumulator AGPRs per wave). Twice the tiles of the 256 x 256
+// NJ x 8 accumulators (NJ = 4: 256 x 128 tiles, 128 accumulator AGPRs per wave; NJ = 6: 256 x 192). Twice the tiles of the 256 x 256
 // loop for the outputs whose 256 x 256 grid quantises badly on 256 CUs (Llama-3-8B at M = 2048: o has 128 tiles ->
 // 256 with no K split; w1|w3 896 = 3.5 waves -> 1792 = 7 whole waves), at 1.5x the operand bytes per MFMA. Same LDS
 // images and slot layout (the W half of a slot is half used), same two sub-steps per 64-deep K-tile and one barrier;
@@ -275,7 +275,7 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 // No in-loop norm statistic (the caller precomputes it: RMSM 0 / 2 only).
 template <int NJ, typename Acc>
 JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc) {
-  static_assert(NJ == 4 || NJ == 8, "n-tiles per wave");
+  static_assert(NJ == 4 || NJ == 6 || NJ == 8, "n-tiles per wave");
   constexpr int ND = NJ;           // W DMAs per wave per K-tile (2 NJ n-tiles x 2 k halves / 4 waves)
   constexpr int NQ = 8 + NJ;       // fragment reads / DMA issues per sub-step
   constexpr int MPS = (8 * NJ) / 16;  // MFMAs per slot (16 slots per sub-step)

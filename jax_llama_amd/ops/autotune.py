@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 11  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split; 11: gemm4 with the weights three K-tiles deep), so older persisted picks are re-measured
+TUNE_VERSION = 11  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split; 11: gemm4 with the weights three K-tiles deep, 256 x 192 tiles), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -275,8 +275,8 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
-# 7: gemm4; 14: gemm4 with the weights three K-tiles deep (160 KiB of LDS); 10: gemm4 on 256 x 128 tiles (not for a K split under the fused norm: its statistic is precomputed);
+TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14, 15)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
+# 7: gemm4; 14: gemm4 with the weights three K-tiles deep (160 KiB of LDS); 10 / 15: gemm4 on 256 x 128 / 192 tiles (not for a K split under the fused norm: its statistic is precomputed);
 # 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
 # plus (ks, XK_TILE) -- gemm4 split-K whose splits exchange their partial blocks in-launch -- for the residual epilogue
 # where tiles x split fit the CUs
@@ -320,6 +320,7 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
 
 XK_TILE = 8  # gemm4 split-K with the in-launch exchange of partial wave blocks (residual epilogue)
 G4N_TILE = 10  # gemm4 on 256 x 128 tiles (csrc/kernels/gemm4w.h g4n_mainloop)
+G4N6_TILE = 15  # gemm4 on 256 x 192 tiles (g4n_mainloop<6>; the 8B qkv at M = 2048 is exactly one wave)
 G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h)
 TUNE_ROUNDS = 3
 
@@ -328,7 +329,7 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
-             if (tm != G4N_TILE or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
+             if (tm not in (G4N_TILE, G4N6_TILE) or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
              and (tm not in G5_TILES or (k % 64 == 0 and m <= 512))]
     if k % 64 == 0 and m <= 512:  # gemm5 also at the deeper splits its 64-deep stages allow (narrow shards, long K)
         cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c]

@@ -287,6 +287,72 @@ def test_gemm4_deep_split_identical(m, n, k, ks):
     _close(a[0].float().cpu(), xs @ w.float().t(), 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("m,n,k", [(2048, 6144, 512), (300, 1008, 256), (256, 4096, 128)])
+def test_gemm4_256x192_identical(m, n, k):
+    """256 x 192 tiles (tile 15, g4n_mainloop<6>): the same per-output MFMA chain as the 256 x 256 gemm4, so the store
+    (fp32 / bf16, precomputed norm), SwiGLU, residual + mirror and split-K partial epilogues are bit-identical to tile 7;
+    ragged N (a last tile narrower than 192 columns) included."""
+    e = ops.ext()
+    torch.manual_seed(m + n + k + 15)
+    x = torch.randn(m, k).to(BF16)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    pg = PackedLinear.from_dense(w, DEV)
+    n2 = n // 32 * 32
+    gp = PackedLinear.from_dense(ref.interleave_gate_up(w[: n2 // 2], w[n2 // 2: n2]), DEV)
+    xg = x.to(DEV)
+    h0 = torch.randn(m, n).to(DEV)
+    rw = torch.empty(m, device=DEV)
+    ws = torch.empty(2 * m * (n + 1), device=DEV)
+
+    def run(tile):
+        o = torch.empty(m, n, dtype=torch.float32, device=DEV)
+        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, 1, None, -1.0, tile)
+        ob = torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, None, 1e-5, tile, None, None, rw)
+        o2 = torch.empty(m, n2 // 2, dtype=BF16, device=DEV)
+        e.gemm(xg, gp.weight, n2, k, o2, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile, None, None, rw)
+        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, None, -1.0, tile)
+        os = torch.empty(m, n, dtype=BF16, device=DEV)
+        e.gemm(xg, pg.weight, n, k, os, ops.MODE_STORE, True, None, 2, ws, -1.0, tile)
+        torch.cuda.synchronize()
+        return [o, ob, o2, hg, mir, os]
+
+    a, b = run(15), run(G4)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), f"output {i}: tile 15 differs from tile 7"
+    _close(a[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
+
+
+@pytest.mark.parametrize("m,s", [(2048, 1), (512, 512), (300, 3)])
+def test_gemm4_256x192_qkv_epilogue(m, s):
+    """The RoPE / KV-cache write epilogue on 256 x 192 tiles (a tile spans 1.5 heads): q, K and V bit-identical to
+    the 256 x 256 gemm4's."""
+    e = ops.ext()
+    h, hkv, dh, k = 32, 8, 128, 1024
+    t = 11 + s + 4
+    b = m // s
+    n = (h + 2 * hkv) * dh
+    assert e.gemm_qkv_direct_ok(m, 15, k)
+    w = (torch.randn(n, k) * 0.05).to(BF16)
+    x = torch.randn(m, k).to(BF16)
+    table = ref.rope_table(dh, 1024, 500000.0)
+    pos = torch.randint(0, 1000, (m,), dtype=torch.int32)
+    pg = PackedLinear.from_dense(w, DEV)
+    outs = {}
+    for tile in (G4, 15):
+        kg = torch.zeros(b, hkv, t, dh, dtype=BF16, device=DEV)
+        vg = torch.zeros_like(kg)
+        qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
+        e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
+                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile, None,
+                   torch.empty(m, device=DEV))
+        torch.cuda.synchronize()
+        outs[tile] = (qg, kg, vg)
+    for i, (u, v) in enumerate(zip(outs[15], outs[G4])):
+        assert torch.equal(u, v), f"qkv output {i}: tile 15 differs from tile 7"
+
+
 def test_gemm4_exchange_split_guards():
     """The exchange plan needs every workgroup resident (tiles x split <= CUs) and a real split."""
     e = ops.ext()

@@ -972,7 +972,7 @@ __global__ void __launch_bounds__(256, 1)
   const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
   if constexpr (NJ != 8) {
     static_assert(!RMS, "the 256 x 128 tile: precomputed statistic");
-    g4n_mainloop<NJ>(g, lds, m0, n0, t0, KT, wu, lane, acc);
+    g4n_mainloop<NJ, decltype(acc), W3>(g, lds, m0, n0, t0, KT, wu, lane, acc);
   } else {
     g4_mainloop<RMS, decltype(acc), DIAG, W3>(g, lds, m0, n0, t0, KT, wu, lane, acc, ss);
   }
@@ -1299,10 +1299,11 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 //      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
 static bool use_g4(int tile, int M, int K);
-constexpr int G4N6_TILE = 15;  // gemm4 on 256 x 192 tiles (g4n_mainloop<6>)
+constexpr int G4N6_TILE = 15;   // gemm4 on 256 x 192 tiles (g4n_mainloop<6>)
+constexpr int G4N6D_TILE = 16;  // the same with the weights three K-tiles deep (g4n_mainloop<6, W3>)
 int gemm_qkv_direct_ok(int M, int tile, int K) {
   return ((tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
-         use_g4(tile, M, K) || (tile == G4N6_TILE && (K & 63) == 0);
+         use_g4(tile, M, K) || ((tile == G4N6_TILE || tile == G4N6D_TILE) && (K & 63) == 0);
 }
 
 // gemm4 (tile config 7; the default for tile 0 once g_g4_default is set): the 4-wave 256 x 256 kernel of gemm4w.h.
@@ -1361,14 +1362,23 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
       return;
     }
   }
-  if constexpr (NJ != 8) {  // 256 x 128 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
+  if constexpr (NJ != 8) {  // 256 x 128 / 192 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
+    constexpr bool D6 = NJ == 6;  // (the deep-W form is built for the 192-column tiles only)
     if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
       if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
-      gemm4_kernel<MODE, 2, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
-                                                            rms_eps, ssq, qa, rms_ws, gm);
+      if (D6 && deep)
+        gemm4_kernel<MODE, 2, NJ, 0, D6><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
+                                                              tn, rms_eps, ssq, qa, rms_ws, gm);
+      else
+        gemm4_kernel<MODE, 2, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                       rms_eps, ssq, qa, rms_ws, gm);
     } else if (!rms) {
-      gemm4_kernel<MODE, 0, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
-                                                            rms_eps, ssq, qa, nullptr, gm);
+      if (D6 && deep)
+        gemm4_kernel<MODE, 0, NJ, 0, D6><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
+                                                              tn, rms_eps, ssq, qa, nullptr, gm);
+      else
+        gemm4_kernel<MODE, 0, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
+                                                       rms_eps, ssq, qa, nullptr, gm);
     }
     return;
   }
@@ -1449,8 +1459,9 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
   // tile config 15: 256 x 192 tiles -- Llama-3-8B qkv (N = 6144) at M = 2048 is 8 x 32 = 256 tiles, one per CU, where
   // the 256 x 256 grid has 192 (0.75 of a wave); the QKV epilogue included
   if constexpr (MODE != MODE_ARGMAX) {
-    if (tile == G4N6_TILE && (K & 63) == 0) {
-      launch_g4<MODE, 6>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
+    if ((tile == G4N6_TILE || tile == G4N6D_TILE) && (K & 63) == 0) {
+      launch_g4<MODE, 6>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, false,
+                         tile == G4N6D_TILE);
       return;
     }
   }
@@ -1620,6 +1631,10 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   ksplit = (KS + kc - 1) / kc;
   // qkv without a K split: the RoPE / KV-write epilogue of the default FA pipeline (256 x 256 tiles, fused norm)
   if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile, K) && rms)) return -1;
+  // the 256 x 128 / 192 tiles take the fused norm only as the precomputed statistic without a K split (launch_g4
+  // would otherwise launch nothing)
+  if ((tile == G4N_TILE || tile == G4N6_TILE || tile == G4N6D_TILE) && rms && (ksplit > 1 || rms_ws == nullptr))
+    return -6;
   const u32x4* w = static_cast<const u32x4*>(W);
   if (ksplit == 1) {
     switch (mode) {

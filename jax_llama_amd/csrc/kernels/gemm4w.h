@@ -273,7 +273,7 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 // images and slot layout (the W half of a slot is half used), same two sub-steps per 64-deep K-tile and one barrier;
 // per sub-step 8 NJ MFMAs with the 8 + NJ fragment reads and 8 + NJ LDS-DMA issues spread over the first slots.
 // No in-loop norm statistic (the caller precomputes it: RMSM 0 / 2 only).
-template <int NJ, typename Acc>
+template <int NJ, typename Acc, bool W3 = false>
 JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc) {
   static_assert(NJ == 4 || NJ == 6 || NJ == 8, "n-tiles per wave");
   constexpr int ND = NJ;           // W DMAs per wave per K-tile (2 NJ n-tiles x 2 k halves / 4 waves)
@@ -298,25 +298,26 @@ JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, i
     const int nt = min((n0 >> 4) + (f >> 1), NTT - 1) - (n0 >> 4);
     offB[j] = ((unsigned)nt * (unsigned)KS + (unsigned)(f & 1)) * 1024u + 16u * (unsigned)lane;
   }
-  auto dma = [&](int t, int j) {  // the j-th of this wave's NQ DMAs of K-tile t (0..7 x, then W)
-    u32x4* slot = lds + (t & 1) * G4_SLOT_U4;
+  // slot images as g4_mainloop: x + W halves of two 64 KiB slots, or (W3) two x slots then three W slots
+  auto xslot = [&](int sl) -> u32x4* { return lds + sl * (W3 ? G4_A_U4 : G4_SLOT_U4); };
+  auto wslot = [&](int sl) -> u32x4* { return W3 ? lds + 2 * G4_A_U4 + sl * G4_B_U4 : lds + sl * G4_SLOT_U4 + G4_A_U4; };
+  auto dma = [&](int t, int j, int wsl) {  // the j-th of this wave's NQ DMAs of K-tile t (0..7 x, then W)
     if (j < 8)
-      glds16(baseA + (size_t)t * 128 + offA[j], slot + (wu + 4 * j) * 64);
+      glds16(baseA + (size_t)t * 128 + offA[j], xslot(t & 1) + (wu + 4 * j) * 64);
     else
-      glds16(baseB + (size_t)t * 2048 + offB[j - 8], slot + G4_A_U4 + (wu + 4 * (j - 8)) * 64);
+      glds16(baseB + (size_t)t * 2048 + offB[j - 8], wslot(wsl) + (wu + 4 * (j - 8)) * 64);
   };
   const int xrd = (wr * 128 + (lane & 15)) * 8;
   const int xc0 = (0 + (lane >> 4)) ^ ((lane >> 1) & 7), xc1 = (4 + (lane >> 4)) ^ ((lane >> 1) & 7);
-  auto rd = [&](u32x4& dst, int slot, int h, int q) {  // q < NJ: W n-tile q of the wave; else x m-tile q - NJ
-    const u32x4* sp = lds + slot * G4_SLOT_U4;
+  auto rd = [&](u32x4& dst, int xs, int wsl, int h, int q) {  // q < NJ: W n-tile q of the wave; else x m-tile q - NJ
     if (q < NJ)
-      dst = sp[G4_A_U4 + ((wc * NJ + q) * 2 + h) * 64 + lane];
+      dst = wslot(wsl)[((wc * NJ + q) * 2 + h) * 64 + lane];
     else
-      dst = sp[xrd + (q - NJ) * 128 + (h ? xc1 : xc0)];
+      dst = xslot(xs)[xrd + (q - NJ) * 128 + (h ? xc1 : xc0)];
   };
   u32x4 w0[NJ], x0[8], w1[NJ], x1[8];
-  auto substep = [&](u32x4 (&wf)[NJ], u32x4 (&xf)[8], u32x4 (&wn)[NJ], u32x4 (&xn)[8], bool do_rd, int rslot, int rh,
-                     bool do_dma, int td) {
+  auto substep = [&](u32x4 (&wf)[NJ], u32x4 (&xf)[8], u32x4 (&wn)[NJ], u32x4 (&xn)[8], bool do_rd, int rslot, int rw,
+                     int rh, bool do_dma, int td, bool do_wdma, int tw, int tws) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #pragma unroll
@@ -325,18 +326,85 @@ JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, i
         g4_mfma(acc[j][i], wf[j], xf[i]);
       }
       if (q < NQ) {
-        if (do_rd) rd(q < NJ ? wn[q] : xn[q - NJ], rslot, rh, q);
-        if (do_dma) dma(td, q);
+        if (do_rd) rd(q < NJ ? wn[q] : xn[q - NJ], rslot, rw, rh, q);
+        if (q < 8 ? do_dma : do_wdma) dma(q < 8 ? td : tw, q, tws);
       }
     }
   };
+  auto mid_barrier = [&]() {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  if constexpr (W3) {  // W three K-tiles deep (g4_mainloop W3): barriers wait for all but the youngest ND W DMAs
+    static_assert(ND < 16, "vmcnt immediate");
+    if (KT > 0) {
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) dma(0, j, 0);
+    }
+    if (KT > 1) {
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) dma(1, j, 1);
+    }
+    if (KT > 2) {
+#pragma unroll
+      for (int j = 8; j < NQ; ++j) dma(2, j, 2);
+      wait_vmcnt<8 + 2 * ND>();
+    } else if (KT > 1) {
+      wait_vmcnt<8 + ND>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (KT > 0) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) rd(q < NJ ? w0[q] : x0[q - NJ], 0, 0, 0, q);
+    }
+    auto vmw_barrier = [&]() {
+      __builtin_amdgcn_s_waitcnt(0x0070 | ND);  // vmcnt(ND) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    int t = 0, wt = 0;
+    for (; t + 3 < KT; ++t) {
+      const int wn1 = wt == 2 ? 0 : wt + 1;
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      vmw_barrier();
+      substep(w1, x1, w0, x0, true, (t + 1) & 1, wn1, 0, true, t + 2, true, t + 3, wt);
+      wt = wn1;
+    }
+    if (t + 2 < KT) {
+      const int wn1 = wt == 2 ? 0 : wt + 1;
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      vmw_barrier();
+      substep(w1, x1, w0, x0, true, (t + 1) & 1, wn1, 0, true, t + 2, false, 0, 0);
+      wt = wn1;
+      ++t;
+    }
+    if (t + 1 < KT) {
+      const int wn1 = wt == 2 ? 0 : wt + 1;
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      mid_barrier();
+      substep(w1, x1, w0, x0, true, (t + 1) & 1, wn1, 0, false, 0, false, 0, 0);
+      wt = wn1;
+      ++t;
+    }
+    if (t < KT) {
+      substep(w0, x0, w1, x1, true, t & 1, wt, 1, false, 0, false, 0, 0);
+      substep(w1, x1, w0, x0, false, 0, 0, 0, false, 0, false, 0, 0);
+    }
+    wait_vmcnt<0>();
+    g4_acc_fence();
+    return;
+  }
   if (KT > 0) {
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) dma(0, j);
+    for (int j = 0; j < NQ; ++j) dma(0, j, 0);
   }
   if (KT > 1) {
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) dma(1, j);
+    for (int j = 0; j < NQ; ++j) dma(1, j, 1);
     wait_vmcnt<NQ>();
   } else {
     wait_vmcnt<0>();
@@ -345,28 +413,23 @@ JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, i
   asm volatile("" ::: "memory");
   if (KT > 0) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) rd(q < NJ ? w0[q] : x0[q - NJ], 0, 0, q);
+    for (int q = 0; q < NQ; ++q) rd(q < NJ ? w0[q] : x0[q - NJ], 0, 0, 0, q);
   }
-  auto mid_barrier = [&]() {
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
   int t = 0;
   for (; t + 2 < KT; ++t) {
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
     mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, true, t + 2);
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, (t + 1) & 1, 0, true, t + 2, true, t + 2, t & 1);
   }
   if (t + 1 < KT) {
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
+    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
     mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, 0, false, 0);
+    substep(w1, x1, w0, x0, true, (t + 1) & 1, (t + 1) & 1, 0, false, 0, false, 0, 0);
     ++t;
   }
   if (t < KT) {
-    substep(w0, x0, w1, x1, true, t & 1, 1, false, 0);
-    substep(w1, x1, w0, x0, false, 0, 0, false, 0);
+    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
+    substep(w1, x1, w0, x0, false, 0, 0, 0, false, 0, false, 0, 0);
   }
   g4_acc_fence();
 }

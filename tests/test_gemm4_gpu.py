@@ -287,9 +287,12 @@ def test_gemm4_deep_split_identical(m, n, k, ks):
     _close(a[0].float().cpu(), xs @ w.float().t(), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("m,n,k", [(2048, 6144, 512), (300, 1008, 256), (256, 4096, 128)])
-def test_gemm4_256x192_identical(m, n, k):
-    """256 x 192 tiles (tile 15, g4n_mainloop<6>): the same per-output MFMA chain as the 256 x 256 gemm4, so the store
+@pytest.mark.parametrize("tile", [15, 16])
+@pytest.mark.parametrize("m,n,k", [(2048, 6144, 512), (300, 1008, 256), (256, 4096, 128), (256, 1536, 192),
+                                   (260, 768, 64)])
+def test_gemm4_256x192_identical(m, n, k, tile):
+    """256 x 192 tiles (tile 15, g4n_mainloop<6>; 16 with the weights three K-tiles deep): the same per-output MFMA
+    chain as the 256 x 256 gemm4, so the store
     (fp32 / bf16, precomputed norm), SwiGLU, residual + mirror and split-K partial epilogues are bit-identical to tile 7;
     ragged N (a last tile narrower than 192 columns) included."""
     e = ops.ext()
@@ -318,9 +321,9 @@ def test_gemm4_256x192_identical(m, n, k):
         torch.cuda.synchronize()
         return [o, ob, o2, hg, mir, os]
 
-    a, b = run(15), run(G4)
+    a, b = run(tile), run(G4)
     for i, (u, v) in enumerate(zip(a, b)):
-        assert torch.equal(u, v), f"output {i}: tile 15 differs from tile 7"
+        assert torch.equal(u, v), f"output {i}: tile {tile} differs from tile 7"
     _close(a[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)
 
 
@@ -340,7 +343,7 @@ def test_gemm4_256x192_qkv_epilogue(m, s):
     pos = torch.randint(0, 1000, (m,), dtype=torch.int32)
     pg = PackedLinear.from_dense(w, DEV)
     outs = {}
-    for tile in (G4, 15):
+    for tile in (G4, 15, 16):
         kg = torch.zeros(b, hkv, t, dh, dtype=BF16, device=DEV)
         vg = torch.zeros_like(kg)
         qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
@@ -349,8 +352,9 @@ def test_gemm4_256x192_qkv_epilogue(m, s):
                    torch.empty(m, device=DEV))
         torch.cuda.synchronize()
         outs[tile] = (qg, kg, vg)
-    for i, (u, v) in enumerate(zip(outs[15], outs[G4])):
-        assert torch.equal(u, v), f"qkv output {i}: tile 15 differs from tile 7"
+    for tile in (15, 16):
+        for i, (u, v) in enumerate(zip(outs[tile], outs[G4])):
+            assert torch.equal(u, v), f"qkv output {i}: tile {tile} differs from tile 7"
 
 
 def test_gemm4_exchange_split_guards():

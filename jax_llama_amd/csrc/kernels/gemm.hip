@@ -1301,6 +1301,7 @@ static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M
 static bool use_g4(int tile, int M, int K);
 constexpr int G4N6_TILE = 15;   // gemm4 on 256 x 192 tiles (g4n_mainloop<6>)
 constexpr int G4N6D_TILE = 16;  // the same with the weights three K-tiles deep (g4n_mainloop<6, W3>)
+constexpr int G4ND_TILE = 17;   // 256 x 128 tiles with the deep weight ring (g4n_mainloop<4, W3>)
 int gemm_qkv_direct_ok(int M, int tile, int K) {
   return ((tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
          use_g4(tile, M, K) || ((tile == G4N6_TILE || tile == G4N6D_TILE) && (K & 63) == 0);
@@ -1363,7 +1364,7 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
     }
   }
   if constexpr (NJ != 8) {  // 256 x 128 / 192 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
-    constexpr bool D6 = NJ == 6;  // (the deep-W form is built for the 192-column tiles only)
+    constexpr bool D6 = true;  // the deep-W forms (tiles 16 / 17) of the 192- and 128-column tiles
     if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
       if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
       if (D6 && deep)
@@ -1451,8 +1452,9 @@ static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
                       const QKVArgs& qa = QKVArgs{}, float* rms_ws = nullptr) {
   if constexpr (MODE != MODE_QKV && MODE != MODE_ARGMAX) {
-    if (tile == G4N_TILE && (K & 63) == 0) {
-      launch_g4<MODE, 4>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws);
+    if ((tile == G4N_TILE || tile == G4ND_TILE) && (K & 63) == 0) {
+      launch_g4<MODE, 4>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, false,
+                         tile == G4ND_TILE);
       return;
     }
   }
@@ -1611,7 +1613,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
                      ws_floats, ksplit, rms_eps, tile, s);
   }
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
-  if (tile == G4N_TILE && ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
+  if ((tile == G4N_TILE || tile == G4ND_TILE) && ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
                            (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
     return -1;  // the 256 x 128 plan: no QKV / argmax epilogue, the fused norm only precomputed without a K split
   if (tile == G4_XK_TILE) {  // gemm4 split-K, the splits exchange their partial blocks in-kernel (residual only)
@@ -1633,7 +1635,8 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile, K) && rms)) return -1;
   // the 256 x 128 / 192 tiles take the fused norm only as the precomputed statistic without a K split (launch_g4
   // would otherwise launch nothing)
-  if ((tile == G4N_TILE || tile == G4N6_TILE || tile == G4N6D_TILE) && rms && (ksplit > 1 || rms_ws == nullptr))
+  if ((tile == G4N_TILE || tile == G4ND_TILE || tile == G4N6_TILE || tile == G4N6D_TILE) && rms &&
+      (ksplit > 1 || rms_ws == nullptr))
     return -6;
   const u32x4* w = static_cast<const u32x4*>(W);
   if (ksplit == 1) {

@@ -275,8 +275,8 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14, 15, 16)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
-# 7: gemm4; 14: gemm4 with the weights three K-tiles deep (160 KiB of LDS); 10 / 15: gemm4 on 256 x 128 / 192 tiles; 16: 15 with 14's deep weights (not for a K split under the fused norm: its statistic is precomputed);
+TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14, 15, 16, 17)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
+# 7: gemm4; 14: gemm4 with the weights three K-tiles deep (160 KiB of LDS); 10 / 15: gemm4 on 256 x 128 / 192 tiles; 16 / 17: 15 / 10 with 14's deep weights (not for a K split under the fused norm: its statistic is precomputed);
 # 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
 # plus (ks, XK_TILE) -- gemm4 split-K whose splits exchange their partial blocks in-launch -- for the residual epilogue
 # where tiles x split fit the CUs
@@ -329,7 +329,7 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
-             if (tm not in (G4N_TILE, G4N6_TILE, G4N6_TILE + 1) or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
+             if (tm not in (G4N_TILE, G4N6_TILE, G4N6_TILE + 1, G4N6_TILE + 2) or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
              and (tm not in G5_TILES or (k % 64 == 0 and m <= 512))]
     if k % 64 == 0 and m <= 512:  # gemm5 also at the deeper splits its 64-deep stages allow (narrow shards, long K)
         cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c]

@@ -368,10 +368,13 @@ def test_gemm4_exchange_split_guards():
     assert e.gemm4_xk_ok(256, 256, 4096, 2)
 
 
+@pytest.mark.parametrize("tile", [10, 17])
 @pytest.mark.parametrize("m,n,k,ks", [(2048, 4096, 4096, 1), (700, 2560, 4096, 1), (300, 768, 2048, 2),
-                                      (512, 1056, 1024, 1), (1000, 6144, 1536, 3), (256, 512, 128, 1)])
-def test_gemm4_256x128_tiles(m, n, k, ks):
-    """Tile config 10 (gemm4 on 256 x 128 tiles, 4 n-tiles per wave): store (fp32 / bf16), SwiGLU, residual + mirror,
+                                      (512, 1056, 1024, 1), (1000, 6144, 1536, 3), (256, 512, 128, 1),
+                                      (256, 512, 192, 1), (256, 512, 64, 1)])
+def test_gemm4_256x128_tiles(m, n, k, ks, tile):
+    """Tile config 10 (gemm4 on 256 x 128 tiles, 4 n-tiles per wave; 17 with the weights three K-tiles deep): store
+    (fp32 / bf16), SwiGLU, residual + mirror,
     split-K partials; the fused norm with its precomputed statistic. The same MFMA chain per output element as the
     256 x 256 gemm4 (tile 7), so bit-identical to it, and fp32-reference close; N not a multiple of 128 included."""
     e = ops.ext()
@@ -402,7 +405,7 @@ def test_gemm4_256x128_tiles(m, n, k, ks):
         torch.cuda.synchronize()
         return outs + [hg, mir]
 
-    t10, t7 = run(10), run(G4)
+    t10, t7 = run(tile), run(G4)
     for i, (a, b) in enumerate(zip(t10, t7)):
         assert torch.equal(a, b), f"output {i}: differs from the 256 x 256 gemm4"
     _close(t10[0], ref.linear(x, w, None, torch.float32), 1e-2, 2e-3)

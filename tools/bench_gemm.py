@@ -102,7 +102,7 @@ def main():
                   e.gemm_set_g4_group(grp)
                   for tile in args.tile:
                     kk = ks or e.gemm_ksplit(m, n, k)
-                    if tile in (10, 15, 16) and kk > 1 and eps > 0:
+                    if tile in (10, 15, 16, 17) and kk > 1 and eps > 0:
                         continue  # (gemm4 256 x 128 / 192: no K split under the fused norm)
                     if kk > 1 and (k // 32) // kk < 4 and tile not in (11, 12):
                         continue

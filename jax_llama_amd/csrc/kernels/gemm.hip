@@ -1613,8 +1613,9 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
                      ws_floats, ksplit, rms_eps, tile, s);
   }
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
-  if ((tile == G4N_TILE || tile == G4ND_TILE) && ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
-                           (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
+  if ((tile == G4N_TILE || tile == G4ND_TILE) &&
+      ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
+       (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
     return -1;  // the 256 x 128 plan: no QKV / argmax epilogue, the fused norm only precomputed without a K split
   if (tile == G4_XK_TILE) {  // gemm4 split-K, the splits exchange their partial blocks in-kernel (residual only)
     if (mode != MODE_RESIDUAL || rms_eps >= 0.f) return -1;

@@ -98,7 +98,9 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
   }
   // slot images: two x + two W halves of 64 KiB slots, or (W3) x slots [0, 2) then three W slots
   auto xslot = [&](int sl) -> u32x4* { return lds + sl * (W3 ? G4_A_U4 : G4_SLOT_U4); };
-  auto wslot = [&](int sl) -> u32x4* { return W3 ? lds + 2 * G4_A_U4 + sl * G4_B_U4 : lds + sl * G4_SLOT_U4 + G4_A_U4; };
+  auto wslot = [&](int sl) -> u32x4* {
+    return W3 ? lds + 2 * G4_A_U4 + sl * G4_B_U4 : lds + sl * G4_SLOT_U4 + G4_A_U4;
+  };
   // the j-th of this wave's 16 DMAs of K-tile t (0..7 x into x slot t & 1, 8..15 W into W slot wsl)
   auto dma = [&](int t, int j, int wsl) {
     if (j < 8) {
@@ -267,8 +269,8 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 
 // ---------------------------------------------------------------------------------------------
 // g4n_mainloop: the same loop for a 256 (M) x 32 NJ (N) workgroup tile -- each wave a 128 (M) x 16 NJ (N) block,
-// NJ x 8 accumulators (NJ = 4: 256 x 128 tiles, 128 accumulator AGPRs per wave; NJ = 6: 256 x 192). Twice the tiles of the 256 x 256
-// loop for the outputs whose 256 x 256 grid quantises badly on 256 CUs (Llama-3-8B at M = 2048: o has 128 tiles ->
+// NJ x 8 accumulators (NJ = 4: 256 x 128 tiles, 128 accumulator AGPRs per wave; NJ = 6: 256 x 192). Twice the
+// tiles of the 256 x 256 loop for the outputs whose 256 x 256 grid quantises badly on 256 CUs (Llama-3-8B at M = 2048: o has 128 tiles ->
 // 256 with no K split; w1|w3 896 = 3.5 waves -> 1792 = 7 whole waves), at 1.5x the operand bytes per MFMA. Same LDS
 // images and slot layout (the W half of a slot is half used), same two sub-steps per 64-deep K-tile and one barrier;
 // per sub-step 8 NJ MFMAs with the 8 + NJ fragment reads and 8 + NJ LDS-DMA issues spread over the first slots.
@@ -300,7 +302,9 @@ JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, i
   }
   // slot images as g4_mainloop: x + W halves of two 64 KiB slots, or (W3) two x slots then three W slots
   auto xslot = [&](int sl) -> u32x4* { return lds + sl * (W3 ? G4_A_U4 : G4_SLOT_U4); };
-  auto wslot = [&](int sl) -> u32x4* { return W3 ? lds + 2 * G4_A_U4 + sl * G4_B_U4 : lds + sl * G4_SLOT_U4 + G4_A_U4; };
+  auto wslot = [&](int sl) -> u32x4* {
+    return W3 ? lds + 2 * G4_A_U4 + sl * G4_B_U4 : lds + sl * G4_SLOT_U4 + G4_A_U4;
+  };
   auto dma = [&](int t, int j, int wsl) {  // the j-th of this wave's NQ DMAs of K-tile t (0..7 x, then W)
     if (j < 8)
       glds16(baseA + (size_t)t * 128 + offA[j], xslot(t & 1) + (wu + 4 * j) * 64);

@@ -275,8 +275,10 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 # (profiles/README.md). Timed once per shape when the library heuristic asks for a split.
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
-TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14, 15, 16, 17)  # gemm2 tiles: 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg);
-# 7: gemm4; 14: gemm4 with the weights three K-tiles deep (160 KiB of LDS); 10 / 15: gemm4 on 256 x 128 / 192 tiles; 16 / 17: 15 / 10 with 14's deep weights (not for a K split under the fused norm: its statistic is precomputed);
+# tile configs: 1 / 2 / 3 gemm2 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg); 7 gemm4; 14 gemm4 with the
+# weights three K-tiles deep (160 KiB of LDS); 10 / 15 gemm4 on 256 x 128 / 192 tiles and 17 / 16 the same with the
+# deep weights (those four: no K split under the fused norm, its statistic is precomputed);
+TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14, 15, 16, 17)
 # 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
 # plus (ks, XK_TILE) -- gemm4 split-K whose splits exchange their partial blocks in-launch -- for the residual epilogue
 # where tiles x split fit the CUs

@@ -845,6 +845,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.attr("DEBUG_BOUNDS") = false;
 #endif
   m.def("attn_set_diag", [](int64_t d) { jla::attn_set_diag((int)d); });
+  // CU placement (placement.hip): streams restricted to a CU set (returned as the raw hipStream_t, wrapped by
+  // torch.cuda.ExternalStream) and a census kernel recording each workgroup's HW_ID / XCC_ID
+  m.def("cu_mask_stream", [](std::vector<int64_t> words) {
+    std::vector<uint32_t> mk(words.begin(), words.end());
+    hipStream_t s = nullptr;
+    rc(jla::cu_mask_stream_create(mk.data(), (int)mk.size(), &s), "cu_mask_stream");
+    return reinterpret_cast<int64_t>(s);
+  });
+  m.def("cu_mask_of", [](int64_t s, int64_t words) {
+    std::vector<uint32_t> mk((size_t)words, 0u);
+    rc(jla::cu_mask_stream_get(reinterpret_cast<hipStream_t>(s), mk.data(), (int)words), "cu_mask_of");
+    return std::vector<int64_t>(mk.begin(), mk.end());
+  });
+  m.def("stream_destroy", [](int64_t s) { rc(jla::stream_destroy(reinterpret_cast<hipStream_t>(s)), "stream_destroy"); });
+  m.def("cu_census", [](Tensor out) {
+    check_gpu(out, "out");
+    check(out.scalar_type() == torch::kInt32 && out.numel() % 2 == 0, "cu_census: int32 [2 * blocks]");
+    rc(jla::cu_census(reinterpret_cast<uint32_t*>(out.data_ptr()), (int)(out.numel() / 2), stream()), "cu_census");
+  });
   m.def("attn_set_v3_kpg", [](int64_t m) { jla::attn_set_v3_kpg((int)m); });
   m.def("attn_set_v3_max_pairs", [](int64_t n) { jla::attn_set_v3_max_pairs((int)n); });
   m.def("attn_set_v5_max_pairs", [](int64_t n) { jla::attn_set_v5_max_pairs((int)n); });

@@ -159,4 +159,10 @@ int car_set_grid(void* state, int grid);  // collective blocks per launch (0: th
 void car_destroy(void* state);
 int decode_update(const int32_t* nxt, int32_t* finished, int32_t* sequences, int32_t* cur_len, int32_t* tokens,
                   int32_t* positions, int32_t* slot, int B, int L, int pad, int eos, hipStream_t s);
+// CU placement (placement.hip): CU-masked streams and a census of where a launch's workgroups run
+int cu_census(uint32_t* out, int blocks, hipStream_t s);
+int cu_mask_stream_create(const uint32_t* mask, int words, hipStream_t* out);
+int cu_mask_stream_get(hipStream_t s, uint32_t* mask, int words);
+int stream_destroy(hipStream_t s);
+
 }  // namespace jla

@@ -85,20 +85,10 @@ def _scratch_users(remarks: str):
     return bad
 
 
-# Kernels allowed to use scratch, by mangled-name substring -> max bytes/lane: rare shapes where a spill is
-# accepted, and epilogue-only spills (2-3 dwords AFTER the main loop; the loop itself is checked
-# spill-free at this bound: its 256 accumulators + two fragment sets use the whole 512-register file).
-SCRATCH_OK = {"attn_decode_v2_kernelILi16E": 1 << 20,
-              # gemm2 FA + fused RMS: a 3-dword spill in the split-K fixup tail (after the main loop)
-              "gemm2_kernelILi0ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16, "gemm2_kernelILi2ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1E": 16,
-              # gemm2 FA + fused RMS, direct RoPE / KV-write epilogue (MODE_QKV): 3 dwords spilled and reloaded in
-              # the LDS-staged epilogue, after the last MFMA (checked in the .s)
-              "gemm2_kernelILi3ELi2ELi4ELb1ELb1ELi8ELi4ELi1ELb1ELi2E": 16,
-              # gemm4 stream-K, bf16/fp32 store: one accumulator tile spilled across the ticket / last-arriver block and
-              # one dword in the segment prologue -- outside the main loop (checked in the .s)
-              "gemm4_sk_kernelILi0E": 32,
-              # (debug-bounds build) gemm4 stream-K QKV: 2 dwords in the epilogue
-              "gemm4_sk_kernelILi3E": 16}
+# Kernels allowed to use scratch, by mangled-name substring -> max bytes/lane (a rare shape where a spill is accepted).
+# Empty: no kernel of the release or the bounds-checked build spills (re-checked in round 6 after the stream-K, fixup
+# and exchange-split plans whose epilogue spills these entries used to allow were deleted).
+SCRATCH_OK: dict = {}
 
 
 def _compile_hip(src: Path, obj: Path, headers, force: bool, extra=()):

@@ -347,34 +347,7 @@ void check_g5_ws(const c10::optional<Tensor>& ws, int64_t k, int64_t ksplit, int
   check(ws->scalar_type() == torch::kFloat32 && ws->numel() >= eks * m * (n + (rms ? 1 : 0)), "gemm ws too small");
 }
 
-// workspace + self-resetting counters of an in-launch hand-off plan (tile 8)
-struct SkWs {
-  float* ws = nullptr;
-  size_t ws_floats = 0;
-  int32_t* tk = nullptr;
-  int n_tk = 0;
-};
-// gemm4 exchange split-K (tile 8) workspace: partial wave blocks + self-resetting counters (+ the error word)
-SkWs check_g4xk_ws(const c10::optional<Tensor>& ws, const c10::optional<Tensor>& tickets, int64_t m, int64_t n,
-                   int64_t ks) {
-  SkWs r;
-  check(ws.has_value() && tickets.has_value(), "gemm tile 8: the exchange needs ws and tickets (gemm4_xk_workspace)");
-  check_gpu(*ws, "gemm4 xk ws");
-  check_gpu(*tickets, "gemm4 xk counts");
-  check(ws->scalar_type() == torch::kFloat32 &&
-            (size_t)ws->numel() >= jla::gemm4_xk_workspace_floats((int)m, (int)n, (int)ks),
-        "gemm4 xk ws too small (gemm4_xk_workspace)");
-  check(tickets->scalar_type() == torch::kInt32 && tickets->numel() >= jla::gemm4_xk_counts((int)m, (int)n),
-        "gemm4 xk counts too small");
-  r.ws = ptr<float>(*ws);
-  r.ws_floats = ws->numel();
-  r.tk = ptr<int32_t>(*tickets);
-  r.n_tk = (int)tickets->numel();
-  return r;
-}
-
-// Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel;
-// tile 8 -> gemm4 split-K with the in-launch exchange of partial blocks (ws/tickets from gemm4_xk_workspace).
+// Tiled MFMA GEMM; ksplit > 1 -> split-K partials in ws + fixed-order reduce/epilogue kernel.
 // rms_ws: optional fp32 scratch (>= M floats) for the row statistic of the fused norm on gemm4 plans without a K
 // split (computed ahead of the GEMM by rms_rowinv); absent: the statistic is summed inside the main loop.
 static float* rms_ws_ptr(const c10::optional<Tensor>& rws, int64_t m, size_t* floats) {
@@ -388,7 +361,7 @@ static float* rms_ws_ptr(const c10::optional<Tensor>& rws, int64_t m, size_t* fl
 
 void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bool accumulate,
           c10::optional<Tensor> mirror, int64_t ksplit, c10::optional<Tensor> ws, double rms_eps, int64_t tile,
-          c10::optional<Tensor> tickets, c10::optional<Tensor> pack_out, c10::optional<Tensor> rms_ws) {
+          c10::optional<Tensor> pack_out, c10::optional<Tensor> rms_ws) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
@@ -403,25 +376,14 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   if (pack_out.has_value()) {
     check(m <= SKINNY_MAX_M && (mode == 1 || mode == 2) && (mode != 1 || mir), "gemm pack_out: decode M, residual "
           "(with its mirror) or SwiGLU");
-    check((ksplit > 1 || tile == 11 || tile == 12) && tile != 8, "gemm pack_out: the split-K reduce-kernel path only");
+    check(ksplit > 1 || tile == 11 || tile == 12, "gemm pack_out: the split-K reduce-kernel path only");
     pqa.pack = packed_ptr(pack_out, m, mode == 2 ? n / 2 : n, "pack_out");
   }
   if (tile == 11 || tile == 12) {  // gemm5 (weight-streaming) partial slabs + the reduce kernel's epilogue, any split
     check_g5_ws(ws, k, ksplit, m, n, rms_eps >= 0);
     rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
                  out.scalar_type() == torch::kFloat32, mir, pqa.pack ? &pqa : nullptr, ptr<float>(*ws), ws->numel(),
-                 ksplit, stream(), (float)rms_eps, (int)tile, nullptr, 0, nullptr, 0),
-       "gemm");
-    return;
-  }
-  if (tile == 8) {  // residual epilogue only: the splits exchange their partial blocks inside the launch
-    check(mode == 1 && rms_eps < 0, "gemm tile 8: residual epilogue, no fused norm");
-    check(pqa.pack == nullptr, "gemm tile 8: no packed output copy");
-    check(jla::gemm4_xk_ok((int)m, (int)n, (int)k, (int)ksplit), "gemm tile 8: needs K % 64 == 0, a split of 2+ "
-          "and tiles x split <= CUs (gemm4_xk_ok)");
-    const SkWs sk = check_g4xk_ws(ws, tickets, m, n, ksplit);
-    rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate, true, mir, nullptr, sk.ws,
-                 sk.ws_floats, ksplit, stream(), -1.f, 8, sk.tk, sk.n_tk, nullptr, 0),
+                 ksplit, stream(), (float)rms_eps, (int)tile, nullptr, 0),
        "gemm");
     return;
   }
@@ -431,7 +393,7 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
   rc(jla::gemm(cbf(x), w.data_ptr(), out.data_ptr(), m, n, k, mode, accumulate,
                out.scalar_type() == torch::kFloat32, mir, pqa.pack ? &pqa : nullptr,
                ksplit > 1 ? ptr<float>(*ws) : nullptr, ksplit > 1 ? ws->numel() : 0, ksplit, stream(),
-               (float)rms_eps, (int)tile, nullptr, 0, rws, rfl),
+               (float)rms_eps, (int)tile, rws, rfl),
      "gemm");
 }
 
@@ -439,19 +401,16 @@ void gemm(Tensor x, Tensor w, int64_t n, int64_t k, Tensor out, int64_t mode, bo
 // applies the fused RMSNorm statistic, otherwise x must already be scaled).
 void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor positions, Tensor kc, Tensor vc,
               Tensor slot, int64_t seq_len, int64_t h, int64_t hkv, int64_t dh, Tensor q, int64_t ksplit,
-              c10::optional<Tensor> ws, double rms_eps, int64_t tile, c10::optional<Tensor> tickets,
-              c10::optional<Tensor> rms_ws) {
+              c10::optional<Tensor> ws, double rms_eps, int64_t tile, c10::optional<Tensor> rms_ws) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
   const int64_t m = x.size(0);
   jla::QKVArgs qa = qkv_args(m, n, table, positions, kc, vc, slot, seq_len, h, hkv, dh, q);
-  check(tile != 8, "gemm_qkv: tile 8 (the exchange split) has the residual epilogue only");
-  (void)tickets;
   if (tile == 11 || tile == 12) {  // gemm5 partial slabs, RoPE / KV write in the reduce kernel
     check_g5_ws(ws, k, ksplit, m, n, rms_eps >= 0);
     rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, ptr<float>(*ws), ws->numel(),
-                 ksplit, stream(), (float)rms_eps, (int)tile, nullptr, 0, nullptr, 0),
+                 ksplit, stream(), (float)rms_eps, (int)tile, nullptr, 0),
        "gemm_qkv");
     return;
   }
@@ -461,7 +420,7 @@ void gemm_qkv(Tensor x, Tensor w, int64_t n, int64_t k, Tensor table, Tensor pos
     size_t rfl = 0;
     float* rws = rms_ws_ptr(rms_ws, m, &rfl);
     rc(jla::gemm(cbf(x), w.data_ptr(), nullptr, m, n, k, MODE_QKV_ID, 0, 0, nullptr, &qa, nullptr, 0, 1, stream(),
-                 (float)rms_eps, (int)tile, nullptr, 0, rws, rfl),
+                 (float)rms_eps, (int)tile, rws, rfl),
        "gemm_qkv");
     return;
   }
@@ -781,24 +740,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("pack_out") = py::none());
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("out"), py::arg("mode"),
         py::arg("accumulate"), py::arg("mirror") = py::none(), py::arg("ksplit") = 1, py::arg("ws") = py::none(),
-        py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("tickets") = py::none(),
-        py::arg("pack_out") = py::none(), py::arg("rms_ws") = py::none());
+        py::arg("rms_eps") = -1.0, py::arg("tile") = 0, py::arg("pack_out") = py::none(),
+        py::arg("rms_ws") = py::none());
   m.def("gemm_qkv_direct_ok", [](int64_t m, int64_t tile, int64_t k) {
     return jla::gemm_qkv_direct_ok((int)m, (int)tile, (int)k) != 0;
   });
   m.def("gemm_set_g4_default", [](int64_t on) { jla::gemm_set_g4_default((int)on); });
   m.def("gemm_set_g4_group", [](int64_t gm) { jla::gemm_set_g4_group((int)gm); });
-  m.def("gemm4_xk_ok", [](int64_t m, int64_t n, int64_t k, int64_t ks) {
-    return jla::gemm4_xk_ok((int)m, (int)n, (int)k, (int)ks) != 0;
-  });
-  m.def("gemm4_xk_workspace", [](int64_t m, int64_t n, int64_t ks) {
-    return py::make_tuple((int64_t)jla::gemm4_xk_workspace_floats((int)m, (int)n, (int)ks),
-                          (int64_t)jla::gemm4_xk_counts((int)m, (int)n));
-  });
   m.def("gemm_qkv", &gemm_qkv, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("table"),
         py::arg("positions"), py::arg("kc"), py::arg("vc"), py::arg("slot"), py::arg("seq_len"), py::arg("h"),
         py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("ksplit"), py::arg("ws"), py::arg("rms_eps") = -1.0,
-        py::arg("tile") = 0, py::arg("tickets") = py::none(), py::arg("rms_ws") = py::none());
+        py::arg("tile") = 0, py::arg("rms_ws") = py::none());
   m.def("gemm_argmax", &gemm_argmax, py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"), py::arg("ws"),
         py::arg("rms_eps"), py::arg("idx"), py::arg("val"), py::arg("rms_ws") = py::none());
   m.def("gemm_argmax_workspace", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_argmax_workspace_floats(m, n); });
@@ -823,6 +775,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
     return jla::qkv_attn_splits((int)m, (int)b, (int)hkv, (int)rep, (int)t_cap, (int)n, (int)cus, (int)spl);
   }, py::arg("m"), py::arg("b"), py::arg("hkv"), py::arg("rep"), py::arg("t_cap"), py::arg("n"), py::arg("cus"),
      py::arg("spl") = 1);
+  m.def("qkv_attn_set_diag", [](int64_t d) { jla::qkv_attn_set_diag((int)d); });
   m.def("qkv_attn_occupancy", [](int64_t m, int64_t rep, int64_t spl) {
     return jla::qkv_attn_occupancy((int)m, (int)rep, (int)spl);
   }, py::arg("m"), py::arg("rep"), py::arg("spl") = 1);

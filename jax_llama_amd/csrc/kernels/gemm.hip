@@ -1019,128 +1019,6 @@ __global__ void __launch_bounds__(256, 1)
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// gemm4 split-K with an in-kernel exchange (tile config 8): for outputs with too few 256 x 256 tiles to fill the chip
-// (Llama-3-8B at M = 2048: o / down have 128 tiles for 256 CUs) the K range is cut over ks co-resident workgroups per
-// tile, and instead of fp32 slabs + a reduce launch the splits hand their partial wave blocks to each other: wave
-// block b (128 x 128 of the tile, 64 KiB of fp32) is OWNED by split b * ks / 4; every other split's wave b publishes
-// its accumulators with write-through (sc1) stores, drains them (vmcnt(0)) and bumps the block's agent-scope counter,
-// then exits; the owner wave polls the counter (bounded: a missing partner sets the error word instead of hanging),
-// lands the ks - 1 partner blocks in its idle K-tile slots by sc1 LDS-DMA, sums them onto its own in a fixed order
-// (at ks = 2 the reduce kernel's p0 + p1) and runs the ordinary epilogue on its block, then resets the counter
-// (cdna_hip_programming.md Guideline 16).
-// No second launch, no full-size slab re-read, and the residual's read-modify-write is spread over the owners.
-// Needs grid = tiles * ks <= CUs (one 128 KiB-LDS workgroup per CU, all resident at once); the launcher checks it.
-// Epilogues without a workgroup barrier only (residual, fp32 / bf16-direct store): the non-owner waves exit early.
-struct G4Xk {
-  float* ws;         // [tiles][4 blocks][ks][64 KiB]: the partial wave blocks
-  int32_t* counts;   // [tiles * 4] arrivals per block (self-resetting), [tiles * 4]: the error word
-  int ks;
-};
-
-template <int MODE, int KS>
-__global__ void __launch_bounds__(256, 1)
-    gemm4_xk_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                    int K, int accumulate, int out_f32, bf16_t* __restrict__ mirror, int kc, int tiles_m, int tiles_n,
-                    int group_m, G4Xk xk) {
-  static_assert(MODE == MODE_RESIDUAL, "exchange epilogues: residual");
-  __shared__ u32x4 lds[2 * G4_SLOT_U4 + 64];
-  const int lane = threadIdx.x & 63;
-  const int wu = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int tiles = tiles_m * tiles_n;
-  const int split = wgid / tiles, pid = wgid - split * tiles;
-  int tm, tn;
-  g4_tile_coords(pid, tiles_m, tiles_n, tm, tn, group_m);
-  const int m0 = tm * G4_BM, n0 = tn * G4_BN;
-  const int t0 = split * kc, KT = max(0, min(K >> 6, t0 + kc) - t0);
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const G4Args g{x, W, out, M, N, K, kc, tiles_m, tiles_n};
-  g4_mainloop<false>(g, lds, m0, n0, t0, KT, wu, lane, acc);
-
-  __syncthreads();  // every wave is past its last LDS read: the K-tile slots take the partner blocks
-  const int owner = (wu * KS) >> 2;
-  const size_t blk = (size_t)pid * 4 + wu;
-  // this block's KS partial slots (64 KiB each); every access write-through / coherent (sc1)
-  u32x4* const slots = reinterpret_cast<u32x4*>(xk.ws + blk * (size_t)KS * 16384);
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(slots, 0, KS * 65536, 0x00020000);
-  int32_t* const cnt = xk.counts + blk;
-  if (split != owner) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, g4_take(acc[j][i])), rsrc,
-                                               split * 65536 + (j * 8 + i) * 1024 + lane * 16, 0, 16);  // (16: sc1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // owner: every partner's block has landed (bounded wait), then the sum in split order
-  {
-    const unsigned long long t_start = wall_clock64();
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < KS - 1) {
-      if (wall_clock64() - t_start > 20000000ull) {  // 200 ms at 100 MHz: a partner never ran
-        if (lane == 0) __hip_atomic_store(xk.counts + (size_t)tiles * 4, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  if constexpr (KS == 2) {
-    // the partner's whole 64 KiB block lands in this wave's half of the (idle) K-tile slots by LDS-DMA: 64 loads in
-    // flight, one wait, then the sum from LDS (p0 + p1: the reduce kernel's order either way round)
-    char* const wl = reinterpret_cast<char*>(lds) + (wu & 1) * 65536;
-    const u32x4* const src = slots + (split ^ 1) * 4096 + lane;
-#pragma unroll
-    for (int f = 0; f < 64; ++f) glds16_asm_sc1(src + f * 64, wl + f * 1024);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const f32x4 p = *reinterpret_cast<const f32x4*>(wl + (j * 8 + i) * 1024 + lane * 16);
-        const f32x4 tsum = g4_take(acc[j][i]) + p;
-        asm volatile("" : "=a"(acc[j][i]) : "0"(tsum));
-      }
-  } else {
-    // one owner wave per workgroup: the KS - 1 partner blocks land two at a time in the two (idle) 64 KiB K-tile slots
-    // (128 DMAs in flight per round), summed from the owner's own split cyclically -- a fixed order per block
-    char* const wl = reinterpret_cast<char*>(lds);
-#pragma unroll
-    for (int d0 = 1; d0 < KS; d0 += 2) {
-      const int nb = d0 + 1 < KS ? 2 : 1;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous round's reads are done with the slots
-#pragma unroll
-      for (int b = 0; b < nb; ++b) {
-        const u32x4* const src = slots + ((split + d0 + b) & (KS - 1)) * 4096 + lane;
-#pragma unroll
-        for (int f = 0; f < 64; ++f) glds16_asm_sc1(src + f * 64, wl + b * 65536 + f * 1024);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          f32x4 tsum = g4_take(acc[j][i]) + *reinterpret_cast<const f32x4*>(wl + (j * 8 + i) * 1024 + lane * 16);
-          if (nb == 2) tsum += *reinterpret_cast<const f32x4*>(wl + 65536 + (j * 8 + i) * 1024 + lane * 16);
-          asm volatile("" : "=a"(acc[j][i]) : "0"(tsum));
-        }
-    }
-  }
-  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  g4_epilogue<MODE, 0>(acc, nullptr, lds, wu, lane, m0, n0, 0,
-                       G4Epi{out, M, N, K, accumulate, out_f32, mirror, tiles_n, -1.f, nullptr, nullptr}, QKVArgs{});
-}
-
-
 // Sum of the ksplit fp32 slabs at float4 e4 in split order: the loads of up to 8 splits are issued before the first
 // add (the round-4 loop waited on each split in turn: 12 dependent L2/HBM round trips for the 70B shard's qkv at M =
 // 256, 9 us for 1.3 MB of output). Same addition order as before, so bit for bit the same sums.
@@ -1299,21 +1177,19 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 //      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
 static bool use_g4(int tile, int M, int K);
-constexpr int G4N6_TILE = 15;   // gemm4 on 256 x 192 tiles (g4n_mainloop<6>)
-constexpr int G4N6D_TILE = 16;  // the same with the weights three K-tiles deep (g4n_mainloop<6, W3>)
-constexpr int G4ND_TILE = 17;   // 256 x 128 tiles with the deep weight ring (g4n_mainloop<4, W3>)
+// gemm4 on narrower tiles, both with the weights three K-tiles deep (W3; the plain-ring forms, tiles 10 / 15, were
+// never picked by the tuner at a bench shape and were removed in round 6):
+constexpr int G4N6D_TILE = 16;  // 256 x 192 tiles (g4n_mainloop<6, W3>)
+constexpr int G4ND_TILE = 17;   // 256 x 128 tiles (g4n_mainloop<4, W3>)
 int gemm_qkv_direct_ok(int M, int tile, int K) {
-  return ((tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) ||
-         use_g4(tile, M, K) || ((tile == G4N6_TILE || tile == G4N6D_TILE) && (K & 63) == 0);
+  return ((tile == 0 || tile == 1) && tile_cfg(tile, M) == 1) || use_g4(tile, M, K) ||
+         (tile == G4N6D_TILE && (K & 63) == 0);
 }
 
 // gemm4 (tile config 7; the default for tile 0 once g_g4_default is set): the 4-wave 256 x 256 kernel of gemm4w.h.
 // Needs K % 64 == 0; data-parallel or plain split-K (MODE_PARTIAL + reduce kernel) only -- the stream-K tail,
 // hybrid and in-kernel fixup plans stay on gemm2.
 constexpr int G4_TILE = 7;
-// tile config 10: gemm4 on 256 x 128 tiles (g4n_mainloop, 4 n-tiles per wave): store / residual / SwiGLU / split-K
-// partials; a fused norm only with the precomputed statistic (no K split)
-constexpr int G4N_TILE = 10;
 static bool g_g4_default = true;
 void gemm_set_g4_default(int on) { g_g4_default = on != 0; }
 constexpr int G4P_TILE = 13;  // persistent gemm4 (gemm4p_kernel)
@@ -1363,23 +1239,15 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
       return;
     }
   }
-  if constexpr (NJ != 8) {  // 256 x 128 / 192 tiles: the statistic precomputed (callers guarantee rms_ws, no K split)
-    constexpr bool D6 = true;  // the deep-W forms (tiles 16 / 17) of the 192- and 128-column tiles
+  if constexpr (NJ != 8) {  // 256 x 128 / 192 tiles (deep W only): the statistic precomputed (callers guarantee rms_ws,
+    //                         no K split)
     if (rms && rms_ws != nullptr && ksplit == 1 && MODE != MODE_PARTIAL) {
       if (rms_rowinv(x, rms_ws, M, K, rms_eps, s) != 0) return;
-      if (D6 && deep)
-        gemm4_kernel<MODE, 2, NJ, 0, D6><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
+      gemm4_kernel<MODE, 2, NJ, 0, true><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
                                                               tn, rms_eps, ssq, qa, rms_ws, gm);
-      else
-        gemm4_kernel<MODE, 2, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
-                                                       rms_eps, ssq, qa, rms_ws, gm);
     } else if (!rms) {
-      if (D6 && deep)
-        gemm4_kernel<MODE, 0, NJ, 0, D6><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
+      gemm4_kernel<MODE, 0, NJ, 0, true><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm,
                                                               tn, rms_eps, ssq, qa, nullptr, gm);
-      else
-        gemm4_kernel<MODE, 0, NJ><<<grid, 256, 0, s>>>(x, w, out, M, N, K, accumulate, out_f32, mirror, kc, tm, tn,
-                                                       rms_eps, ssq, qa, nullptr, gm);
     }
     return;
   }
@@ -1415,55 +1283,23 @@ static void launch_g4(const bf16_t* x, const u32x4* w, void* out, int M, int N, 
 #undef JLA_G4
 }
 
-// gemm4 split-K with the in-kernel exchange (tile config 8): partial wave blocks + self-resetting counters
-constexpr int G4_XK_TILE = 8;
-static int num_cus();
-static int g4_xk_tiles(int M, int N) { return ((M + G4_BM - 1) / G4_BM) * ((N + G4_BN - 1) / G4_BN); }
-size_t gemm4_xk_workspace_floats(int M, int N, int ks) { return (size_t)g4_xk_tiles(M, N) * 4 * ks * 16384; }
-int gemm4_xk_counts(int M, int N) { return g4_xk_tiles(M, N) * 4 + 1; }
-// the plan applies: a real split, every workgroup resident at once (one per CU)
-int gemm4_xk_ok(int M, int N, int K, int ks) {
-  return (K & 63) == 0 && (ks == 2 || ks == 4 || ks == 8) && (K >> 6) >= ks && g4_xk_tiles(M, N) * ks <= num_cus();
-}
-
-static int launch_g4_xk(const bf16_t* x, const u32x4* w, float* out, int M, int N, int K, int accumulate,
-                        bf16_t* mirror, int ks, float* ws, size_t ws_floats, int32_t* counts, int n_counts,
-                        hipStream_t s) {
-  if (!gemm4_xk_ok(M, N, K, ks) || ws == nullptr || ws_floats < gemm4_xk_workspace_floats(M, N, ks) ||
-      counts == nullptr || n_counts < gemm4_xk_counts(M, N))
-    return -3;
-  const int tm = (M + G4_BM - 1) / G4_BM, tn = (N + G4_BN - 1) / G4_BN;
-  const int KS64 = K >> 6, kc = (KS64 + ks - 1) / ks;
-  const int gm = g4_group_m(tm, tn, K);
-#define JLA_XK(KSV)                                                                                               \
-  if (ks == KSV) {                                                                                                \
-    gemm4_xk_kernel<MODE_RESIDUAL, KSV><<<tm * tn * ks, 256, 0, s>>>(x, w, out, M, N, K, accumulate, 1, mirror, kc, \
-                                                                     tm, tn, gm, G4Xk{ws, counts, ks});           \
-    JLA_CHECK_LAUNCH();                                                                                           \
-    return 0;                                                                                                     \
-  }
-  JLA_XK(2) JLA_XK(4) JLA_XK(8)
-#undef JLA_XK
-  return -1;
-}
-
 template <int MODE>
 static void launch_g2(const bf16_t* x, const u32x4* w, void* out, int M, int N, int K, int accumulate, int out_f32,
                       bf16_t* mirror, int kc, int ksplit, float rms_eps, float* ssq, int tile, hipStream_t s,
                       const QKVArgs& qa = QKVArgs{}, float* rms_ws = nullptr) {
   if constexpr (MODE != MODE_QKV && MODE != MODE_ARGMAX) {
-    if ((tile == G4N_TILE || tile == G4ND_TILE) && (K & 63) == 0) {
+    if (tile == G4ND_TILE && (K & 63) == 0) {
       launch_g4<MODE, 4>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, false,
-                         tile == G4ND_TILE);
+                         true);
       return;
     }
   }
-  // tile config 15: 256 x 192 tiles -- Llama-3-8B qkv (N = 6144) at M = 2048 is 8 x 32 = 256 tiles, one per CU, where
+  // tile config 16: 256 x 192 tiles -- Llama-3-8B qkv (N = 6144) at M = 2048 is 8 x 32 = 256 tiles, one per CU, where
   // the 256 x 256 grid has 192 (0.75 of a wave); the QKV epilogue included
   if constexpr (MODE != MODE_ARGMAX) {
-    if ((tile == G4N6_TILE || tile == G4N6D_TILE) && (K & 63) == 0) {
+    if (tile == G4N6D_TILE && (K & 63) == 0) {
       launch_g4<MODE, 6>(x, w, out, M, N, K, accumulate, out_f32, mirror, ksplit, rms_eps, ssq, s, qa, rms_ws, false,
-                         tile == G4N6D_TILE);
+                         true);
       return;
     }
   }
@@ -1606,22 +1442,17 @@ static int launch_g5(const bf16_t* x, const u32x4* w, void* out, int M, int N, i
 
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps, int tile, int32_t* tickets, int n_tickets, float* rms_ws, size_t rms_ws_floats) {
+         float rms_eps, int tile, float* rms_ws, size_t rms_ws_floats) {
   if (tile == G5_TILE || tile == G5_TILE + 1) {
     if (mode == MODE_ARGMAX || (rms_eps >= 0.f && mode == MODE_RESIDUAL)) return -1;
     return launch_g5(x, static_cast<const u32x4*>(W), out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ws,
                      ws_floats, ksplit, rms_eps, tile, s);
   }
   if (rms_ws != nullptr && rms_ws_floats < (size_t)M) rms_ws = nullptr;  // too small: the in-loop statistic
-  if ((tile == G4N_TILE || tile == G4ND_TILE) &&
+  if (tile == G4ND_TILE &&
       ((K & 63) || (mode == MODE_QKV && ksplit <= 1) || mode == MODE_ARGMAX ||
        (rms_eps >= 0.f && mode != MODE_RESIDUAL && (ksplit > 1 || rms_ws == nullptr))))
     return -1;  // the 256 x 128 plan: no QKV / argmax epilogue, the fused norm only precomputed without a K split
-  if (tile == G4_XK_TILE) {  // gemm4 split-K, the splits exchange their partial blocks in-kernel (residual only)
-    if (mode != MODE_RESIDUAL || rms_eps >= 0.f) return -1;
-    return launch_g4_xk(x, static_cast<const u32x4*>(W), static_cast<float*>(out), M, N, K, accumulate, mirror,
-                        ksplit, ws, ws_floats, tickets, n_tickets, s);
-  }
   if (M <= 0) return 0;
   if ((N & 15) || (K & 31)) return -1;
   if (mode == MODE_SWIGLU && (N & 31)) return -1;
@@ -1636,7 +1467,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile, K) && rms)) return -1;
   // the 256 x 128 / 192 tiles take the fused norm only as the precomputed statistic without a K split (launch_g4
   // would otherwise launch nothing)
-  if ((tile == G4N_TILE || tile == G4ND_TILE || tile == G4N6_TILE || tile == G4N6D_TILE) && rms &&
+  if ((tile == G4ND_TILE || tile == G4N6D_TILE) && rms &&
       (ksplit > 1 || rms_ws == nullptr))
     return -6;
   const u32x4* w = static_cast<const u32x4*>(W);

@@ -560,6 +560,7 @@ struct FusedAttn {
   int32_t* sync;            // [0] qkv-done counter, [1] attention-seen counter (both self-resetting), [2] error word
   int splits, grid_q, t_cap;
   float scale_log2;
+  int diag;                 // tools / tests only (qkv_attn_set_diag): 1 = the qkv workgroups never publish
 };
 
 // SPL: K of the qkv GEMV cut over SPL workgroups per column group (the split GEMV's last-arriver sum; only that
@@ -577,7 +578,7 @@ __global__ void __launch_bounds__(256)
     // the workgroup's barrier, then one agent-scope add
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(fa.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && !fa.diag) __hip_atomic_fetch_add(fa.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   extern __shared__ __attribute__((aligned(16))) char ldsq[];
@@ -601,12 +602,15 @@ __global__ void __launch_bounds__(256)
   for (int i = 0; i < 8; ++i) kr[i] = u32x4{0u, 0u, 0u, 0u};
   ad6_issue<false>(k0, kr, vslot, kb, vb, T, lane);
 
-  // 2. wait until every qkv workgroup has published (one polling lane, bounded)
+  // 2. wait until every qkv workgroup has published (one polling lane, bounded). A timeout is sticky: the error word
+  //    stays set (the host raises at its next poll: ops.check_inlaunch), the counters are never reset again (a late
+  //    publish would leave them off by its count), and every later launch's attention workgroups skip the wait and
+  //    write nothing -- no token is ever computed from a stale q / K / V without the error word saying so.
   int* flag = reinterpret_cast<int*>(ldsq + 4 * AD6_SLOT_BYTES + 1008);
   if (threadIdx.x == 0) {
+    int err = __hip_atomic_load(fa.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const long long t0 = (long long)wall_clock64();
-    int err = 0;
-    while (__hip_atomic_load(fa.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fa.grid_q) {
+    while (!err && __hip_atomic_load(fa.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fa.grid_q) {
       if ((long long)wall_clock64() - t0 > 20000000LL) {  // 0.2 s at the 100 MHz constant clock
         __hip_atomic_store(fa.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         err = 1;
@@ -614,13 +618,16 @@ __global__ void __launch_bounds__(256)
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    (void)err;
-    // the last attention workgroup past the wait resets both counters for the next launch
-    const int seen = __hip_atomic_fetch_add(fa.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (seen == (int)gridDim.x - fa.grid_q - 1) {
+    // the last attention workgroup past the wait resets both counters for the next launch -- unless some workgroup
+    // of this launch (or an earlier one) timed out: the acq_rel add orders a timed-out workgroup's error store before
+    // its arrival, and the last arriver's error load after every arrival
+    const int seen = __hip_atomic_fetch_add(fa.sync + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen == (int)gridDim.x - fa.grid_q - 1 &&
+        __hip_atomic_load(fa.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       __hip_atomic_store(fa.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(fa.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    *flag = err;
   }
   __syncthreads();
   // the prefetch landed during the qkv phase: retire it here, before any branch (hipcc must never copy a ring
@@ -628,6 +635,7 @@ __global__ void __launch_bounds__(256)
   ::wait_vmcnt<0>();
 #pragma unroll
   for (int i = 0; i < 8; ++i) pin(kr[i]);
+  if (*flag) return;  // failed state (timeout now or earlier): the output is not written
   const int split_lo = sp * QA_SPLIT_KEYS;
   const bool split_live = split_lo < hi && split_lo + QA_SPLIT_KEYS > lo;
   if (!split_live) {
@@ -836,6 +844,9 @@ int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, i
   return grid <= cus * qkv_attn_occupancy(M, rep, spl) ? splits : 0;
 }
 
+static int g_qa_diag = 0;
+void qkv_attn_set_diag(int d) { g_qa_diag = d; }
+
 int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
                     bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
                     int t_cap, int splits, int spl, hipStream_t s) {
@@ -852,7 +863,7 @@ int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float r
   }
   if (splits < 1 || splits > QA_MAX_SPLITS || splits * QA_SPLIT_KEYS < t_cap) return -1;
   const FusedAttn fa{out, out_pack, kv_start, ws, tickets, sync, splits, grid_q, t_cap,
-                     1.4426950408889634f / sqrtf((float)AD6_DH)};
+                     1.4426950408889634f / sqrtf((float)AD6_DH), g_qa_diag};
   const int use_rms = rms_eps >= 0.f;
   const float eps = use_rms ? rms_eps : 0.f;
   const int mt = M <= 16 ? 1 : 2;

@@ -45,7 +45,8 @@ constexpr long long TPRES_REGION = 64 * 64 * 4;  // up to 64 rows x 64 columns x
 // qkv_attn_splits (0 = not applicable: run the two kernels); ws >= pairs * splits * rep * 132 floats, tickets >= pairs,
 // sync >= 3 int32 (zeroed once, self-resetting)
 int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl = 1);
-int qkv_attn_occupancy(int M, int rep, int spl = 1);  // resident workgroups per CU the fused launch counts on
+int qkv_attn_occupancy(int M, int rep, int spl = 1);
+void qkv_attn_set_diag(int d);  // tests only: 1 = the qkv workgroups never publish (forces the timeout path)  // resident workgroups per CU the fused launch counts on
 int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
                     bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
                     int t_cap, int splits, int spl, hipStream_t s);  // spl 2: K of the qkv GEMV over 2 (qa.sk_ws/sk_tk)
@@ -68,12 +69,6 @@ void gemm_set_g4_group(int gm);
 int gemm5_ksplit(int K, int ksplit);
 int clock_probe(int iters, int grid, unsigned long long* out, hipStream_t s);  // [cycles, 100 MHz ticks]
 void gemm5_set_diag(int d);  // tools only: gemm5 ablations (wrong results)  // gemm5 (tiles 11 / 12): the effective split over 64-deep K-stages
-// tile config 8: gemm4 split-K whose splits exchange their partial wave blocks inside the launch (residual
-// epilogue): ws >= gemm4_xk_workspace_floats(M, N, ks), tickets >= gemm4_xk_counts(M, N) int32 zero-initialised
-// once (self-resetting; the last one is the error word); only where gemm4_xk_ok (all workgroups resident)
-size_t gemm4_xk_workspace_floats(int M, int N, int ks);
-int gemm4_xk_counts(int M, int N);
-int gemm4_xk_ok(int M, int N, int K, int ks);
 size_t gemm_workspace_floats(int M, int N, int K);
 // rms_eps >= 0: x is the UNscaled activation and each output row is scaled by rsqrt(mean(x^2) + eps)
 // (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
@@ -81,8 +76,7 @@ size_t gemm_workspace_floats(int M, int N, int K);
 // 8 gemm4 exchange split (above), 11 / 12 gemm5
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
-         float rms_eps = -1.f, int tile = 0, int32_t* tickets = nullptr, int n_tickets = 0,
-         float* rms_ws = nullptr, size_t rms_ws_floats = 0);
+         float rms_eps = -1.f, int tile = 0, float* rms_ws = nullptr, size_t rms_ws_floats = 0);
 // rms_ws (>= M floats): with the fused norm, a gemm4 plan without a K split computes the row statistic ahead of
 // the GEMM into it (rms_rowinv) instead of inside its main loop; null: in-loop statistic
 // greedy lm_head: GEMM + first-max argmax epilogue (ws >= gemm_argmax_workspace_floats(M, N) floats)

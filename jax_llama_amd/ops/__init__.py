@@ -313,31 +313,19 @@ def _tiled_input(x, rms_eps, fused=False):
     return x if x.dtype == BF16 else x.to(BF16)
 
 
-XK_TILE = 8  # gemm4 split-K with the in-launch exchange of partial blocks (csrc/kernels/gemm.hip gemm4_xk_kernel)
-XK_COUNTS = 4096  # counters of the exchange: one fixed-size array (no reallocation under graphs)
 G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h): 256- / 128-column workgroups
 
 
-def xk_workspace(e, m, n, ks, device):
-    """Partial-block buffer + self-resetting counters (and the error word) of the exchange plan."""
-    floats, counts = e.gemm4_xk_workspace(m, n, ks)
-    return (workspace.get("gemm_xk", floats, torch.float32, device),
-            workspace.get_zeroed("gemm_xk_counts", max(XK_COUNTS, counts), torch.int32, device))
-
-
 def _gemm_ws(e, m, n, k, device, mode=MODE_STORE, rms=False):
-    """(split-K factor, tile config, workspace, tickets) of the tuned plan for this shape and epilogue: partial slabs
-    for a split summed by the reduce kernel, or the exchange plan's block buffer + counters (tile 8)."""
+    """(split-K factor, tile config, workspace) of the tuned plan for this shape and epilogue: the partial slabs of a
+    split summed by the reduce kernel (gemm5, tiles 11 / 12: always)."""
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, rms)
     if tm in G5_TILES:  # weight-streaming split-K (any split, slabs always): partial slabs + the reduce kernel
         eks = e.gemm5_ksplit(k, ks)
-        return ks, tm, workspace.get("gemm_ws", eks * m * (n + 1), torch.float32, device), None
-    if tm == XK_TILE:
-        ws, tk = xk_workspace(e, m, n, ks, device)
-        return ks, tm, ws, tk
+        return ks, tm, workspace.get("gemm_ws", eks * m * (n + 1), torch.float32, device)
     # split-K slabs [ks][m][n] + the fused-RMS partial sums of squares [ks][m]
     ws = workspace.get("gemm_ws", ks * m * (n + 1), torch.float32, device) if ks > 1 else None
-    return ks, tm, ws, None
+    return ks, tm, ws
 
 
 def _rms_ws(x, fused: bool, ks: int):
@@ -354,20 +342,20 @@ def _tiled(e, x, weight, n, k, out, mode, rms_eps, accumulate, mirror=None, pack
     reduce epilogue also writes the packed copy of the bf16 output (plans that ``_tiled_packs``)."""
     fused = _fused_rms(e, mode, rms_eps)
     xb = _tiled_input(x, rms_eps, fused)
-    ks, tm, ws, tk = _gemm_ws(e, x.shape[0], n, k, x.device, mode, fused)
-    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm, tk,
+    ks, tm, ws = _gemm_ws(e, x.shape[0], n, k, x.device, mode, fused)
+    e.gemm(xb, weight, n, k, out, mode, bool(accumulate), mirror, ks, ws, float(rms_eps) if fused else -1.0, tm,
            pack_out, _rms_ws(x, fused, ks))
 
 
 def _tiled_packs(e, m, n, k, device, mode, rms_eps) -> bool:
     """Whether the tiled GEMM's tuned plan for this decode shape can write a packed output copy: the plain split-K
-    path, whose reduce kernel runs the epilogue (not ks = 1 or the exchange plan)."""
+    path, whose reduce kernel runs the epilogue (not ks = 1)."""
     if e is None or m > SKINNY_M or mode not in (MODE_RESIDUAL, MODE_SWIGLU):
         return False
     ks, tm = autotune.choose_gemm_plan(e, m, n, k, device, mode, _fused_rms(e, mode, rms_eps))
     if tm in G5_TILES:
         return True
-    return ks > 1 and tm != XK_TILE
+    return ks > 1
 
 
 def _variant(e, x, w, mode, x_packed=None, pack_out=None, no_split=False) -> int:
@@ -462,14 +450,14 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
     v = TILED if m > e.SKINNY_MAX_M else _variant(e, x, w, MODE_QKV, x_packed)
     if v == TILED:
         # (same plan key as the plain linear() below: QKV is tuned as a store with the fused norm)
-        ks, tm, ws, _ = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
+        ks, tm, ws = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, _fused_rms(e, MODE_QKV, rms_eps))
         fused = _fused_rms(e, MODE_QKV, rms_eps)
         if ks == 1 and fused and QKV_DIRECT and e.gemm_qkv_direct_ok(m, tm, w.k):
             # enough tiles, no K split: the GEMM's own RoPE / KV-write epilogue (no qkv round trip, no rope kernel)
             q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
             e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                        k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                       int(head_dim), q, 1, None, float(rms_eps), tm, None, _rms_ws(x, fused, 1))
+                       int(head_dim), q, 1, None, float(rms_eps), tm, _rms_ws(x, fused, 1))
             return q
         if ks == 1:  # enough tiles: plain GEMM, then the RoPE/KV-write kernel
             qkv = linear(x, w, rms_eps=rms_eps)
@@ -478,7 +466,7 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
         q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
         e.gemm_qkv(_tiled_input(x, rms_eps, fused), w.weight, w.n, w.k, table, positions.reshape(-1).to(torch.int32),
                    k_cache, v_cache, _slot_tensor(slot0, x.device), int(seq_len), int(n_heads), int(n_kv_heads),
-                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm, None)
+                   int(head_dim), q, ks, ws, float(rms_eps) if fused else -1.0, tm)
         return q
     q = torch.empty(m, n_heads, head_dim, dtype=BF16, device=x.device)
     ws, tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, x.device)
@@ -501,6 +489,26 @@ QKV_ATTN = int(os.environ.get("JLA_QKV_ATTN", "1"))
 # still fits the CUs; JLA_QKV_ATTN_SPL=1: one workgroup per column group (A/B)
 QKV_ATTN_SPL = int(os.environ.get("JLA_QKV_ATTN_SPL", "2"))
 _CUS = {}
+
+
+class InLaunchTimeout(RuntimeError):
+    """An in-launch wait gave up (the fused qkv + attention launch: a qkv workgroup never published)."""
+
+
+def check_inlaunch() -> None:
+    """Raise InLaunchTimeout if a fused qkv + attention launch recorded a timeout in its error word
+    (``qa_sync[2]``, csrc/kernels/gemv.hip qkv_attn_kernel). The device side is sticky -- the counters are no longer
+    reset and every later launch writes no output -- so after a timeout the fused path is refused for the rest of the
+    process (the words re-zeroed, the workspace generation bumped so a captured decode graph is re-captured without it).
+    Reads device memory (synchronises); called by the engine's host poll."""
+    global QKV_ATTN
+    for (name, _dev, _dt), buf in list(workspace._bufs.items()):
+        if name.startswith("zeroed:") and name.endswith("qa_sync") and buf.is_cuda and int(buf[2].item()):
+            QKV_ATTN = 0
+            buf.zero_()
+            workspace.generation += 1
+            raise InLaunchTimeout("fused qkv + attention launch: the attention workgroups timed out waiting for the qkv "
+                                  "workgroups (error word qa_sync[2]); the fused path is now off for this process")
 
 
 def _num_cus(device) -> int:

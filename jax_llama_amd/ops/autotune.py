@@ -78,7 +78,7 @@ def tune_file() -> str:
     return os.path.join(base, "jax_llama_amd", f"tune_{ARCH}.json")
 
 
-TUNE_VERSION = 11  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split; 11: gemm4 with the weights three K-tiles deep, 256 x 192 tiles), so older persisted picks are re-measured
+TUNE_VERSION = 12  # bumped when a candidate set changes (2: split-K GEMV 16-19; 3: 4-tile split-K 26; 4: gemm4 tile 7; 5: gemm4 stream-K; 6: never-picked GEMV variants removed; 7: gemm4 256 x 128 tiles; 8: gemm5 tiles 11 / 12; 9: gemm4 rasterised in groups of 4 m-tiles; 10: stream-K / hybrid plans replaced by the exchange split; 11: gemm4 with the weights three K-tiles deep, 256 x 192 tiles; 12: the never-picked tiles 8 / 10 / 15 removed), so older persisted picks are re-measured
 
 
 def _key_str(kind: str, key: Tuple) -> str:
@@ -89,7 +89,7 @@ def _load():
     if _LOADED["done"]:
         return
     _LOADED["done"] = True
-    if os.environ.get("JLA_TUNE_PERSIST", "1") == "0":
+    if not _persist_on():
         return
     try:
         with open(tune_file()) as f:
@@ -102,8 +102,14 @@ def _load():
 _PERSISTED: Dict[str, object] = {}
 
 
+def _persist_on() -> bool:
+    """Picks are persisted unless disabled, or unless the candidate set is restricted for an A/B run (JLA_TUNE_TILES):
+    a pick among a subset must never be reused by a run that searches the whole set."""
+    return os.environ.get("JLA_TUNE_PERSIST", "1") != "0" and not os.environ.get("JLA_TUNE_TILES")
+
+
 def _save(kind: str, key: Tuple, value):
-    if os.environ.get("JLA_TUNE_PERSIST", "1") == "0":
+    if not _persist_on():
         return
     _PERSISTED[_key_str(kind, key)] = list(value) if isinstance(value, tuple) else value
     path = tune_file()
@@ -276,13 +282,13 @@ def measured() -> Dict[Tuple, Dict[int, float]]:
 _KS_CACHE: Dict[Tuple, Tuple[int, int]] = {}
 KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
 # tile configs: 1 / 2 / 3 gemm2 256x256, 128x256, 128x128 (csrc/kernels/gemm.hip tile_cfg); 7 gemm4; 14 gemm4 with the
-# weights three K-tiles deep (160 KiB of LDS); 10 / 15 gemm4 on 256 x 128 / 192 tiles and 17 / 16 the same with the
-# deep weights (those four: no K split under the fused norm, its statistic is precomputed);
-TILE_CANDIDATES = (1, 2, 3, 7, 10, 11, 12, 14, 15, 16, 17)
-# 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h; 256 / 128 columns per workgroup, M <= 256 per tile);
-# plus (ks, XK_TILE) -- gemm4 split-K whose splits exchange their partial blocks in-launch -- for the residual epilogue
-# where tiles x split fit the CUs
-if os.environ.get("JLA_TUNE_TILES"):  # A/B tooling: restrict the tile candidates, e.g. JLA_TUNE_TILES=1,2,3,7,10,11,12
+# weights three K-tiles deep (160 KiB of LDS); 17 / 16 gemm4 on 256 x 128 / 192 tiles with the deep weights (no K split
+# under the fused norm, its statistic is precomputed); 11 / 12: gemm5, the weight-streaming split-K kernel (gemm5ws.h;
+# 256 / 128 columns per workgroup, M <= 256 per tile). What the bench shapes pick (BENCH_r05 gemm_plan_choice):
+#   Llama-3-8B M = 1024 / 2048: qkv 16 / 17, o 17, gate_up 7 / 14 / 16, down 14 / 17 (split 2), lm_head 14;
+#   Llama-3-70B M = 256 (MP 1 and the MP 8 shard): 1 / 3 (split 4 / 12), 11 / 12 (gemm5 splits), 14, 17.
+TILE_CANDIDATES = (1, 2, 3, 7, 11, 12, 14, 16, 17)
+if os.environ.get("JLA_TUNE_TILES"):  # A/B tooling: restrict the tile candidates, e.g. JLA_TUNE_TILES=1,2,3,7,11,12
     TILE_CANDIDATES = tuple(int(v) for v in os.environ["JLA_TUNE_TILES"].split(","))
 TUNE_MAX_M = 2048
 
@@ -320,9 +326,7 @@ def choose_gemm_ksplit(e, m: int, n: int, k: int, device) -> int:
     return choose_gemm_plan(e, m, n, k, device)[0]
 
 
-XK_TILE = 8  # gemm4 split-K with the in-launch exchange of partial wave blocks (residual epilogue)
-G4N_TILE = 10  # gemm4 on 256 x 128 tiles (csrc/kernels/gemm4w.h g4n_mainloop)
-G4N6_TILE = 15  # gemm4 on 256 x 192 tiles (g4n_mainloop<6>; the 8B qkv at M = 2048 is exactly one wave)
+G4N_TILES = (16, 17)  # gemm4 on 256 x 192 / 128 tiles (csrc/kernels/gemm4w.h g4n_mainloop, deep weights)
 G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h)
 TUNE_ROUNDS = 3
 
@@ -331,18 +335,10 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     kt = k // 32
     ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
-             if (tm not in (G4N_TILE, G4N6_TILE, G4N6_TILE + 1, G4N6_TILE + 2) or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
+             if (tm not in G4N_TILES or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
              and (tm not in G5_TILES or (k % 64 == 0 and m <= 512))]
     if k % 64 == 0 and m <= 512:  # gemm5 also at the deeper splits its 64-deep stages allow (narrow shards, long K)
         cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c]
-    xk = None
-    if mode == 1:  # the exchange split: every split count whose workgroups all fit the CUs at once
-        xks = [c for c in (2, 3, 4, 6, 8) if e.gemm4_xk_ok(m, n, k, c)]
-        cands += [(c, XK_TILE) for c in xks]
-        if xks:
-            fl, counts = e.gemm4_xk_workspace(m, n, max(xks))
-            xk = (torch.empty(fl, dtype=torch.float32, device=device),
-                  torch.zeros(counts, dtype=torch.int32, device=device))
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)
@@ -362,13 +358,11 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
     rms_ws = torch.empty(m, dtype=torch.float32, device=device)  # as ops._rms_ws: the statistic ahead of gemm4
 
     def run(c, tm, i):
-        if tm == XK_TILE:
-            e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, xk[0], eps, tm, xk[1])
-        elif tm in G5_TILES:
+        if tm in G5_TILES:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws, eps, tm)
         else:
             e.gemm(x, ws_w[i % copies], n, k, out, mode, True, mirror, c, ws if c > 1 else None, eps, tm,
-                   None, None, rms_ws if c == 1 and eps > 0 else None)
+                   None, rms_ws if c == 1 and eps > 0 else None)
 
     for c, tm in cands:  # warm every variant (code objects, caches) before any timing
         for i in range(2):
@@ -386,7 +380,7 @@ def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int
             ev1.synchronize()
             times[(c, tm)] = min(times[(c, tm)], ev0.elapsed_time(ev1) / iters)
     best = min(cands, key=times.get)
-    del ws_w, ws, xk
+    del ws_w, ws
     return best
 
 

@@ -228,7 +228,7 @@ class DecodeEngine:
     def _graph_state(self):
         # the graph records buffer addresses: the scratch workspaces (ops.workspace) and the sampling mode
         return (self.gc.do_sample, self.key_mask is not None, ops.workspace.generation, _fused_greedy(),
-                ops.ARGMAX_FUSED_MIN_M, ops.SKINNY_ARGMAX, self.model.comm.reduce_dtype)
+                ops.ARGMAX_FUSED_MIN_M, ops.SKINNY_ARGMAX, ops.QKV_ATTN, self.model.comm.reduce_dtype)
 
     def _ensure_graph(self):
         if self._graph is not None and self._graph_key == self._graph_state():
@@ -249,9 +249,16 @@ class DecodeEngine:
         """Host poll (every ``check_every`` steps): True once every row has finished. Also raises if a
         custom TP collective gave up waiting for a peer."""
         done = bool(self.finished.all().item())
-        self.model.comm.check()
-        ops.check_bounds()  # bounds-checked debug build only (JLA_DEBUG_BOUNDS=1): out-of-range device indices
+        self._check()
         return done
+
+    def _check(self):
+        """Device-side failure words: a custom TP collective that gave up on a peer (comm.check), an in-launch wait
+        that timed out (ops.check_inlaunch: the fused qkv + attention launch), out-of-range indices (debug build)."""
+        self.model.comm.check()
+        if self.device.type == "cuda":
+            ops.check_inlaunch()
+        ops.check_bounds()  # bounds-checked debug build only (JLA_DEBUG_BOUNDS=1): out-of-range device indices
 
     def run(self, input_ids, attention_mask, gc: GenerationConfig) -> torch.Tensor:
         self.gc = gc
@@ -293,7 +300,7 @@ class DecodeEngine:
                 break
             if step % self.check_every == 0 and self._poll():
                 break
-        self.model.comm.check()
+        self._check()
         return self.sequences
 
 

@@ -31,11 +31,11 @@ def _run_all(e, xg, pg, gp, h0, n, k, ks, ws, tile, rms_ws=None):
     for eps in (-1.0, 1e-5):
         rw = rms_ws if eps > 0 else None
         o = torch.empty(xg.shape[0], n, dtype=torch.float32, device=DEV)
-        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, rw)
+        e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, rw)
         ob = torch.empty(xg.shape[0], n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, rw)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, rw)
         o2 = torch.empty(xg.shape[0], n // 2, dtype=BF16, device=DEV)
-        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile, None, None, rw)
+        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile, None, rw)
         outs += [o, ob, o2]
     hg, mir = h0.clone(), torch.empty(h0.shape, dtype=BF16, device=DEV)
     e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, tile)
@@ -108,7 +108,7 @@ def test_gemm4_qkv_rope_epilogue(m, s, n_heads):
         kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
         qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
         e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
-                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile, None,
+                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile,
                    torch.empty(m, device=DEV) if tile == G4 else None)
         outs[tile] = (qg.cpu(), kg.cpu(), vg.cpu())
     qg, kg, vg = outs[G4]
@@ -147,7 +147,7 @@ def test_gemm4_argmax(m, n, k):
             assert torch.equal(v0.cpu(), v1.cpu())
             if eps > 0:  # the precomputed statistic: same as the stored-logits path with the same statistic
                 rw = torch.empty(m, device=DEV)
-                e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, G4, None, None, rw)
+                e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, G4, None, rw)
                 e.argmax(logits, i0, v0)
                 e.gemm_argmax(xg, pg.weight, n, k, ws, eps, i1, v1, rw)
                 torch.cuda.synchronize()
@@ -175,48 +175,6 @@ def test_gemm4_model_prefill_matches_gemm2():
     _close(got, base, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("m,n,k,ks", [(2048, 4096, 4096, 2), (2048, 4096, 14336, 2), (700, 2560, 4096, 2),
-                                      (300, 768, 2048, 4), (256, 8192, 1024, 4), (256, 8192, 3584, 8),
-                                      (513, 1008, 1024, 2)])
-def test_gemm4_exchange_split(m, n, k, ks):
-    """Tile config 8 (gemm4 split-K whose splits hand their partial 128 x 128 wave blocks to the block's owner inside
-    the launch, residual epilogue): at split 2 bit-identical to the same split through fp32 slabs + the reduce
-    kernel, otherwise within fp32 rounding of it; fp32-reference close, reproducible, the counters reset themselves
-    and the error word stays clear. Shapes: Llama-3-8B o / down at M = 2048, the 70B MP 8 o / down shards at M = 256, ragged M / N."""
-    e = ops.ext()
-    if not e.gemm4_xk_ok(m, n, k, ks):
-        pytest.skip("more workgroups than CUs on this device")
-    torch.manual_seed(m + n + k + ks)
-    x = torch.randn(m, k).to(BF16)
-    w = (torch.randn(n, k) * 0.05).to(BF16)
-    pg = PackedLinear.from_dense(w, DEV)
-    xg = x.to(DEV)
-    h0 = torch.randn(m, n).to(DEV)
-    floats, counts = e.gemm4_xk_workspace(m, n, ks)
-    ws = torch.empty(floats, device=DEV)
-    cnt = torch.zeros(counts, dtype=torch.int32, device=DEV)
-    slabs = torch.empty(ks * m * (n + 1), device=DEV)
-
-    def run(tile):
-        hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws if tile == 8 else slabs, -1.0, tile,
-               cnt if tile == 8 else None)
-        torch.cuda.synchronize()
-        return hg, mir
-
-    a1, a2, red = run(8), run(8), run(G4)
-    assert int(cnt.abs().sum()) == 0, "counters / error word"
-    for u, v in zip(a1, a2):
-        assert torch.equal(u, v), "not reproducible"
-    if ks == 2:  # (the owner sums from its own split cyclically: the reduce kernel's order only at ks = 2)
-        for u, v in zip(a1, red):
-            assert torch.equal(u, v), "differs from the slab + reduce path"
-    else:
-        _close(a1[0], red[0], 1e-5, 1e-5)
-    _close(a1[0], ref.linear_residual(x, w, h0.cpu().clone()), 1e-2, 1e-3)
-    torch.testing.assert_close(a1[1].cpu(), a1[0].cpu().to(BF16), rtol=0, atol=0)
-
-
 @pytest.mark.parametrize("tile", [13, 14])
 @pytest.mark.parametrize("m,n,k", [(2048, 4096, 1024), (700, 2560, 512), (4352, 1536, 256), (256, 1280, 192),
                                    (256, 2048, 128), (300, 1024, 64)])
@@ -240,9 +198,9 @@ def test_gemm4_persistent_identical(m, n, k, tile):
         o = torch.empty(m, n, dtype=torch.float32, device=DEV)
         e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, 1, None, -1.0, tile)
         ob = torch.empty(m, n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, None, 1e-5, tile, None, None, rw)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, None, 1e-5, tile, None, rw)
         o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
-        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile, None, None, rw)
+        e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile, None, rw)
         o3 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
         e.gemm(xg, gp.weight, n, k, o3, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile)
         hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
@@ -287,11 +245,11 @@ def test_gemm4_deep_split_identical(m, n, k, ks):
     _close(a[0].float().cpu(), xs @ w.float().t(), 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("tile", [15, 16])
+@pytest.mark.parametrize("tile", [16])
 @pytest.mark.parametrize("m,n,k", [(2048, 6144, 512), (300, 1008, 256), (256, 4096, 128), (256, 1536, 192),
                                    (260, 768, 64)])
 def test_gemm4_256x192_identical(m, n, k, tile):
-    """256 x 192 tiles (tile 15, g4n_mainloop<6>; 16 with the weights three K-tiles deep): the same per-output MFMA
+    """256 x 192 tiles (tile 16, g4n_mainloop<6> with the weights three K-tiles deep): the same per-output MFMA
     chain as the 256 x 256 gemm4, so the store
     (fp32 / bf16, precomputed norm), SwiGLU, residual + mirror and split-K partial epilogues are bit-identical to tile 7;
     ragged N (a last tile narrower than 192 columns) included."""
@@ -311,9 +269,9 @@ def test_gemm4_256x192_identical(m, n, k, tile):
         o = torch.empty(m, n, dtype=torch.float32, device=DEV)
         e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, 1, None, -1.0, tile)
         ob = torch.empty(m, n, dtype=BF16, device=DEV)
-        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, None, 1e-5, tile, None, None, rw)
+        e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, 1, None, 1e-5, tile, None, rw)
         o2 = torch.empty(m, n2 // 2, dtype=BF16, device=DEV)
-        e.gemm(xg, gp.weight, n2, k, o2, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile, None, None, rw)
+        e.gemm(xg, gp.weight, n2, k, o2, ops.MODE_SWIGLU, True, None, 1, None, 1e-5, tile, None, rw)
         hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
         e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, 1, None, -1.0, tile)
         os = torch.empty(m, n, dtype=BF16, device=DEV)
@@ -336,44 +294,33 @@ def test_gemm4_256x192_qkv_epilogue(m, s):
     t = 11 + s + 4
     b = m // s
     n = (h + 2 * hkv) * dh
-    assert e.gemm_qkv_direct_ok(m, 15, k)
+    assert e.gemm_qkv_direct_ok(m, 16, k)
     w = (torch.randn(n, k) * 0.05).to(BF16)
     x = torch.randn(m, k).to(BF16)
     table = ref.rope_table(dh, 1024, 500000.0)
     pos = torch.randint(0, 1000, (m,), dtype=torch.int32)
     pg = PackedLinear.from_dense(w, DEV)
     outs = {}
-    for tile in (G4, 15, 16):
+    for tile in (G4, 16):
         kg = torch.zeros(b, hkv, t, dh, dtype=BF16, device=DEV)
         vg = torch.zeros_like(kg)
         qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
         e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
-                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile, None,
+                   torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, tile,
                    torch.empty(m, device=DEV))
         torch.cuda.synchronize()
         outs[tile] = (qg, kg, vg)
-    for tile in (15, 16):
+    for tile in (16,):
         for i, (u, v) in enumerate(zip(outs[tile], outs[G4])):
             assert torch.equal(u, v), f"qkv output {i}: tile {tile} differs from tile 7"
 
 
-def test_gemm4_exchange_split_guards():
-    """The exchange plan needs every workgroup resident (tiles x split <= CUs) and a real split."""
-    e = ops.ext()
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    assert not e.gemm4_xk_ok(2048, 4096, 4096, 1)
-    assert not e.gemm4_xk_ok(256 * cus, 256, 4096, 2)
-    assert not e.gemm4_xk_ok(256, 256, 64 * 3, 4)  # fewer K-tiles than splits
-    assert not e.gemm4_xk_ok(256, 256, 4096, 3)  # splits of 2, 4 or 8
-    assert e.gemm4_xk_ok(256, 256, 4096, 2)
-
-
-@pytest.mark.parametrize("tile", [10, 17])
+@pytest.mark.parametrize("tile", [17])
 @pytest.mark.parametrize("m,n,k,ks", [(2048, 4096, 4096, 1), (700, 2560, 4096, 1), (300, 768, 2048, 2),
                                       (512, 1056, 1024, 1), (1000, 6144, 1536, 3), (256, 512, 128, 1),
                                       (256, 512, 192, 1), (256, 512, 64, 1)])
 def test_gemm4_256x128_tiles(m, n, k, ks, tile):
-    """Tile config 10 (gemm4 on 256 x 128 tiles, 4 n-tiles per wave; 17 with the weights three K-tiles deep): store
+    """Tile config 17 (gemm4 on 256 x 128 tiles, 4 n-tiles per wave, the weights three K-tiles deep): store
     (fp32 / bf16), SwiGLU, residual + mirror,
     split-K partials; the fused norm with its precomputed statistic. The same MFMA chain per output element as the
     256 x 256 gemm4 (tile 7), so bit-identical to it, and fp32-reference close; N not a multiple of 128 included."""
@@ -394,11 +341,11 @@ def test_gemm4_256x128_tiles(m, n, k, ks, tile):
         for eps in ((-1.0, 1e-5) if ks == 1 else (-1.0,)):
             r = rw if eps > 0 else None
             o = torch.empty(m, n, dtype=torch.float32, device=DEV)
-            e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, r)
+            e.gemm(xg, pg.weight, n, k, o, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, r)
             ob = torch.empty(m, n, dtype=BF16, device=DEV)
-            e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, None, r)
+            e.gemm(xg, pg.weight, n, k, ob, ops.MODE_STORE, True, None, ks, ws, eps, tile, None, r)
             o2 = torch.empty(m, n // 2, dtype=BF16, device=DEV)
-            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile, None, None, r)
+            e.gemm(xg, gp.weight, n, k, o2, ops.MODE_SWIGLU, True, None, ks, ws, eps, tile, None, r)
             outs += [o, ob, o2]
         hg, mir = h0.clone(), torch.empty(m, n, dtype=BF16, device=DEV)
         e.gemm(xg, pg.weight, n, k, hg, ops.MODE_RESIDUAL, True, mir, ks, ws, -1.0, tile)

@@ -94,7 +94,7 @@ def test_gemm5_qkv_rope_epilogue(tile, m, s, n_heads, hkv, ks):
     kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
     qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
     e.gemm_qkv(x.to(DEV), pg.weight, n, k, table.to(DEV), pos.to(DEV), kg, vg,
-               torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, ks, ws, 1e-5, tile, None, None)
+               torch.tensor([11], dtype=torch.int32, device=DEV), s, h, hkv, dh, qg, ks, ws, 1e-5, tile, None)
     torch.cuda.synchronize()
     _close(qg, q, 2e-2, 2e-2)
     _close(kg, kc, 2e-2, 2e-2)

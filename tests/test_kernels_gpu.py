@@ -548,7 +548,7 @@ def test_qkv_rope_direct_epilogue(m, s, n_heads):
         kg, vg = torch.zeros_like(kc, device=DEV), torch.zeros_like(vc, device=DEV)
         qg = torch.empty(m, h, dh, dtype=BF16, device=DEV)
         e.gemm_qkv(x.to(DEV), pg.weight, n, k, args[0], args[1], kg, vg, torch.tensor([11], dtype=torch.int32,
-                   device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, 1, None)
+                   device=DEV), s, h, hkv, dh, qg, 1, None, 1e-5, 1)
         outs.append((qg.cpu(), kg.cpu(), vg.cpu()))
     qg, kg, vg = outs[0]
     _close(qg, q, 2e-2, 2e-2)

@@ -102,47 +102,35 @@ def main():
                   e.gemm_set_g4_group(grp)
                   for tile in args.tile:
                     kk = ks or e.gemm_ksplit(m, n, k)
-                    if tile in (10, 15, 16, 17) and kk > 1 and eps > 0:
+                    if tile in (16, 17) and kk > 1 and eps > 0:
                         continue  # (gemm4 256 x 128 / 192: no K split under the fused norm)
                     if kk > 1 and (k // 32) // kk < 4 and tile not in (11, 12):
                         continue
                     if tile in (11, 12) and (k % 64 or (k // 64) // kk < 1):
                         continue
-                    tk = None
-                    for fx in (0,):
-                      tk = None
-                      if tile == 8:  # gemm4 exchange split (residual epilogue only)
-                          if mode != 1 or not e.gemm4_xk_ok(m, n, k, kk):
-                              continue
-                          floats, counts = e.gemm4_xk_workspace(m, n, kk)
-                          ws = torch.empty(floats, device=DEV, dtype=torch.float32)
-                          tk = torch.zeros(counts, device=DEV, dtype=torch.int32)
-                      else:
-                          ws = torch.empty(max(1, kk * m * (n + 1)), device=DEV, dtype=torch.float32)
+                    ws = torch.empty(max(1, kk * m * (n + 1)), device=DEV, dtype=torch.float32)
+                    tcfg = tile
+                    rws = torch.empty(m, device=DEV) if (eps > 0 and kk == 1 and tile not in (11, 12)) else None
 
-                      tcfg = tile
-
-                      rws = torch.empty(m, device=DEV) if (eps > 0 and kk == 1 and tile not in (11, 12)) else None
-
-                      def run(i, kk=kk, ws=ws, tile=tcfg, tk=tk, rws=rws):
-                          e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
-                                 ws if (kk > 1 or tile in (11, 12)) else None, eps, tile, tk, None, rws)
-                      res[f"v{impl}_ks{kk}_t{tile}" + (f"_diag{diag}" if diag else "") + (f"_g{grp}" if grp else "")  + "" +
-                          (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
-                      run(0)
-                      if mode != 0 or (diag & 255):  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
-                          continue
-                      got = out.float()
-                      if ref is None:
-                          xs = x.float()
-                          if eps > 0:
-                              xs = xs * torch.rsqrt(xs.pow(2).mean(-1, keepdim=True) + eps)
-                          ref = (xs @ dense[0].float().t())
-                      err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
-                      assert err < 2e-2 or (tile >= 50 and (tile - 50) & 14), (name, m, impl, kk, err)
-                      if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
-                          f0 = first.setdefault((kk, tile), got.clone())
-                          assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
+                    def run(i, kk=kk, ws=ws, tile=tcfg, rws=rws):
+                        e.gemm(x, packed[i % copies].weight, n, k, out, mode, True, mir if mode == 1 else None, kk,
+                               ws if (kk > 1 or tile in (11, 12)) else None, eps, tile, None, rws)
+                    res[f"v{impl}_ks{kk}_t{tile}" + (f"_diag{diag}" if diag else "") + (f"_g{grp}" if grp else "")  + "" +
+                        (f"_r{rnd}" if args.rounds > 1 else "")] = timeit(run, iters)
+                    run(0)
+                    if mode != 0 or (diag & 255):  # (numerics of the other epilogues: tests/test_gemm4_gpu.py)
+                        continue
+                    got = out.float()
+                    if ref is None:
+                        xs = x.float()
+                        if eps > 0:
+                            xs = xs * torch.rsqrt(xs.pow(2).mean(-1, keepdim=True) + eps)
+                        ref = (xs @ dense[0].float().t())
+                    err = (got - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+                    assert err < 2e-2 or (tile >= 50 and (tile - 50) & 14), (name, m, impl, kk, err)
+                    if impl >= 2 and tile < 5:  # gemm2 pipeline variants must agree bit for bit (same per-accumulator order)
+                        f0 = first.setdefault((kk, tile), got.clone())
+                        assert torch.equal(f0, got), ("variant mismatch", name, m, impl, kk, tile)
             e.gemm5_set_diag(0)
             e.gemm_set_g4_group(0)
             if not args.no_blas and mode == 0:

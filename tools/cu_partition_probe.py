@@ -6,8 +6,8 @@
 3. the GEMM (--op, tile --tile) alone on the other 256 - k CUs, and on all CUs;
 4. both at once on the two masked streams.
 
-One JSON line per k. ``model_us`` = what the partitioned half-layer costs against the serial one:
-``max(tA_k, tG_rest)`` vs ``tA_all + tG_all``.
+One JSON line per k: ``both_us`` (the two sides at once) against ``serial_all_us`` (each alone on the whole chip, in
+sequence).
 
   python tools/cu_partition_probe.py --k 64 96 128 160
 """
@@ -107,7 +107,7 @@ def main():
             ops.attention(q, kc, vc, slot, kv_start)
 
         def gemm():
-            e.gemm(x, w.weight, n, k, out, mode, True, mir, 1, None, eps, args.tile, None, None, rws if eps > 0 else None)
+            e.gemm(x, w.weight, n, k, out, mode, True, mir, 1, None, eps, args.tile, None, rws if eps > 0 else None)
 
         ta_all = timed(attn)
         tg_all = timed(gemm)
@@ -118,12 +118,6 @@ def main():
         sg = torch.cuda.ExternalStream(e.cu_mask_stream(mask_words(range(kk, ncu), ncu)))
         rec = {"k": kk, "census_attn_side": census(e, sa), "census_gemm_side": census(e, sg)}
         if not args.census_only:
-            def on(s, fn):
-                def run():
-                    with torch.cuda.stream(s):
-                        fn()
-                return run
-
             def both():
                 cur = torch.cuda.current_stream()
                 sa.wait_stream(cur)

@@ -85,7 +85,7 @@ def main():
     side = torch.cuda.Stream()
     for tile in args.tiles:
         def gemm(tile=tile):
-            e.gemm(x, w.weight, n, k, out, mode, True, mir, 1, None, eps, tile, None, None,
+            e.gemm(x, w.weight, n, k, out, mode, True, mir, 1, None, eps, tile, None,
                    rws if eps > 0 else None)
 
         def par(first_g):

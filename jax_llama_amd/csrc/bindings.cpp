@@ -831,7 +831,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_set_v6", [](int64_t mode) { jla::attn_set_v6((int)mode); });
   m.def("attn_set_v6_wpp", [](int64_t wpp) { jla::attn_set_v6_wpp((int)wpp); });
   m.def("attn_v6_wpp", [](int64_t pairs) { return jla::attn_v6_wpp((int)pairs); });
-  m.def("attn_set_v1_min_wgs", [](int64_t n) { jla::attn_set_v1_min_wgs((int)n); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),
         py::arg("nsplit"), py::arg("out_pack") = py::none());

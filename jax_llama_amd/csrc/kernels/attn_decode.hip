@@ -1,19 +1,20 @@
-// Decode attention (one query position per sequence) over the bf16 KV cache, one pass, split-KV.
+// Decode attention (one query position per sequence) over the bf16 KV cache, one pass.
 //
 // Reference: FlaxLLaMAAttention with a cache (model.py:169-199 cache write/pad mask, :236-267 mask
 // + bias, :269-270 repeat_kv, :277-291 softmax(QK^T/sqrt(Dh)) V). Here the mask is computed from
 // (kv_start, slot, optional key mask) in-kernel, GQA is pure indexing (the REP query heads that
-// share a kv head are processed by one workgroup so K/V are read from HBM once), and only keys
+// share a kv head are processed together so K/V are read from HBM once), and only keys
 // [kv_start, slot] are touched (the reference attends over the whole cache length).
 //
-// Workgroup = (split, kv head, batch row): 4 waves, CH = 16*KPG keys. Each 16-lane group owns KPG
-// key rows (16 lanes x 16 B = one 256 B row of Dh = 128 bf16); rows are interleaved across groups
-// so one wave-wide load fetches 4 consecutive cache rows (1 KiB contiguous). ALL K and V rows of
-// the chunk are issued up front (one memory round trip per workgroup), then QK^T (16-lane
-// reductions), softmax (wave + LDS max/sum), P.V in registers, and a cross-wave LDS reduction.
-// With nsplit > 1 each split publishes (m, l, o[Dh]) with write-through stores and bumps a
-// per-(b, kv head) ticket; the last arriver merges the splits (log-sum-exp) and writes bf16 out,
-// so decode attention is ONE launch (release/acquire recipe: cdna_hip_programming.md Guideline 16,
+// One kernel per regime (attn_decode below picks by (row, kv head) pairs and query heads per kv head, REP):
+//   v5  split small batch, <= 64 pairs (<= 256 at REP >= 8)   -- the latency-bound B = 1..8 steps
+//   v6  matrix-core scores / P.V, REP >= 8 and 8..2047 pairs  -- the 70B tensor-parallel shard (attn_decode_mma.hip)
+//   v3  one workgroup per pair, up to 4096 pairs (REP <= 8)    -- mid batches
+//   v4  one wave per pair, register ring, one split, no key mask -- large batches (the B = 2048 headline)
+//   v2  one wave per (pair, key split), LDS ring, optional key mask -- large batches with a padding mask, and the
+//       fallback for every other shape (REP 16 mid batches)
+// With splits, each split publishes (m, l, o[Dh]) with write-through stores and bumps a per-pair ticket; the last
+// arriver merges the splits (log-sum-exp), so decode attention is ONE launch (cdna_hip_programming.md Guideline 16,
 // sc1-store / sc1-load form; the last arriver resets the ticket for the next replay).
 // Rows with no valid key produce 0 (never NaN: -inf maxima are guarded).
 #include "common.h"
@@ -29,237 +30,10 @@ JLA_DEV float ld_wt(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int REP, int KPG>
-__global__ void __launch_bounds__(AD_WAVES * 64)
-    attn_decode_v1_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
-                       const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
-                       const uint8_t* __restrict__ key_mask, int mask_len, bf16_t* __restrict__ out,
-                       float* __restrict__ ws, int32_t* __restrict__ tickets, int H, int Hkv, int T, int t_cap,
-                       int nsplit, float scale) {
-  constexpr int CH = 16 * KPG;
-  __shared__ float red_m[AD_WAVES][REP];
-  __shared__ float red_l[AD_WAVES][REP];
-  __shared__ float red_o[AD_WAVES][REP][AD_DH];
-  __shared__ int last_flag;
-
-  const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int slot = slot_ptr[0];
-  if (slot >= T && threadIdx.x == 0) JLA_FLAG(JLA_BOUNDS_ATTN_T);  // keys past the cache are never read
-  const int lo = kv_start[b];
-  const int c0 = split * CH;
-  const int c1 = min(c0 + CH, min(t_cap, slot + 1));  // keys [c0, c1) of this split
-  const int h0 = kvh * REP;
-  const uint8_t* mrow = key_mask ? key_mask + (size_t)b * mask_len : nullptr;
-  const bool any = c0 < c1 && c1 > lo;
-
-  float m_h[REP], l_h[REP];
-  float o[REP][8];
-#pragma unroll
-  for (int h = 0; h < REP; ++h) {
-    m_h[h] = -INFINITY;
-    l_h[h] = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[h][e] = 0.f;
-  }
-
-  if (any) {
-    // ---- issue every K and V row of the chunk (clamped rows for keys past the end: masked)
-    const size_t head_off = ((size_t)b * Hkv + kvh) * T * AD_DH + 8 * li;
-    u32x4 kr[KPG], vr[KPG];
-    int jv[KPG];
-#pragma unroll
-    for (int r = 0; r < KPG; ++r) {
-      const int j = c0 + w * 4 + g + 16 * r;
-      jv[r] = j;
-      const int jc = min(j, c1 - 1);
-      kr[r] = *reinterpret_cast<const u32x4*>(kc + head_off + (size_t)jc * AD_DH);
-    }
-#pragma unroll
-    for (int r = 0; r < KPG; ++r) {
-      const int jc = min(jv[r], c1 - 1);
-      vr[r] = *reinterpret_cast<const u32x4*>(vc + head_off + (size_t)jc * AD_DH);
-    }
-    // q for this lane's 8 dims (pre-scaled by 1/sqrt(Dh))
-    float qf[REP][8];
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(q + ((size_t)b * H + h0 + h) * AD_DH + 8 * li);
-      unpack8(v, qf[h]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) qf[h][e] *= scale;
-    }
-    // ---- scores (every lane of a 16-lane group ends with the full dot product)
-    float sc[REP][KPG];
-#pragma unroll
-    for (int r = 0; r < KPG; ++r) {
-      float kf[8];
-      unpack8(kr[r], kf);
-      const int j = jv[r];
-      bool valid = j < c1 && j >= lo;
-      if (mrow && j < mask_len) valid = valid && mrow[j] != 0;
-#pragma unroll
-      for (int h = 0; h < REP; ++h) {
-        float d = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += qf[h][e] * kf[e];
-        d = row16_sum(d);  // DPP: every lane of the 16-lane row gets the full dot product
-        sc[h][r] = valid ? d : -INFINITY;
-      }
-    }
-    // ---- per-head max over the chunk: registers -> 4 groups (xor 16, 32) -> 4 waves (LDS)
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-      float mx = sc[h][0];
-#pragma unroll
-      for (int r = 1; r < KPG; ++r) mx = fmaxf(mx, sc[h][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      m_h[h] = mx;
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int h = 0; h < REP; ++h) red_m[w][h] = m_h[h];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-      float mx = red_m[0][h];
-#pragma unroll
-      for (int ww = 1; ww < AD_WAVES; ++ww) mx = fmaxf(mx, red_m[ww][h]);
-      m_h[h] = mx;
-    }
-    // ---- p = exp(s - m); P.V into this lane's 8 dims
-#pragma unroll
-    for (int r = 0; r < KPG; ++r) {
-      float vf[8];
-      unpack8(vr[r], vf);
-#pragma unroll
-      for (int h = 0; h < REP; ++h) {
-        const float p = (sc[h][r] == -INFINITY) ? 0.f : __expf(sc[h][r] - m_h[h]);
-        l_h[h] += p;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[h][e] += p * vf[e];
-      }
-    }
-    // l: each key's p was added by all 16 lanes of its group -> sum over groups, count once
-#pragma unroll
-    for (int h = 0; h < REP; ++h) {
-      float l = l_h[h];
-      l += __shfl_xor(l, 16, 64);
-      l += __shfl_xor(l, 32, 64);
-      l_h[h] = l;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = o[h][e];
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        o[h][e] = v;
-      }
-    }
-    if (g == 0) {
-#pragma unroll
-      for (int h = 0; h < REP; ++h) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red_o[w][h][8 * li + e] = o[h][e];
-        if (li == 0) red_l[w][h] = l_h[h];
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- this split's (m, l, o) per head: thread t -> (head, d)
-  float* part = ws + (((size_t)b * Hkv + kvh) * nsplit + split) * REP * (AD_DH + 2);
-  for (int i = threadIdx.x; i < REP * AD_DH; i += AD_WAVES * 64) {
-    const int h = i / AD_DH, d = i - h * AD_DH;
-    float ov = 0.f, lv = 0.f, mv = -INFINITY;
-    if (any) {
-#pragma unroll
-      for (int ww = 0; ww < AD_WAVES; ++ww) {
-        ov += red_o[ww][h][d];
-        lv += red_l[ww][h];
-      }
-      mv = m_h[h];
-    }
-    if (nsplit == 1) {
-      out[((size_t)b * H + h0 + h) * AD_DH + d] = f2bf(lv > 0.f ? ov / lv : 0.f);
-    } else {
-      st_wt(part + h * (AD_DH + 2) + 2 + d, ov);
-      if (d == 0) {
-        st_wt(part + h * (AD_DH + 2), mv);
-        st_wt(part + h * (AD_DH + 2) + 1, lv);
-      }
-    }
-  }
-  if (nsplit == 1) return;
-
-  // ---- publish: every storing wave drains its write-through stores, then one ticket add
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t* tk = tickets + (size_t)b * Hkv + kvh;
-    const int prev = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == nsplit - 1;
-    if (last) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // reset for next replay
-    last_flag = last;
-  }
-  __syncthreads();
-  if (!last_flag) return;
-
-  // ---- last arriver: merge all splits of this (b, kv head) with sc1 loads, in parallel:
-  // (1) every (split, head) max/sum loaded by its own thread, (2) per-head weights in LDS,
-  // (3) each (head, d) thread sums the splits' o with independent loads (8 in flight).
-  const float* base = ws + ((size_t)b * Hkv + kvh) * nsplit * REP * (AD_DH + 2);
-  float* wsh = &red_o[0][0][0];  // reuse: [nsplit][REP] weights (nsplit * REP <= 4 * REP * 128)
-  for (int i = threadIdx.x; i < nsplit * REP; i += AD_WAVES * 64) wsh[i] = ld_wt(base + (size_t)i * (AD_DH + 2));
-  __syncthreads();
-  if (threadIdx.x < REP) {
-    const int h = threadIdx.x;
-    float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, wsh[s * REP + h]);
-    red_m[0][h] = M;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nsplit * REP; i += AD_WAVES * 64) {
-    const float M = red_m[0][i % REP], m = wsh[i];
-    wsh[i] = (m == -INFINITY || M == -INFINITY) ? 0.f : __expf(m - M);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < REP * AD_DH; i += AD_WAVES * 64) {
-    const int h = i / AD_DH, d = i - h * AD_DH;
-    float num = 0.f, den = 0.f;
-    int s = 0;
-    for (; s + 8 <= nsplit; s += 8) {
-      float ov[8], lv[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float* ps = base + ((size_t)(s + q) * REP + h) * (AD_DH + 2);
-        lv[q] = ld_wt(ps + 1);
-        ov[q] = ld_wt(ps + 2 + d);
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float f = wsh[(s + q) * REP + h];
-        den += f * lv[q];
-        num += f * ov[q];
-      }
-    }
-    for (; s < nsplit; ++s) {
-      const float* ps = base + ((size_t)s * REP + h) * (AD_DH + 2);
-      const float f = wsh[s * REP + h];
-      den += f * ld_wt(ps + 1);
-      num += f * ld_wt(ps + 2 + d);
-    }
-    out[((size_t)b * H + h0 + h) * AD_DH + d] = f2bf(den > 0.f ? num / den : 0.f);
-  }
-}
-
-
 // ---------------------------------------------------------------------------------------------
 // v3 (small batch): ONE workgroup per (batch row, kv head) and no cross-workgroup merge.
 //
-// At B <= 64 the decode attention moves well under a MiB and v1's critical path is latency: load ->
+// At B <= 64 the decode attention moves well under a MiB and a split kernel's critical path is latency: load ->
 // score -> publish partials -> ticket -> last arriver reloads every split -> merge (~10 us at B = 1
 // whatever the split count: profiles/r2_attn_decode_small_batch_ab.jsonl). Here 8 waves split the
 // valid keys [kv_start, slot] into interleaved 16-lane rows (chunk of 32 * KPG keys per step, the next
@@ -632,26 +406,25 @@ __global__ void __launch_bounds__(AD5_WAVES * 64)
 // ---------------------------------------------------------------------------------------------
 // v2 (default): streaming decode attention, one WAVE per work item (batch row, kv head, key split).
 //
-// v1 above gives every 128-key chunk its own workgroup (load everything, compute, merge), so a CU's
-// HBM queue drains between a workgroup's load burst and its compute/merge phases and every chunk
-// pays a merge; it held ~3-3.8 TB/s. Here each wave streams its item's keys in chunks of 4*KPG rows
+// The round-1 kernel (v1, removed in round 6) gave every 128-key chunk its own workgroup (load everything, compute,
+// merge), so a CU's HBM queue drained between a workgroup's load burst and its compute/merge phases and every chunk
+// paid a merge; it held ~3-3.8 TB/s. Here each wave streams its item's keys in chunks of 4*KPG rows
 // through two register buffers (chunk c+1 in flight while chunk c is scored), keeps a running
 // (max, sum, o) per query head (online softmax), and needs no workgroup barrier at all. Splits are
 // only used when B*Hkv alone cannot fill the chip (small batch / long context): the split count
 // targets >= `waves_target` waves, and the last-arriving wave of a (b, kv head) merges the splits'
-// (m, l, o) (sc1 stores -> vmcnt(0) -> one agent-scope ticket add per wave, as in v1).
+// (m, l, o) (sc1 stores -> vmcnt(0) -> one agent-scope ticket add per wave).
 //
 // Lane layout per chunk: lane = 16*g + li; row r of lane group g is key k0 + CK*c + 4*r + g, and
 // the lane holds dims [8*li, 8*li + 8) of it, so one wave load instruction covers 4 consecutive
 // cache rows (1 KiB contiguous). QK^T: 8 FMAs + a 16-lane DPP sum; P.V: lane-local over the group's
 // rows, summed across the 4 groups once per item.
-static int g_attn_impl = 2;
 static int g_attn_waves_target = 2048;
 static int g_attn_v2_min_pairs = 4096;
-static int g_attn_diag = 0;
+static int g_attn_diag = 0;  // tools only: 1 = v2 / v4 stream K/V without the math (wrong results)
 // register-ring streaming kernel (v4) for one-split large batches without a key mask: 5-12 % faster than v2 at
-// B = 512-2048 (profiles/r2_attn_decode_v4_vs_v2.jsonl); impl 2 (default) / 8 use it, 3-7 pin a v2 geometry
-static bool g_attn_v4 = true;  // tools only: 1 = v2 streams K/V without the math (wrong results)
+// B = 512-2048 (profiles/r2_attn_decode_v4_vs_v2.jsonl); impl 2 (default) uses it, impl 4 pins v2 (KPG 4, 2 slots)
+static bool g_attn_v4 = true;
 void attn_set_diag(int d) { g_attn_diag = d; }
 void attn_set_impl(int impl, int waves_target);
 
@@ -1057,54 +830,40 @@ __global__ void __launch_bounds__(64)
   }
 }
 
-// v1 keys per 16-lane group: the largest chunk (fewest splits to merge) that still gives the launch
-// ~256+ workgroups -- at small batch the kernel is latency-bound and more, shorter splits finish sooner
-// (B = 1, T = 384: 24 -> 96 workgroups)
-static int g_v1_min_wgs = 256;
-void attn_set_v1_min_wgs(int n) { g_v1_min_wgs = n; }
-static int kpg_v1(int rep, int B = 1 << 20, int Hkv = 1, int T = 1) {
-  int kpg = rep <= 4 ? 8 : (rep == 8 ? 4 : 2);
-  while (kpg > 2 && (long long)B * Hkv * ((T + 16 * kpg - 1) / (16 * kpg)) < g_v1_min_wgs) kpg >>= 1;
-  return kpg;
-}
-static int g_kpg_small = 8, g_ns = 2;  // v2 ring geometry for REP <= 4 (A/B: attn_set_impl)
-// impl 2 (default) picks the geometry by size: at >= 16384 (row, kv head) pairs (B >= 2048 at 8 kv heads) the
-// 17-KiB (KPG 4, 2 slots) ring -- 9 waves per CU instead of 4 -- streams 5.4-5.8 TB/s against 4.0-5.6 for
-// (KPG 8, 2 slots), which stays best at B = 1024 (profiles/r2_attn_decode_b2048_geometry.jsonl)
+static int g_kpg_small = 8;  // v2 ring geometry for REP <= 4 below 16384 pairs (impl 4: 4)
+// the geometry by size: at >= 16384 (row, kv head) pairs (B >= 2048 at 8 kv heads) the 17-KiB (KPG 4, 2 slots) ring --
+// 9 waves per CU instead of 4 -- streams 5.4-5.8 TB/s against 4.0-5.6 for (KPG 8, 2 slots), which stays best at
+// B = 1024 (profiles/r2_attn_decode_b2048_geometry.jsonl)
 static bool g_geo_auto = true;
-static int geo_v2(int pairs) { return (g_geo_auto && pairs >= 16384) ? 42 : g_kpg_small * 10 + g_ns; }
-static int kpg_v2(int rep, int pairs) { return rep <= 4 ? geo_v2(pairs) / 10 : (rep == 8 ? 2 : 1); }
+static int kpg_v2(int rep, int pairs) {
+  if (rep <= 4) return (g_geo_auto && pairs >= 16384) ? 4 : g_kpg_small;
+  return rep == 8 ? 2 : 1;
+}
 
-// impl 1 = v1; 2 = default (v4 where it applies, else v2 with the size-chosen geometry); 8 = same as 2;
-// 3 = v2 (KPG 2, 4 slots); 4 = v2 (KPG 4, 2 slots); 5 = same as 2; 6 = v2 (KPG 4, 4 slots); 7 = (KPG 4, 3 slots)
+// impl 2 = default dispatch; 4 = v2 with the (KPG 4, 2 slots) ring and no v4 (tests / A/B).
+// waves_target > 0: v2's split count target; < 0: v2 (or v4) down to -waves_target pairs
 void attn_set_impl(int impl, int waves_target) {
-  g_attn_impl = impl == 1 ? 1 : 2;  // 8: v2 dispatch with the v4 register-ring kernel where it applies
-  g_kpg_small = impl == 3 ? 2 : (impl == 2 || impl == 5 ? 8 : 4);
-  g_geo_auto = impl == 2;
-  g_attn_v4 = impl == 2 || impl == 8;
-  g_ns = impl == 3 ? 4 : (impl == 7 ? 3 : (impl == 6 ? 4 : 2));
+  g_kpg_small = impl == 4 ? 4 : 8;
+  g_geo_auto = impl != 4;
+  g_attn_v4 = impl != 4;
   if (waves_target > 0) g_attn_waves_target = waves_target;
   g_attn_v2_min_pairs = waves_target < 0 ? -waves_target : 4096;  // < 0: force v2 down to -target pairs
 }
 
-// v2 streams whole (b, kv head) pairs; below ~4096 pairs (B = 512 at 8 kv heads) v1's
-// chunk-per-workgroup design is as fast or faster (profiles/r1_attn_decode_v2_ab.jsonl,
-// r1_attn_decode_v2_geometry.jsonl), so smaller batches stay on v1.
+// v2 streams whole (b, kv head) pairs from ~4096 pairs (B = 512 at 8 kv heads) up.
 // The one-split register-ring stream (v4) also serves batches above the decode GEMV's rows (B > 64) below the v2
 // threshold: at rep <= 4 from there on, at rep 8 from 2048 (row, kv head) pairs. Graph-timed with cold K/V
 // (profiles/r3_attn_decode_v4_midbatch.jsonl): Llama-3-8B B = 128 / 256 (T 384) 71.9 / 129 us (v3) -> 57.9 / 70.5;
 // Llama-3-70B B = 256 (T 256 / 384) 158 / 206 -> 87 / 125; v3 stays ahead at B <= 64 (where it also writes the
 // packed copy the o projection's GEMV reads) and at rep 8 below 2048 pairs.
 static bool v4_midbatch(int B, int Hkv, int rep) {
-  return g_attn_impl == 2 && g_attn_v4 && g_attn_v2_min_pairs == 4096 && rep <= 8 &&
+  return g_attn_v4 && g_attn_v2_min_pairs == 4096 && rep <= 8 &&
          ((rep <= 4 && B > 32) || (rep == 8 && B * Hkv >= 2048));
 }
-static bool use_v2(int B, int Hkv, int rep) {
-  return g_attn_impl == 2 && (B * Hkv >= g_attn_v2_min_pairs || v4_midbatch(B, Hkv, rep));
-}
+static bool use_v2(int B, int Hkv, int rep) { return B * Hkv >= g_attn_v2_min_pairs || v4_midbatch(B, Hkv, rep); }
 
 // v3 (one workgroup per (row, kv head), no split merge) below this many (row, kv head) pairs
-static int g_attn_v3_max_pairs = 4096;  // up to the v2 threshold: faster than v1 at B = 1..256 (8 kv heads)
+static int g_attn_v3_max_pairs = 4096;  // up to the v2 threshold: faster than the split kernels at B = 1..256 (8 kv heads)
 void attn_set_v3_max_pairs(int n) { g_attn_v3_max_pairs = n; }
 static bool use_v3(int B, int Hkv, int rep) {
   return rep <= 8 && !use_v2(B, Hkv, rep) && B * Hkv <= g_attn_v3_max_pairs;
@@ -1122,7 +881,7 @@ void attn_set_v3_kpg(int mult) { g_v3_kpg_mult = mult >= 4 ? 4 : (mult >= 2 ? 2 
 // two tie at 64 pairs and v3 wins at 128)
 static bool use_v5(int B, int Hkv, int rep) {
   const int pairs = B * Hkv;
-  return g_attn_impl == 2 && rep <= 16 && (rep & (rep - 1)) == 0 &&
+  return rep <= 16 && (rep & (rep - 1)) == 0 &&
          (pairs <= g_attn_v5_max_pairs || (rep >= 8 && pairs <= 4 * g_attn_v5_max_pairs));
 }
 // v6 (attn_decode_mma.hip: scores and P.V on the matrix cores, one workgroup per pair, no workspace): 0 off,
@@ -1134,7 +893,7 @@ static bool use_v5(int B, int Hkv, int rep) {
 static int g_attn_v6 = 1;
 void attn_set_v6(int mode) { g_attn_v6 = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
 static bool use_v6(int B, int Hkv, int rep) {
-  if (g_attn_v6 == 0 || g_attn_impl != 2 || rep > 16 || (rep & (rep - 1))) return false;
+  if (g_attn_v6 == 0 || rep > 16 || (rep & (rep - 1))) return false;
   if (g_attn_v6 == 2) return true;
   return rep >= 8 && B * Hkv >= 8 && B * Hkv < 2048;
 }
@@ -1147,17 +906,13 @@ int attn_decode_chunk(int B, int Hkv, int T, int rep) {
   if (use_v6(B, Hkv, rep)) return T;
   if (use_v5(B, Hkv, rep)) return 16 * kpg5(rep);
   if (use_v3(B, Hkv, rep)) return T;
-  return use_v2(B, Hkv, rep) ? 4 * kpg_v2(rep, B * Hkv) : 16 * kpg_v1(rep, B, Hkv, T);
+  return 4 * kpg_v2(rep, B * Hkv);
 }
 
 int attn_decode_splits(int B, int Hkv, int T, int rep) {
   if (use_v6(B, Hkv, rep)) return 1;
   if (use_v5(B, Hkv, rep)) return (T + 16 * kpg5(rep) - 1) / (16 * kpg5(rep));
   if (use_v3(B, Hkv, rep)) return 1;
-  if (!use_v2(B, Hkv, rep)) {
-    const int ch = 16 * kpg_v1(rep, B, Hkv, T);
-    return (T + ch - 1) / ch;
-  }
   if (v4_midbatch(B, Hkv, rep)) return 1;  // one split: the v4 stream (v2 with a key mask)
   const int pairs = B * Hkv;
   const int max_split = T > 64 ? (T + 63) / 64 : 1;  // >= 64 keys per split
@@ -1219,25 +974,6 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
 #undef JLA_AD3
     return -1;
   }
-  if (!use_v2(B, Hkv, rep)) {
-    dim3 grid(nsplit, Hkv, B);
-    const int kpg = kpg_v1(rep, B, Hkv, t_cap);
-#define JLA_AD(R, K)                                                                                           \
-  if (rep == R && kpg == K) {                                                                                  \
-    attn_decode_v1_kernel<R, K><<<grid, AD_WAVES * 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len,  \
-                                                               out, ws, tickets, H, Hkv, T, t_cap, nsplit,     \
-                                                               scale);                                         \
-    JLA_CHECK_LAUNCH();                                                                                        \
-    return 0;                                                                                                  \
-  }
-    JLA_AD(1, 8) JLA_AD(1, 4) JLA_AD(1, 2)
-    JLA_AD(2, 8) JLA_AD(2, 4) JLA_AD(2, 2)
-    JLA_AD(4, 8) JLA_AD(4, 4) JLA_AD(4, 2)
-    JLA_AD(8, 4) JLA_AD(8, 2)
-    JLA_AD(16, 2)
-    return -1;
-#undef JLA_AD
-  }
   const int items = B * Hkv * nsplit;
   if (g_attn_v4 && nsplit == 1 && !key_mask && rep <= 8) {
 #define JLA_AD4(R, K, U)                                                                                         \
@@ -1270,30 +1006,12 @@ int attn_decode(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32
     attn_decode_v2_kernel<R, KPG, NS, false><<<items, 64, 0, s>>>(q, kc, vc, slot, kv_start, key_mask, mask_len, out, \
                                                                   ws, tickets, B, H, Hkv, T, t_cap, nsplit,          \
                                                                   split_len, scale, g_attn_diag);
-  const int geo = geo_v2(B * Hkv);
+  const bool k8 = kpg_v2(rep, B * Hkv) == 8;
   switch (rep) {
-    case 1:
-    case 2:
-    case 4:
-      // REP <= 4 shares one body per geometry (REP only sizes the register arrays)
-      if (rep == 1) {
-        if (geo == 82) { JLA_AD2(1, 8, 2) } else { JLA_AD2(1, 4, 2) }
-      } else if (rep == 2) {
-        if (geo == 82) { JLA_AD2(2, 8, 2) } else { JLA_AD2(2, 4, 2) }
-      } else {
-        if (geo == 43) {
-          JLA_AD2(4, 4, 3)
-        } else if (geo == 24) {
-          JLA_AD2(4, 2, 4)
-        } else if (geo == 82) {
-          JLA_AD2(4, 8, 2)
-        } else if (geo == 44) {
-          JLA_AD2(4, 4, 4)
-        } else {
-          JLA_AD2(4, 4, 2)
-        }
-      }
-      break;
+    // REP <= 4 shares one body per geometry (REP only sizes the register arrays)
+    case 1: if (k8) { JLA_AD2(1, 8, 2) } else { JLA_AD2(1, 4, 2) } break;
+    case 2: if (k8) { JLA_AD2(2, 8, 2) } else { JLA_AD2(2, 4, 2) } break;
+    case 4: if (k8) { JLA_AD2(4, 8, 2) } else { JLA_AD2(4, 4, 2) } break;
     case 8: JLA_AD2(8, 2, 4) break;
     case 16: JLA_AD2(16, 1, 4) break;
     default: return -1;

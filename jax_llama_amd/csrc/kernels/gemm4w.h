@@ -275,9 +275,10 @@ JLA_DEV void g4_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, in
 // images and slot layout (the W half of a slot is half used), same two sub-steps per 64-deep K-tile and one barrier;
 // per sub-step 8 NJ MFMAs with the 8 + NJ fragment reads and 8 + NJ LDS-DMA issues spread over the first slots.
 // No in-loop norm statistic (the caller precomputes it: RMSM 0 / 2 only).
-template <int NJ, typename Acc, bool W3 = false>
+template <int NJ, typename Acc, bool W3 = true>
 JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, int KT, int wu, int lane, Acc& acc) {
   static_assert(NJ == 4 || NJ == 6 || NJ == 8, "n-tiles per wave");
+  static_assert(W3, "the narrow tiles keep the weights three K-tiles deep (the two-slot form was removed in round 6)");
   constexpr int ND = NJ;           // W DMAs per wave per K-tile (2 NJ n-tiles x 2 k halves / 4 waves)
   constexpr int NQ = 8 + NJ;       // fragment reads / DMA issues per sub-step
   constexpr int MPS = (8 * NJ) / 16;  // MFMAs per slot (16 slots per sub-step)
@@ -340,7 +341,7 @@ JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, i
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  if constexpr (W3) {  // W three K-tiles deep (g4_mainloop W3): barriers wait for all but the youngest ND W DMAs
+  {  // W three K-tiles deep (g4_mainloop W3): barriers wait for all but the youngest ND W DMAs
     static_assert(ND < 16, "vmcnt immediate");
     if (KT > 0) {
 #pragma unroll
@@ -400,42 +401,7 @@ JLA_DEV void g4n_mainloop(const G4Args& g, u32x4* lds, int m0, int n0, int t0, i
     }
     wait_vmcnt<0>();
     g4_acc_fence();
-    return;
   }
-  if (KT > 0) {
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) dma(0, j, 0);
-  }
-  if (KT > 1) {
-#pragma unroll
-    for (int j = 0; j < NQ; ++j) dma(1, j, 1);
-    wait_vmcnt<NQ>();
-  } else {
-    wait_vmcnt<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (KT > 0) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) rd(q < NJ ? w0[q] : x0[q - NJ], 0, 0, 0, q);
-  }
-  int t = 0;
-  for (; t + 2 < KT; ++t) {
-    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
-    mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, (t + 1) & 1, 0, true, t + 2, true, t + 2, t & 1);
-  }
-  if (t + 1 < KT) {
-    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
-    mid_barrier();
-    substep(w1, x1, w0, x0, true, (t + 1) & 1, (t + 1) & 1, 0, false, 0, false, 0, 0);
-    ++t;
-  }
-  if (t < KT) {
-    substep(w0, x0, w1, x1, true, t & 1, t & 1, 1, false, 0, false, 0, 0);
-    substep(w1, x1, w0, x0, false, 0, 0, 0, false, 0, false, 0, 0);
-  }
-  g4_acc_fence();
 }
 
 // Staged bf16 epilogue, in two steps on the wave's private 32 KiB of the (now idle) staging array:

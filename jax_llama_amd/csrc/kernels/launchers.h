@@ -91,10 +91,9 @@ int rope_kv_write(const bf16_t* qkv, const float* table, int table_len, const in
                   hipStream_t s);
 
 int attn_decode_chunk(int B, int Hkv, int T, int rep);
-void attn_set_v1_min_wgs(int n);
 void attn_set_v5_max_pairs(int n);
 void attn_set_v5_fold(int n);       // v5 last-arriver merge: splits per load round (12 default, 4: the first version)  // split small-batch decode kernel up to n (row, kv head) pairs (0 off, <0 default)
-void attn_set_v3_max_pairs(int n);  // single-workgroup-per-(row, kv head) decode kernel up to n pairs (0: off)  // v1 split sizing: smallest chunk giving >= n workgroups (default 256)
+void attn_set_v3_max_pairs(int n);  // single-workgroup-per-(row, kv head) decode kernel up to n pairs (0: off)
 void attn_set_impl(int impl, int waves_target);
 void attn_set_diag(int d);
 void attn_set_v3_kpg(int mult);  // small-batch decode attention: key rows per lane per chunk x mult (1, 2, 4)

@@ -5,10 +5,10 @@ evicts L2 and the Infinity Cache, as the weight stream of a real step does). Tim
 
   python tools/bench_attn_decode.py --model llama3-70b --tp 8 --shapes 1x192 1x384 32x384 --impls 2 5
 
-impl (ext.attn_set_impl / attn_set_v3_max_pairs): 2 = default dispatch; 1 = the split v1 kernel (v3 off);
+impl (ext.attn_set_impl / attn_set_v3_max_pairs): 2 = default dispatch; 3 = v3 (one workgroup per pair) forced;
 5 = split small-batch kernel (v5) where it applies; 6 = v5 with the first merge (4 splits per load round);
-7 = v4 (register ring, one split) forced; 9 = v2 (LDS-DMA ring) forced; 60 = v6 (matrix cores), 61 / 62 / 64 / 68 = v6
-with 1 / 2 / 4 / 8 waves per (row, kv head) pair. Prints one JSON line per (shape, impl).
+7 = v4 (register ring, one split) forced; 9 = v2 (LDS-DMA ring, KPG 4, 2 slots) forced; 60 = v6 (matrix cores),
+61 / 62 / 64 / 68 = v6 with 1 / 2 / 4 / 8 waves per (row, kv head) pair. Prints one JSON line per (shape, impl).
 """
 from __future__ import annotations
 
@@ -30,14 +30,14 @@ def set_impl(e, impl):
     # 60: the MFMA kernel (v6) with its default waves per pair; 61 / 62 / 64 / 68: v6 with 1 / 2 / 4 / 8 waves per pair
     e.attn_set_v6(2 if 60 <= impl <= 68 else 0)
     e.attn_set_v6_wpp(impl - 60 if 61 <= impl <= 68 else 0)
-    e.attn_set_v3_max_pairs(0 if impl == 1 else 4096)
+    e.attn_set_v3_max_pairs(4096)
     if impl in (7, 9):
         # the streaming kernels at any pair count, one split: 7 = v4 register ring, 9 = v2 (LDS-DMA ring)
-        e.attn_set_impl(3 if impl == 9 else 2, 1)  # waves target 1 -> one split
-        e.attn_set_impl(3 if impl == 9 else 2, -1)  # v2/v4 down to 1 pair
+        e.attn_set_impl(4 if impl == 9 else 2, 1)  # waves target 1 -> one split
+        e.attn_set_impl(4 if impl == 9 else 2, -1)  # v2/v4 down to 1 pair
         e.attn_set_v3_max_pairs(0)
     if hasattr(e, "attn_set_v5_max_pairs"):
-        e.attn_set_v5_max_pairs(4096 if impl in (5, 6) else (0 if impl in (1, 3, 7, 9) else -1))
+        e.attn_set_v5_max_pairs(4096 if impl in (5, 6) else (0 if impl in (3, 7, 9) else -1))
     if hasattr(e, "attn_set_v5_fold"):
         e.attn_set_v5_fold(4 if impl == 6 else (12 if impl == 5 else 0))
 

@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[1, 6])
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--ops", nargs="+", default=None, help="subset of qkv o gate_up down lm_head attn")
-    ap.add_argument("--attn-impls", default="1:0,2:4096", help="impl:waves_target pairs for attn A/B")
+    ap.add_argument("--attn-impls", default="2:4096,4:4096", help="impl:waves_target pairs for attn A/B")
     ap.add_argument("--attn-shapes", nargs="*", default=None, help="BxT decode attention shapes (default: a sweep)")
     ap.add_argument("--v3-kpg", type=int, nargs="*", default=[0],
                     help="small-batch decode attention (v3) chunk-depth multipliers to sweep (0: by size, the default)")
@@ -126,7 +126,7 @@ def main():
             impl = impl % 100
             e.attn_set_impl(impl, target)
             e.attn_set_v3_kpg(kpg)
-            e.attn_set_v3_max_pairs(0 if impl == 1 else 4096)  # impl 1: the split v1 kernel even at small batch
+            e.attn_set_v3_max_pairs(4096)
             us = timeit(lambda i: ops.attention(q, kc, vc, slot, ks))
             o = ops.attention(q, kc, vc, slot, ks).float()
             ref_out = o if ref_out is None else ref_out

@@ -52,9 +52,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp", type=int, default=1)
-    # Serving-throughput operating point: 2048 concurrent sequences per replica (KV cache 103 GB of the
-    # 288 GB HBM; ~41 ms per decode step); latency points are reported separately.
-    ap.add_argument("--batch", type=int, default=2048, help="sequences per replica")
+    # Serving-throughput operating point: 4096 concurrent sequences per replica (KV cache 103 GB of the 288 GB HBM; ~71
+    # ms per decode step). Against 2048 on one box: 43.5k vs 41.5k tok/s -- the o / down / qkv projections fill the chip
+    # without K splits at M = 4096 (profiles/r6_bench_batch_4096_vs_2048.jsonl); the prefill runs in two row chunks of
+    # 2048 x 128 tokens (runtime/engine.py PREFILL_TOKENS). Latency points are reported separately.
+    ap.add_argument("--batch", type=int, default=4096, help="sequences per replica")
     ap.add_argument("--prompt-len", type=int, default=128)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count (INVALID for the metric)")

@@ -43,6 +43,11 @@ class KVCache:
         self.index = 0
         self.index_t.zero_()
 
+    def rows(self, b0: int, b1: int) -> "KVCacheRows":
+        """The cache of batch rows ``[b0, b1)`` (every layer): a view whose per-layer K / V are contiguous slices, for a
+        prefill run in row chunks (runtime/engine.py)."""
+        return KVCacheRows(self, b0, b1)
+
     def nbytes(self) -> int:
         return 2 * self.k.numel() * self.k.element_size()
 
@@ -56,3 +61,29 @@ class KVCache:
             }
             for i in range(self.k.shape[0])
         }
+
+
+class KVCacheRows:
+    """Rows ``[b0, b1)`` of a KVCache: ``layer(i)`` gives contiguous ``[b1 - b0, Hkv, T, Dh]`` views; the slot index is
+    the parent's (one position for every row)."""
+
+    def __init__(self, parent: KVCache, b0: int, b1: int):
+        self.parent = parent
+        self.b0, self.b1 = b0, b1
+        self.batch_size = b1 - b0
+        self.max_length = parent.max_length
+
+    @property
+    def device(self):
+        return self.parent.device
+
+    @property
+    def index(self):
+        return self.parent.index
+
+    @property
+    def index_t(self):
+        return self.parent.index_t
+
+    def layer(self, i: int):
+        return self.parent.k[i, self.b0:self.b1], self.parent.v[i, self.b0:self.b1]

@@ -290,7 +290,8 @@ KS_CANDIDATES = (1, 2, 3, 4, 6, 8, 12, 16)
 TILE_CANDIDATES = (1, 2, 3, 7, 11, 12, 14, 16, 17)
 if os.environ.get("JLA_TUNE_TILES"):  # A/B tooling: restrict the tile candidates, e.g. JLA_TUNE_TILES=1,2,3,7,11,12
     TILE_CANDIDATES = tuple(int(v) for v in os.environ["JLA_TUNE_TILES"].split(","))
-TUNE_MAX_M = 2048
+# decode-sized M measured per shape (above: the C++ heuristic; prefill-sized M have enough 256 x 256 tiles)
+TUNE_MAX_M = int(os.environ.get("JLA_TUNE_MAX_M", "4096"))
 
 
 def choose_gemm_plan(e, m: int, n: int, k: int, device, mode: int = 0, rms: bool = False) -> Tuple[int, int]:

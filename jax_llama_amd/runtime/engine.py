@@ -53,6 +53,9 @@ class GenerationConfig:
     seed: int = 0
 
 
+# prompt tokens per prefill forward (DecodeEngine._prefill_rows): larger batches run their prefill in row chunks
+PREFILL_TOKENS = int(os.environ.get("JLA_PREFILL_TOKENS", str(1 << 18)))
+
 # greedy decoding takes the argmax inside the lm_head GEMM epilogue (JLA_FUSED_ARGMAX=0: logits + argmax)
 FUSED_GREEDY = os.environ.get("JLA_FUSED_ARGMAX", "1") != "0"
 
@@ -205,8 +208,7 @@ class DecodeEngine:
         self.sequences[:, :s] = ids
         self.finished.zero_()
         pos_dev = positions.to(dev)
-        logits, *_ = model.forward_tokens(ids, pos_dev, self.cache, 0, self.kv_start, self.key_mask,
-                                          logits_mode=self._logits_mode())
+        logits = self._prefill_rows(ids, pos_dev)
         self.cache.advance(s)
         # state for the loop body: cur_len = S (also the sampler's Philox step), token/pos of the
         # last prompt position
@@ -219,6 +221,28 @@ class DecodeEngine:
         self._update(nxt)
         self.cache.index = s  # host mirror (decode steps track the slot on the device)
         return s + 1
+
+    def _prefill_rows(self, ids: torch.Tensor, pos_dev: torch.Tensor):
+        """The prompt forward, in row chunks of at most PREFILL_TOKENS tokens: every kernel then sees at most the
+        token count the GEMMs already saturate the chip with (M = 262144: 2048 rows x 128), whatever the batch, and no
+        activation index of a larger batch can pass 2^31 elements. One chunk up to that size (the common case)."""
+        b, s = ids.shape
+        rows = max(1, PREFILL_TOKENS // max(1, s))
+        mode = self._logits_mode()
+        if b <= rows:
+            logits, *_ = self.model.forward_tokens(ids, pos_dev, self.cache, 0, self.kv_start, self.key_mask,
+                                                   logits_mode=mode)
+            return logits
+        parts = []
+        for b0 in range(0, b, rows):
+            b1 = min(b, b0 + rows)
+            km = self.key_mask[b0:b1] if self.key_mask is not None else None
+            lg, *_ = self.model.forward_tokens(ids[b0:b1], pos_dev[b0:b1], self.cache.rows(b0, b1), 0,
+                                               self.kv_start[b0:b1], km, logits_mode=mode)
+            parts.append(lg)
+        if isinstance(parts[0], tuple):  # greedy: (idx, val) per chunk
+            return tuple(torch.cat([p[i] for p in parts]) for i in range(len(parts[0])))
+        return torch.cat(parts)
 
     def prefill_only(self, input_ids, attention_mask, gc: GenerationConfig) -> int:
         """Prefill + first token only (time-to-first-token measurement)."""

@@ -104,6 +104,25 @@ def test_greedy_generation_matches_oracle():
     assert torch.equal(got.long(), want)
 
 
+@pytest.mark.parametrize("do_sample", [False, True])
+def test_prefill_row_chunks_match_one_forward(do_sample, monkeypatch):
+    """The engine's prefill in row chunks (large batches: at most PREFILL_TOKENS prompt tokens per forward, each chunk
+    writing its own rows of the KV cache) generates exactly what one whole-batch prefill does, padding mask included."""
+    from jax_llama_amd.runtime import engine
+    from jax_llama_amd.runtime.engine import GenerationConfig
+    cfg = tiny_config(num_hidden_layers=2)
+    model, *_ = build(cfg, seed=4)
+    toks, mask = left_padded_batch([4, 7, 2, 7, 5], 7, cfg.vocab_size, pad=2, seed=3)
+    gc = GenerationConfig(max_length=14, do_sample=do_sample, temperature=0.8, top_p=0.95, pad_token_id=2,
+                          eos_token_id=-1, seed=11)
+    whole = model.generate(toks, attention_mask=mask, generation_config=gc).sequences.clone()
+    engine._ENGINES.clear()
+    monkeypatch.setattr(engine, "PREFILL_TOKENS", 14)  # 2 rows per forward: chunks of 2, 2, 1
+    chunked = model.generate(toks, attention_mask=mask, generation_config=gc).sequences
+    engine._ENGINES.clear()
+    assert torch.equal(whole, chunked)
+
+
 def test_sampling_is_seeded_and_valid():
     cfg = tiny_config(num_hidden_layers=2)
     model, *_ = build(cfg, seed=5)

@@ -13,6 +13,10 @@ Variants: 1 = GEMV 4 waves (1 or 2 tiles/WG), 5 = GEMV 4 tiles/WG, 6 = GEMV 2 ti
 register ring (M > 16, bf16 activations), 20 = 2 tiles x 8 waves, 16 = K over 2 workgroups, packed-x 12 / 15 / 18 / 21 /
 22 / 26, 7 = tiled MFMA GEMM with split-K (gemm.hip; a candidate for M > 16, always used for M > 64). ``JLA_GEMV_VARIANT`` pins one; ``JLA_AUTOTUNE=0`` disables tuning.
 
+Shipped picks: ``ops/tune_gfx950.json`` (measured on an MI355X for the bench, latency and tensor-parallel shapes) is
+loaded first, so plans are identical on every box and nothing is measured for those shapes; shapes it lacks are
+measured as above.
+
 Tensor parallelism: inside ``tp_scope(comm)`` (the model's forward under TP) a decision is collective -- rank 0
 of the TP group measures and broadcasts its choice, so every rank runs the same plans (a rank on a slower plan
 would set the pace of every collective). Persistence: decisions are kept per (arch, shape) in a JSON table
@@ -85,18 +89,31 @@ def _key_str(kind: str, key: Tuple) -> str:
     return f"{kind}@{TUNE_VERSION}:" + ",".join(str(k).replace("torch.", "") for k in key)
 
 
+# The packaged table: picks measured on an MI355X with tools/bench_full.sh (JLA_TUNE_FILE) for the bench / latency /
+# tensor-parallel shapes, shipped with the package so every box runs the same plans (the tuner's interleaved minimum
+# flips between near-tied plans from box to box) and skips the first-use measurements. The user's file overrides it;
+# JLA_TUNE_PACKAGED=0 ignores it (every shape measured on this device).
+PACKAGED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"tune_{ARCH}.json")
+
+
+def _read_table(path: str) -> Dict[str, object]:
+    try:
+        with open(path) as f:
+            data = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    return data if isinstance(data, dict) else {}
+
+
 def _load():
     if _LOADED["done"]:
         return
     _LOADED["done"] = True
     if not _persist_on():
         return
-    try:
-        with open(tune_file()) as f:
-            data = json.load(f)
-    except (OSError, ValueError):
-        return
-    _PERSISTED.update(data if isinstance(data, dict) else {})
+    if os.environ.get("JLA_TUNE_PACKAGED", "1") != "0":
+        _PERSISTED.update(_read_table(PACKAGED_FILE))
+    _PERSISTED.update(_read_table(tune_file()))
 
 
 _PERSISTED: Dict[str, object] = {}
@@ -332,14 +349,23 @@ G5_TILES = (11, 12)  # gemm5 weight-streaming split-K (csrc/kernels/gemm5ws.h)
 TUNE_ROUNDS = 3
 
 
+# split-K candidates whose fp32 partial slabs (split x M x N) exceed this are not measured: a K split only pays where the
+# output has too few tiles, i.e. small M x N, and the scratch of a split lm_head at M = 4096 would be tens of GB
+TUNE_WS_BYTES = int(float(os.environ.get("JLA_TUNE_WS_GB", "4")) * (1 << 30))
+
+
 def _measure_plan(e, m, n, k, device, heur, mode=0, rms=False) -> Tuple[int, int]:
     kt = k // 32
-    ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4} | {heur})
+
+    def fits(c):
+        return c * m * (n + 1) * 4 <= TUNE_WS_BYTES
+
+    ks_c = sorted({c for c in KS_CANDIDATES if kt // c >= 4 and fits(c)} | ({heur} if fits(heur) else set()) | {1})
     cands = [(c, tm) for tm in TILE_CANDIDATES for c in ks_c
              if (tm not in G4N_TILES or (k % 64 == 0 and not (c > 1 and rms and mode != 1)))
              and (tm not in G5_TILES or (k % 64 == 0 and m <= 512))]
     if k % 64 == 0 and m <= 512:  # gemm5 also at the deeper splits its 64-deep stages allow (narrow shards, long K)
-        cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c]
+        cands += [(c, tm) for tm in G5_TILES for c in (24, 32, 48) if (k // 64) // c >= 2 and c not in ks_c and fits(c)]
     nbytes = n * k * 2
     copies = max(2, min(16, (640 << 20) // max(nbytes, 1) + 1))
     ws_w = [torch.empty(n // 16, k // 32, 64, 8, dtype=torch.bfloat16, device=device).normal_(0, 0.02)

@@ -36,7 +36,7 @@ setup(
     version="0.1.0",
     description="MI355X-native (gfx950) LLaMA-1/2/3 inference with the LSaldyt/JAX_llama API",
     packages=find_packages(include=["jax_llama_amd", "jax_llama_amd.*"]),
-    package_data={"jax_llama_amd": ["_C*.so", "_bpe*.so", "csrc/**/*"]},
+    package_data={"jax_llama_amd": ["_C*.so", "_bpe*.so", "csrc/**/*", "ops/tune_*.json"]},
     include_package_data=True,
     python_requires=">=3.10",
     install_requires=["torch", "numpy", "sentencepiece", "regex"],

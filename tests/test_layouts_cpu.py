@@ -62,3 +62,23 @@ def test_pinned_variant_respects_packed_rules(monkeypatch):
     for pinned, xp, po, mode, want in cases:
         monkeypatch.setattr(ops, "GEMV_VARIANT", pinned)
         assert ops._variant(None, x, w, mode, xp, po) == want, (pinned, mode)
+
+
+def test_packaged_tune_table_is_current():
+    """The shipped picks (ops/tune_gfx950.json, measured on an MI355X by tools/bench_full.sh) are keyed at the current
+    TUNE_VERSION and name only plans the tuner could pick today: tile configs of TILE_CANDIDATES (or the gemm5 deep
+    splits) and GEMV variants of the candidate lists -- a candidate-set change without a new table fails here."""
+    import json
+    from jax_llama_amd.ops import autotune
+    with open(autotune.PACKAGED_FILE) as f:
+        table = json.load(f)
+    assert table, "empty packaged table"
+    gemv_ok = {1, 5, 6, 10, 16, 20, autotune.TILED_VARIANT, *autotune.XP_CANDIDATES}
+    for key, v in table.items():
+        kind, rest = key.split("@", 1)
+        assert int(rest.split(":", 1)[0]) == autotune.TUNE_VERSION, key
+        if kind == "gemm":
+            ks, tile = v
+            assert tile in autotune.TILE_CANDIDATES and ks >= 1, (key, v)
+        else:
+            assert kind == "gemv" and v in gemv_ok, (key, v)

@@ -291,8 +291,7 @@ def _tp_rank_proxy(args):
            "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),
            "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
            # qkv, attention, wo, w1|w3, w2 (+ the two all-reduce launches when the row-parallel GEMVs do not fuse them)
-           "fused_row_parallel": comm.fused is not None,
-           "launches_per_layer_decode": 5 if comm.fused is not None else 7}
+           "fused_row_parallel": comm.fused is not None}
     try:
         out["points"] = [decode_latency(model, b, args.prompt_len, args.gen_len, seed=11)
                          for b in args.proxy_batches]

@@ -811,6 +811,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
     rc(jla::cu_mask_stream_get(reinterpret_cast<hipStream_t>(s), mk.data(), (int)words), "cu_mask_of");
     return std::vector<int64_t>(mk.begin(), mk.end());
   });
+  m.def("graph_kernel_nodes", [](int64_t g) {
+    const int n = jla::graph_kernel_nodes(reinterpret_cast<hipGraph_t>(g));
+    check(n >= 0, "graph_kernel_nodes: hipGraphGetNodes failed");
+    return n;
+  });
   m.def("stream_destroy", [](int64_t s) { rc(jla::stream_destroy(reinterpret_cast<hipStream_t>(s)), "stream_destroy"); });
   m.def("cu_census", [](Tensor out) {
     check_gpu(out, "out");
@@ -830,6 +835,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("gemm5_ksplit", [](int64_t k, int64_t ks) { return jla::gemm5_ksplit((int)k, (int)ks); });
   m.def("attn_set_v6", [](int64_t mode) { jla::attn_set_v6((int)mode); });
   m.def("attn_set_v6_wpp", [](int64_t wpp) { jla::attn_set_v6_wpp((int)wpp); });
+  m.def("attn_set_v6_diag", [](int64_t d) { jla::attn_set_v6_diag((int)d); });
   m.def("attn_v6_wpp", [](int64_t pairs) { return jla::attn_v6_wpp((int)pairs); });
   m.def("attn_decode", &attn_decode, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("slot"),
         py::arg("kv_start"), py::arg("key_mask").none(true), py::arg("out"), py::arg("ws"), py::arg("tickets"), py::arg("t_cap"),

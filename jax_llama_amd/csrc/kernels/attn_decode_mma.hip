@@ -27,7 +27,8 @@
 
 namespace jla {
 
-template <int REP, int WPP>
+// DIAG (tools only, attn_set_v6_diag; wrong results): 1 = no compute, 2 = no K loads, 4 = no V DMAs
+template <int REP, int WPP, int DIAG = 0>
 __global__ void __launch_bounds__(WPP * 64)
     attn_decode_v6_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
                           const int32_t* __restrict__ slot_ptr, const int32_t* __restrict__ kv_start,
@@ -62,13 +63,19 @@ __global__ void __launch_bounds__(WPP * 64)
   const int n_steps = lo < hi ? (hi - 1) / AD6_STEP - s_begin + 1 : 0;
   const int my_steps = n_steps > w ? (n_steps - w + WPP - 1) / WPP : 0;
   auto issue = [&](int step, u32x4 (&kr)[8], char* vslot) {
-    ad6_issue<false>((s_begin + step) * AD6_STEP, kr, vslot, kb, vb, T, lane);
+    ad6_issue<false, DIAG>((s_begin + step) * AD6_STEP, kr, vslot, kb, vb, T, lane);
   };
+  constexpr int NV = (DIAG & 2 ? 0 : 8) + (DIAG & 4 ? 0 : 8);  // vector-memory ops per step
   Ad6Acc st;
   ad6_init(st);
   // valid = false: a ring slot loaded past the wave's last step (clamped addresses, fully masked, adds nothing)
   auto compute = [&](int step, bool valid, u32x4 (&kr)[8], const char* vslot) {
-    ad6_compute<REP>(st, kr, qf, vslot, (s_begin + step) * AD6_STEP, valid, lo, hi, mrow, mask_len, scale_log2, lane);
+    if constexpr (DIAG & 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pin(kr[i]);
+    } else {
+      ad6_compute<REP>(st, kr, qf, vslot, (s_begin + step) * AD6_STEP, valid, lo, hi, mrow, mask_len, scale_log2, lane);
+    }
   };
 
   // Two-slot ring, branch-free around the loads (a branch there makes hipcc merge in-flight ring registers with
@@ -85,11 +92,11 @@ __global__ void __launch_bounds__(WPP * 64)
     issue(step_of(0), ka, slotA);
     for (int i = 0; i < my_steps; i += 2) {
       issue(step_of(i + 1), kb2, slotB);
-      wait_vmcnt<16>();  // step i (slot A) landed; step i + 1 stays in flight
+      wait_vmcnt<NV>();  // step i (slot A) landed; step i + 1 stays in flight
       compute(step_of(i), true, ka, slotA);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot A's V reads are done: refill it
       issue(step_of(i + 2), ka, slotA);
-      wait_vmcnt<16>();
+      wait_vmcnt<NV>();
       compute(step_of(i + 1), i + 1 < my_steps, kb2, slotB);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -159,6 +166,8 @@ __global__ void __launch_bounds__(WPP * 64)
 // waves per (row, kv head) pair: enough workgroups to cover the CUs, fewer waves (less merge) for many pairs;
 // attn_set_v6_wpp pins it (A/B)
 static int g_v6_wpp = 0;
+static int g_v6_diag = 0;
+void attn_set_v6_diag(int d) { g_v6_diag = d & 7; }
 void attn_set_v6_wpp(int wpp) { g_v6_wpp = (wpp == 1 || wpp == 2 || wpp == 4 || wpp == 8) ? wpp : 0; }
 int attn_v6_wpp(int pairs) {
   if (g_v6_wpp) return g_v6_wpp;
@@ -171,6 +180,18 @@ int attn_decode_v6(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const in
   const int rep = H / Hkv, pairs = B * Hkv;
   const float scale_log2 = 1.4426950408889634f / sqrtf((float)AD6_DH);
   const int wpp = attn_v6_wpp(pairs);
+  if (g_v6_diag && rep == 8 && wpp == 2) {  // tools only: the ablation instances of the 70B shape (wrong results)
+#define JLA_AD6D(D)                                                                                                \
+  if (g_v6_diag == D) {                                                                                            \
+    attn_decode_v6_kernel<8, 2, D><<<pairs, 128, 2 * AD6_WAVE_LDS, s>>>(q, kc, vc, slot, kv_start, key_mask,       \
+                                                                         mask_len, out, H, Hkv, T, t_cap,          \
+                                                                         scale_log2, out_pack);                    \
+    JLA_CHECK_LAUNCH();                                                                                            \
+    return 0;                                                                                                      \
+  }
+    JLA_AD6D(1) JLA_AD6D(2) JLA_AD6D(3) JLA_AD6D(4) JLA_AD6D(5)
+#undef JLA_AD6D
+  }
 #define JLA_AD6(R, W)                                                                                              \
   if (rep == R && wpp == W) {                                                                                      \
     attn_decode_v6_kernel<R, W><<<pairs, W * 64, W * AD6_WAVE_LDS, s>>>(q, kc, vc, slot, kv_start, key_mask,       \

@@ -90,11 +90,13 @@ JLA_DEV void ad6_q_ready(u32x4 (&qf)[4], int lane) {  // after the wait that ret
 // issue one 32-key step starting at key0 (rows clamped to T - 1): V rows into vslot by LDS-DMA (1 KiB block bi = rows
 // 4bi .. 4bi+3, lane L -> row 4bi + L / 16, slot L % 16 <- source chunk slot ^ swz(row)), K rows into kr by asm loads
 // (key l & 15 of block kk, bytes 64jj + 16c). 16 vector-memory ops; the caller counts the waits. SC1: agent-coherent.
-template <bool SC1>
+// DIAG (tools only, wrong results): 2 = no K loads, 4 = no V DMAs
+template <bool SC1, int DIAG = 0>
 JLA_DEV void ad6_issue(int key0, u32x4 (&kr)[8], char* vslot, const bf16_t* kb, const bf16_t* vb, int T, int lane) {
   const int c = lane >> 4, j = lane & 15;
 #pragma unroll
   for (int bi = 0; bi < 8; ++bi) {
+    if constexpr (DIAG & 4) break;
     const int row = 4 * bi + (lane >> 4);
     const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
     const int key = min(key0 + row, T - 1);
@@ -105,6 +107,7 @@ JLA_DEV void ad6_issue(int key0, u32x4 (&kr)[8], char* vslot, const bf16_t* kb, 
   }
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
+    if constexpr (DIAG & 2) break;
     const int key = min(key0 + 16 * kk + j, T - 1);
     const bf16_t* p = kb + (size_t)key * AD6_DH + 8 * c;
 #pragma unroll

@@ -117,6 +117,7 @@ int attn_decode_v6(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const in
                    hipStream_t s, bf16_t* out_pack);
 void attn_set_v6(int mode);
 void attn_set_v6_wpp(int wpp);
+void attn_set_v6_diag(int d);  // tools only: v6 ablations (1 no compute, 2 no K loads, 4 no V DMAs; wrong results)
 int attn_v6_wpp(int pairs);
 void attn_prefill_set_impl(int impl);  // 2 = GQA-shared MFMA 32x32 flash kernel (default), 1 = v1
 int attn_prefill(const bf16_t* q, const bf16_t* kc, const bf16_t* vc, const int32_t* slot, const int32_t* kv_start,
@@ -157,5 +158,6 @@ int cu_census(uint32_t* out, int blocks, hipStream_t s);
 int cu_mask_stream_create(const uint32_t* mask, int words, hipStream_t* out);
 int cu_mask_stream_get(hipStream_t s, uint32_t* mask, int words);
 int stream_destroy(hipStream_t s);
+int graph_kernel_nodes(hipGraph_t g);  // kernel nodes of a captured graph (< 0: error)
 
 }  // namespace jla

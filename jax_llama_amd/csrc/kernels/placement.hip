@@ -8,6 +8,8 @@
 // created with a CU mask (hipExtStreamCreateWithCUMask; bit i = CU i of the device's logical numbering).
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "common.h"
 
 namespace jla {
@@ -40,5 +42,21 @@ int cu_mask_stream_get(hipStream_t s, uint32_t* mask, int words) {
 }
 
 int stream_destroy(hipStream_t s) { return hipStreamDestroy(s) == hipSuccess ? 0 : -2; }
+
+// kernel launches recorded in a captured graph (torch.cuda.CUDAGraph.raw_cuda_graph()): the decode step's launch count
+// as the hardware sees it (bench.py reports it per layer)
+int graph_kernel_nodes(hipGraph_t g) {
+  size_t n = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess) return -2;
+  if (n == 0) return 0;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess) return -2;
+  int k = 0;
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[i], &t) == hipSuccess && t == hipGraphNodeTypeKernel) ++k;
+  }
+  return k;
+}
 
 }  // namespace jla

@@ -43,10 +43,12 @@ def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256,
     eng.prefill(prompts, None)  # warm prefill: ``prefill_ms``
     ev1.record()
     eng._decode_step()  # eager step: sizes the workspaces before capture
+    eng.keep_graph = True
     eng._ensure_graph()
     eng._graph.replay()
     torch.cuda.synchronize(dev)
     ttft_ms = ev0.elapsed_time(ev1)
+    kernels = graph_kernels(eng._graph)
     eng.prefill(prompts, None)  # back to the first decode position: the timed replays cover the whole window
     torch.cuda.synchronize(dev)
     if barrier is not None:
@@ -61,7 +63,20 @@ def decode_latency(model, batch: int, prompt_len: int = 128, gen_len: int = 256,
     del eng
     return {"batch": batch, "decode_ms_per_token": round(ms, 4),
             "decode_tokens_per_sec": round(batch * 1000.0 / ms, 2), "prefill_ms": round(ttft_ms, 3),
-            "steps": steps, "kv_len_mean": round(prompt_len + 1 + (steps - 1) / 2, 1)}
+            "steps": steps, "kv_len_mean": round(prompt_len + 1 + (steps - 1) / 2, 1),
+            # launches of one decode step, counted from the captured graph's kernel nodes (every layer, lm_head,
+            # sampler, state update)
+            "kernels_per_step": kernels,
+            "kernels_per_layer": round(kernels / model.config.num_hidden_layers, 2) if kernels >= 0 else None}
+
+
+def graph_kernels(graph) -> int:
+    """Kernel nodes of a captured torch.cuda.CUDAGraph (hipGraphGetNodes; -1 when the raw graph is unavailable)."""
+    from .. import ops
+    try:
+        return int(ops.ext().graph_kernel_nodes(int(graph.raw_cuda_graph())))
+    except (AttributeError, RuntimeError):
+        return -1
 
 
 def time_to_first_token(model, batch: int, prompt_len: int, reps: int = 3, seed: int = 0,

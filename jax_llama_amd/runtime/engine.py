@@ -150,6 +150,7 @@ class DecodeEngine:
         self.key_mask: Optional[torch.Tensor] = None
         self._graph = None
         self._graph_key = None
+        self.keep_graph = False  # keep the captured graph's topology (runtime/benchmark.py counts its kernel nodes)
         self._gen: Optional[torch.Generator] = None
         self.gc: Optional[GenerationConfig] = None
 
@@ -260,7 +261,7 @@ class DecodeEngine:
         for _ in range(3):
             key = self._graph_state()
             torch.cuda.synchronize(self.device)
-            g = torch.cuda.CUDAGraph()
+            g = torch.cuda.CUDAGraph(keep_graph=self.keep_graph)
             # Capture records kernels without executing them; state buffers are static.
             with torch.cuda.graph(g):
                 self._decode_step()

@@ -28,6 +28,11 @@ from jax_llama_amd.config import get_preset  # noqa: E402
 def set_impl(e, impl):
     e.attn_set_impl(2, 4096)
     # 60: the MFMA kernel (v6) with its default waves per pair; 61 / 62 / 64 / 68: v6 with 1 / 2 / 4 / 8 waves per pair
+    # 600 + d: v6 at 2 waves per pair with ablation d (attn_set_v6_diag: 1 no compute, 2 no K loads, 4 no V DMAs)
+    if hasattr(e, "attn_set_v6_diag"):
+        e.attn_set_v6_diag(impl - 600 if 601 <= impl <= 607 else 0)
+    if 601 <= impl <= 607:
+        impl = 62
     e.attn_set_v6(2 if 60 <= impl <= 68 else 0)
     e.attn_set_v6_wpp(impl - 60 if 61 <= impl <= 68 else 0)
     e.attn_set_v3_max_pairs(4096)

@@ -243,6 +243,7 @@ def main():
         extra("mp1_point", lambda: res.__setitem__("mp1_point", _mp1_point(args)))
     if not args.no_calibration:  # last: the GEMM / copy probes of this box, next to the numbers above
         extra("calibration", lambda: res.__setitem__("calibration", calibration(dev)))
+        _box_rooflines(res)
     res["gemm_plan_choice"] = {f"m{k[0]}_n{k[1]}_k{k[2]}_mode{k[3]}{'_rms' if k[4] else ''}": f"ks{v[0]}_tile{v[1]}"
                                for k, v in autotune.ksplit_table().items()}
     res["gemv_variant_choice"] = autotune.variant_table()
@@ -258,6 +259,17 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _box_rooflines(res):
+    """Every ``hbm_roofline_ms_per_token`` (streamed bytes / the fixed 6.29 TB/s) gets a ``..._box`` twin divided by this
+    box's own sequential read rate (calibration ``stream_read_seq_tbps``), so a point reads against its box."""
+    tbps = (res.get("calibration") or {}).get("stream_read_seq_tbps")
+    if not tbps:
+        return
+    for d in (res, res.get("tp_rank_proxy"), res.get("mp1_point")):
+        if isinstance(d, dict) and "hbm_roofline_ms_per_token" in d:
+            d["hbm_roofline_ms_per_token_box"] = round(d["hbm_roofline_ms_per_token"] * 6.29 / tbps, 4)
 
 
 def _emit(res, json_out):

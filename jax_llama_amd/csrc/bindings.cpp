@@ -109,6 +109,10 @@ void prefetch(Tensor t, int64_t grid) {
     rc((int)hipMalloc(reinterpret_cast<void**>(&sink), 64), "prefetch sink");
   }
   const int64_t nbytes = t.numel() * t.element_size() / 16 * 16;
+  if (grid < 0) {  // the sequential streaming-read probe (calibration): each wave one contiguous range, -grid blocks
+    rc(jla::stream_probe(t.data_ptr(), nbytes, (int)-grid, sink, stream()), "stream_probe");
+    return;
+  }
   rc(jla::prefetch(t.data_ptr(), nbytes, (int)grid, sink, stream()), "prefetch");
 }
 

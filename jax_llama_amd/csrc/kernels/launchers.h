@@ -16,6 +16,7 @@ int rms_scale_bf16(const bf16_t* x, bf16_t* out, int M, int D, float eps, hipStr
 int rms_rowinv(const bf16_t* x, float* inv, int M, int D, float eps, hipStream_t s);  // inv[M] = 1/sqrt(mean(x^2)+eps)
 int residual_add(float* h, const void* p, int p_bf16, bf16_t* hb, long long n, hipStream_t s);
 int prefetch(const void* p, long long nbytes, int grid, unsigned* sink, hipStream_t s);
+int stream_probe(const void* p, long long nbytes, int grid, unsigned* sink, hipStream_t s);  // bytes read: per-wave contiguous ranges
 int gemm_f32(const float* x, const float* w, float* y, int M, int N, int K, hipStream_t s);
 int rmsnorm(const float* x, const float* w, float* out, int M, int D, float eps, hipStream_t s);
 

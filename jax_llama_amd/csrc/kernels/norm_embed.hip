@@ -214,6 +214,36 @@ int prefetch(const void* p, long long nbytes, int grid, unsigned* sink, hipStrea
   return 0;
 }
 
+// Streaming-read probe in the decode kernels' own access pattern (runtime/benchmark.py calibration,
+// stream_read_seq_tbps): each wave reads ONE contiguous range front to back, 1 KiB per wave instruction, U
+// instructions in flight -- as the decode attention streams a (row, kv head) pair and the GEMV a weight column group
+// (the grid-strided prefetch_kernel above scatters every wave's loads over the whole buffer and reads ~20 % slower).
+__global__ void __launch_bounds__(256) stream_probe_kernel(const u32x4* __restrict__ p, long long n16_per_wave,
+                                                           unsigned* __restrict__ sink, unsigned key) {
+  constexpr int U = 8;
+  const int lane = threadIdx.x & 63;
+  const long long wave = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const u32x4* q = p + wave * n16_per_wave;
+  unsigned acc = 0;
+  for (long long i = lane; i + (U - 1) * 64 < n16_per_wave; i += U * 64) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = q[i + u * 64];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u][0] ^ v[u][3];
+  }
+  if (acc == key) sink[0] = acc;
+}
+
+int stream_probe(const void* p, long long nbytes, int grid, unsigned* sink, hipStream_t s) {
+  const long long waves = (long long)grid * 4;
+  const long long per = nbytes / 16 / waves / 512 * 512;  // whole 8 KiB groups per wave
+  if (per <= 0) return -1;
+  stream_probe_kernel<<<grid, 256, 0, s>>>(static_cast<const u32x4*>(p), per, sink, 0x9e3779b9u);
+  JLA_CHECK_LAUNCH();
+  return 0;
+}
+
 // Shader-clock probe (runtime/benchmark.py calibration): every workgroup keeps its SIMDs' matrix pipes busy with
 // dependent MFMA chains for `iters` rounds, the first lane of workgroup 0 reads the shader cycle counter (s_memtime)
 // and the constant 100 MHz counter (s_memrealtime) before and after: cycles / real time = the clock the chip runs at

@@ -144,10 +144,11 @@ def calibration(device) -> Dict[str, object]:
     """Fixed-work probes that tell a slower box from a kernel regression (bench.py ``calibration``):
       * bf16 GEMM TFLOP/s of one fixed 8192^3 shape on this framework's tiled GEMM and on the vendor library
         (torch.mm -> hipBLASLt);
-      * ``stream_read_tbps``: a 2 GiB read-only stream through the repo's own streaming-read kernel (norm_embed.hip
-        prefetch_kernel, 16 loads in flight per lane, 4 workgroups per CU) -- the same kind of traffic as a decode
-        weight stream, so it and the rooflines (weight bytes / 6.29e12) compare like with like; ``copy_tbps`` (a torch
-        copy, read + write bytes) is kept beside it;
+      * ``stream_read_tbps``: a 2 GiB read-only stream through the repo's grid-strided streaming-read kernel
+        (norm_embed.hip prefetch_kernel, 16 loads in flight per lane, 4 workgroups per CU); ``stream_read_seq_tbps``:
+        the same bytes in the decode kernels' pattern (one contiguous range per wave, stream_probe_kernel) -- the box's
+        read roofline, which bench.py divides the streamed bytes by (``hbm_roofline_ms_per_token_box``) beside the fixed
+        6.29 TB/s of the guide's copy measurement; ``copy_tbps`` (a torch copy, read + write bytes) is kept beside them;
       * ``sclk_mhz_mfma_probe``: the shader clock measured in-kernel (cycle counter over the constant 100 MHz counter)
         under a dependent-MFMA loop on constant, low-entropy operands -- an upper bound: a GEMM on random data draws
         more power and the chip gives clock back (gate_up at M = 8192 ran at ~1.65 GHz effective under the profiler,
@@ -201,6 +202,10 @@ def calibration(device) -> Dict[str, object]:
     cus = torch.cuda.get_device_properties(device).multi_processor_count
     ms = timed(lambda: ext_prefetch(e, src, 4 * cus), 5)  # (cus: set above)
     out["stream_read_tbps"] = round(src.numel() * 4 / ms / 1e9, 2)
+    # the decode kernels' own pattern: each wave one contiguous range, 1 KiB per instruction (norm_embed.hip
+    # stream_probe_kernel; 8 workgroups per CU) -- the read rate a decode weight / KV stream can reach on this box
+    ms = timed(lambda: ext_prefetch(e, src, -8 * cus), 5)
+    out["stream_read_seq_tbps"] = round(src.numel() * 4 / ms / 1e9, 2)
     dst = torch.empty_like(src)
     ms = timed(lambda: dst.copy_(src), 5)
     out["copy_tbps"] = round(2 * src.numel() * 4 / ms / 1e9, 2)

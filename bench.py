@@ -111,14 +111,18 @@ def main():
     def step():
         return model.generate(prompts, generation_config=gc).sequences
 
-    for _ in range(args.warmup):
+    progress = _progress if ctx.rank == 0 else (lambda msg: None)
+    t_start = time.perf_counter()
+    for i in range(args.warmup):
         step()
+        progress(f"warmup {i + 1}/{args.warmup} done ({time.perf_counter() - t_start:.1f} s)")
     torch.cuda.synchronize(dev)
     ctx.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         out = step()
+        progress(f"timed step {i + 1}/{args.steps} issued ({time.perf_counter() - t0:.1f} s)")
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     ctx.barrier()
@@ -177,6 +181,7 @@ def main():
     failed = {"any": False}
 
     def extra(key, fn):
+        progress(f"side point {key} ...")
         ok = True
         if failed["any"]:
             res[key] = {"skipped": "an earlier extra point failed on some rank"}
@@ -272,6 +277,12 @@ def _box_rooflines(res):
             d["hbm_roofline_ms_per_token_box"] = round(d["hbm_roofline_ms_per_token"] * 6.29 / tbps, 4)
 
 
+def _progress(msg: str) -> None:
+    """A progress line on stderr (the one JSON result line stays alone on stdout): long phases -- a B = 4096 generate
+    call takes ~24 s, the 70B points minutes -- never look hung to a watchdog on the job's output."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def _emit(res, json_out):
     line = json.dumps(res)
     print(line, flush=True)
@@ -304,9 +315,12 @@ def _tp_rank_proxy(args):
            "hbm_roofline_ms_per_token": round(model.streamed_weight_bytes_per_token() / 6.29e12 * 1e3, 4),
            # qkv, attention, wo, w1|w3, w2 (+ the two all-reduce launches when the row-parallel GEMVs do not fuse them)
            "fused_row_parallel": comm.fused is not None}
+    _progress("tp_rank_proxy: model ready")
     try:
-        out["points"] = [decode_latency(model, b, args.prompt_len, args.gen_len, seed=11)
-                         for b in args.proxy_batches]
+        out["points"] = []
+        for b in args.proxy_batches:
+            out["points"].append(decode_latency(model, b, args.prompt_len, args.gen_len, seed=11))
+            _progress(f"tp_rank_proxy: B = {b} done")
     finally:
         del model
         comm.close()
@@ -326,6 +340,7 @@ def _mp1_point(args):
     cfg = get_preset(args.mp1_model, max_seq_len=max(2048, args.prompt_len + args.gen_len))
     resident_gb = round(torch.cuda.memory_allocated() / 1e9, 2)  # what the earlier points left allocated
     model = LLaMAForCausalLM(cfg, device="cuda", _do_init=False).init_random(seed=77)
+    _progress("mp1_point: model ready")
     try:
         p = decode_latency(model, args.mp1_batch, args.prompt_len, args.gen_len, seed=12)
         return {"model": args.mp1_model, "mp": 1, "weight_gb_per_gpu": round(model.weight_bytes() / 1e9, 3),

@@ -82,20 +82,24 @@ def test_bench_regime_greedy_matches_small_batch(llama3_8b_2l):
 
 
 @pytest.mark.timeout(600)
-def test_headline_regime_b2048_prompt128(llama3_8b_2l):
-    """The exact benchmarked regime (bench.py: B = 2048, 128-token prompts): the M = 262,144-row prefill plans
-    (tile-0 GEMMs, flash prefill) and the B = 2048 decode plans (tuned tiled GEMMs, v4 attention, the fused-argmax
-    lm_head), 32 generated tokens; 8 spread rows against the same rows run at B = 8, both judged by the fp32
-    oracle's teacher-forced argmax gap (reference jax_test.py:427-490, 492-522)."""
+def test_headline_regime_b4096_prompt128(llama3_8b_2l):
+    """The exact benchmarked regime (bench.py: B = 4096, 128-token prompts): the prefill in two row chunks of
+    M = 262,144 rows (tile-0 GEMMs, flash prefill; runtime/engine.py PREFILL_TOKENS) and the B = 4096 decode plans
+    (tuned tiled GEMMs, v4 attention, the fused-argmax lm_head), 32 generated tokens; 8 rows spread over both chunks
+    against the same rows run at B = 8, both judged by the fp32 oracle's teacher-forced argmax gap (reference
+    jax_test.py:427-490, 492-522)."""
+    from jax_llama_amd.runtime import engine
     from jax_llama_amd.runtime.benchmark import synthetic_prompts
     from jax_llama_amd.runtime.engine import GenerationConfig
     cfg, model, oracle = llama3_8b_2l
-    b, s, gen = 2048, 128, 32
+    b, s, gen = 4096, 128, 32
+    assert b * s > engine.PREFILL_TOKENS  # the chunked prefill
     prompts = synthetic_prompts(cfg.vocab_size, b, s, seed=21)
     gc = GenerationConfig(max_length=s + gen, do_sample=False, pad_token_id=0, eos_token_id=-1)
     big = model.generate(prompts, generation_config=gc).sequences.cpu()
+    engine._ENGINES.clear()
     torch.cuda.empty_cache()
-    rows = [0, 1, 255, 256, 1023, 1024, 2000, 2047]
+    rows = [0, 1, 1023, 2047, 2048, 3000, 4000, 4095]
     small = model.generate(prompts[rows], generation_config=gc).sequences.cpu()
     ones = torch.ones(len(rows), s, dtype=torch.int32)
     gap_big = argmax_gap(oracle, big[rows], ones, s)

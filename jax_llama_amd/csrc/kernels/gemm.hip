@@ -1177,7 +1177,7 @@ size_t gemm_workspace_floats(int M, int N, int K) {
 //      for decode shapes with few 256-wide tiles (o / qkv projections) it replaces split-K partial slabs.
 static int tile_cfg(int tile, int M) { return tile >= 1 && tile <= 3 ? tile : (M <= 128 ? 2 : 1); }
 static bool use_g4(int tile, int M, int K);
-// gemm4 on narrower tiles, both with the weights three K-tiles deep (W3; the plain-ring forms, tiles 10 / 15, were
+// gemm4 on narrower tiles, both with the weights three K-tiles deep (W3; the two-slot forms, tiles 10 / 15, were
 // never picked by the tuner at a bench shape and were removed in round 6):
 constexpr int G4N6D_TILE = 16;  // 256 x 192 tiles (g4n_mainloop<6, W3>)
 constexpr int G4ND_TILE = 17;   // 256 x 128 tiles (g4n_mainloop<4, W3>)

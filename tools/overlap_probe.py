@@ -7,7 +7,7 @@ on tile config ``--tiles``, the decode attention (the default dispatch, or ``--a
 and G || A (each order of launch) on two streams; prints one JSON line per (tile, order) with the overlap fraction
 ``(tG + tA - tGA) / min(tG, tA)`` (1 = the shorter one fully hidden, 0 = serialised).
 
-  python tools/overlap_probe.py --tiles 16 17 10 7
+  python tools/overlap_probe.py --tiles 16 17 14 7
 """
 from __future__ import annotations
 
@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--t", type=int, default=384, help="cache slots")
     ap.add_argument("--keys", type=int, default=256)
     ap.add_argument("--op", default="gate_up", choices=["gate_up", "down", "o", "qkv"])
-    ap.add_argument("--tiles", type=int, nargs="+", default=[16, 17, 10, 7])
+    ap.add_argument("--tiles", type=int, nargs="+", default=[16, 17, 14, 7])
     ap.add_argument("--attn-v", type=int, default=0, help="attn_set_v7 mode (0 = default dispatch)")
     ap.add_argument("--diag", action="store_true", help="attention: the stream-only build (no math; wrong results)")
     args = ap.parse_args()

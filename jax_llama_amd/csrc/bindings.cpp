@@ -8,6 +8,7 @@
 
 #include "kernels/launchers.h"
 
+#define MODE_RESIDUAL_ID 1
 #define MODE_QKV_ID 3
 #define MODE_TPRESID_ID 9
 #define MODE_ARGMAX_ID 8  // common.h MODE_ARGMAX
@@ -302,7 +303,9 @@ void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, T
                      Tensor kc, Tensor vc, Tensor slot, int64_t h, int64_t hkv, int64_t dh, Tensor q, Tensor kv_start,
                      Tensor out, c10::optional<Tensor> out_pack, Tensor ws, Tensor tickets, Tensor sync, int64_t t_cap,
                      int64_t splits, c10::optional<Tensor> x_packed, int64_t spl, c10::optional<Tensor> sk_ws,
-                     c10::optional<Tensor> sk_tk) {
+                     c10::optional<Tensor> sk_tk, c10::optional<Tensor> o_w, int64_t o_n, int64_t o_k,
+                     c10::optional<Tensor> o_h, c10::optional<Tensor> o_hb, c10::optional<Tensor> o_hb_pack,
+                     int64_t tp_state) {
   check_gpu(x, "x");
   check_packed(w, n, k);
   check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "linear_qkv_attn: x bf16 [M, K]");
@@ -314,10 +317,11 @@ void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, T
   check(out.scalar_type() == torch::kBFloat16 && out.numel() == m * h * dh, "out bf16 [B, H * Dh]");
   check(ws.scalar_type() == torch::kFloat32 && ws.numel() >= m * hkv * splits * (h / hkv) * (dh + 4), "ws too small");
   check(tickets.scalar_type() == torch::kInt32 && tickets.numel() >= m * hkv, "tickets int32 [pairs]");
-  check(sync.scalar_type() == torch::kInt32 && sync.numel() >= 3, "sync int32 [3]");
+  check(sync.scalar_type() == torch::kInt32 && (size_t)sync.numel() >= jla::qkv_attn_sync_ints(),
+        "sync int32 [qkv_attn_sync_ints()]");
   check(t_cap <= kc.size(2), "t_cap <= cache length");
   const jla::bf16_t* xp = packed_ptr(x_packed, m, k, "x_packed");
-  check(spl == 1 || spl == 2, "linear_qkv_attn: spl 1 or 2");
+  check(spl >= 1 && spl <= 4 && (spl <= 2 || m <= 16), "linear_qkv_attn: spl 1..4 (3 / 4 at M <= 16)");
   if (spl > 1) {  // the split qkv GEMV's slabs + tickets (skinny_workspace)
     check(sk_ws.has_value() && sk_tk.has_value(), "linear_qkv_attn spl 2: sk_ws and sk_tk (skinny_workspace)");
     check_gpu(*sk_ws, "sk_ws");
@@ -329,9 +333,37 @@ void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, T
     qa.sk_tk = ptr<int32_t>(*sk_tk);
     qa.sk_ws_floats = (int)sk_ws->numel();
   }
+  // the fused o projection (o_w): h += out @ Wo^T with the residual epilogue (tp_state 0) or the TP exchange
+  jla::QKVArgs qo{};
+  float* oh = nullptr;
+  int o_mode = 0;
+  if (o_w.has_value()) {
+    check_packed(*o_w, o_n, o_k);
+    check(o_k == h * dh, "linear_qkv_attn: Wo has H * Dh input columns");
+    check(o_h.has_value() && o_hb.has_value(), "linear_qkv_attn: the fused o projection needs h and hb");
+    check_gpu(*o_h, "h");
+    check_gpu(*o_hb, "hb");
+    check(o_h->scalar_type() == torch::kFloat32 && o_h->numel() == m * o_n && o_hb->scalar_type() == torch::kBFloat16 &&
+              o_hb->numel() == m * o_n, "linear_qkv_attn: h fp32 / hb bf16 [M, N_o]");
+    const int og = jla::qkv_attn_o_groups((int)m, (int)(h / hkv), (int)o_n, (int)o_k);
+    check(og > 0, "linear_qkv_attn: the o projection cannot be fused at this shape (qkv_attn_o_groups)");
+    oh = ptr<float>(*o_h);
+    qo.res_bf16 = bf(*o_hb);
+    qo.pack = packed_ptr(o_hb_pack, m, o_n, "o_hb_pack");
+    o_mode = MODE_RESIDUAL_ID;
+    if (tp_state) {
+      void* st = reinterpret_cast<void*>(tp_state);
+      check(og <= jla::CAR_WG_COUNTERS && og * jla::TPRES_REGION <= jla::car_max_bytes(st),
+            "linear_qkv_attn: too many o workgroups for the TP buffer");
+      qo.tp = jla::car_device(st);
+      o_mode = MODE_TPRESID_ID;
+    }
+  }
   rc(jla::linear_qkv_attn(xp ? xp : cbf(x), w.data_ptr(), m, n, k, (float)rms_eps, qa, xp != nullptr, bf(out),
                           packed_ptr(out_pack, m, h * dh, "out_pack"), ptr<int32_t>(kv_start), ptr<float>(ws),
-                          ptr<int32_t>(tickets), ptr<int32_t>(sync), (int)t_cap, (int)splits, (int)spl, stream()),
+                          ptr<int32_t>(tickets), ptr<int32_t>(sync), (int)t_cap, (int)splits, (int)spl, stream(),
+                          o_w.has_value() ? o_w->data_ptr() : nullptr, oh, (int)o_n, (int)o_k, o_mode,
+                          o_w.has_value() ? &qo : nullptr),
      "linear_qkv_attn");
 }
 
@@ -773,16 +805,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
         py::arg("h"), py::arg("hkv"), py::arg("dh"), py::arg("q"), py::arg("kv_start"), py::arg("out"),
         py::arg("out_pack"), py::arg("ws"), py::arg("tickets"), py::arg("sync"), py::arg("t_cap"), py::arg("splits"),
         py::arg("x_packed") = py::none(), py::arg("spl") = 1, py::arg("sk_ws") = py::none(),
-        py::arg("sk_tk") = py::none());
+        py::arg("sk_tk") = py::none(), py::arg("o_w") = py::none(), py::arg("o_n") = 0, py::arg("o_k") = 0,
+        py::arg("o_h") = py::none(), py::arg("o_hb") = py::none(), py::arg("o_hb_pack") = py::none(),
+        py::arg("tp_state") = 0);
   m.def("qkv_attn_splits", [](int64_t m, int64_t b, int64_t hkv, int64_t rep, int64_t t_cap, int64_t n, int64_t cus,
-                              int64_t spl) {
-    return jla::qkv_attn_splits((int)m, (int)b, (int)hkv, (int)rep, (int)t_cap, (int)n, (int)cus, (int)spl);
+                              int64_t spl, int64_t o_groups) {
+    return jla::qkv_attn_splits((int)m, (int)b, (int)hkv, (int)rep, (int)t_cap, (int)n, (int)cus, (int)spl,
+                                (int)o_groups);
   }, py::arg("m"), py::arg("b"), py::arg("hkv"), py::arg("rep"), py::arg("t_cap"), py::arg("n"), py::arg("cus"),
-     py::arg("spl") = 1);
+     py::arg("spl") = 1, py::arg("o_groups") = 0);
+  m.def("qkv_attn_o_groups", [](int64_t m, int64_t rep, int64_t n, int64_t k) {
+    return jla::qkv_attn_o_groups((int)m, (int)rep, (int)n, (int)k);
+  });
+  m.def("qkv_attn_sync_ints", []() { return (int64_t)jla::qkv_attn_sync_ints(); });
+  m.def("qkv_attn_set_o_nt", [](int64_t nt) { jla::qkv_attn_set_o_nt((int)nt); });
   m.def("qkv_attn_set_diag", [](int64_t d) { jla::qkv_attn_set_diag((int)d); });
-  m.def("qkv_attn_occupancy", [](int64_t m, int64_t rep, int64_t spl) {
-    return jla::qkv_attn_occupancy((int)m, (int)rep, (int)spl);
-  }, py::arg("m"), py::arg("rep"), py::arg("spl") = 1);
+  m.def("qkv_attn_set_stamps", [](c10::optional<Tensor> t) {  // int64 [>= grid * 8]; None: off (keep t alive)
+    if (t.has_value()) {
+      check_gpu(*t, "stamps");
+      check(t->scalar_type() == torch::kInt64, "stamps int64");
+    }
+    jla::qkv_attn_set_stamps(t.has_value() ? reinterpret_cast<unsigned long long*>(t->data_ptr()) : nullptr);
+  });
+  m.def("qkv_attn_occupancy", [](int64_t m, int64_t rep, int64_t spl, int64_t o_groups) {
+    return jla::qkv_attn_occupancy((int)m, (int)rep, (int)spl, (int)o_groups);
+  }, py::arg("m"), py::arg("rep"), py::arg("spl") = 1, py::arg("o_groups") = 0);
   m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);

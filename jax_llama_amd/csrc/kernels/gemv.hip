@@ -39,113 +39,39 @@ JLA_DEV void st_sc1_b16(bf16_t* p, bf16_t v) {
   asm volatile("global_store_short %0, %1, off sc1" ::"v"(p), "v"((unsigned)v) : "memory");
 }
 
-// The GEMV body of one workgroup (bx: column group, by / gy: K split index / count), shared by linear_skinny_kernel
-// and the fused qkv + attention launch. SC1: the QKV epilogue's q / cache stores are write-through (sc1), for the
-// attention workgroups of the same launch.
-template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false, bool SC1 = false>
-JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
-                         int K, float eps, int use_rms, int accumulate, int out_f32, const QKVArgs& qa, int bx, int by,
-                         int gy) {
+// The epilogue of one skinny workgroup: the cross-wave reduction of its accumulators (and RMS row sums) through LDS,
+// then the MODE's fused output. Shared by skinny_body and the o-projection workgroups of the fused decode launch.
+template <int MT, int NT, int MODE, int NW, bool SPLIT, bool SC1>
+JLA_DEV void skinny_epilogue(const f32x4 (&acc)[MT][NT], const float (&ss)[MT], int tp_calls, void* __restrict__ out,
+                             int M, int N, int K, float eps, int use_rms, int accumulate, int out_f32,
+                             const QKVArgs& qa, int bx, int by, int gy) {
   extern __shared__ float smem[];
   float* red = smem;                              // [NW][MT][NT][64][4]
   float* red_ss = red + NW * MT * NT * 256;       // [NW][MT][16]
   float* inv_rms = red_ss + NW * MT * 16;         // [MT*16]
-
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
-  const int KS = K >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NTT = N >> 4;
   const int nt0 = bx * NT;
-  // SPLIT: K is cut over gy workgroups per column group; this one streams k-steps [kb, kb + kn)
-  int kb = 0, kn = KS;
-  if constexpr (SPLIT) {
-    kb = (int)((long long)KS * by / gy);
-    kn = (int)((long long)KS * (by + 1) / gy) - kb;
-  }
-
-  const u32x4* wt[NT];
+  // the residual values this thread's epilogue elements add to, loaded now: the load's round trip hides behind the
+  // LDS reduction (and, with the TP exchange, behind its granule round trips) instead of following them
+  constexpr int EPT = (MT * NT * 256 + NW * 64 - 1) / (NW * 64);  // epilogue elements per thread
+  float hpre[EPT];     // MODE_RESIDUAL: h at (m, col)
+  float2 hpre2[EPT];   // MODE_TPRESID: h at (m, col .. col + 1), even columns
+  if constexpr (MODE == MODE_RESIDUAL || MODE == MODE_TPRESID) {
+    const float* h = static_cast<const float*>(out);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) wt[t] = W + ((size_t)min(nt0 + t, NTT - 1) * KS + kb) * 64 + lane;
-  const XT* xp[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int row = min(mt * 16 + (lane & 15), M - 1);  // padding rows re-read the last row (not stored)
-    // XP: activations pre-packed as MFMA A fragments [MT][KS][64 lanes][8] (1 KiB contiguous per k-step,
-    // like the weights) instead of row-major (16 rows x 64 B = 16 half-used cache lines per fragment)
-    xp[mt] = XP ? x + (((size_t)mt * KS + kb) * 64 + lane) * 8 : x + (size_t)row * K + (size_t)kb * 32 + 8 * (lane >> 4);
-  }
-  const u32x4* zfrag = g_zero_frag + lane;
-  const XT* zx = reinterpret_cast<const XT*>(g_zero_frag);
-  // MODE_TPRESID: this workgroup's call counter (parity + granule tag), read now so the uncached round trip hides
-  // behind the weight stream
-  int tp_calls = 0;
-  if constexpr (MODE == MODE_TPRESID) {
-    if (threadIdx.x == 0)
-      tp_calls = __hip_atomic_load(static_cast<const CarDevice*>(qa.tp)->wg_ctr + bx, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-  }
-
-  const int n = (kn - w + NW - 1) / NW;  // k-steps of this wave: ks = kb + w + i*NW, i < n
-
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ss[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
-
-  u32x4 bq[U][NT] = {};
-  XRaw<XT> aq[U][MT] = {};
-  constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
-  // hand-counted ring (see asm_load_nt) where the assembly check passes: every bf16-activation
-  // variant (the decode path: the residual stream's bf16 mirror) up to 8 waves, single or doubled ring,
-  // and fp32 at MT = 1
-  constexpr int U_BASE = ((NT == 1 ? 8 : 4) / MT) < 2 ? 2 : ((NT == 1 ? 8 : 4) / MT);
-  constexpr bool ASM = (MT == 1 || sizeof(XT) == 2) && NW <= 8 && U <= 2 * U_BASE;
-  auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
-    const bool valid = i < n;
-    const size_t ks = (size_t)(w + i * NW);
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      asm_load_nt<ASM>(b[t], valid ? (const void*)(wt[t] + ks * 64) : (const void*)zfrag);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) a[mt].template load<ASM>(valid ? xp[mt] + ks * (XP ? 512 : 32) : zx);
-  };
-  // No separate prologue: the first trip computes on the zero-initialised slots (MFMA adds 0) while
-  // issuing k-steps 0..U-1, so every ring register has exactly one definition site (the tied
-  // refill) and the compiler never needs to copy an in-flight register across the loop entry.
-  for (int i0 = -U; i0 < n; i0 += U) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (ASM) {
-        wait_vmcnt<L * (U - 1)>();  // slot u (the oldest L loads) has landed
-#pragma unroll
-        for (int t = 0; t < NT; ++t) pin(bq[u][t]);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+    for (int j = 0; j < EPT; ++j) {
+      const int e = threadIdx.x + j * NW * 64;
+      const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
+      const int m = mt * 16 + ml;
+      const bool ok = e < MT * NT * 256 && m < M && nt0 + t < NTT;
+      const size_t idx = (size_t)m * N + (nt0 + t) * 16 + c;
+      if constexpr (MODE == MODE_RESIDUAL) {
+        hpre[j] = ok && accumulate ? h[idx] : 0.f;
+      } else {
+        hpre2[j] = ok && !(c & 1) ? *reinterpret_cast<const float2*>(h + idx) : make_float2(0.f, 0.f);
       }
-      u32x4 af[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) af[mt] = aq[u][mt].frag(ss[mt]);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(af[mt], bq[u][t], acc[mt][t]);
-      issue(i0 + U + u, bq[u], aq[u]);  // refill: k-step U ahead (zero fragment past the end)
-    }
-  }
-  if constexpr (ASM) {
-    // retire the past-the-end refills, and keep every ring register live until then: a register
-    // the compiler thinks is dead could otherwise be reused while its load is still in flight
-    wait_vmcnt<0>();
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) pin(bq[u][t]);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
     }
   }
 
@@ -280,10 +206,12 @@ JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, 
       for (int p = 0; p < d.world; ++p) st_sys8(rsrc(d.buf[p]), par_base + (long long)d.rank * d.max_bytes + g, gv);
     }
     const bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-    for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = threadIdx.x + j * NW * 64;
       const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
       const int m = mt * 16 + ml;
-      if ((c & 1) || m >= M || nt0 + t >= NTT) continue;
+      if (e >= MT * NT * 256 || (c & 1) || m >= M || nt0 + t >= NTT) continue;
       const long long g = wg_base + ((long long)m * (NT * 16) + t * 16 + c) * 4;
       float s0 = 0.f, s1 = 0.f;
       for (int p = 0; p < d.world; ++p) {
@@ -307,8 +235,7 @@ JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, 
       }
       const int col = (nt0 + t) * 16 + c;
       const size_t idx = (size_t)m * N + col;
-      const float2 hv = *reinterpret_cast<const float2*>(h + idx);
-      const float n0 = hv.x + s0, n1 = hv.y + s1;
+      const float n0 = hpre2[j].x + s0, n1 = hpre2[j].y + s1;
       *reinterpret_cast<float2*>(h + idx) = make_float2(n0, n1);
       const uint32_t pk = pack2bf(n0, n1);
       if (qa.res_bf16) *reinterpret_cast<uint32_t*>(qa.res_bf16 + idx) = pk;
@@ -317,7 +244,10 @@ JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, 
     if (threadIdx.x == 0)
       __hip_atomic_store(d.wg_ctr + bx, calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    for (int e = threadIdx.x; e < MT * NT * 256; e += NW * 64) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = threadIdx.x + j * NW * 64;
+      if (e >= MT * NT * 256) break;
       const int c = e & 15, ml = (e >> 4) & 15, t = (e >> 8) % NT, mt = e / (256 * NT);
       const int m = mt * 16 + ml;
       const int ln = (ml >> 2) * 16 + c, i = ml & 3;
@@ -379,7 +309,7 @@ JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, 
         const size_t idx = (size_t)m * N + col;
         if constexpr (MODE == MODE_RESIDUAL) {
           float* o = static_cast<float*>(out);
-          const float nv = accumulate ? o[idx] + v : v;
+          const float nv = accumulate ? hpre[j] + v : v;
           o[idx] = nv;
           if (qa.res_bf16) qa.res_bf16[idx] = f2bf(nv);
           if (qa.pack) qa.pack[pack_off(m, col, N)] = f2bf(nv);
@@ -392,6 +322,115 @@ JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, 
       }
     }
   }
+}
+
+// The GEMV body of one workgroup (bx: column group, by / gy: K split index / count), shared by linear_skinny_kernel
+// and the fused qkv + attention launch. SC1: the QKV epilogue's q / cache stores are write-through (sc1), for the
+// attention workgroups of the same launch.
+template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false, bool SC1 = false>
+JLA_DEV void skinny_body(const XT* __restrict__ x, const u32x4* __restrict__ W, void* __restrict__ out, int M, int N,
+                         int K, float eps, int use_rms, int accumulate, int out_f32, const QKVArgs& qa, int bx, int by,
+                         int gy) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
+  const int KS = K >> 5;
+  const int NTT = N >> 4;
+  const int nt0 = bx * NT;
+  // SPLIT: K is cut over gy workgroups per column group; this one streams k-steps [kb, kb + kn)
+  int kb = 0, kn = KS;
+  if constexpr (SPLIT) {
+    kb = (int)((long long)KS * by / gy);
+    kn = (int)((long long)KS * (by + 1) / gy) - kb;
+  }
+
+  const u32x4* wt[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) wt[t] = W + ((size_t)min(nt0 + t, NTT - 1) * KS + kb) * 64 + lane;
+  const XT* xp[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int row = min(mt * 16 + (lane & 15), M - 1);  // padding rows re-read the last row (not stored)
+    // XP: activations pre-packed as MFMA A fragments [MT][KS][64 lanes][8] (1 KiB contiguous per k-step,
+    // like the weights) instead of row-major (16 rows x 64 B = 16 half-used cache lines per fragment)
+    xp[mt] = XP ? x + (((size_t)mt * KS + kb) * 64 + lane) * 8 : x + (size_t)row * K + (size_t)kb * 32 + 8 * (lane >> 4);
+  }
+  const u32x4* zfrag = g_zero_frag + lane;
+  const XT* zx = reinterpret_cast<const XT*>(g_zero_frag);
+  // MODE_TPRESID: this workgroup's call counter (parity + granule tag), read now so the uncached round trip hides
+  // behind the weight stream
+  int tp_calls = 0;
+  if constexpr (MODE == MODE_TPRESID) {
+    if (threadIdx.x == 0)
+      tp_calls = __hip_atomic_load(static_cast<const CarDevice*>(qa.tp)->wg_ctr + bx, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  const int n = (kn - w + NW - 1) / NW;  // k-steps of this wave: ks = kb + w + i*NW, i < n
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ss[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ss[mt] = 0.f;
+
+  u32x4 bq[U][NT] = {};
+  XRaw<XT> aq[U][MT] = {};
+  constexpr int L = NT + MT * XRaw<XT>::LOADS;  // loads per ring slot
+  // hand-counted ring (see asm_load_nt) where the assembly check passes: every bf16-activation
+  // variant (the decode path: the residual stream's bf16 mirror) up to 8 waves, single or doubled ring,
+  // and fp32 at MT = 1
+  constexpr int U_BASE = ((NT == 1 ? 8 : 4) / MT) < 2 ? 2 : ((NT == 1 ? 8 : 4) / MT);
+  constexpr bool ASM = (MT == 1 || sizeof(XT) == 2) && NW <= 8 && U <= 2 * U_BASE;
+  auto issue = [&](int i, u32x4* b, XRaw<XT>* a) {
+    const bool valid = i < n;
+    const size_t ks = (size_t)(w + i * NW);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      asm_load_nt<ASM>(b[t], valid ? (const void*)(wt[t] + ks * 64) : (const void*)zfrag);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) a[mt].template load<ASM>(valid ? xp[mt] + ks * (XP ? 512 : 32) : zx);
+  };
+  // No separate prologue: the first trip computes on the zero-initialised slots (MFMA adds 0) while
+  // issuing k-steps 0..U-1, so every ring register has exactly one definition site (the tied
+  // refill) and the compiler never needs to copy an in-flight register across the loop entry.
+  for (int i0 = -U; i0 < n; i0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (ASM) {
+        wait_vmcnt<L * (U - 1)>();  // slot u (the oldest L loads) has landed
+#pragma unroll
+        for (int t = 0; t < NT; ++t) pin(bq[u][t]);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+      }
+      u32x4 af[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) af[mt] = aq[u][mt].frag(ss[mt]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[mt][t] = mfma16x16x32(af[mt], bq[u][t], acc[mt][t]);
+      issue(i0 + U + u, bq[u], aq[u]);  // refill: k-step U ahead (zero fragment past the end)
+    }
+  }
+  if constexpr (ASM) {
+    // retire the past-the-end refills, and keep every ring register live until then: a register
+    // the compiler thinks is dead could otherwise be reused while its load is still in flight
+    wait_vmcnt<0>();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) pin(bq[u][t]);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) aq[u][mt].pin_regs();
+    }
+  }
+
+  skinny_epilogue<MT, NT, MODE, NW, SPLIT, SC1>(acc, ss, tp_calls, out, M, N, K, eps, use_rms, accumulate, out_f32, qa,
+                                               bx, by, gy);
 }
 
 template <typename XT, int MT, int NT, int MODE, int NW, int U, bool XP = false, bool SPLIT = false>
@@ -557,32 +596,44 @@ struct FusedAttn {
   const int32_t* kv_start;  // [B]
   float* ws;                // [pairs][splits][REP][QA_PART] write-through partials
   int32_t* tickets;         // [pairs] merge tickets (self-resetting)
-  int32_t* sync;            // [0] qkv-done counter, [1] attention-seen counter (both self-resetting), [2] error word
+  int32_t* sync;            // [0] qkv-done counter, [1] attention-seen counter (both self-resetting), [2] error word,
+                            // [3] attention-done counter (self-resetting), [QO_GO + QO_GO_STRIDE * ob] the go flag of
+                            // o workgroup ob (fused o projection; each cleared by its workgroup)
   int splits, grid_q, t_cap;
   float scale_log2;
   int diag;                 // tools / tests only (qkv_attn_set_diag): 1 = the qkv workgroups never publish
+  int grid_a, grid_o;       // attention workgroups (pairs x splits); o-projection workgroups (0: no fused o)
+  unsigned long long* stamps;  // tools only (qkv_attn_set_stamps): [grid][8] phase timestamps (wall clock, 100 MHz)
 };
+// phase timestamp i of this workgroup (tools/qkv_attn_timeline.py); a no-op unless a stamp buffer is set
+JLA_DEV void qa_stamp(const FusedAttn& fa, int i) {
+  if (fa.stamps && threadIdx.x == 0) fa.stamps[(size_t)blockIdx.x * 8 + i] = wall_clock64();
+}
+// The fused o projection (FO > 0): the last grid_o workgroups of the launch compute h += attn_out @ Wo^T (FO 16-column
+// tiles each, K <= 32 x 4 waves x QO_PF) with the standalone GEMV's residual (or TP-exchange, MODE_TPRESID) epilogue.
+struct FusedO {
+  const u32x4* W;  // packed Wo [N / 16][K / 32][64 lanes] u32x4
+  float* h;        // fp32 residual [M, N]
+  int N, K;
+};
+constexpr int QO_PF = 8;  // k-steps per wave held in registers (o weights fetched while qkv / attention run)
+// one go flag per o workgroup, a cache line apart: the workgroups poll their own lines (256 pollers of one counter made
+// that line's memory channel a hotspot the whole launch queued behind: the fused o measured 1.1 ms per token slower)
+constexpr int QO_GO = 64, QO_GO_STRIDE = 16, QO_MAX_GROUPS = 1024;
 
-// SPL: K of the qkv GEMV cut over SPL workgroups per column group (the split GEMV's last-arriver sum; only that
-// workgroup writes q / the cache rows, but every qkv workgroup counts itself in the publish below)
-template <int MT, int NT, int NW, int U, bool XP, int REP, int SPL>
-__global__ void __launch_bounds__(256)
-    qkv_attn_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, int M, int N, int K, float eps,
-                    int use_rms, QKVArgs qa, FusedAttn fa) {
-  static_assert(NW == 4, "4-wave workgroups (the attention side uses 4 waves x 32 keys)");
-  if ((int)blockIdx.x < fa.grid_q) {
-    skinny_body<bf16_t, MT, NT, MODE_QKV, NW, U, XP, (SPL > 1), true>(x, W, nullptr, M, N, K, eps, use_rms, 0, 0, qa,
-                                                                      (int)blockIdx.x / SPL, (int)blockIdx.x % SPL,
-                                                                      SPL);
-    // publish (Guideline 16, sc1-store + agent-counter form): every storing wave drains its write-through stores,
-    // the workgroup's barrier, then one agent-scope add
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0 && !fa.diag) __hip_atomic_fetch_add(fa.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
+// 16-byte store of the attention output: write-through (sc1) when the o projection of the same launch reads it
+template <bool SC1>
+JLA_DEV void qa_store16(bf16_t* p, u32x4 v) {
+  if constexpr (SC1)
+    st_sc1_x4(p, v);
+  else
+    *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// The attention workgroups of the fused launch (workgroup a of pairs x splits). SCO: output stores write-through.
+template <int REP, bool SCO>
+JLA_DEV void qa_attention(const QKVArgs& qa, const FusedAttn& fa, int a) {
   extern __shared__ __attribute__((aligned(16))) char ldsq[];
-  const int a = blockIdx.x - fa.grid_q;
   const int pair = a / fa.splits, sp = a - pair * fa.splits;
   const int b = pair / qa.Hkv, kvh = pair - b * qa.Hkv;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -605,7 +656,7 @@ __global__ void __launch_bounds__(256)
   // 2. wait until every qkv workgroup has published (one polling lane, bounded). A timeout is sticky: the error word
   //    stays set (the host raises at its next poll: ops.check_inlaunch), the counters are never reset again (a late
   //    publish would leave them off by its count), and every later launch's attention workgroups skip the wait and
-  //    write nothing -- no token is ever computed from a stale q / K / V without the error word saying so.
+  //    write zeros -- no token is ever computed from a stale q / K / V without the error word saying so.
   int* flag = reinterpret_cast<int*>(ldsq + 4 * AD6_SLOT_BYTES + 1008);
   if (threadIdx.x == 0) {
     int err = __hip_atomic_load(fa.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -622,7 +673,7 @@ __global__ void __launch_bounds__(256)
     // of this launch (or an earlier one) timed out: the acq_rel add orders a timed-out workgroup's error store before
     // its arrival, and the last arriver's error load after every arrival
     const int seen = __hip_atomic_fetch_add(fa.sync + 1, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (seen == (int)gridDim.x - fa.grid_q - 1 &&
+    if (seen == fa.grid_a - 1 &&
         __hip_atomic_load(fa.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       __hip_atomic_store(fa.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(fa.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -630,19 +681,27 @@ __global__ void __launch_bounds__(256)
     *flag = err;
   }
   __syncthreads();
+  qa_stamp(fa, 1);
   // the prefetch landed during the qkv phase: retire it here, before any branch (hipcc must never copy a ring
   // register that is still in flight)
   ::wait_vmcnt<0>();
 #pragma unroll
   for (int i = 0; i < 8; ++i) pin(kr[i]);
-  if (*flag) return;  // failed state (timeout now or earlier): the output is not written
+  if (*flag) {  // failed state (timeout now or earlier): the pair's output is zeros (the host raises at its next poll)
+    if (sp == 0 && threadIdx.x < REP * 16) {
+      const int col = (kvh * REP + (threadIdx.x >> 4)) * AD6_DH + 8 * (threadIdx.x & 15);
+      qa_store16<SCO>(fa.out + (size_t)b * qa.H * AD6_DH + col, u32x4{0u, 0u, 0u, 0u});
+      if (fa.out_pack) qa_store16<SCO>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH), u32x4{0u, 0u, 0u, 0u});
+    }
+    return;
+  }
   const int split_lo = sp * QA_SPLIT_KEYS;
   const bool split_live = split_lo < hi && split_lo + QA_SPLIT_KEYS > lo;
   if (!split_live) {
     if (sp == 0 && lo >= hi && threadIdx.x < REP * 16) {  // a row with no valid key: zeros (as the other kernels)
       const int col = (kvh * REP + (threadIdx.x >> 4)) * AD6_DH + 8 * (threadIdx.x & 15);
-      *reinterpret_cast<u32x4*>(fa.out + (size_t)b * qa.H * AD6_DH + col) = u32x4{0u, 0u, 0u, 0u};
-      if (fa.out_pack) *reinterpret_cast<u32x4*>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH)) = u32x4{0u, 0u, 0u, 0u};
+      qa_store16<SCO>(fa.out + (size_t)b * qa.H * AD6_DH + col, u32x4{0u, 0u, 0u, 0u});
+      if (fa.out_pack) qa_store16<SCO>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH), u32x4{0u, 0u, 0u, 0u});
     }
     return;
   }
@@ -686,6 +745,7 @@ __global__ void __launch_bounds__(256)
 
   // 5. the 4 waves through LDS (the V slots are free once every wave is past its step)
   __syncthreads();
+  qa_stamp(fa, 2);
   float* sm_o = reinterpret_cast<float*>(ldsq);  // [4][REP][128]
   float* sm_ml = sm_o + 4 * REP * AD6_DH;        // [4][REP][2]
   {
@@ -730,8 +790,8 @@ __global__ void __launch_bounds__(256)
     for (int e = 0; e < 8; ++e) r[e] = o8[e] * inv;
     const u32x4 v = pack8(r);
     const int col = (kvh * REP + h) * AD6_DH + d0;
-    *reinterpret_cast<u32x4*>(fa.out + (size_t)b * qa.H * AD6_DH + col) = v;
-    if (fa.out_pack) *reinterpret_cast<u32x4*>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH)) = v;
+    qa_store16<SCO>(fa.out + (size_t)b * qa.H * AD6_DH + col, v);
+    if (fa.out_pack) qa_store16<SCO>(fa.out_pack + pack_off(b, col, qa.H * AD6_DH), v);
   };
   if (nlive <= 1) {  // the pair's only live split: no merge
     if (chunk) write_out(num, L);
@@ -793,25 +853,160 @@ __global__ void __launch_bounds__(256)
   write_out(o8, den);
 }
 
+// The o-projection workgroups of the fused launch (workgroup ob of grid_o; NTO 16-column tiles, MODE_RESIDUAL or
+// MODE_TPRESID): each wave issues its QO_PF k-steps of weights (k-steps w, w + 4, ...) at once, so the weight stream
+// lands while the qkv and attention workgroups run; one lane polls the attention-done counter (bounded, as the
+// attention side's wait); the waves load the attention output agent-coherently (this launch wrote it write-through),
+// multiply, and run the standalone GEMV's epilogue (skinny_epilogue: LDS reduction, residual + mirrors, or the TP
+// granule exchange with the peers' workgroup ob).
+template <int NTO, int OMODE>
+JLA_DEV void qa_o_proj(const FusedAttn& fa, const FusedO& fo, const QKVArgs& qo, int M, int ob) {
+  extern __shared__ __attribute__((aligned(16))) char ldsq[];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int KS = fo.K >> 5, NTT = fo.N >> 4, nt0 = ob * NTO;
+  int tp_calls = 0;
+  if constexpr (OMODE == MODE_TPRESID) {
+    if (threadIdx.x == 0)
+      tp_calls = __hip_atomic_load(static_cast<const CarDevice*>(qo.tp)->wg_ctr + ob, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const u32x4* zfrag = g_zero_frag + lane;
+  u32x4 bw[QO_PF][NTO];
+#pragma unroll
+  for (int i = 0; i < QO_PF; ++i) {
+    const int ks = w + 4 * i;
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) {
+      bw[i][t] = u32x4{0u, 0u, 0u, 0u};
+      asm_load_nt<true>(bw[i][t], ks < KS ? (const void*)(fo.W + ((size_t)min(nt0 + t, NTT - 1) * KS + ks) * 64 + lane)
+                                          : (const void*)zfrag);
+    }
+  }
+  int* flag = reinterpret_cast<int*>(ldsq + 4 * AD6_SLOT_BYTES + 1008);
+  if (threadIdx.x == 0) {
+    // this workgroup's go flag (set by the last attention workgroup to finish), bounded; cleared for the next launch.
+    // A timeout (or an attention-side one: the error word) is sticky: h is not updated now or in any later launch.
+    int* go = fa.sync + QO_GO + QO_GO_STRIDE * ob;
+    int err = 0;
+    const long long t0 = (long long)wall_clock64();
+    while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if ((long long)wall_clock64() - t0 > 20000000LL) {  // 0.2 s
+        __hip_atomic_store(fa.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        err = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!err) __hip_atomic_store(go, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = err || __hip_atomic_load(fa.sync + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  }
+  __syncthreads();
+  qa_stamp(fa, 1);
+  ::wait_vmcnt<0>();  // the weights (retired before any branch: no in-flight register is ever copied)
+#pragma unroll
+  for (int i = 0; i < QO_PF; ++i)
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) pin(bw[i][t]);
+  if (*flag) return;  // failed state: h is not updated (the host raises at its next poll)
+  // the attention output, row-major [M, K]: padding rows re-read the last row (not stored)
+  const bf16_t* xr = fa.out + (size_t)min(lane & 15, M - 1) * fo.K + 8 * (lane >> 4);
+  u32x4 xa[QO_PF];
+#pragma unroll
+  for (int i = 0; i < QO_PF; ++i) {
+    const int ks = w + 4 * i;
+    xa[i] = u32x4{0u, 0u, 0u, 0u};
+    asm_load_sc1(xa[i], ks < KS ? (const void*)(xr + (size_t)ks * 32) : (const void*)zfrag);
+  }
+  ::wait_vmcnt<0>();
+  f32x4 acc[1][NTO];
+#pragma unroll
+  for (int t = 0; t < NTO; ++t) acc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < QO_PF; ++i) {
+    pin(xa[i]);
+#pragma unroll
+    for (int t = 0; t < NTO; ++t) acc[0][t] = mfma16x16x32(xa[i], bw[i][t], acc[0][t]);
+  }
+  const float ss[1] = {0.f};
+  qa_stamp(fa, 2);
+  skinny_epilogue<1, NTO, OMODE, 4, false, false>(acc, ss, tp_calls, fo.h, M, fo.N, fo.K, 0.f, 0, 1, 1, qo, ob, 0, 1);
+}
+
+// SPL: K of the qkv GEMV cut over SPL workgroups per column group (the split GEMV's last-arriver sum; only that
+// workgroup writes q / the cache rows, but every qkv workgroup counts itself in the publish below).
+// FO > 0: the launch also runs the o projection (qa_o_proj, FO tiles per workgroup, epilogue OMODE) on its last
+// fa.grid_o workgroups; the attention workgroups then store their output write-through and count themselves done.
+template <int MT, int NT, int NW, int U, bool XP, int REP, int SPL, int FO, int OMODE>
+__global__ void __launch_bounds__(256)
+    qkv_attn_kernel(const bf16_t* __restrict__ x, const u32x4* __restrict__ W, int M, int N, int K, float eps,
+                    int use_rms, QKVArgs qa, FusedAttn fa, FusedO fo, QKVArgs qo) {
+  static_assert(NW == 4, "4-wave workgroups (the attention side uses 4 waves x 32 keys)");
+  qa_stamp(fa, 0);
+  if ((int)blockIdx.x < fa.grid_q) {
+    skinny_body<bf16_t, MT, NT, MODE_QKV, NW, U, XP, (SPL > 1), true>(x, W, nullptr, M, N, K, eps, use_rms, 0, 0, qa,
+                                                                      (int)blockIdx.x / SPL, (int)blockIdx.x % SPL,
+                                                                      SPL);
+    qa_stamp(fa, 1);
+    // publish (Guideline 16, sc1-store + agent-counter form): every storing wave drains its write-through stores,
+    // the workgroup's barrier, then one agent-scope add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && !fa.diag) __hip_atomic_fetch_add(fa.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qa_stamp(fa, 2);
+    return;
+  }
+  if constexpr (FO > 0) {
+    static_assert(MT == 1, "fused o projection: M <= 16");
+    const int ob = (int)blockIdx.x - fa.grid_q - fa.grid_a;
+    if (ob >= 0) {
+      qa_o_proj<FO, OMODE>(fa, fo, qo, M, ob);
+      qa_stamp(fa, 3);
+      return;
+    }
+  }
+  qa_attention<REP, (FO > 0)>(qa, fa, (int)blockIdx.x - fa.grid_q);
+  qa_stamp(fa, 3);
+  if constexpr (FO > 0) {
+    // done (same publish form): every path out of qa_attention, stores drained, then one add per workgroup; the last
+    // one to finish resets the counter and sets every o workgroup's go flag (one store per thread)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    extern __shared__ __attribute__((aligned(16))) char ldsq[];
+    int* last = reinterpret_cast<int*>(ldsq + 4 * AD6_SLOT_BYTES + 1012);
+    if (threadIdx.x == 0) {
+      const int prev = __hip_atomic_fetch_add(fa.sync + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last = prev == fa.grid_a - 1;
+      if (*last) __hip_atomic_store(fa.sync + 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (*last)
+      for (int i = threadIdx.x; i < fa.grid_o; i += 256)
+        __hip_atomic_store(fa.sync + QO_GO + QO_GO_STRIDE * i, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qa_stamp(fa, 4);
+  }
+}
+
 size_t qkv_attn_lds(int mt) {
   const size_t attn = 4 * AD6_SLOT_BYTES + 1024;  // V slots, the merge's (m, l) and a flag (the merge reuses the slots)
   const size_t gemv = sizeof(float) * (4 * mt * 1 * 256 + 4 * mt * 16 + mt * 16 + 4);  // NT = 1, NW = 4
+  // (the o workgroups' epilogue: NT <= 2 tiles at MT = 1, 8.4 KiB, below both)
   return attn > gemv ? attn : gemv;
 }
 
 // workgroups of the fused launch that are resident at once per CU (occupancy API, one below its answer as a margin:
 // cdna_hip_programming.md warns it can be one block too high; at least 1)
 // (MT m-tiles: the GEMV ring depth U = 8 / MT, as launch_skinny)
-template <int MT, int REP, int SPL>
+template <int MT, int REP, int SPL, int FO = 0, int OMODE = 0>
 static int qkv_attn_per_cu() {
   static int cached = 0;
   if (cached == 0) {
     int a = 0, b = 0;
     const size_t lds = qkv_attn_lds(MT);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, qkv_attn_kernel<MT, 1, 4, 8 / MT, false, REP, SPL>, 256,
-                                                     lds) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, qkv_attn_kernel<MT, 1, 4, 8 / MT, true, REP, SPL>, 256,
-                                                     lds) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, qkv_attn_kernel<MT, 1, 4, 8 / MT, false, REP, SPL, FO, OMODE>,
+                                                     256, lds) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, qkv_attn_kernel<MT, 1, 4, 8 / MT, true, REP, SPL, FO, OMODE>,
+                                                     256, lds) != hipSuccess)
       a = b = 1;
     const int n = a < b ? a : b;
     cached = n > 1 ? n - 1 : 1;
@@ -829,32 +1024,60 @@ static int qkv_attn_per_cu_rep(int rep) {
     default: return 0;
   }
 }
+// the fused-o instances: one m-tile, 8 query heads per kv head (the Llama-3-70B tensor-parallel shard)
+template <int SPL, int FO>
+static int qkv_attn_per_cu_o() {
+  const int a = qkv_attn_per_cu<1, 8, SPL, FO, MODE_RESIDUAL>(), b = qkv_attn_per_cu<1, 8, SPL, FO, MODE_TPRESID>();
+  return a < b ? a : b;
+}
+
+static int g_qa_o_nt = 2;  // o tiles per workgroup of the fused o projection (1 or 2; qkv_attn_set_o_nt, for A/B)
+void qkv_attn_set_o_nt(int nt) { g_qa_o_nt = nt == 1 ? 1 : 2; }
+int qkv_attn_o_groups(int M, int rep, int N, int K) {
+  if (M < 1 || M > 16 || rep != 8 || (N & 15) || (K & 31) || K > 32 * 4 * QO_PF) return 0;
+  const int g = ((N >> 4) + g_qa_o_nt - 1) / g_qa_o_nt;
+  return g <= QO_MAX_GROUPS ? g : 0;
+}
+size_t qkv_attn_sync_ints() { return QO_GO + (size_t)QO_GO_STRIDE * QO_MAX_GROUPS; }
 
 // 0 when the fused launch does not apply (then the caller runs the qkv GEMV and the attention kernel). Every workgroup
-// of the launch must be resident at once (the attention workgroups wait for the qkv ones).
-int qkv_attn_occupancy(int M, int rep, int spl) {
+// of the launch must be resident at once (the attention workgroups wait for the qkv ones, the o workgroups for the
+// attention ones).
+int qkv_attn_occupancy(int M, int rep, int spl, int o_groups) {
+  if (o_groups > 0) {
+    if (M > 16 || rep != 8) return 0;
+    if (g_qa_o_nt == 1) return spl == 2 ? qkv_attn_per_cu_o<2, 1>() : qkv_attn_per_cu_o<1, 1>();
+    return spl == 2 ? qkv_attn_per_cu_o<2, 2>() : qkv_attn_per_cu_o<1, 2>();
+  }
+  if (spl == 4) return M <= 16 ? qkv_attn_per_cu_rep<1, 4>(rep) : 0;  // (K over 3 / 4: one m-tile only)
+  if (spl == 3) return M <= 16 ? qkv_attn_per_cu_rep<1, 3>(rep) : 0;
   if (spl == 2) return M <= 16 ? qkv_attn_per_cu_rep<1, 2>(rep) : qkv_attn_per_cu_rep<2, 2>(rep);
   return M <= 16 ? qkv_attn_per_cu_rep<1, 1>(rep) : qkv_attn_per_cu_rep<2, 1>(rep);
 }
-int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl) {
+int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl, int o_groups) {
   if (M != B || M > 32 || (rep & (rep - 1)) || rep > 16 || t_cap > QA_MAX_SPLITS * QA_SPLIT_KEYS) return 0;
-  if ((spl != 1 && spl != 2) || (spl > 1 && (N >> 4) > GEMV_SPLIT_MAX_GROUPS)) return 0;
+  if (spl < 1 || spl > 4 || (spl > 2 && (M > 16 || o_groups > 0)) || (spl > 1 && (N >> 4) > GEMV_SPLIT_MAX_GROUPS) ||
+      o_groups < 0)
+    return 0;
   const int splits = (t_cap + QA_SPLIT_KEYS - 1) / QA_SPLIT_KEYS;
-  const int grid = (N >> 4) * spl + B * Hkv * splits;
-  return grid <= cus * qkv_attn_occupancy(M, rep, spl) ? splits : 0;
+  const int grid = (N >> 4) * spl + B * Hkv * splits + o_groups;
+  return grid <= cus * qkv_attn_occupancy(M, rep, spl, o_groups) ? splits : 0;
 }
 
 static int g_qa_diag = 0;
 void qkv_attn_set_diag(int d) { g_qa_diag = d; }
+static unsigned long long* g_qa_stamps = nullptr;
+void qkv_attn_set_stamps(unsigned long long* p) { g_qa_stamps = p; }
 
 int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
                     bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
-                    int t_cap, int splits, int spl, hipStream_t s) {
+                    int t_cap, int splits, int spl, hipStream_t s, const void* o_w, float* o_h, int o_n, int o_k,
+                    int o_mode, const QKVArgs* qo) {
   if (M <= 0) return 0;
   if (M > 32 || (N & 15) || (K & 31) || qa.Dh != AD6_DH || qa.S != 1 || qa.H % qa.Hkv) return -1;
   const int rep = qa.H / qa.Hkv;
   const int grid_q = (N >> 4) * spl, pairs = M * qa.Hkv;
-  if (spl != 1 && spl != 2) return -1;
+  if (spl < 1 || spl > 4 || (spl > 2 && M > 16)) return -1;
   if (spl > 1) {  // the split GEMV's slabs and tickets (as launch_skinny checks them)
     const int mt0 = M <= 16 ? 1 : 2;
     if ((N >> 4) > GEMV_SPLIT_MAX_GROUPS || !qa.sk_ws || !qa.sk_tk || (K >> 5) < spl ||
@@ -862,29 +1085,55 @@ int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float r
       return -3;
   }
   if (splits < 1 || splits > QA_MAX_SPLITS || splits * QA_SPLIT_KEYS < t_cap) return -1;
-  const FusedAttn fa{out, out_pack, kv_start, ws, tickets, sync, splits, grid_q, t_cap,
-                     1.4426950408889634f / sqrtf((float)AD6_DH), g_qa_diag};
+  // the fused o projection: h += out @ Wo^T (Wo [o_n, o_k], o_k = H * Dh)
+  int grid_o = 0;
+  if (o_w) {
+    grid_o = qkv_attn_o_groups(M, rep, o_n, o_k);
+    if (!grid_o || !o_h || !qo || o_k != qa.H * AD6_DH || (o_mode != MODE_RESIDUAL && o_mode != MODE_TPRESID) ||
+        (o_mode == MODE_TPRESID && !qo->tp))
+      return -1;
+  }
+  const FusedAttn fa{out,    out_pack, kv_start, ws, tickets, sync, splits, grid_q, t_cap,
+                     1.4426950408889634f / sqrtf((float)AD6_DH), g_qa_diag, pairs * splits, grid_o, g_qa_stamps};
+  const FusedO fo{static_cast<const u32x4*>(o_w), o_h, o_n, o_k};
+  const QKVArgs qo_v = qo ? *qo : QKVArgs{};
   const int use_rms = rms_eps >= 0.f;
   const float eps = use_rms ? rms_eps : 0.f;
   const int mt = M <= 16 ? 1 : 2;
   const size_t lds = qkv_attn_lds(mt);
-  const int grid = grid_q + pairs * splits;
-#define JLA_QA_S(MTV, R, SP)                                                                                        \
-  if (mt == MTV && rep == R && spl == SP) {                                                                         \
-    if (xp)                                                                                                         \
-      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, true, R, SP><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M, N, \
-                                                                              K, eps, use_rms, qa, fa);             \
-    else                                                                                                            \
-      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, false, R, SP><<<grid, 256, lds, s>>>(x, static_cast<const u32x4*>(W), M,  \
-                                                                               N, K, eps, use_rms, qa, fa);         \
-    JLA_CHECK_LAUNCH();                                                                                             \
-    return 0;                                                                                                       \
+  const int grid = grid_q + pairs * splits + grid_o;
+  const u32x4* Wq = static_cast<const u32x4*>(W);
+#define JLA_QA_K(MTV, R, SP, FOV, OM)                                                                             \
+  {                                                                                                               \
+    if (xp)                                                                                                       \
+      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, true, R, SP, FOV, OM><<<grid, 256, lds, s>>>(x, Wq, M, N, K, eps,         \
+                                                                                      use_rms, qa, fa, fo, qo_v);  \
+    else                                                                                                          \
+      qkv_attn_kernel<MTV, 1, 4, 8 / MTV, false, R, SP, FOV, OM><<<grid, 256, lds, s>>>(x, Wq, M, N, K, eps,        \
+                                                                                       use_rms, qa, fa, fo, qo_v); \
+    JLA_CHECK_LAUNCH();                                                                                           \
+    return 0;                                                                                                     \
   }
+  if (grid_o > 0) {
+#define JLA_QA_O(SP, FOV)                                                                  \
+  if (spl == SP && g_qa_o_nt == FOV) {                                                     \
+    if (o_mode == MODE_TPRESID) JLA_QA_K(1, 8, SP, FOV, MODE_TPRESID)                      \
+    JLA_QA_K(1, 8, SP, FOV, MODE_RESIDUAL)                                                 \
+  }
+    JLA_QA_O(1, 1) JLA_QA_O(1, 2) JLA_QA_O(2, 1) JLA_QA_O(2, 2)
+#undef JLA_QA_O
+    return -1;
+  }
+#define JLA_QA_S(MTV, R, SP) \
+  if (mt == MTV && rep == R && spl == SP) JLA_QA_K(MTV, R, SP, 0, 0)
 #define JLA_QA(MTV, R) JLA_QA_S(MTV, R, 1) JLA_QA_S(MTV, R, 2)
-  JLA_QA(1, 1) JLA_QA(1, 2) JLA_QA(1, 4) JLA_QA(1, 8) JLA_QA(1, 16)
+#define JLA_QA1(R) JLA_QA(1, R) JLA_QA_S(1, R, 3) JLA_QA_S(1, R, 4)
+  JLA_QA1(1) JLA_QA1(2) JLA_QA1(4) JLA_QA1(8) JLA_QA1(16)
   JLA_QA(2, 1) JLA_QA(2, 2) JLA_QA(2, 4) JLA_QA(2, 8) JLA_QA(2, 16)
+#undef JLA_QA1
 #undef JLA_QA
 #undef JLA_QA_S
+#undef JLA_QA_K
   return -1;
 }
 

@@ -44,13 +44,21 @@ constexpr long long TPRES_REGION = 64 * 64 * 4;  // up to 64 rows x 64 columns x
 
 // fused small-batch qkv projection + decode attention (gemv.hip qkv_attn_kernel): one launch; splits from
 // qkv_attn_splits (0 = not applicable: run the two kernels); ws >= pairs * splits * rep * 132 floats, tickets >= pairs,
-// sync >= 3 int32 (zeroed once, self-resetting)
-int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl = 1);
-int qkv_attn_occupancy(int M, int rep, int spl = 1);
-void qkv_attn_set_diag(int d);  // tests only: 1 = the qkv workgroups never publish (forces the timeout path)  // resident workgroups per CU the fused launch counts on
+// sync >= qkv_attn_sync_ints() int32 (zeroed once, self-resetting). With o_w, the same launch also runs the o projection into the residual
+// (o_mode MODE_RESIDUAL: h += out @ Wo^T + qo->res_bf16 / qo->pack mirrors; MODE_TPRESID: the TP granule exchange of
+// qo->tp first); o_groups = qkv_attn_o_groups(...) (0: the o projection cannot be fused at this shape).
+int qkv_attn_o_groups(int M, int rep, int N, int K);
+size_t qkv_attn_sync_ints();
+void qkv_attn_set_o_nt(int nt);  // o tiles per fused-o workgroup (1 / 2; tools, A/B)
+int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl = 1, int o_groups = 0);
+int qkv_attn_occupancy(int M, int rep, int spl = 1, int o_groups = 0);  // resident workgroups per CU it counts on
+void qkv_attn_set_stamps(unsigned long long* p);  // tools: [grid][8] phase timestamps per workgroup (nullptr: off)
+void qkv_attn_set_diag(int d);  // tests only: 1 = the qkv workgroups never publish (forces the timeout path)
 int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float rms_eps, const QKVArgs& qa, bool xp,
                     bf16_t* out, bf16_t* out_pack, const int32_t* kv_start, float* ws, int32_t* tickets, int32_t* sync,
-                    int t_cap, int splits, int spl, hipStream_t s);  // spl 2: K of the qkv GEMV over 2 (qa.sk_ws/sk_tk)
+                    int t_cap, int splits, int spl, hipStream_t s,  // spl 2: K of the qkv GEMV over 2 (qa.sk_ws/sk_tk)
+                    const void* o_w = nullptr, float* o_h = nullptr, int o_n = 0, int o_k = 0, int o_mode = 0,
+                    const QKVArgs* qo = nullptr);
 int linear_skinny(const void* x, int x_is_f32, const void* W, void* out, int M, int N, int K, int mode,
                   float rms_eps, int accumulate, int out_f32, const QKVArgs* qkv, int variant, hipStream_t s);
 // split-K GEMV variants 16 / 18 / 26 (K over gridDim.y workgroups per column group, last arriver sums + epilogue): their slab

@@ -8,7 +8,8 @@ layout and hipGraph capture see one flat set of tensors:
 
   attention: [RMSNorm folded] qkv GEMV/GEMM + RoPE + KV-cache write (one kernel in decode), cache
              attention (split-KV decode / flash prefill, GQA by indexing), wo with the residual add
-             fused into its epilogue (+ TP all-reduce)                       -- model.py:383-392
+             fused into its epilogue (+ TP all-reduce); at small batch qkv + attention (+ wo) are one
+             launch                                                          -- model.py:383-392
   mlp:       [RMSNorm folded] w1|w3 GEMV/GEMM with SiLU*up epilogue, w2 with the residual add
              (+ TP all-reduce)                                               -- model.py:394-398
 
@@ -38,14 +39,26 @@ class LLaMAAttention:
                  output_attentions: bool = False, pk: Optional["PackedActs"] = None) -> Optional[torch.Tensor]:
         m, lw = self.model, self.weights
         kc, vc = cache.layer(self.layer_idx)
-        splits = 0 if output_attentions else ops.qkv_attention_splits(hb, lw.qkv, kc, seq_len, m.n_heads,
-                                                                       m.n_kv_heads, key_mask)
-        if splits:  # small-batch decode: qkv projection + attention in one launch
-            att_p = pk.att if pk is not None else None
+        splits = og = 0
+        o_state = None
+        if not output_attentions:
+            # the o projection in the same launch where it fits (the 70B tensor-parallel shard at small batch)
+            og = ops.qkv_attention_o_groups(hb, lw.o, m.n_heads, m.n_kv_heads) if seq_len == 1 else 0
+            o_state = m.comm.fused_o_state(hb, lw.o) if og else None
+            og = og if o_state is not None else 0
+            splits = ops.qkv_attention_splits(hb, lw.qkv, kc, seq_len, m.n_heads, m.n_kv_heads, key_mask, og)
+            if og and not splits:
+                og = 0
+                splits = ops.qkv_attention_splits(hb, lw.qkv, kc, seq_len, m.n_heads, m.n_kv_heads, key_mask)
+        if splits:  # small-batch decode: qkv projection + attention (+ o projection) in one launch
+            hb_p = pk.hb if pk else None
+            o = (lw.o, h, hb, hb_p, o_state) if og else None
+            att_p = pk.att if pk is not None and not og else None
             a = ops.linear_qkv_attention(hb, lw.qkv, m.eps, m.rope, positions, kc, vc, slot0, kv_start, m.n_heads,
                                          m.n_kv_heads, m.head_dim, splits, x_packed=pk.hb_in() if pk else None,
-                                         out_packed=att_p)
-            m._row_parallel(a, lw.o, h, hb, x_packed=att_p, mirror_packed=pk.hb if pk else None)
+                                         out_packed=att_p, o=o)
+            if not og:
+                m._row_parallel(a, lw.o, h, hb, x_packed=att_p, mirror_packed=hb_p)
             if pk is not None and pk.hb is not None:
                 pk.hb_ok = True
             return None

@@ -486,8 +486,16 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
 # =2: wherever the launch fits.
 QKV_ATTN = int(os.environ.get("JLA_QKV_ATTN", "1"))
 # K of the fused launch's qkv GEMV over 2 workgroups per column group (the split GEMV's last-arriver sum) when the grid
-# still fits the CUs; JLA_QKV_ATTN_SPL=1: one workgroup per column group (A/B)
+# still fits the CUs; JLA_QKV_ATTN_SPL=1: one workgroup per column group; 3 / 4: more splits (M <= 16), which lost at
+# the 70B shard's B = 1: 4.73 (2) vs 4.84 (3) / 4.87 (4) ms per token (profiles/r6_qkv_attn_o_timeline.jsonl)
 QKV_ATTN_SPL = int(os.environ.get("JLA_QKV_ATTN_SPL", "2"))
+# ... and the o projection in the same launch (its workgroups fetch their Wo slice while qkv / attention run, then wait
+# for the attention output; the residual or TP-exchange epilogue of the standalone GEMV): M <= 16, 8 query heads per kv
+# head, H * Dh <= 1024 -- the 70B tensor-parallel shard. Bit-identical to the two launches, one launch fewer per layer,
+# but not faster: the shard's B = 1 step measured 4.76 / 4.79 and 4.73 / 4.76 ms per token without / with it
+# (profiles/r6_qkv_attn_o_timeline.jsonl: the o weight stream competes with the qkv GEMV's per-CU stream, and the chain
+# after the attention -- go flag, x load, the TP exchange -- is as long as the standalone o GEMV). JLA_QKV_ATTN_O=1: on.
+QKV_ATTN_O = int(os.environ.get("JLA_QKV_ATTN_O", "0"))
 _CUS = {}
 
 
@@ -498,7 +506,7 @@ class InLaunchTimeout(RuntimeError):
 def check_inlaunch() -> None:
     """Raise InLaunchTimeout if a fused qkv + attention launch recorded a timeout in its error word
     (``qa_sync[2]``, csrc/kernels/gemv.hip qkv_attn_kernel). The device side is sticky -- the counters are no longer
-    reset and every later launch writes no output -- so after a timeout the fused path is refused for the rest of the
+    reset and every later launch writes zeros -- so after a timeout the fused path is refused for the rest of the
     process (the words re-zeroed, the workspace generation bumped so a captured decode graph is re-captured without it).
     Reads device memory (synchronises); called by the engine's host poll."""
     global QKV_ATTN
@@ -507,8 +515,9 @@ def check_inlaunch() -> None:
             QKV_ATTN = 0
             buf.zero_()
             workspace.generation += 1
-            raise InLaunchTimeout("fused qkv + attention launch: the attention workgroups timed out waiting for the qkv "
-                                  "workgroups (error word qa_sync[2]); the fused path is now off for this process")
+            raise InLaunchTimeout("fused qkv + attention launch: a wait timed out (the attention workgroups on the qkv "
+                                  "workgroups, or the o workgroups on the attention ones; error word qa_sync[2]); the "
+                                  "fused path is now off for this process")
 
 
 def _num_cus(device) -> int:
@@ -518,34 +527,49 @@ def _num_cus(device) -> int:
     return _CUS[key]
 
 
+def qkv_attention_o_groups(x: torch.Tensor, w_o, n_heads: int, n_kv_heads: int) -> int:
+    """Workgroups of the o projection when the fused decode launch can also run it (``linear_qkv_attention(o=...)``),
+    else 0."""
+    if not QKV_ATTN_O or not _is_gpu(x):
+        return 0
+    return int(ext().qkv_attn_o_groups(x.shape[0], n_heads // n_kv_heads, w_o.n, w_o.k))
+
+
 def qkv_attention_splits(x: torch.Tensor, w, k_cache: torch.Tensor, seq_len: int, n_heads: int, n_kv_heads: int,
-                         key_mask: Optional[torch.Tensor] = None) -> int:
+                         key_mask: Optional[torch.Tensor] = None, o_groups: int = 0) -> int:
     """Attention workgroups per (row, kv head) pair of the fused qkv + attention launch for this decode step, or 0
     when it does not apply (prefill, a key mask, M > 32, a cache longer than 512, or a grid the CUs cannot hold at
-    once)."""
+    once). ``o_groups``: the launch also holds the o projection's workgroups (``qkv_attention_o_groups``)."""
     if not QKV_ATTN or seq_len != 1 or key_mask is not None or not _is_gpu(x) or x.dtype != BF16:
         return 0
     m = x.shape[0]
     if QKV_ATTN == 1 and (m > 4 or n_heads < 8 * n_kv_heads):
         return 0
     return int(ext().qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n,
-                                     _num_cus(x.device), 1))
+                                     _num_cus(x.device), 1, int(o_groups)))
 
 
-def _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, device) -> int:
-    if QKV_ATTN_SPL > 1 and e.qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n,
-                                               _num_cus(device), 2) > 0:
-        return 2
+def _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, device, o_groups=0) -> int:
+    """K of the fused launch's qkv GEMV over QKV_ATTN_SPL workgroups per column group, or the most below it whose
+    grid still fits the CUs at once."""
+    for spl in range(min(max(QKV_ATTN_SPL, 1), 4), 1, -1):
+        if e.qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n, _num_cus(device), spl,
+                             int(o_groups)) > 0:
+            return spl
     return 1
 
 
 def linear_qkv_attention(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.Tensor, positions: torch.Tensor,
                          k_cache: torch.Tensor, v_cache: torch.Tensor, slot0, kv_start: torch.Tensor, n_heads: int,
                          n_kv_heads: int, head_dim: int, splits: int, x_packed: Optional[torch.Tensor] = None,
-                         out_packed: Optional[torch.Tensor] = None, spl: Optional[int] = None) -> torch.Tensor:
+                         out_packed: Optional[torch.Tensor] = None, spl: Optional[int] = None,
+                         o: Optional[tuple] = None) -> torch.Tensor:
     """One decode token per row: ``linear_qkv_rope`` + ``attention`` in one launch (``qkv_attention_splits`` > 0).
     Returns the attention output ``[B, H * Dh]`` bf16 (``out_packed``: its packed copy for the o projection).
-    ``spl``: K of the qkv GEMV over 1 or 2 workgroups per column group (default: 2 where the grid fits)."""
+    ``spl``: K of the qkv GEMV over 1 or 2 workgroups per column group (default: 2 where the grid fits).
+    ``o = (w_o, h, hb, hb_pack, tp_state)``: the same launch also runs the o projection into the residual
+    (``h += out @ Wo^T``, ``hb`` / ``hb_pack`` its bf16 mirrors; ``tp_state`` a fused custom all-reduce instance for the
+    tensor-parallel exchange, 0 at world 1) -- ``splits`` must then come from ``qkv_attention_splits(o_groups=...)``."""
     e = ext()
     m = x.shape[0]
     dev = x.device
@@ -554,15 +578,22 @@ def linear_qkv_attention(x: torch.Tensor, w, rms_eps: Optional[float], table: to
     out = torch.empty(m, n_heads * head_dim, dtype=BF16, device=dev)
     ws = workspace.get("qa_ws", m * n_kv_heads * splits * rep * (head_dim + 4), torch.float32, dev)
     tickets = workspace.get_zeroed("qa_tickets", max(m * n_kv_heads, 64), torch.int32, dev)
-    sync = workspace.get_zeroed("qa_sync", 4, torch.int32, dev)
-    spl = _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, dev) if spl is None else int(spl)
+    sync = workspace.get_zeroed("qa_sync", int(e.qkv_attn_sync_ints()), torch.int32, dev)
+    og = 0 if o is None else int(e.qkv_attn_o_groups(m, rep, o[0].n, o[0].k))
+    spl = _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, dev, og) if spl is None else int(spl)
     sk_ws = sk_tk = None
     if spl > 1:
         sk_ws, sk_tk = _skinny_ws(e, m, w.n, w.k, MODE_QKV, dev)
+    ow = oh = ohb = ohp = None
+    on = ok = 0
+    tp_state = 0
+    if o is not None:
+        wo, oh, ohb, ohp, tp_state = o
+        ow, on, ok = wo.weight, wo.n, wo.k
     e.linear_qkv_attn(x, w.weight, w.n, w.k, -1.0 if rms_eps is None else float(rms_eps), table,
                       positions.reshape(-1).to(torch.int32), k_cache, v_cache, _slot_tensor(slot0, dev), n_heads,
                       n_kv_heads, head_dim, q, kv_start, out, out_packed, ws, tickets, sync, k_cache.shape[2], splits,
-                      x_packed, spl, sk_ws, sk_tk)
+                      x_packed, spl, sk_ws, sk_tk, ow, on, ok, oh, ohb, ohp, int(tp_state or 0))
     return out
 
 

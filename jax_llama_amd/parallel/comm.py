@@ -151,6 +151,18 @@ class TPComm:
         f.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=hb_pack)
         return True
 
+    def fused_o_state(self, x: torch.Tensor, w) -> Optional[int]:
+        """The custom all-reduce state a fused decode launch's o projection exchanges its partials through (the GEMV
+        epilogue's granule exchange, as ``linear_residual_``): 0 at world 1 (plain residual epilogue), None when the
+        fused path does not apply (then the o projection runs through ``linear_residual_`` / the two-step path)."""
+        if self.size == 1:
+            return 0
+        f = self.fused
+        if (f is None or self.reduce_dtype != torch.bfloat16 or not x.is_cuda or x.dtype != torch.bfloat16
+                or not f.can_fuse(x.shape[0], w.n)):
+            return None
+        return f._live()
+
     def packs_residual(self, nbytes: int) -> bool:
         """Whether ``all_reduce_residual_`` of an ``nbytes`` partial can also write a packed hb copy."""
         return self.size == 1 or (self.custom is not None and 0 < nbytes <= self.custom.max_bytes and nbytes % 16 == 0)

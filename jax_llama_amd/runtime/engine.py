@@ -302,6 +302,13 @@ class DecodeEngine:
                     torch.cuda.manual_seed(int(gc.seed))
         try:
             return self._run(input_ids, attention_mask)
+        except Exception:
+            # a failed step (a peer or in-launch timeout, an error mid-decode) can leave non-finite rows in this
+            # engine's cache beyond where the next prompt writes; the kernels mask keys past the valid length by
+            # probability 0, and 0 x NaN is NaN: zero the cache so the next call starts as from a fresh engine
+            self.cache.k.zero_()
+            self.cache.v.zero_()
+            raise
         finally:
             if rng_saved is not None:
                 torch.cuda.set_rng_state(rng_saved, self.device)

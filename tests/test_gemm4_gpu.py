@@ -153,7 +153,7 @@ def test_gemm4_argmax(m, n, k):
                 torch.cuda.synchronize()
                 assert torch.equal(i0.cpu(), i1.cpu()) and torch.equal(v0.cpu(), v1.cpu())
     finally:
-        e.gemm_set_g4_default(0)
+        e.gemm_set_g4_default(1)  # (the production default)
 
 
 def test_gemm4_model_prefill_matches_gemm2():
@@ -166,12 +166,13 @@ def test_gemm4_model_prefill_matches_gemm2():
                      vocab_size=1024)
     model = LLaMAForCausalLM(cfg, device=DEV, seed=0)
     toks = torch.randint(3, cfg.vocab_size, (2, 160), dtype=torch.int32)
-    base = model(toks).logits.float().cpu()
     try:
+        e.gemm_set_g4_default(0)
+        base = model(toks).logits.float().cpu()
         e.gemm_set_g4_default(1)
         got = model(toks).logits.float().cpu()
     finally:
-        e.gemm_set_g4_default(0)
+        e.gemm_set_g4_default(1)  # (the production default)
     _close(got, base, 2e-2, 2e-2)
 
 

@@ -711,25 +711,30 @@ def test_gemm_argmax_fused(m, n, k):
         wt[dst] = wt[src]
     pg = PackedLinear.from_dense(wt, DEV)
     xg = x.to(DEV)
-    for eps in (-1.0, 1e-5):
-        logits = torch.empty(m, n, dtype=torch.float32, device=DEV)
-        e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, 1)
-        i0 = torch.empty(m, dtype=torch.int32, device=DEV)
-        v0 = torch.empty(m, dtype=torch.float32, device=DEV)
-        e.argmax(logits, i0, v0)
-        ws = torch.empty(e.gemm_argmax_workspace(m, n), dtype=torch.float32, device=DEV)
-        i1 = torch.empty_like(i0)
-        v1 = torch.empty_like(v0)
-        e.gemm_argmax(xg, pg.weight, n, k, ws, eps, i1, v1)
-        torch.cuda.synchronize()
-        assert torch.equal(i0.cpu(), i1.cpu()), (eps, (i0 != i1).nonzero()[:8])
-        assert torch.equal(v0.cpu(), v1.cpu())
-        r = ref.linear(x, wt, None if eps < 0 else eps, torch.float32)
-        agree = (r.argmax(-1).to(torch.int32) == i1.cpu()).float().mean().item()
-        assert agree > 0.97, agree  # bf16 rounding may flip near-ties against the fp32 reference
-    # the op-level API picks the fused path from ARGMAX_FUSED_MIN_M rows on
-    idx, val = ops.linear_argmax(xg, pg, 1e-5)
-    assert torch.equal(idx.cpu(), i1.cpu()) and torch.equal(val.cpu(), v1.cpu())
+    # the gemm2 plan on both sides (tile 1 here; gemm_argmax off gemm4, whose pairing test_gemm4_gpu checks)
+    e.gemm_set_g4_default(0)
+    try:
+        for eps in (-1.0, 1e-5):
+            logits = torch.empty(m, n, dtype=torch.float32, device=DEV)
+            e.gemm(xg, pg.weight, n, k, logits, ops.MODE_STORE, True, None, 1, None, eps, 1)
+            i0 = torch.empty(m, dtype=torch.int32, device=DEV)
+            v0 = torch.empty(m, dtype=torch.float32, device=DEV)
+            e.argmax(logits, i0, v0)
+            ws = torch.empty(e.gemm_argmax_workspace(m, n), dtype=torch.float32, device=DEV)
+            i1 = torch.empty_like(i0)
+            v1 = torch.empty_like(v0)
+            e.gemm_argmax(xg, pg.weight, n, k, ws, eps, i1, v1)
+            torch.cuda.synchronize()
+            assert torch.equal(i0.cpu(), i1.cpu()), (eps, (i0 != i1).nonzero()[:8])
+            assert torch.equal(v0.cpu(), v1.cpu())
+            r = ref.linear(x, wt, None if eps < 0 else eps, torch.float32)
+            agree = (r.argmax(-1).to(torch.int32) == i1.cpu()).float().mean().item()
+            assert agree > 0.97, agree  # bf16 rounding may flip near-ties against the fp32 reference
+        # the op-level API picks the fused path from ARGMAX_FUSED_MIN_M rows on
+        idx, val = ops.linear_argmax(xg, pg, 1e-5)
+        assert torch.equal(idx.cpu(), i1.cpu()) and torch.equal(val.cpu(), v1.cpu())
+    finally:
+        e.gemm_set_g4_default(1)
 
 
 @pytest.mark.parametrize("variant", [12, 15, 18, 21, 22, 26, 7])
@@ -952,3 +957,77 @@ def test_qkv_attention_fused_launch(b, hkv, rep, t, slot, spl):
     else:  # (M > 16: the unfused GEMV cuts K over 8 waves, the fused launch over 4 -- another summation order)
         _close(kd, ku, 1e-2, 1e-2)
         _close(vd, vu, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("tp", [False, True])
+@pytest.mark.parametrize("nt", [2, 1])
+@pytest.mark.parametrize("b,t,slot,spl", [(1, 40, 17, 2), (1, 384, 300, 1), (3, 200, 199, 2), (16, 512, 130, 2)])
+def test_qkv_attention_fused_o_projection(b, t, slot, spl, nt, tp):
+    """The fused decode launch with the o projection on its last workgroups (gemv.hip qa_o_proj): the residual after
+    the launch equals the standalone GEMV of the same geometry applied to the launch's attention output -- bit for bit
+    (variant 6 / 1: 2 / 1 tiles x 4 waves, the same per-wave k-step order and the same epilogue), in the residual
+    epilogue (world 1) and the TP granule exchange (a world-1 fused all-reduce instance) -- and the fp32 reference of
+    h + attention @ Wo^T within bf16 tolerance; the packed mirror equals the row-major one; a second step agrees."""
+    from jax_llama_amd.parallel.custom_allreduce import CustomAllReduce
+    e = ops.ext()
+    dh, k, hkv, rep = 128, 1024, 1, 8
+    h_ = hkv * rep
+    n, d = (h_ + 2 * hkv) * dh, 2048
+    torch.manual_seed(b * 10 + t)
+    x = torch.randn(b, k).to(BF16)
+    w = (torch.randn(n, k) * 0.03).to(BF16)
+    wo = (torch.randn(d, h_ * dh) * 0.03).to(BF16)
+    h0 = torch.randn(b, d)
+    table = ref.rope_table(dh, 1024, 500000.0)
+    pos = torch.full((b,), slot, dtype=torch.int32)
+    kc0, vc0 = _cache(b, hkv, t, dh)
+    kv_start = torch.tensor([3 * i % 50 for i in range(b)], dtype=torch.int32)
+    pw, pwo = PackedLinear.from_dense(w, DEV), PackedLinear.from_dense(wo, DEV)
+    xd, sl = x.to(DEV), torch.tensor([slot], dtype=torch.int32, device=DEV)
+    car = CustomAllReduce.local(max_bytes=CustomAllReduce.fused_bytes(d)) if tp else None
+    e.qkv_attn_set_o_nt(nt)
+    try:
+        og = e.qkv_attn_o_groups(b, rep, d, h_ * dh)
+        assert og == (d // 16 + nt - 1) // nt
+        splits = e.qkv_attn_splits(b, b, hkv, rep, t, n, ops._num_cus(xd.device), spl, og)
+        if splits == 0:
+            pytest.skip("this grid does not fit the CUs at once")
+
+        def step():
+            kd, vd = kc0.to(DEV), vc0.to(DEV)
+            hd = h0.to(DEV)
+            hbd = torch.empty(b, d, dtype=BF16, device=DEV)
+            hbp = ops.packed_empty(b, d, DEV)
+            a = ops.linear_qkv_attention(xd, pw, 1e-5, table.to(DEV), pos.to(DEV), kd, vd, sl, kv_start.to(DEV), h_,
+                                         hkv, dh, splits, spl=spl,
+                                         o=(pwo, hd, hbd, hbp, car._live() if tp else 0))
+            torch.cuda.synchronize()
+            return a, hd, hbd, hbp
+
+        a, hd, hbd, hbp = step()
+        a2, hd2, hbd2, _ = step()
+        # the standalone GEMV of the same geometry on the launch's own attention output
+        hu = h0.to(DEV)
+        hbu = torch.empty(b, d, dtype=BF16, device=DEV)
+        try:
+            ops.GEMV_VARIANT = 6 if nt == 2 else 1
+            if tp:
+                ops.linear_tp_residual(a, pwo, hu, hbu, car._live())
+            else:
+                ops.linear_residual(a, pwo, hu, mirror=hbu)
+            torch.cuda.synchronize()
+        finally:
+            ops.GEMV_VARIANT = 0
+    finally:
+        e.qkv_attn_set_o_nt(2)
+        if car is not None:
+            car.close()
+    assert torch.equal(hd, hu) and torch.equal(hbd, hbu)
+    assert torch.equal(hbd, hd.to(BF16))
+    assert torch.equal(ref.unpack_act(hbp.cpu(), b), hbd.cpu())
+    assert torch.equal(a, a2) and torch.equal(hd, hd2) and torch.equal(hbd, hbd2)
+    kcr, vcr = kc0.clone(), vc0.clone()
+    q = ref.linear_qkv_rope(x.float(), w, 1e-5, table, pos, kcr, vcr, slot, 1, h_, hkv, dh)
+    att = ref.attention(q.reshape(b, 1, h_, dh), kcr, vcr, slot, kv_start).reshape(b, h_ * dh)
+    _close(a, att, 2e-2, 2e-2)
+    _close(hd, h0 + a.float().cpu() @ wo.float().t(), 1e-2, 1e-2)

@@ -196,3 +196,28 @@ def test_output_attentions_gpu_same_logits_and_causal_weights():
     assert w.shape == (2, cfg.num_attention_heads, 9, 9)
     assert torch.allclose(w.sum(-1), torch.ones_like(w.sum(-1)), atol=1e-4)
     assert torch.all(torch.triu(w[0, 0], 1) == 0)
+
+
+def test_decode_fused_o_projection_matches_two_launches():
+    """Greedy decode with the Llama-3-70B tensor-parallel shard's attention geometry (8 query heads per kv head,
+    H * Dh = 1024) and the o projection inside the fused qkv + attention launch (ops.QKV_ATTN_O) produces exactly the
+    tokens of the two-launch step with the standalone GEMV of the same geometry (variant 6: 2 tiles x 4 waves; the two
+    are bit-identical, tests/test_kernels_gpu.py test_qkv_attention_fused_o_projection), graph-captured decode."""
+    from jax_llama_amd import ops
+    cfg = gpu_config(hidden_size=1024, intermediate_size=512, num_attention_heads=8, num_key_value_heads=1,
+                     vocab_size=512, num_hidden_layers=2)
+    model = LLaMAForCausalLM(cfg, device="cuda", _do_init=False).init_random(seed=11)
+    ids = torch.randint(3, cfg.vocab_size, (1, 12), dtype=torch.int32)
+    gc = GenerationConfig(max_length=48, do_sample=False, pad_token_id=0, eos_token_id=-1)
+    x = torch.zeros(1, cfg.hidden_size, dtype=torch.bfloat16, device="cuda")
+    saved_v, saved_o = ops.GEMV_VARIANT, ops.QKV_ATTN_O
+    try:
+        ops.GEMV_VARIANT = 6
+        out = {}
+        for fo in (0, 1):
+            ops.QKV_ATTN_O = fo
+            assert ops.qkv_attention_o_groups(x, model.layers[0].o, 8, 1) == (1024 // 32 if fo else 0)
+            out[fo] = model.generate(ids, generation_config=gc).sequences.cpu()
+    finally:
+        ops.GEMV_VARIANT, ops.QKV_ATTN_O = saved_v, saved_o
+    assert torch.equal(out[0], out[1])

@@ -729,6 +729,36 @@ void linear_tp_residual(int64_t state, Tensor x, Tensor w, int64_t n, int64_t k,
              tickets ? *tickets : Tensor(), packed_ptr(x_packed, m, k, "x_packed"));
 }
 
+// Row-parallel tiled projection (decode batches past the GEMV's rows) with the TP all-reduce and residual add in its
+// split-K reduce (gemm.hip gemm_reduce_tp_kernel): h (fp32) += sum over the group of x @ W^T, hb = bf16(h). A split plan
+// (ksplit > 1, or gemm5 tiles 11 / 12) and the shared gemm workspace; one exchange region per 4096 output elements.
+void gemm_tp_residual(int64_t state, Tensor x, Tensor w, int64_t n, int64_t k, Tensor h, Tensor hb, int64_t ksplit,
+                      Tensor ws, int64_t tile) {
+  check_gpu(x, "x");
+  check_gpu(h, "h");
+  check_gpu(hb, "hb");
+  check_packed(w, n, k);
+  check(x.dim() == 2 && x.size(1) == k && x.scalar_type() == torch::kBFloat16, "x must be bf16 [M, K]");
+  const int64_t m = x.size(0);
+  check(h.scalar_type() == torch::kFloat32 && h.numel() == m * n && hb.scalar_type() == torch::kBFloat16 &&
+            hb.numel() == m * n, "h fp32 / hb bf16 [M, N]");
+  void* st = reinterpret_cast<void*>(state);
+  const int64_t groups = jla::gemm_tp_groups((int)m, (int)n);
+  check(groups <= jla::CAR_WG_COUNTERS && groups * jla::TPRES_REGION <= jla::car_max_bytes(st),
+        "gemm_tp_residual: the output does not fit the fused exchange buffer");
+  const bool g5 = tile == 11 || tile == 12;
+  check(g5 || ksplit > 1, "gemm_tp_residual: a split-K plan (the exchange lives in the reduce)");
+  if (g5)
+    check_g5_ws(ws, k, ksplit, m, n, false);
+  else
+    check_gemm_ws(ws, ksplit, m, n);
+  jla::QKVArgs qa{};
+  qa.tp = jla::car_device(st);
+  rc(jla::gemm(cbf(x), w.data_ptr(), h.data_ptr(), m, n, k, MODE_TPRESID_ID, 1, 1, bf(hb), &qa, ptr<float>(ws),
+               ws.numel(), ksplit, stream(), -1.f, (int)tile, nullptr, 0),
+     "gemm_tp_residual");
+}
+
 // (value fp32, index int32) all-gathers of the vocab-parallel sampler. mode 0: out_i[n] = index of the first max over
 // ranks (out_v optional); mode 1: out_v/out_i [n / k, world * k]
 void car_pairs(int64_t state, int64_t mode, Tensor vals, Tensor idx, int64_t idx_offset, int64_t k,
@@ -833,6 +863,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {  // _C, or _C_dbg for the bounds-chec
   m.def("attn_decode_packs", &jla::attn_decode_packs);
   m.def("skinny_workspace", &skinny_workspace);
   m.def("linear_skinny_argmax", &linear_skinny_argmax);
+  m.def("gemm_tp_residual", &gemm_tp_residual, py::arg("state"), py::arg("x"), py::arg("w"), py::arg("n"), py::arg("k"),
+        py::arg("h"), py::arg("hb"), py::arg("ksplit"), py::arg("ws"), py::arg("tile"));
+  m.def("gemm_tp_groups", [](int64_t m, int64_t n) { return (int64_t)jla::gemm_tp_groups((int)m, (int)n); });
   m.def("linear_tp_residual", &linear_tp_residual, py::arg("state"), py::arg("x"), py::arg("w"), py::arg("n"),
         py::arg("k"), py::arg("h"), py::arg("hb"), py::arg("variant"), py::arg("x_packed") = py::none(),
         py::arg("hb_pack") = py::none(), py::arg("ws") = py::none(), py::arg("tickets") = py::none());

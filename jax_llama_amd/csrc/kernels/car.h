@@ -52,4 +52,85 @@ JLA_DEV unsigned gran_tag(int calls) { return 0x7FC00000u | ((unsigned)calls & 0
 // the same slots (the instance's self-test) never carry a fused call's tag
 JLA_DEV unsigned gran_tag_fused(int calls) { return 0xFFC00000u | ((unsigned)calls & 0x003FFFFFu); }
 
+// The fused epilogues' gather (gemv.hip MODE_TPRESID, gemm.hip gemm_reduce_tp_kernel): the 8-byte granule at `off` of
+// this rank's buffer once it carries `tag`. One load in the common case; otherwise poll, bounded by the group's timeout
+// (then the error word is set and the stale granule returned: the host raises at its next poll). give_up: another
+// workgroup already timed out -- no second wait.
+JLA_DEV u32x2 car_granule(const CarDevice& d, __amdgpu_buffer_rsrc_t mine, long long off, unsigned tag, bool give_up) {
+  u32x2 r = ld_sys8(mine, off);
+  if (r[1] != tag && !give_up) {
+    const long long t0 = (long long)wall_clock64();
+    while (r[1] != tag) {
+      if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
+        __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      if (__hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+      __builtin_amdgcn_s_sleep(1);
+      r = ld_sys8(mine, off);
+    }
+  }
+  return r;
+}
+
+// The gather of a whole group: granule `off + p * stride` of this rank's buffer for every rank p, every load issued
+// before any is checked -- one round trip for the group instead of one per rank (a check on each load before the next
+// one serialised world round trips per element) -- then a granule still without its tag is polled alone. W: the
+// loads issued (the world size, rounded up to 1 / 2 / 4 / 8; ranks past the world re-read rank 0's granule, never an
+// address outside the buffer -- hipcc issues such predicated loads unconditionally).
+template <int W>
+JLA_DEV void car_gather8_w(const CarDevice& d, __amdgpu_buffer_rsrc_t mine, long long off, long long stride,
+                           unsigned tag, bool give_up, u32x2 (&r)[CAR_MAX_WORLD]) {
+#pragma unroll
+  for (int p = 0; p < W; ++p) r[p] = ld_sys8(mine, off + (long long)(p < d.world ? p : 0) * stride);
+#pragma unroll
+  for (int p = 0; p < W; ++p)
+    if (p < d.world && r[p][1] != tag) r[p] = car_granule(d, mine, off + (long long)p * stride, tag, give_up);
+}
+JLA_DEV void car_gather8(const CarDevice& d, __amdgpu_buffer_rsrc_t mine, long long off, long long stride,
+                         unsigned tag, bool give_up, u32x2 (&r)[CAR_MAX_WORLD]) {
+  if (d.world == 1)
+    car_gather8_w<1>(d, mine, off, stride, tag, give_up, r);
+  else if (d.world == 2)
+    car_gather8_w<2>(d, mine, off, stride, tag, give_up, r);
+  else if (d.world <= 4)
+    car_gather8_w<4>(d, mine, off, stride, tag, give_up, r);
+  else
+    car_gather8_w<8>(d, mine, off, stride, tag, give_up, r);
+}
+// two adjacent granules per rank (16 bytes, one load; each 8-byte half carries its own tag), polled as a pair
+template <int W>
+JLA_DEV void car_gather16_w(const CarDevice& d, __amdgpu_buffer_rsrc_t mine, long long off, long long stride,
+                            unsigned tag, bool give_up, u32x4 (&r)[CAR_MAX_WORLD]) {
+#pragma unroll
+  for (int p = 0; p < W; ++p) r[p] = ld_sys16(mine, off + (long long)(p < d.world ? p : 0) * stride);
+#pragma unroll
+  for (int p = 0; p < W; ++p) {
+    if (p < d.world && (r[p][1] != tag || r[p][3] != tag) && !give_up) {
+      const long long o = off + (long long)p * stride;
+      const long long t0 = (long long)wall_clock64();
+      do {
+        if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
+          __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        if (__hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        __builtin_amdgcn_s_sleep(1);
+        r[p] = ld_sys16(mine, o);
+      } while (r[p][1] != tag || r[p][3] != tag);
+    }
+  }
+}
+JLA_DEV void car_gather16(const CarDevice& d, __amdgpu_buffer_rsrc_t mine, long long off, long long stride,
+                          unsigned tag, bool give_up, u32x4 (&r)[CAR_MAX_WORLD]) {
+  if (d.world == 1)
+    car_gather16_w<1>(d, mine, off, stride, tag, give_up, r);
+  else if (d.world == 2)
+    car_gather16_w<2>(d, mine, off, stride, tag, give_up, r);
+  else if (d.world <= 4)
+    car_gather16_w<4>(d, mine, off, stride, tag, give_up, r);
+  else
+    car_gather16_w<8>(d, mine, off, stride, tag, give_up, r);
+}
+
 }  // namespace jla

@@ -16,6 +16,7 @@
 // projection (reference ops: model.py:210/294/338/736, :58-92, :169-199, :392/:398).
 #include <type_traits>
 
+#include "car.h"
 #include "common.h"
 #include "gemm4w.h"
 #include "gemm5ws.h"
@@ -1142,6 +1143,87 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Split-K reduce of a row-parallel projection with the tensor-parallel all-reduce and the residual add in its epilogue
+// (MODE_TPRESID: the tiled GEMM's counterpart of gemv.hip's fused epilogue, for decode batches past the GEMV's 64 rows;
+// reference partition.py:67,70 -- the psum of the row-sharded wo / w2). Workgroup w sums the splits of elements
+// [4096 w, 4096 (w + 1)) of the M x N output, rounds each pair to bf16 (the partial the unfused reduce stores) and
+// pushes it as {2 x bf16, tag} granules into region w of every rank's buffer -- the GEMV workgroup w's TPRES_REGION and
+// call counter, so every call that touches region w is ordered by one counter and allreduce.hip's parity argument
+// holds -- then gathers the ranks' granules from its own buffer, sums them in rank order in fp32 and adds into h (and
+// the bf16 mirror). Bit-identical to the bf16 partial + car_reduce_kernel; one launch and one HBM round trip of the
+// partial fewer.
+constexpr int TPR_ELEMS = 4096;  // elements per workgroup: 2048 granules of 8 bytes = one TPRES_REGION
+static_assert(TPR_ELEMS / 2 * 8 == TPRES_REGION, "one fused-exchange region per workgroup");
+__global__ void __launch_bounds__(256)
+    gemm_reduce_tp_kernel(const float* __restrict__ ws, int ksplit, float* __restrict__ h, bf16_t* __restrict__ hb,
+                          int M, int N, const CarDevice* __restrict__ dev) {
+  const CarDevice& d = *dev;  // by reference (a by-value copy indexed with runtime p would live in scratch)
+  const int w = blockIdx.x;
+  const size_t slab4 = (size_t)M * N / 4;
+  __shared__ int s_calls;
+  if (threadIdx.x == 0) s_calls = __hip_atomic_load(d.wg_ctr + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  // this thread's 4 float4 groups (coalesced: group j covers threads' consecutive float4s); h loaded now, its round trip
+  // behind the exchange
+  u32x2 gq[4];
+  f32x4 hv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t e4 = (size_t)w * (TPR_ELEMS / 4) + j * 256 + threadIdx.x;
+    gq[j] = u32x2{0u, 0u};
+    hv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (e4 < slab4) {
+      const float4 v = sum_splits(ws, ksplit, slab4, e4);
+      gq[j] = u32x2{pack2bf(v.x, v.y), pack2bf(v.z, v.w)};
+      hv[j] = *reinterpret_cast<const f32x4*>(h + e4 * 4);
+    }
+  }
+  __syncthreads();
+  const int calls = s_calls;
+  const unsigned tag = gran_tag_fused(calls);
+  const long long wg_base = (long long)w * TPRES_REGION;
+  const long long par_base = (long long)(calls & 1) * d.world * d.max_bytes;
+  // granule (j, thread, half) at wg_base + ((j * 256 + thread) * 2 + half) * 8
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t e4 = (size_t)w * (TPR_ELEMS / 4) + j * 256 + threadIdx.x;
+    if (e4 >= slab4) continue;
+    const long long g = wg_base + (long long)(j * 256 + threadIdx.x) * 16;
+    for (int p = 0; p < d.world; ++p) {  // (8-byte stores: the unit the protocol relies on landing whole)
+      const __amdgpu_buffer_rsrc_t rp = rsrc(d.buf[p]);
+      const long long o = par_base + (long long)d.rank * d.max_bytes + g;
+      st_sys8(rp, o, u32x2{gq[j][0], tag});
+      st_sys8(rp, o + 8, u32x2{gq[j][1], tag});
+    }
+  }
+  const bool give_up = __hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+  const __amdgpu_buffer_rsrc_t mine = rsrc(d.buf[d.rank]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const size_t e4 = (size_t)w * (TPR_ELEMS / 4) + j * 256 + threadIdx.x;
+    if (e4 >= slab4) continue;
+    const long long g = wg_base + (long long)(j * 256 + threadIdx.x) * 16;
+    float sm[4] = {0.f, 0.f, 0.f, 0.f};
+    u32x4 r[CAR_MAX_WORLD];
+    car_gather16(d, mine, par_base + g, d.max_bytes, tag, give_up, r);
+#pragma unroll
+    for (int p = 0; p < CAR_MAX_WORLD; ++p) {
+      if (p < d.world) {
+        sm[0] += __uint_as_float(r[p][0] << 16);
+        sm[1] += __uint_as_float(r[p][0] & 0xffff0000u);
+        sm[2] += __uint_as_float(r[p][2] << 16);
+        sm[3] += __uint_as_float(r[p][2] & 0xffff0000u);
+      }
+    }
+    f32x4 n;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) n[i] = hv[j][i] + sm[i];
+    *reinterpret_cast<f32x4*>(h + e4 * 4) = n;
+    *reinterpret_cast<u32x2*>(hb + e4 * 4) = u32x2{pack2bf(n[0], n[1]), pack2bf(n[2], n[3])};
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(d.wg_ctr + w, calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+int gemm_tp_groups(int M, int N) { return (int)(((size_t)M * N + TPR_ELEMS - 1) / TPR_ELEMS); }
+
 // The 256 x 256 gemm2 runs the full-line x staging pipeline (FA) with each K-tile's weight loads issued between the
 // MFMAs (FAM = 2): 6-21 % faster than fragment-shaped x and 1-8 % faster than issuing the loads up front on the
 // Llama-3-8B projections (profiles/r1_gemm2_fullline_x_ab.jsonl, r1_gemm2_fam_ab.jsonl). The other pipeline forms
@@ -1396,6 +1478,11 @@ static int launch_reduce(const float* ws, int ksplit, void* out, int M, int N, i
       gemm_reduce_kernel<MODE_QKV><<<rgrid, 256, 0, s>>>(ws, ksplit, out, M, N, accumulate, 0, nullptr, qa, ssq, K,
                                                          eps);
       break;
+    case MODE_TPRESID:  // out = h (fp32 residual), mirror = hb, qkv->tp = the TP group's CarDevice
+      if (!qkv || !qa.tp || !mirror || ssq || (N & 3)) return -1;
+      gemm_reduce_tp_kernel<<<gemm_tp_groups(M, N), 256, 0, s>>>(ws, ksplit, static_cast<float*>(out), mirror, M, N,
+                                                                 static_cast<const CarDevice*>(qa.tp));
+      break;
     default: return -1;
   }
   JLA_CHECK_LAUNCH();
@@ -1444,7 +1531,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps, int tile, float* rms_ws, size_t rms_ws_floats) {
   if (tile == G5_TILE || tile == G5_TILE + 1) {
-    if (mode == MODE_ARGMAX || (rms_eps >= 0.f && mode == MODE_RESIDUAL)) return -1;
+    if (mode == MODE_ARGMAX || (rms_eps >= 0.f && (mode == MODE_RESIDUAL || mode == MODE_TPRESID))) return -1;
     return launch_g5(x, static_cast<const u32x4*>(W), out, M, N, K, mode, accumulate, out_f32, mirror, qkv, ws,
                      ws_floats, ksplit, rms_eps, tile, s);
   }
@@ -1463,6 +1550,7 @@ int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mod
   if (ksplit < 1) ksplit = 1;
   const int kc = (KS + ksplit - 1) / ksplit;
   ksplit = (KS + kc - 1) / kc;
+  if (mode == MODE_TPRESID && (ksplit == 1 || rms)) return -1;  // the exchange lives in the split-K reduce
   // qkv without a K split: the RoPE / KV-write epilogue of the default FA pipeline (256 x 256 tiles, fused norm)
   if (mode == MODE_QKV && ksplit == 1 && !(gemm_qkv_direct_ok(M, tile, K) && rms)) return -1;
   // the 256 x 128 / 192 tiles take the fused norm only as the precomputed statistic without a K split (launch_g4

@@ -214,24 +214,22 @@ JLA_DEV void skinny_epilogue(const f32x4 (&acc)[MT][NT], const float (&ss)[MT], 
       if (e >= MT * NT * 256 || (c & 1) || m >= M || nt0 + t >= NTT) continue;
       const long long g = wg_base + ((long long)m * (NT * 16) + t * 16 + c) * 4;
       float s0 = 0.f, s1 = 0.f;
-      for (int p = 0; p < d.world; ++p) {
-        const long long off = par_base + (long long)p * d.max_bytes + g;
-        u32x2 r = ld_sys8(mine, off);
-        if (r[1] != tag && !give_up) {  // slow path only: the common case is one load per granule
-          const long long t0 = (long long)wall_clock64();
-          while (r[1] != tag) {
-            if ((long long)wall_clock64() - t0 > d.timeout_ticks) {
-              __hip_atomic_store(d.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              break;
-            }
-            // another workgroup already gave up: stop too (one timeout per failure, not one per resident wave)
-            if (__hip_atomic_load(d.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-            __builtin_amdgcn_s_sleep(1);
-            r = ld_sys8(mine, off);
+      if constexpr (EPT <= 2) {  // every rank's granule in one round trip (the small-batch, latency-bound calls)
+        u32x2 r[CAR_MAX_WORLD];
+        car_gather8(d, mine, par_base + g, d.max_bytes, tag, give_up, r);
+#pragma unroll
+        for (int p = 0; p < CAR_MAX_WORLD; ++p) {
+          if (p < d.world) {
+            s0 += __uint_as_float(r[p][0] << 16);
+            s1 += __uint_as_float(r[p][0] & 0xffff0000u);
           }
         }
-        s0 += __uint_as_float(r[0] << 16);
-        s1 += __uint_as_float(r[0] & 0xffff0000u);
+      } else {  // (more elements per thread: the gather's registers would spill; one round trip per rank)
+        for (int p = 0; p < d.world; ++p) {
+          const u32x2 r = car_granule(d, mine, par_base + (long long)p * d.max_bytes + g, tag, give_up);
+          s0 += __uint_as_float(r[0] << 16);
+          s1 += __uint_as_float(r[0] & 0xffff0000u);
+        }
       }
       const int col = (nt0 + t) * 16 + c;
       const size_t idx = (size_t)m * N + col;

@@ -83,6 +83,10 @@ size_t gemm_workspace_floats(int M, int N, int K);
 // (fused RMSNorm; not for MODE_RESIDUAL); split-K then needs ws >= ksplit * M * (N + 1) floats.
 // tile: gemm2 tile config 1 = 256x256, 2 = 128x256, 3 = 128x128, 0 = by M; 7 / 10 gemm4 (256 x 256 / 256 x 128),
 // 8 gemm4 exchange split (above), 11 / 12 gemm5
+// workgroups (= fused-exchange regions and call counters) of gemm()'s MODE_TPRESID reduce at M x N: the row-parallel
+// projection's split-K reduce with the TP all-reduce and residual add in its epilogue (out = h, mirror = hb,
+// qkv->tp = the group's CarDevice; split plans only)
+int gemm_tp_groups(int M, int N);
 int gemm(const bf16_t* x, const void* W, void* out, int M, int N, int K, int mode, int accumulate, int out_f32,
          bf16_t* mirror, const QKVArgs* qkv, float* ws, size_t ws_floats, int ksplit, hipStream_t s,
          float rms_eps = -1.f, int tile = 0, float* rms_ws = nullptr, size_t rms_ws_floats = 0);

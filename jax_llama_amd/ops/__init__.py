@@ -293,6 +293,22 @@ def linear_tp_residual(x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, st
     return h
 
 
+def tiled_tp_residual(x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor, state: int) -> bool:
+    """Row-parallel tiled projection with the all-reduce in its split-K reduce (csrc/kernels/gemm.hip
+    gemm_reduce_tp_kernel): ``h (fp32) += sum over the TP group of x @ W^T``, ``hb = bf16(h)``. Bit-identical to
+    ``linear`` (bf16 partial) + ``TPComm.all_reduce_residual_``. Runs the tuned plan of the unfused partial GEMM; False
+    (nothing done) when that plan has no K split (the exchange lives in the reduce)."""
+    e = ext()
+    m = x.shape[0]
+    assert x.dtype == BF16 and x.is_contiguous(), (x.dtype, x.shape)
+    ks, tm = autotune.choose_gemm_plan(e, m, w.n, w.k, x.device, MODE_STORE, False)
+    if tm not in G5_TILES and ks <= 1:
+        return False
+    ks, tm, ws = _gemm_ws(e, m, w.n, w.k, x.device, MODE_STORE, False)
+    e.gemm_tp_residual(state, x, w.weight, w.n, w.k, h, hb, ks, ws, tm)
+    return True
+
+
 TILED = 7  # decode-kernel "variant" id of the 128x128 MFMA GEMM (split-K for mid M)
 # qkv projection without a K split (B = 2048 decode, prefill): RoPE + KV write in the GEMM epilogue (JLA_QKV_DIRECT=0:
 # plain GEMM + rope_kv_kernel, for A/B)

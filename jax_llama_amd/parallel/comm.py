@@ -28,6 +28,9 @@ import torch.distributed as dist
 # GEMV-fused row-parallel all-reduce at decode (csrc/kernels/gemv.hip MODE_TPRESID); JLA_TP_FUSED=0: a separate
 # collective kernel after each row-parallel GEMV
 FUSED = os.environ.get("JLA_TP_FUSED", "1") != "0"
+# ... and past the GEMV's 64 rows, in the tiled GEMM's split-K reduce (gemm.hip gemm_reduce_tp_kernel);
+# JLA_TP_FUSED_TILED=0: GEMM partial + the collective kernel
+FUSED_TILED = os.environ.get("JLA_TP_FUSED_TILED", "1") != "0"
 # prefill-sized row-parallel partials over RCCL in bf16 (half the bytes, bf16 accumulation) instead of fp32
 RCCL_BF16 = os.environ.get("JLA_TP_RCCL_BF16", "0") == "1"
 
@@ -146,10 +149,16 @@ class TPComm:
         done) otherwise -- the caller then runs ``linear`` + ``all_reduce_residual_``."""
         f = self.fused
         if (f is None or self.size == 1 or self.reduce_dtype != torch.bfloat16 or not x.is_cuda
-                or x.dtype != torch.bfloat16 or not f.can_fuse(x.shape[0], w.n)):
+                or x.dtype != torch.bfloat16):
             return False
-        f.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=hb_pack)
-        return True
+        m = x.shape[0]
+        if f.can_fuse(m, w.n):
+            f.linear_residual_(x, w, h, hb, x_packed=x_packed, hb_pack=hb_pack)
+            return True
+        # past the GEMV's rows: the tiled GEMM's split-K reduce runs the exchange (when its plan splits K)
+        if FUSED_TILED and hb_pack is None and m > 64 and f.can_fuse_tiled(m, w.n):
+            return f.tiled_residual_(x, w, h, hb)
+        return False
 
     def fused_o_state(self, x: torch.Tensor, w) -> Optional[int]:
         """The custom all-reduce state a fused decode launch's o projection exchanges its partials through (the GEMV

@@ -281,6 +281,20 @@ class CustomAllReduce:
         with ops.autotune.tp_scope(self):
             ops.linear_tp_residual(x, w, h, hb, self._live(), x_packed=x_packed, hb_pack=hb_pack)
 
+    def can_fuse_tiled(self, m: int, n: int) -> bool:
+        """The tiled GEMM's fused path (decode batches past the GEMV's rows): one region + counter per 4096 output
+        elements (csrc/kernels/gemm.hip gemm_reduce_tp_kernel)."""
+        groups = (m * n + 4095) // 4096
+        return (m > 0 and n % 4 == 0 and groups <= self.WG_COUNTERS and groups * self.TPRES_REGION <= self.max_bytes
+                and (self.share == 1 or self.share * groups <= self.SHARED_MAX_GROUPS))
+
+    def tiled_residual_(self, x: torch.Tensor, w, h: torch.Tensor, hb: torch.Tensor) -> bool:
+        """``h += sum_ranks(x @ W^T)``, ``hb = bf16(h)`` with the exchange in the split-K reduce of the tiled GEMM.
+        False (nothing done) when the tuned plan for this shape has no K split. Rank 0 picks the plan."""
+        from .. import ops
+        with ops.autotune.tp_scope(self):
+            return ops.tiled_tp_residual(x, w, h, hb, self._live())
+
     @staticmethod
     def fused_bytes(hidden: int) -> int:
         """Slot bytes the fused path needs for a row-parallel output of ``hidden`` columns."""

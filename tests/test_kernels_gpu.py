@@ -1031,3 +1031,49 @@ def test_qkv_attention_fused_o_projection(b, t, slot, spl, nt, tp):
     att = ref.attention(q.reshape(b, 1, h_, dh), kcr, vcr, slot, kv_start).reshape(b, h_ * dh)
     _close(a, att, 2e-2, 2e-2)
     _close(hd, h0 + a.float().cpu() @ wo.float().t(), 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("m,n,k,ks,tile", [(96, 1024, 512, 2, 7), (256, 8192, 3584, 4, 7), (200, 2048, 1024, 3, 1),
+                                           (130, 4096, 1024, 2, 11), (65, 512, 256, 2, 17)])
+def test_tiled_tp_residual_fused_reduce(m, n, k, ks, tile):
+    """Row-parallel tiled projection with the TP all-reduce and residual add in its split-K reduce (gemm.hip
+    gemm_reduce_tp_kernel, MODE_TPRESID) on a world-1 fused instance: bit-identical h and mirror to the same plan's
+    bf16 partial + the standalone residual all-reduce (car_reduce_kernel), over several calls (both parities,
+    counters advancing) and interleaved with the GEMV's fused epilogue on the same counters; and h + x @ W^T of the
+    fp32 reference within bf16 tolerance. Includes the Llama-3-70B MP 8 down projection at B = 256 and a gemm5 plan."""
+    from jax_llama_amd.parallel.custom_allreduce import CustomAllReduce
+    e = ops.ext()
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    w = PackedLinear.random(n, k, DEV, 0.02, g)
+    x = (torch.randn(m, k, device=DEV, generator=g)).to(BF16)
+    h0 = torch.randn(m, n, device=DEV, generator=g)
+    fused = CustomAllReduce.local(max_bytes=CustomAllReduce.fused_bytes(max(n, 8192)))
+    coll = CustomAllReduce.local(max_bytes=16 << 20)
+    try:
+        assert fused.can_fuse_tiled(m, n)
+        g5 = tile in (11, 12)
+        wsn = (e.gemm5_ksplit(k, ks) if g5 else ks) * m * (n + 1)
+        ws = torch.empty(wsn, dtype=torch.float32, device=DEV)
+        hs = torch.randn(16, 512, device=DEV, generator=g)
+        xs = torch.randn(16, 512, device=DEV, generator=g).to(BF16)
+        ws_small = PackedLinear.random(512, 512, DEV, 0.02, g)
+        for rep in range(3):
+            h1, h2 = h0.clone(), h0.clone()
+            hb1 = torch.empty(m, n, dtype=BF16, device=DEV)
+            hb2 = torch.empty_like(hb1)
+            e.gemm_tp_residual(fused._live(), x, w.weight, n, k, h1, hb1, ks, ws, tile)
+            part = torch.empty(m, n, dtype=BF16, device=DEV)
+            e.gemm(x, w.weight, n, k, part, ops.MODE_STORE, True, None, ks, ws, -1.0, tile)
+            coll.all_reduce_residual_(part, h2, hb2)
+            torch.cuda.synchronize()
+            assert torch.equal(h1, h2) and torch.equal(hb1, hb2), rep
+            # a GEMV call with the fused epilogue on the same instance (shared per-workgroup counters)
+            hsb = torch.empty(16, 512, dtype=BF16, device=DEV)
+            ops.linear_tp_residual(xs, ws_small, hs, hsb, fused._live())
+        torch.cuda.synchronize()
+        assert fused.error() == 0 and coll.error() == 0
+    finally:
+        fused.close()
+        coll.close()
+    want = h0.cpu() + x.float().cpu() @ w.dense().float().cpu().t()
+    _close(h1, want, 2e-2, 2e-2)

@@ -62,7 +62,8 @@ def _gpu_params(cfg, seed):
 def _fused_row_parallel_check(comm, rank, n):
     """GEMV-fused row-parallel all-reduce (csrc/kernels/gemv.hip MODE_TPRESID) vs linear + the standalone residual
     all-reduce: bit-identical h, mirror and packed mirror at every decode m-tile count, row-major and packed x
-    inputs, over several calls (both parities, counters advancing)."""
+    inputs, over several calls (both parities, counters advancing); then the tiled GEMM's fused reduce at 96 / 160
+    rows."""
     from jax_llama_amd import ops
     from jax_llama_amd.models.weights import PackedLinear
     g = torch.Generator(device="cuda").manual_seed(100 + rank)
@@ -89,6 +90,25 @@ def _fused_row_parallel_check(comm, rank, n):
             torch.cuda.synchronize()
             ok = ok and torch.equal(h1, h2) and torch.equal(hb1, hb2) and torch.equal(pk1, pk2)
     ops.GEMV_VARIANT = saved
+    # past the GEMV's rows: the exchange in the tiled GEMM's split-K reduce (gemm.hip gemm_reduce_tp_kernel) vs the
+    # same plan's bf16 partial + the standalone residual all-reduce
+    e = ops.ext()
+    for m, tile in ((96, 1), (160, 7)):
+        if not comm.fused.can_fuse_tiled(m, n):
+            continue
+        x = torch.randn(m, n, device="cuda", generator=g).to(torch.bfloat16)
+        ws = torch.empty(2 * m * (n + 1), dtype=torch.float32, device="cuda")
+        h0 = torch.randn(m, n, device="cuda", generator=g)
+        for rep in range(2):
+            h1, h2 = h0.clone(), h0.clone()
+            hb1 = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            hb2 = torch.empty_like(hb1)
+            e.gemm_tp_residual(comm.fused._live(), x, w.weight, n, n, h1, hb1, 2, ws, tile)
+            part = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            e.gemm(x, w.weight, n, n, part, ops.MODE_STORE, True, None, 2, ws, -1.0, tile)
+            comm.all_reduce_residual_(part, h2, hb2)
+            torch.cuda.synchronize()
+            ok = ok and torch.equal(h1, h2) and torch.equal(hb1, hb2)
     return bool(ok)
 
 

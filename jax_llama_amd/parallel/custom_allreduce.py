@@ -164,7 +164,8 @@ class CustomAllReduce:
         must fall back to RCCL, not corrupt a generation): ``rounds`` rounds of every path with rank- and
         round-dependent data, every word checked exactly on the host. ``collective``: granule one-shot (fp32 sum
         and the bf16 residual epilogue), flag one-shot (> the granule limit), two-shot, and the (value, index) pair
-        gather; ``fused``: the GEMV-fused row-parallel exchange (gemv.hip MODE_TPRESID). The verdict and the paths
+        gather; ``fused``: the GEMV-fused row-parallel exchange (gemv.hip MODE_TPRESID) and the tiled GEMM's fused reduce
+        (gemm.hip gemm_reduce_tp_kernel). The verdict and the paths
         checked are kept in ``self.litmus``."""
         rounds = self.LITMUS_ROUNDS if rounds is None else rounds
         world, rank = self.world, self.rank
@@ -194,6 +195,19 @@ class CustomAllReduce:
                 self.linear_residual_(x, w, h, hb)
                 ok = ok and torch.equal(h.cpu(), want) and torch.equal(hb.cpu(), want.to(torch.bfloat16))
                 paths = ["fused_gemv"]
+                # the tiled GEMM's split-K reduce with the exchange (gemm.hip gemm_reduce_tp_kernel: 16-byte gathers)
+                mt = 96
+                if self.can_fuse_tiled(mt, n):
+                    from .. import ops
+                    xt = torch.ones(mt, k, dtype=torch.bfloat16, device="cuda")
+                    ht = (torch.arange(mt * n, dtype=torch.float32) % 13).reshape(mt, n).cuda()
+                    hbt = torch.empty(mt, n, dtype=torch.bfloat16, device="cuda")
+                    ws = torch.empty(2 * mt * (n + 1), dtype=torch.float32, device="cuda")
+                    ops.ext().gemm_tp_residual(self._live(), xt, w.weight, n, k, ht, hbt, 2, ws, 1)
+                    wt = (torch.arange(mt * n, dtype=torch.float32) % 13).reshape(mt, n) + sum(
+                        wmat(r).float().sum(1) for r in range(world))[None, :]
+                    ok = ok and torch.equal(ht.cpu(), wt) and torch.equal(hbt.cpu(), wt.to(torch.bfloat16))
+                    paths = ["fused_gemv", "fused_tiled_reduce"]
                 continue
             # granule one-shot (fp32 sum), flag one-shot (fp32, above the granule limit), two-shot (forced)
             for name, n, ts in (("granule", 16 * 1024, False), ("flag", 192 * 1024, False), ("two_shot", 64 * 1024, True)):

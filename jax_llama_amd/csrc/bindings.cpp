@@ -321,7 +321,7 @@ void linear_qkv_attn(Tensor x, Tensor w, int64_t n, int64_t k, double rms_eps, T
         "sync int32 [qkv_attn_sync_ints()]");
   check(t_cap <= kc.size(2), "t_cap <= cache length");
   const jla::bf16_t* xp = packed_ptr(x_packed, m, k, "x_packed");
-  check(spl >= 1 && spl <= 4 && (spl <= 2 || m <= 16), "linear_qkv_attn: spl 1..4 (3 / 4 at M <= 16)");
+  check(spl == 1 || spl == 2, "linear_qkv_attn: spl 1 or 2");
   if (spl > 1) {  // the split qkv GEMV's slabs + tickets (skinny_workspace)
     check(sk_ws.has_value() && sk_tk.has_value(), "linear_qkv_attn spl 2: sk_ws and sk_tk (skinny_workspace)");
     check_gpu(*sk_ws, "sk_ws");

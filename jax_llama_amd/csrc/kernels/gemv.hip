@@ -1047,16 +1047,13 @@ int qkv_attn_occupancy(int M, int rep, int spl, int o_groups) {
     if (g_qa_o_nt == 1) return spl == 2 ? qkv_attn_per_cu_o<2, 1>() : qkv_attn_per_cu_o<1, 1>();
     return spl == 2 ? qkv_attn_per_cu_o<2, 2>() : qkv_attn_per_cu_o<1, 2>();
   }
-  if (spl == 4) return M <= 16 ? qkv_attn_per_cu_rep<1, 4>(rep) : 0;  // (K over 3 / 4: one m-tile only)
-  if (spl == 3) return M <= 16 ? qkv_attn_per_cu_rep<1, 3>(rep) : 0;
   if (spl == 2) return M <= 16 ? qkv_attn_per_cu_rep<1, 2>(rep) : qkv_attn_per_cu_rep<2, 2>(rep);
   return M <= 16 ? qkv_attn_per_cu_rep<1, 1>(rep) : qkv_attn_per_cu_rep<2, 1>(rep);
 }
 int qkv_attn_splits(int M, int B, int Hkv, int rep, int t_cap, int N, int cus, int spl, int o_groups) {
   if (M != B || M > 32 || (rep & (rep - 1)) || rep > 16 || t_cap > QA_MAX_SPLITS * QA_SPLIT_KEYS) return 0;
-  if (spl < 1 || spl > 4 || (spl > 2 && (M > 16 || o_groups > 0)) || (spl > 1 && (N >> 4) > GEMV_SPLIT_MAX_GROUPS) ||
-      o_groups < 0)
-    return 0;
+  // (K over 3 / 4 workgroups measured slower than 2 at the 70B shard's B = 1: profiles/r6_qkv_attn_o_timeline.jsonl)
+  if ((spl != 1 && spl != 2) || (spl > 1 && (N >> 4) > GEMV_SPLIT_MAX_GROUPS) || o_groups < 0) return 0;
   const int splits = (t_cap + QA_SPLIT_KEYS - 1) / QA_SPLIT_KEYS;
   const int grid = (N >> 4) * spl + B * Hkv * splits + o_groups;
   return grid <= cus * qkv_attn_occupancy(M, rep, spl, o_groups) ? splits : 0;
@@ -1075,7 +1072,7 @@ int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float r
   if (M > 32 || (N & 15) || (K & 31) || qa.Dh != AD6_DH || qa.S != 1 || qa.H % qa.Hkv) return -1;
   const int rep = qa.H / qa.Hkv;
   const int grid_q = (N >> 4) * spl, pairs = M * qa.Hkv;
-  if (spl < 1 || spl > 4 || (spl > 2 && M > 16)) return -1;
+  if (spl != 1 && spl != 2) return -1;
   if (spl > 1) {  // the split GEMV's slabs and tickets (as launch_skinny checks them)
     const int mt0 = M <= 16 ? 1 : 2;
     if ((N >> 4) > GEMV_SPLIT_MAX_GROUPS || !qa.sk_ws || !qa.sk_tk || (K >> 5) < spl ||
@@ -1125,10 +1122,8 @@ int linear_qkv_attn(const bf16_t* x, const void* W, int M, int N, int K, float r
 #define JLA_QA_S(MTV, R, SP) \
   if (mt == MTV && rep == R && spl == SP) JLA_QA_K(MTV, R, SP, 0, 0)
 #define JLA_QA(MTV, R) JLA_QA_S(MTV, R, 1) JLA_QA_S(MTV, R, 2)
-#define JLA_QA1(R) JLA_QA(1, R) JLA_QA_S(1, R, 3) JLA_QA_S(1, R, 4)
-  JLA_QA1(1) JLA_QA1(2) JLA_QA1(4) JLA_QA1(8) JLA_QA1(16)
+  JLA_QA(1, 1) JLA_QA(1, 2) JLA_QA(1, 4) JLA_QA(1, 8) JLA_QA(1, 16)
   JLA_QA(2, 1) JLA_QA(2, 2) JLA_QA(2, 4) JLA_QA(2, 8) JLA_QA(2, 16)
-#undef JLA_QA1
 #undef JLA_QA
 #undef JLA_QA_S
 #undef JLA_QA_K

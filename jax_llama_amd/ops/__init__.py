@@ -502,8 +502,8 @@ def linear_qkv_rope(x: torch.Tensor, w, rms_eps: Optional[float], table: torch.T
 # =2: wherever the launch fits.
 QKV_ATTN = int(os.environ.get("JLA_QKV_ATTN", "1"))
 # K of the fused launch's qkv GEMV over 2 workgroups per column group (the split GEMV's last-arriver sum) when the grid
-# still fits the CUs; JLA_QKV_ATTN_SPL=1: one workgroup per column group; 3 / 4: more splits (M <= 16), which lost at
-# the 70B shard's B = 1: 4.73 (2) vs 4.84 (3) / 4.87 (4) ms per token (profiles/r6_qkv_attn_o_timeline.jsonl)
+# still fits the CUs; JLA_QKV_ATTN_SPL=1: one workgroup per column group (3 / 4 splits were built and lost at the 70B
+# shard's B = 1: 4.84 / 4.87 vs 4.73 ms per token, profiles/r6_qkv_attn_o_timeline.jsonl, and were removed)
 QKV_ATTN_SPL = int(os.environ.get("JLA_QKV_ATTN_SPL", "2"))
 # ... and the o projection in the same launch (its workgroups fetch their Wo slice while qkv / attention run, then wait
 # for the attention output; the residual or TP-exchange epilogue of the standalone GEMV): M <= 16, 8 query heads per kv
@@ -566,12 +566,9 @@ def qkv_attention_splits(x: torch.Tensor, w, k_cache: torch.Tensor, seq_len: int
 
 
 def _qkv_attention_spl(e, m, w, k_cache, n_heads, n_kv_heads, device, o_groups=0) -> int:
-    """K of the fused launch's qkv GEMV over QKV_ATTN_SPL workgroups per column group, or the most below it whose
-    grid still fits the CUs at once."""
-    for spl in range(min(max(QKV_ATTN_SPL, 1), 4), 1, -1):
-        if e.qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n, _num_cus(device), spl,
-                             int(o_groups)) > 0:
-            return spl
+    if QKV_ATTN_SPL > 1 and e.qkv_attn_splits(m, m, n_kv_heads, n_heads // n_kv_heads, k_cache.shape[2], w.n,
+                                               _num_cus(device), 2, int(o_groups)) > 0:
+        return 2
     return 1
 
 

@@ -137,3 +137,52 @@ def test_autotune_table_persists(tmp_path, monkeypatch):
     assert autotune._persisted("gemv", key) == 9
     assert autotune._persisted("gemm", (2048, 4096, 4096, 1, False)) == (2, 1)
     assert autotune._persisted("gemm", (1, 2, 3, 0, False)) is None
+
+
+def test_fused_row_parallel_routing():
+    """Which row-parallel path a decode projection takes (parallel/comm.py linear_residual_, fused_o_state): the GEMV's
+    fused epilogue up to 64 rows, the tiled GEMM's fused split-K reduce past them while the output fits the instance's
+    exchange regions (one per 4096 elements; ranks sharing a device: all their workgroups resident at once), else
+    nothing (the caller's partial + collective); the fused decode launch's o projection exchanges through the same
+    instance (0 at world 1). Routing only: the kernels are GPU-tested (test_tp_gpu.py, test_kernels_gpu.py)."""
+    from jax_llama_amd.parallel.comm import TPComm
+    from jax_llama_amd.parallel.custom_allreduce import CustomAllReduce
+
+    calls = []
+
+    class FakeFused(CustomAllReduce):
+        def __init__(self, max_bytes, share=1):  # no device state: the capability checks are host arithmetic
+            self.max_bytes, self.share, self.state, self.failed = max_bytes, share, 7, False
+
+        def linear_residual_(self, *a, **k):
+            calls.append("gemv")
+
+        def tiled_residual_(self, *a, **k):
+            calls.append("tiled")
+            return True
+
+    class W:
+        n, k = 8192, 3584
+
+    f = FakeFused(CustomAllReduce.fused_bytes(8192))
+    assert f.can_fuse(64, 8192) and not f.can_fuse(65, 8192)
+    assert f.can_fuse_tiled(256, 8192) and not f.can_fuse_tiled(257, 8192)  # 512 regions of 16 KiB = 8 MiB
+    assert not FakeFused(CustomAllReduce.fused_bytes(8192), share=2).can_fuse_tiled(256, 8192)
+    assert FakeFused(CustomAllReduce.fused_bytes(8192), share=2).can_fuse_tiled(64, 4096)
+    comm = TPComm(size=8, rank=0, group=None, custom=None, reduce_dtype=torch.bfloat16, fused=f)
+
+    class X:  # a decode activation's attributes as the routing reads them
+        is_cuda, dtype = True, torch.bfloat16
+
+        def __init__(self, m):
+            self.shape = (m, 3584)
+
+    for m, want in ((1, "gemv"), (64, "gemv"), (128, "tiled"), (256, "tiled")):
+        calls.clear()
+        assert comm.linear_residual_(X(m), W(), None, None) is True and calls == [want], (m, calls)
+    calls.clear()
+    assert comm.linear_residual_(X(300), W(), None, None) is False and calls == []
+    assert comm.fused_o_state(X(1), W()) == 7
+    assert TPComm(size=1, rank=0, group=None).fused_o_state(X(1), W()) == 0
+    assert TPComm(size=8, rank=0, group=None, custom=None, reduce_dtype=torch.bfloat16,
+                  fused=None).fused_o_state(X(1), W()) is None

@@ -583,8 +583,10 @@ static int dispatch_tp(const void* x, const void* W, void* out, int M, int N, in
 // workgroup then polls the qkv-done counter (every qkv workgroup adds to it once its write-through q / K / V stores
 // have drained), the waves load the pair's q and re-load the one cache row this launch wrote (write-through loads),
 // score their step, merge through LDS, and the pair's splits merge by last arriver (write-through partials + ticket).
-// Co-residency: the host launches this only when every workgroup fits on the CUs at once (grid <= CUs), so the
-// attention workgroups' waits always end; each wait is also bounded (the error word records a timeout).
+// Optionally (FO > 0) a third kind on the last workgroups runs the o projection into the residual (qa_o_proj), waiting
+// on go flags the last attention workgroup sets. Every wait is on lower-numbered workgroups (dispatched first), and the
+// host launches this only when every workgroup fits on the CUs at once (grid <= CUs x the occupancy API's count), so
+// the waits always end; each is also bounded (the error word records a timeout).
 constexpr int QA_SPLIT_KEYS = 128;  // keys per attention workgroup (4 waves x one 32-key step)
 constexpr int QA_MAX_SPLITS = 4;    // attention workgroups per (row, kv head) pair: cache length <= 512
 constexpr int QA_PART = AD6_DH + 4; // floats per (split, head) partial: O[128], m, l, pad

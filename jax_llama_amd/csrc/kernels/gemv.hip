@@ -707,12 +707,9 @@ JLA_DEV void qa_attention(const QKVArgs& qa, const FusedAttn& fa, int a) {
   }
 
   // 3. the pair's q (written by this launch: write-through loads) and the cache row at `slot` (K lanes holding that
-  //    key / V DMA lanes of that row re-load it agent-coherently; each conditional load is drained in its own block,
-  //    so no merge of an in-flight register)
+  //    key / V DMA lanes of that row re-load it agent-coherently), all issued before one wait: one round trip, not
+  //    three (tools/check_asm_ring.py verifies no in-flight register is copied across the conditional re-loads)
   u32x4 qf[4];
-  ad6_load_q<REP, true>(qf, qa.q + ((size_t)b * qa.H + kvh * REP) * AD6_DH, lane);
-  ::wait_vmcnt<0>();  // q: nothing in flight before the conditional re-loads
-  ad6_q_ready<REP>(qf, lane);
   {
     const int key0 = k0;
     const int c = lane >> 4, j = lane & 15;
@@ -722,7 +719,6 @@ JLA_DEV void qa_attention(const QKVArgs& qa, const FusedAttn& fa, int a) {
         const bf16_t* p = kb + (size_t)slot * AD6_DH + 8 * c;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) asm_load_sc1(kr[4 * kk + jj], p + 32 * jj);
-        ::wait_vmcnt<0>();
       }
     }
     const int vrow = slot - key0;  // 0 .. 31 when the new row is in this wave's step
@@ -735,7 +731,11 @@ JLA_DEV void qa_attention(const QKVArgs& qa, const FusedAttn& fa, int a) {
       }
     }
   }
+  ad6_load_q<REP, true>(qf, qa.q + ((size_t)b * qa.H + kvh * REP) * AD6_DH, lane);
   ::wait_vmcnt<0>();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pin(kr[i]);
+  ad6_q_ready<REP>(qf, lane);
 
   // 4. this wave's step, then its (m, l, O)
   Ad6Acc st;

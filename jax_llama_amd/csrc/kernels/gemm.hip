@@ -671,33 +671,33 @@ __global__ void __launch_bounds__(256 * WM)
       __syncthreads();  // the half-tile is consumed before the other wave row overwrites it
     }
   } else {
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
+    auto piece = [&](int i, int r, int j) {
       const int tile = (n0 >> 4) + wc * NTW + j;
-      if (tile >= NTT) continue;
-      const int col = tile * 16 + c;
+      const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
+      if (tile >= NTT || row >= M) return;
+      const size_t idx = (size_t)row * N + tile * 16 + c;
+      const float v = acc[i][j][r];
+      if constexpr (MODE == MODE_PARTIAL) {
+        static_cast<float*>(out)[(size_t)split * M * N + idx] = v;
+      } else if constexpr (MODE == MODE_RESIDUAL) {
+        float* o = static_cast<float*>(out);
+        const float nv = accumulate ? o[idx] + v : v;
+        o[idx] = nv;
+        if (mirror) mirror[idx] = f2bf(nv);
+      } else if (out_f32) {
+        static_cast<float*>(out)[idx] = v;
+      } else {
+        static_cast<bf16_t*>(out)[idx] = f2bf(v);
+      }
+    };
+    // rows outer, n-tiles inner: a row's adjacent 64-byte pieces back to back (as gemm4's fp32 epilogue; 2-4 % on the
+    // split qkv / gate_up slabs and the residual o, profiles/r6_g2_epilogue_order_ab.jsonl)
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
-          if (row >= M) continue;
-          const size_t idx = (size_t)row * N + col;
-          const float v = acc[i][j][r];
-          if constexpr (MODE == MODE_PARTIAL) {
-            static_cast<float*>(out)[(size_t)split * M * N + idx] = v;
-          } else if constexpr (MODE == MODE_RESIDUAL) {
-            float* o = static_cast<float*>(out);
-            const float nv = accumulate ? o[idx] + v : v;
-            o[idx] = nv;
-            if (mirror) mirror[idx] = f2bf(nv);
-          } else if (out_f32) {
-            static_cast<float*>(out)[idx] = v;
-          } else {
-            static_cast<bf16_t*>(out)[idx] = f2bf(v);
-          }
-        }
-    }
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) piece(i, r, j);
   }
 }
 
@@ -916,27 +916,28 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
       });
     }
   } else {  // PARTIAL / RESIDUAL: fp32, one 16-byte piece per lane per tile
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
+    // rows outer, tiles inner: consecutive instructions take the two 64-byte halves of each 128-byte line of h (and the
+    // adjacent 32-byte pieces of the mirror's line) back to back -- 4-7 % faster than tiles outer on the o projection,
+    // 1.5-3.5 % on down, M = 4096 and 32768 (profiles/r6_g4_epilogue_order_ab.jsonl)
+    auto piece = [&](int j, int i) {
       const int tile = (n0 >> 4) + wc * NJ + j;
-      if (tile >= NTT) continue;
-      const int col = tile * 16 + 4 * q;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = rbase + 16 * i;
-        if (row >= M) continue;
-        const size_t idx = (size_t)row * N + col;
-        const f32x4 v = tile_val(j, i);
-        if constexpr (MODE == MODE_PARTIAL) {
-          *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = v;
-        } else {
-          f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(out) + idx);
-          const f32x4 nv = accumulate ? *o + v : v;
-          *o = nv;
-          if (mirror) *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
-        }
+      const int row = rbase + 16 * i;
+      if (tile >= NTT || row >= M) return;
+      const size_t idx = (size_t)row * N + tile * 16 + 4 * q;
+      const f32x4 v = tile_val(j, i);
+      if constexpr (MODE == MODE_PARTIAL) {
+        *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = v;
+      } else {
+        f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(out) + idx);
+        const f32x4 nv = accumulate ? *o + v : v;
+        *o = nv;
+        if (mirror) *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
       }
-    }
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) piece(j, i);
   }
 }
 

@@ -112,6 +112,8 @@ __global__ void __launch_bounds__(256) rms_rowinv_kernel(const bf16_t* __restric
   if (row >= M) return;
   const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * D);
   float s0 = 0.f, s1 = 0.f;
+  // 4 of the row's 16-byte pieces per lane in flight at once (D = 4096: all 8 in two round trips, not eight)
+#pragma unroll 4
   for (int i = lane; i < D / 8; i += 64) {
     const u32x4 v = xr[i];
 #pragma unroll

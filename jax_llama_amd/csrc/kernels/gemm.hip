@@ -671,33 +671,50 @@ __global__ void __launch_bounds__(256 * WM)
       __syncthreads();  // the half-tile is consumed before the other wave row overwrites it
     }
   } else {
-    auto piece = [&](int i, int r, int j) {
-      const int tile = (n0 >> 4) + wc * NTW + j;
-      const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
-      if (tile >= NTT || row >= M) return;
-      const size_t idx = (size_t)row * N + tile * 16 + c;
-      const float v = acc[i][j][r];
-      if constexpr (MODE == MODE_PARTIAL) {
-        static_cast<float*>(out)[(size_t)split * M * N + idx] = v;
-      } else if constexpr (MODE == MODE_RESIDUAL) {
-        float* o = static_cast<float*>(out);
-        const float nv = accumulate ? o[idx] + v : v;
-        o[idx] = nv;
-        if (mirror) mirror[idx] = f2bf(nv);
-      } else if (out_f32) {
-        static_cast<float*>(out)[idx] = v;
-      } else {
-        static_cast<bf16_t*>(out)[idx] = f2bf(v);
-      }
-    };
     // rows outer, n-tiles inner: a row's adjacent 64-byte pieces back to back (as gemm4's fp32 epilogue; 2-4 % on the
-    // split qkv / gate_up slabs and the residual o, profiles/r6_g2_epilogue_order_ab.jsonl)
+    // split qkv / gate_up slabs and the residual o, profiles/r6_g2_epilogue_order_ab.jsonl); residual: the m-tile's h
+    // values loaded before any is used (one round trip per m-tile, not per value)
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i) {
+      float hv[4][NTW];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) piece(i, r, j);
+        for (int j = 0; j < NTW; ++j) hv[r][j] = 0.f;
+      if constexpr (MODE == MODE_RESIDUAL) {
+        if (accumulate) {  // (unconditional loads at clamped addresses: no per-load branch and join wait)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < NTW; ++j) {
+              const int tile = min((n0 >> 4) + wc * NTW + j, NTT - 1);
+              const int row = min(m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r, M - 1);
+              hv[r][j] = static_cast<const float*>(out)[(size_t)row * N + tile * 16 + c];
+            }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          const int tile = (n0 >> 4) + wc * NTW + j;
+          const int row = m0 + (wr * MT + i) * 16 + 4 * (lane >> 4) + r;
+          if (tile >= NTT || row >= M) continue;
+          const size_t idx = (size_t)row * N + tile * 16 + c;
+          const float v = acc[i][j][r];
+          if constexpr (MODE == MODE_PARTIAL) {
+            static_cast<float*>(out)[(size_t)split * M * N + idx] = v;
+          } else if constexpr (MODE == MODE_RESIDUAL) {
+            const float nv = hv[r][j] + v;
+            static_cast<float*>(out)[idx] = nv;
+            if (mirror) mirror[idx] = f2bf(nv);
+          } else if (out_f32) {
+            static_cast<float*>(out)[idx] = v;
+          } else {
+            static_cast<bf16_t*>(out)[idx] = f2bf(v);
+          }
+        }
+    }
   }
 }
 
@@ -919,25 +936,39 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
     // rows outer, tiles inner: consecutive instructions take the two 64-byte halves of each 128-byte line of h (and the
     // adjacent 32-byte pieces of the mirror's line) back to back -- 4-7 % faster than tiles outer on the o projection,
     // 1.5-3.5 % on down, M = 4096 and 32768 (profiles/r6_g4_epilogue_order_ab.jsonl)
-    auto piece = [&](int j, int i) {
-      const int tile = (n0 >> 4) + wc * NJ + j;
+    // residual: a row's h pieces of every tile are loaded before any is used -- with the stores in between (which may
+    // alias h as far as hipcc knows) the loads were issued one at a time, a full memory round trip per 16-byte piece
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
       const int row = rbase + 16 * i;
-      if (tile >= NTT || row >= M) return;
-      const size_t idx = (size_t)row * N + tile * 16 + 4 * q;
-      const f32x4 v = tile_val(j, i);
-      if constexpr (MODE == MODE_PARTIAL) {
-        *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = v;
-      } else {
-        f32x4* o = reinterpret_cast<f32x4*>(static_cast<float*>(out) + idx);
-        const f32x4 nv = accumulate ? *o + v : v;
-        *o = nv;
-        if (mirror) *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
+      f32x4 hv[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) hv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (MODE == MODE_RESIDUAL) {
+        if (accumulate) {  // (unconditional loads at clamped addresses: a per-load branch made hipcc wait at each join)
+          const float* hrow = static_cast<const float*>(out) + (size_t)min(row, M - 1) * N + 4 * q;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            hv[j] = *reinterpret_cast<const f32x4*>(hrow + min((n0 >> 4) + wc * NJ + j, NTT - 1) * 16);
+        }
       }
-    };
+      // every result of the row first, then the stores (a store between two uses made hipcc wait for the store too)
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < NJ; ++j) hv[j] += tile_val(j, i);  // (accumulate 0 / partial: hv is zero, 0 + v = v exactly)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) piece(j, i);
+      for (int j = 0; j < NJ; ++j) {
+        const int tile = (n0 >> 4) + wc * NJ + j;
+        if (tile >= NTT || row >= M) continue;
+        const size_t idx = (size_t)row * N + tile * 16 + 4 * q;
+        if constexpr (MODE == MODE_PARTIAL) {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(out) + (size_t)split * M * N + idx) = hv[j];
+        } else {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(out) + idx) = hv[j];
+          if (mirror)
+            *reinterpret_cast<u32x2*>(mirror + idx) = u32x2{pack2bf(hv[j][0], hv[j][1]), pack2bf(hv[j][2], hv[j][3])};
+        }
+      }
+    }
   }
 }
 

@@ -862,22 +862,31 @@ JLA_DEV void g4_epilogue(Acc& acc, float* ss, u32x4* lds, int wu, int lane, int 
     // RoPE on the two (even, odd) pairs of the lane's 4 columns in fp32, then staged: 16-byte pieces of a row go to
     // q or to the k / v cache row at slot[0] + (position in the sequence); same arithmetic as gemm2's /
     // gemm_reduce_kernel's QKV epilogue (reference model.py:58-92, :169-199)
+    // the positions of this lane's 8 rows, then per n-tile the 8 rows' RoPE factors, each batch loaded before any
+    // value is used (loaded where used, behind the staged stores, they went one memory round trip at a time)
+    int posr[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) posr[i] = qa.positions[min(rbase + 16 * i, M - 1)];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (posr[i] < 0 || posr[i] >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
+      posr[i] = posr[i] < 0 ? 0 : (posr[i] >= qa.table_len ? qa.table_len - 1 : posr[i]);
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int gcol = n0 + wc * WN + 16 * j + 4 * q;
       const int head = gcol / qa.Dh, d0 = gcol - head * qa.Dh;
+      float4 cs[8];  // (loaded for every head; used for q and k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        cs[i] = *reinterpret_cast<const float4*>(qa.table + (size_t)posr[i] * (qa.Dh >> 1) + (d0 >> 1));
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int grow = min(rbase + 16 * i, M - 1);
         const f32x4 tv = tile_val(j, i);
         float v0 = tv[0], v1 = tv[1], v2 = tv[2], v3 = tv[3];
         if (head < qa.H + qa.Hkv) {
-          int pos = qa.positions[grow];
-          if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
-          pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
-          const float4 cs = *reinterpret_cast<const float4*>(qa.table + (size_t)pos * (qa.Dh >> 1) + (d0 >> 1));
-          const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
-          const float r2 = v2 * cs.z - v3 * cs.w, r3 = v2 * cs.w + v3 * cs.z;
+          const float r0 = v0 * cs[i].x - v1 * cs[i].y, r1 = v0 * cs[i].y + v1 * cs[i].x;
+          const float r2 = v2 * cs[i].z - v3 * cs[i].w, r3 = v2 * cs[i].w + v3 * cs[i].z;
           v0 = r0;
           v1 = r1;
           v2 = r2;

@@ -58,6 +58,15 @@ JLA_DEV void skinny_epilogue(const f32x4 (&acc)[MT][NT], const float (&ss)[MT], 
   constexpr int EPT = (MT * NT * 256 + NW * 64 - 1) / (NW * 64);  // epilogue elements per thread
   float hpre[EPT];     // MODE_RESIDUAL: h at (m, col)
   float2 hpre2[EPT];   // MODE_TPRESID: h at (m, col .. col + 1), even columns
+  int ppre[EPT];       // MODE_QKV: the element's row position (its RoPE factor is one dependent load fewer later)
+  if constexpr (MODE == MODE_QKV) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = threadIdx.x + j * NW * 64;
+      const int m = (e / (256 * NT)) * 16 + ((e >> 4) & 15);
+      ppre[j] = qa.positions[min(m, M - 1)];
+    }
+  }
   if constexpr (MODE == MODE_RESIDUAL || MODE == MODE_TPRESID) {
     const float* h = static_cast<const float*>(out);
 #pragma unroll
@@ -278,7 +287,7 @@ JLA_DEV void skinny_epilogue(const f32x4 (&acc)[MT][NT], const float (&ss)[MT], 
         float r = v;
         if (head < qa.H + qa.Hkv) {
           const float pv = reduced(mt, t, ln ^ 1, i) * inv_rms[m];
-          int pos = qa.positions[m];
+          int pos = ppre[j];
           if (pos < 0 || pos >= qa.table_len) JLA_FLAG(JLA_BOUNDS_ROPE_POS);
           pos = pos < 0 ? 0 : (pos >= qa.table_len ? qa.table_len - 1 : pos);
           const float2 cs = qa.table[(size_t)pos * (qa.Dh >> 1) + (d >> 1)];
